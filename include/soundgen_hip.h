@@ -1,0 +1,215 @@
+/*
+ * soundgen_hip.h — C-ABI of libsoundgen_hip.so, the MI355X-native engine for
+ * soundgen's additive-source + formant-filter hot path.
+ *
+ * Reference interfaces this ABI replaces (nemochina2008/soundgen_beta, R):
+ *   soundgen()            R/soundgen.R:208-862   -> sg_soundgen / sg_plan_batch+sg_execute
+ *   generateHarmonics()   R/source.R:173-471     -> sg_generate_harmonics
+ *   generateNoise()       R/source.R:57-138      -> sg_generate_noise
+ *   getSpectralEnvelope() R/sourceSpectrum.R:261-566 -> sg_spectral_envelope
+ *   getRolloff()          R/sourceSpectrum.R:71-186  -> sg_get_rolloff (host helper)
+ *   seewave::stft/istft + z*env (R/soundgen.R:779-806) -> sg_formant_filter
+ *
+ * Conventions (mirroring R's .Call world):
+ *   - plain pointers + sizes, doubles on the host side (R numeric vectors);
+ *   - every function returns 0 or a negative SG_E_* code; no C++ exception
+ *     ever crosses this boundary; sg_last_error() gives the message;
+ *   - random draws are INJECTED (R draws them in the reference's order and
+ *     passes them in): standard normals and standard uniforms are consumed
+ *     sequentially in R's draw order (see DESIGN.md "Randomness").
+ *   - "NA" anchors/formants are encoded as n == 0; NULL scalars as NaN.
+ */
+#ifndef SOUNDGEN_HIP_H
+#define SOUNDGEN_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SG_ABI_VERSION 1
+
+enum {
+  SG_OK = 0,
+  SG_E_ARG = -1,         /* invalid argument (R: stop()) */
+  SG_E_DOMAIN = -2,      /* R would error inside approx()/spline() etc. */
+  SG_E_RANDOM = -3,      /* injected random stream exhausted */
+  SG_E_UNSUPPORTED = -4, /* valid in R but not yet supported (e.g. loess) */
+  SG_E_DEVICE = -5,      /* HIP runtime error */
+  SG_E_CAPACITY = -6,    /* output buffer too small */
+  SG_E_NOMEM = -7
+};
+
+/* A data.frame(time, value) of anchors. n == 0 encodes NA / NULL. */
+typedef struct sg_anchors {
+  int32_t n;
+  const double* time;
+  const double* value;
+} sg_anchors;
+
+/* A list of formants, each a data.frame(time, freq, amp, width) with
+ * n_points[f] rows; arrays are concatenated over formants. n_formants == 0
+ * encodes NA. f1_index is the position of the formant named "f1" (-1 if
+ * absent; needed by the nasalization branch, R/sourceSpectrum.R:469-504). */
+typedef struct sg_formants {
+  int32_t n_formants;
+  int32_t f1_index;
+  const int32_t* n_points;
+  const double* time;
+  const double* freq;
+  const double* amp;
+  const double* width;
+} sg_formants;
+
+/* Injected random streams (R's rnorm()/runif() draw order). */
+typedef struct sg_random {
+  const double* normals;
+  int64_t n_normals;
+  const double* uniforms;
+  int64_t n_uniforms;
+} sg_random;
+
+/* Formals of generateHarmonics(), R/source.R:173-205 (pitch and amplAnchors
+ * are separate arguments). */
+typedef struct sg_harm_params {
+  double attackLen, nonlinBalance, nonlinDep, jitterDep, jitterLen;
+  double vibratoFreq, vibratoDep, shimmerDep, creakyBreathy;
+  double rolloff, rolloffOct, rolloffKHz, rolloffParab, rolloffParabHarm;
+  double rolloffLip, rolloff_perAmpl, temperature, pitchDriftDep;
+  double pitchDriftFreq, randomWalk_trendStrength, shortestEpoch, subFreq;
+  double subDep, amDep, amFreq, overlap, samplingRate, pitchFloor;
+  double pitchCeiling, pitchSamplingRate, throwaway;
+} sg_harm_params;
+
+/* Formals of soundgen(), R/soundgen.R:208-277. tempEffects is flattened in
+ * the order sylLenDep, formDrift, formDisp, pitchDriftDep, pitchDriftFreq,
+ * pitchAnchorsDep, noiseAnchorsDep, amplAnchorsDep. vocalTract NaN = NULL. */
+typedef struct sg_soundgen_args {
+  double repeatBout, nSyl, sylLen, pauseLen;
+  sg_anchors pitchAnchors, pitchAnchorsGlobal;
+  double temperature;
+  double tempEffects[8];
+  double maleFemale, creakyBreathy, nonlinBalance, nonlinDep;
+  double jitterLen, jitterDep, vibratoFreq, vibratoDep, shimmerDep;
+  double attackLen, rolloff, rolloffOct, rolloffKHz, rolloffParab;
+  double rolloffParabHarm, rolloffLip;
+  sg_formants formants;
+  double formantDep, formantDepStoch, vocalTract;
+  double subFreq, subDep, shortestEpoch, amDep, amFreq, amShape;
+  sg_anchors noiseAnchors;
+  sg_formants formantsNoise;
+  double rolloffNoise;
+  sg_anchors mouthAnchors, amplAnchors, amplAnchorsGlobal;
+  double samplingRate, windowLength, overlap, addSilence;
+  double pitchFloor, pitchCeiling, pitchSamplingRate, throwaway;
+  int32_t invalidArgAction; /* 0 adjust, 1 abort, 2 ignore */
+} sg_soundgen_args;
+
+/* One call of a batch: either a whole soundgen() call or a bare
+ * generateHarmonics() call on a given pitch contour. */
+enum { SG_CALL_SOUNDGEN = 0, SG_CALL_HARMONICS = 1 };
+typedef struct sg_call_desc {
+  int32_t kind;
+  /* SG_CALL_SOUNDGEN */
+  const sg_soundgen_args* args;
+  /* SG_CALL_HARMONICS */
+  const double* pitch;
+  int64_t pitch_len;
+  const sg_harm_params* harm;
+  sg_anchors amplAnchors;
+  /* random draws for this call (both kinds) */
+  sg_random random;
+} sg_call_desc;
+
+typedef struct sg_ctx sg_ctx;
+typedef struct sg_plan sg_plan;
+
+/* ---- context ---------------------------------------------------------- */
+int sg_ctx_create(int device, sg_ctx** out);
+void sg_ctx_destroy(sg_ctx* ctx);
+const char* sg_last_error(const sg_ctx* ctx);
+int sg_abi_version(void);
+/* Fill the defaults of generateHarmonics()/soundgen() formals. */
+void sg_default_harm_params(sg_harm_params* p);
+void sg_default_soundgen_args(sg_soundgen_args* a);
+
+/* ---- batch path (planned on host, executed on device) ------------------ */
+/* All integer/length bookkeeping happens here, bit-exact with R. */
+int sg_plan_batch(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls,
+                  sg_plan** out);
+void sg_plan_destroy(sg_plan* plan);
+int64_t sg_plan_n_calls(const sg_plan* plan);
+int64_t sg_plan_total_samples(const sg_plan* plan);
+/* per-call output length and offset into the packed output (int64 each) */
+int sg_plan_lengths(const sg_plan* plan, int64_t* out_len, int64_t* out_off);
+/* per-call status (0 ok or SG_E_*): a failed call marks its slot, the batch
+ * does not abort (SURVEY §5 failure detection). */
+int sg_plan_status(const sg_plan* plan, int32_t* out_status);
+/* Bytes of device workspace the plan needs (descriptors + scratch). */
+int64_t sg_plan_device_bytes(const sg_plan* plan);
+/* Upload descriptors/inputs to HBM (outside any timed region). */
+int sg_plan_upload(sg_ctx* ctx, sg_plan* plan);
+/* Run every kernel of the plan on `stream` (hipStream_t, NULL = ctx stream)
+ * writing fp32 samples into device buffer d_out (packed, offsets as above).
+ * No host synchronisation inside; graph-capturable. */
+int sg_execute(sg_ctx* ctx, sg_plan* plan, float* d_out, void* stream);
+/* Profiling: when enabled, sg_execute brackets the sine-bank launch with
+ * HIP events on the launch stream; sg_profile_read returns the average
+ * duration (ms) over the recorded executes and clears them. */
+int sg_set_profiling(sg_ctx* ctx, int on);
+int sg_profile_read(sg_ctx* ctx, double* sine_ms_avg, int64_t* n);
+int sg_synchronize(sg_ctx* ctx);
+/* Message of a failed call (status != 0). */
+const char* sg_plan_call_message(const sg_plan* plan, int64_t i);
+/* Per-kernel launch statistics of the last sg_execute (for roofline). */
+int sg_plan_kernel_stats(const sg_plan* plan, int64_t* harm_samples,
+                         int64_t* harm_terms, int64_t* harm_amp_bytes,
+                         int64_t* fft_frames);
+
+/* ---- function-level entries mirroring the R API (synchronous) ---------- */
+int sg_generate_harmonics(sg_ctx* ctx, const double* pitch, int64_t len,
+                          const sg_harm_params* p, sg_anchors amplAnchors,
+                          const sg_random* rnd, double* out, int64_t cap,
+                          int64_t* out_len);
+int sg_soundgen(sg_ctx* ctx, const sg_soundgen_args* a, const sg_random* rnd,
+                double* out, int64_t cap, int64_t* out_len);
+/* generateNoise(len, noiseAnchors, rolloffNoise, attackLen,
+ * windowLength_points, samplingRate, overlap, throwaway, filterNoise);
+ * filterNoise is nr x filter_nc column-major (NULL/0 = NA). */
+int sg_generate_noise(sg_ctx* ctx, int64_t len, sg_anchors noiseAnchors,
+                      double rolloffNoise, double attackLen,
+                      int32_t windowLength_points, double samplingRate,
+                      double overlap, double throwaway,
+                      const double* filterNoise, int32_t filter_nc,
+                      const sg_random* rnd, double* out);
+/* getSpectralEnvelope(nr, nc, formants, formantDep, rolloffLip,
+ * mouthAnchors, mouthOpenThres, openMouthBoost, vocalTract, temperature,
+ * formDrift, formDisp, formantDepStoch, smoothLinearFactor, samplingRate,
+ * speedSound) -> out[nr*nc] column-major. */
+int sg_spectral_envelope(sg_ctx* ctx, int32_t nr, int32_t nc,
+                         const sg_formants* formants, double formantDep,
+                         double rolloffLip, sg_anchors mouthAnchors,
+                         double mouthOpenThres, double openMouthBoost,
+                         double vocalTract, double temperature,
+                         double formDrift, double formDisp,
+                         double formantDepStoch, double smoothLinearFactor,
+                         double samplingRate, double speedSound,
+                         const sg_random* rnd, double* out);
+/* STFT(hamming) x envelope -> ISTFT(hann OLA) -> /max, R/soundgen.R:743-807.
+ * env is nr x env_nc (env_nc == 1: stationary). out cap >= len. */
+int sg_formant_filter(sg_ctx* ctx, const double* sound, int64_t len,
+                      const double* env, int32_t env_nc,
+                      int32_t windowLength_points, double overlap,
+                      double* out, int64_t cap, int64_t* out_len);
+/* getRolloff() (host helper; R returns H x nGC). out cap = nHarmonics*nGC */
+int sg_get_rolloff(const double* pitch_per_gc, int32_t n_gc,
+                   int32_t nHarmonics, double rolloff, double rolloffOct,
+                   double rolloffParab, double rolloffParabHarm,
+                   double rolloffKHz, double baseline, double throwaway,
+                   double samplingRate, double* out, int32_t* out_rows);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SOUNDGEN_HIP_H */

@@ -1,0 +1,76 @@
+"""R-level API mirror: soundgen(), generateHarmonics(), getRolloff().
+
+Same names, argument meanings, defaults and error behaviour as the reference
+(R/soundgen.R:208, R/source.R:173, R/sourceSpectrum.R:71); every synthesis
+runs on the GPU through libsoundgen_hip.so. Random draws are injected
+(`normals`, `uniforms`: R's rnorm()/runif() draws in the reference order).
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _abi, native, rargs
+
+
+def _ctx(device):
+    return native.default_context(device)
+
+
+def generateHarmonics(pitch, amplAnchors=rargs.NA, normals=None, uniforms=None, device=0, **kw):
+    """generateHarmonics(pitch, ...) — R/source.R:173-471."""
+    h = rargs.Holder()
+    p = rargs.fill_harm_params(kw)
+    pitch = h.arr(pitch)
+    rnd = h.random(normals, uniforms)
+    sr = p.samplingRate
+    cap = int(np.ceil(len(pitch) / p.pitchSamplingRate * sr * 1.2)) + int(sr) + 4096
+    out = np.zeros(cap)
+    n = C.c_int64()
+    ctx = _ctx(device)
+    L = native.lib()
+    rc = L.sg_generate_harmonics(ctx.ptr, _abi.dptr(pitch), len(pitch), C.byref(p),
+                                 h.anchors(rargs.as_anchors(amplAnchors)), C.byref(rnd), _abi.dptr(out), cap,
+                                 C.byref(n))
+    if rc == _abi.SG_E_CAPACITY:
+        out = np.zeros(n.value)
+        rc = L.sg_generate_harmonics(ctx.ptr, _abi.dptr(pitch), len(pitch), C.byref(p),
+                                     h.anchors(rargs.as_anchors(amplAnchors)), C.byref(rnd), _abi.dptr(out),
+                                     n.value, C.byref(n))
+    native.check(rc, ctx.ptr)
+    return out[:n.value].copy()
+
+
+def soundgen(normals=None, uniforms=None, device=0, **kw):
+    """soundgen(...) — R/soundgen.R:208-862. Returns the waveform (float64)."""
+    h = rargs.Holder()
+    a = rargs.fill_soundgen_args(h, kw)
+    rnd = h.random(normals, uniforms)
+    ctx = _ctx(device)
+    L = native.lib()
+    n = C.c_int64()
+    cap = 1 << 16
+    while True:
+        out = np.zeros(cap)
+        rc = L.sg_soundgen(ctx.ptr, C.byref(a), C.byref(rnd), _abi.dptr(out), cap, C.byref(n))
+        if rc == _abi.SG_E_CAPACITY:
+            cap = n.value
+            continue
+        native.check(rc, ctx.ptr)
+        return out[:n.value].copy()
+
+
+def getRolloff(pitch_per_gc=(440,), nHarmonics=100, rolloff=-12, rolloffOct=-2, rolloffParab=0,
+               rolloffParabHarm=2, rolloffParabCeiling=None, rolloffKHz=-6, baseline=200, throwaway=-120,
+               samplingRate=16000, plot=False):
+    """getRolloff() — R/sourceSpectrum.R:71-186 (host helper; H x nGC matrix)."""
+    if rolloffParabCeiling is not None:
+        raise NotImplementedError("rolloffParabCeiling")
+    p = np.ascontiguousarray(np.atleast_1d(np.asarray(pitch_per_gc, dtype=np.float64)))
+    out = np.zeros(nHarmonics * len(p))
+    rows = C.c_int32()
+    rc = native.lib().sg_get_rolloff(_abi.dptr(p), len(p), nHarmonics, rolloff, rolloffOct, rolloffParab,
+                                     rolloffParabHarm, rolloffKHz, baseline, throwaway, samplingRate,
+                                     _abi.dptr(out), C.byref(rows))
+    native.check(rc)
+    H = rows.value
+    return out[:H * len(p)].reshape(len(p), H).T.copy()

@@ -1,0 +1,107 @@
+"""Batch path: plan (host, bit-exact bookkeeping) -> upload (HBM) ->
+execute (HIP kernels, no host sync) for a list of independent calls.
+
+A call is a dict:
+  {"kind": "harmonics", "pitch": array, "params": {...}, "amplAnchors": ...,
+   "normals": array|None, "uniforms": array|None}
+  {"kind": "soundgen", "args": {...R soundgen() args...}, "normals":..., "uniforms":...}
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _abi, native, rargs
+
+
+class Plan:
+    def __init__(self, calls, ctx=None):
+        """Plan `calls`. ctx may be None: planning is host-only."""
+        self.ctx = ctx
+        self.holder = rargs.Holder()
+        n = len(calls)
+        descs = (_abi.sg_call_desc * max(n, 1))()
+        self._structs = []
+        for i, c in enumerate(calls):
+            d = descs[i]
+            kind = c.get("kind", "soundgen")
+            d.random = self.holder.random(c.get("normals"), c.get("uniforms"))
+            if kind == "harmonics":
+                d.kind = _abi.SG_CALL_HARMONICS
+                p = self.holder.arr(c["pitch"])
+                d.pitch, d.pitch_len = _abi.dptr(p), len(p)
+                hp = rargs.fill_harm_params(c.get("params", {}))
+                self._structs.append(hp)
+                d.harm = C.pointer(hp)
+                d.amplAnchors = self.holder.anchors(rargs.as_anchors(c.get("amplAnchors")))
+            else:
+                d.kind = _abi.SG_CALL_SOUNDGEN
+                a = rargs.fill_soundgen_args(self.holder, c.get("args", {}))
+                self._structs.append(a)
+                d.args = C.pointer(a)
+        self._descs = descs
+        self.ptr = C.c_void_p()
+        L = native.lib()
+        native.check(L.sg_plan_batch(ctx.ptr if ctx else None, descs, n, C.byref(self.ptr)), ctx.ptr if ctx else None)
+        self.n = n
+        self.lengths = np.zeros(n, dtype=np.int64)
+        self.offsets = np.zeros(n, dtype=np.int64)
+        i64p = C.POINTER(C.c_int64)
+        L.sg_plan_lengths(self.ptr, self.lengths.ctypes.data_as(i64p), self.offsets.ctypes.data_as(i64p))
+        self.status = np.zeros(n, dtype=np.int32)
+        L.sg_plan_status(self.ptr, self.status.ctypes.data_as(C.POINTER(C.c_int32)))
+        self.total = int(L.sg_plan_total_samples(self.ptr))
+        self.uploaded = False
+
+    def message(self, i):
+        return native.lib().sg_plan_call_message(self.ptr, i).decode()
+
+    def stats(self):
+        v = [C.c_int64() for _ in range(4)]
+        native.lib().sg_plan_kernel_stats(self.ptr, *[C.byref(x) for x in v])
+        return dict(harm_samples=v[0].value, harm_terms=v[1].value, harm_amp_bytes=v[2].value,
+                    fft_frames=v[3].value)
+
+    def device_bytes(self):
+        return int(native.lib().sg_plan_device_bytes(self.ptr))
+
+    def upload(self, ctx=None):
+        ctx = ctx or self.ctx
+        native.check(native.lib().sg_plan_upload(ctx.ptr, self.ptr), ctx.ptr)
+        self.ctx = ctx
+        self.uploaded = True
+
+    def execute(self, d_out_ptr, stream_ptr=None):
+        """Run the kernels writing fp32 samples to device pointer d_out_ptr."""
+        native.check(native.lib().sg_execute(self.ctx.ptr, self.ptr, C.c_void_p(d_out_ptr),
+                                             C.c_void_p(stream_ptr) if stream_ptr else None), self.ctx.ptr)
+
+    def close(self):
+        if self.ptr:
+            native.lib().sg_plan_destroy(self.ptr)
+            self.ptr = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def synthesize(calls, device=0):
+    """Plan + run a batch on one GPU; returns a list of float32 numpy arrays."""
+    import torch
+    ctx = native.default_context(device)
+    plan = Plan(calls, ctx)
+    plan.upload()
+    out = torch.empty(max(plan.total, 1), dtype=torch.float32, device="cuda:%d" % device)
+    stream = torch.cuda.current_stream(device)
+    plan.execute(out.data_ptr(), stream.cuda_stream)
+    stream.synchronize()
+    host = out.cpu().numpy()
+    res = []
+    for i in range(plan.n):
+        if plan.status[i] != 0:
+            res.append(native.SoundgenError(int(plan.status[i]), plan.message(i)))
+        else:
+            res.append(host[plan.offsets[i]:plan.offsets[i] + plan.lengths[i]].copy())
+    return res

@@ -1,0 +1,310 @@
+// sg_api.cpp — C-ABI of libsoundgen_hip.so: context, batch plan/upload/
+// execute, and the synchronous function-level entries mirroring the R API.
+// No C++ exception crosses this boundary.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "sg_plan.h"
+#include "sg_exec.h"
+
+struct sg_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  bool profiling = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
+};
+
+struct sg_plan {
+  sg::Batch B;
+  sg::DevicePlan D;
+};
+
+namespace {
+
+int set_err(sg_ctx* ctx, int code, const std::string& m) {
+  if (ctx) ctx->err = m;
+  return code;
+}
+
+#define HIPCHK(x)                                                                         \
+  do {                                                                                    \
+    hipError_t _e = (x);                                                                  \
+    if (_e != hipSuccess)                                                                 \
+      throw sg::SgError(SG_E_DEVICE, std::string(#x) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+template <class F>
+int guarded(sg_ctx* ctx, F&& f) {
+  try {
+    return f();
+  } catch (const sg::SgError& e) {
+    return set_err(ctx, e.code, e.what());
+  } catch (const std::bad_alloc&) {
+    return set_err(ctx, SG_E_NOMEM, "out of host memory");
+  } catch (const std::exception& e) {
+    return set_err(ctx, SG_E_ARG, e.what());
+  }
+}
+
+// Rolls a Batch back to a checkpoint when planning one call fails.
+struct Checkpoint {
+  size_t segs, epochs, knots, amps, tiles, pieces, syls, syl_tiles, cknots, noise, filt, mixes, bouts, frames;
+  int64_t w_total, harm_samples, harm_terms, harm_amp_bytes, fft_frames, scratch;
+  explicit Checkpoint(const sg::Batch& B)
+      : segs(B.segs.size()), epochs(B.epochs.size()), knots(B.knots.size()), amps(B.amps.size()),
+        tiles(B.tiles.size()), pieces(B.pieces.size()), syls(B.syls.size()), syl_tiles(B.syl_tiles.size()),
+        cknots(B.cknots.size()), noise(0), filt(0), mixes(0), bouts(0), frames(0), w_total(B.w_total),
+        harm_samples(B.harm_samples), harm_terms(B.harm_terms), harm_amp_bytes(B.harm_amp_bytes),
+        fft_frames(B.fft_frames), scratch(0) {}
+  void restore(sg::Batch& B) const {
+    B.segs.resize(segs); B.epochs.resize(epochs); B.knots.resize(knots); B.amps.resize(amps);
+    B.tiles.resize(tiles); B.pieces.resize(pieces); B.syls.resize(syls); B.syl_tiles.resize(syl_tiles);
+    B.cknots.resize(cknots); B.w_total = w_total; B.harm_samples = harm_samples; B.harm_terms = harm_terms;
+    B.harm_amp_bytes = harm_amp_bytes; B.fft_frames = fft_frames;
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+int sg_abi_version(void) { return SG_ABI_VERSION; }
+
+void sg_default_harm_params(sg_harm_params* p) {
+  *p = sg_harm_params{50, 0, 0, 0, 1, 100, 0, 0, 0, -18, -2, -6, 0, 3, 6, 12, 0, .5, .125, .5, 300, 100,
+                      0, 0, 30, 75, 16000, 75, 3500, 3500, -120};
+}
+
+int sg_ctx_create(int device, sg_ctx** out) {
+  *out = nullptr;
+  auto* c = new (std::nothrow) sg_ctx();
+  if (!c) return SG_E_NOMEM;
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return SG_E_DEVICE;
+  }
+  *out = c;
+  return SG_OK;
+}
+
+void sg_ctx_destroy(sg_ctx* ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  for (auto& ev : ctx->prof_events) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
+  if (ctx->stream) hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+const char* sg_last_error(const sg_ctx* ctx) { return ctx ? ctx->err.c_str() : ""; }
+
+int sg_plan_batch(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, sg_plan** out) {
+  return guarded(ctx, [&]() {
+    auto P = std::make_unique<sg_plan>();
+    sg::Batch& B = P->B;
+    B.call_len.assign(n_calls, 0);
+    B.call_off.assign(n_calls, 0);
+    B.call_status.assign(n_calls, 0);
+    B.call_msg.assign(n_calls, "");
+    int64_t off = 0;
+    for (int64_t c = 0; c < n_calls; ++c) {
+      const sg_call_desc& d = calls[c];
+      Checkpoint cp(B);
+      const int first_syl = (int)B.syls.size();
+      try {
+        sg::Rng R;
+        R.s = &d.random;
+        int64_t L = 0;
+        if (d.kind == SG_CALL_HARMONICS) {
+          if (!d.pitch || !d.harm) throw sg::SgError(SG_E_ARG, "harmonics call without pitch/params");
+          L = sg::plan_harmonics(B, d.pitch, d.pitch_len, *d.harm, d.amplAnchors, R, off, false);
+          sg::tile_syllables(B, first_syl);
+        } else if (d.kind == SG_CALL_SOUNDGEN) {
+          if (!d.args) throw sg::SgError(SG_E_ARG, "soundgen call without args");
+          L = sg::plan_soundgen(B, *d.args, R, off, first_syl);
+        } else {
+          throw sg::SgError(SG_E_ARG, "unknown call kind");
+        }
+        B.call_off[c] = off;
+        B.call_len[c] = L;
+        off += L;
+      } catch (const sg::SgError& e) {
+        cp.restore(B);
+        sg::restore_soundgen_tail(B, first_syl);
+        B.call_status[c] = e.code;
+        B.call_msg[c] = e.what();
+        B.call_off[c] = off;
+        B.call_len[c] = 0;
+      }
+    }
+    B.total_out = off;
+    sg::finalize_plan(B);
+    *out = P.release();
+    return SG_OK;
+  });
+}
+
+void sg_plan_destroy(sg_plan* plan) {
+  if (!plan) return;
+  sg::device_free(plan->D);
+  delete plan;
+}
+
+int64_t sg_plan_n_calls(const sg_plan* plan) { return plan ? (int64_t)plan->B.call_len.size() : 0; }
+int64_t sg_plan_total_samples(const sg_plan* plan) { return plan ? plan->B.total_out : 0; }
+
+int sg_plan_lengths(const sg_plan* plan, int64_t* out_len, int64_t* out_off) {
+  if (!plan) return SG_E_ARG;
+  const size_t n = plan->B.call_len.size();
+  if (out_len) std::memcpy(out_len, plan->B.call_len.data(), n * sizeof(int64_t));
+  if (out_off) std::memcpy(out_off, plan->B.call_off.data(), n * sizeof(int64_t));
+  return SG_OK;
+}
+
+int sg_plan_status(const sg_plan* plan, int32_t* out_status) {
+  if (!plan) return SG_E_ARG;
+  std::memcpy(out_status, plan->B.call_status.data(), plan->B.call_status.size() * sizeof(int32_t));
+  return SG_OK;
+}
+
+const char* sg_plan_call_message(const sg_plan* plan, int64_t i) {
+  if (!plan || i < 0 || i >= (int64_t)plan->B.call_msg.size()) return "";
+  return plan->B.call_msg[i].c_str();
+}
+
+int64_t sg_plan_device_bytes(const sg_plan* plan) { return plan ? sg::device_bytes(plan->B) : 0; }
+
+int sg_plan_upload(sg_ctx* ctx, sg_plan* plan) {
+  return guarded(ctx, [&]() {
+    HIPCHK(hipSetDevice(ctx->device));
+    sg::device_upload(plan->B, plan->D, ctx->stream);
+    return SG_OK;
+  });
+}
+
+int sg_execute(sg_ctx* ctx, sg_plan* plan, float* d_out, void* stream) {
+  return guarded(ctx, [&]() {
+    if (!plan->D.uploaded) throw sg::SgError(SG_E_ARG, "sg_execute: plan not uploaded");
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (ctx->profiling) {
+      HIPCHK(hipEventCreate(&e0));
+      HIPCHK(hipEventCreate(&e1));
+    }
+    sg::device_execute(plan->B, plan->D, d_out, s, e0, e1);
+    if (ctx->profiling) ctx->prof_events.emplace_back(e0, e1);
+    return SG_OK;
+  });
+}
+
+int sg_set_profiling(sg_ctx* ctx, int on) {
+  ctx->profiling = on != 0;
+  return SG_OK;
+}
+
+// Average duration (ms) of the sine-bank kernel over the executes recorded
+// since profiling was enabled (events are on the launch stream).
+int sg_profile_read(sg_ctx* ctx, double* sine_ms_avg, int64_t* n) {
+  return guarded(ctx, [&]() {
+    double tot = 0;
+    int64_t cnt = 0;
+    for (auto& ev : ctx->prof_events) {
+      HIPCHK(hipEventSynchronize(ev.second));
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, ev.first, ev.second));
+      tot += ms;
+      ++cnt;
+      hipEventDestroy(ev.first);
+      hipEventDestroy(ev.second);
+    }
+    ctx->prof_events.clear();
+    *sine_ms_avg = cnt ? tot / cnt : 0;
+    *n = cnt;
+    return SG_OK;
+  });
+}
+
+int sg_plan_kernel_stats(const sg_plan* plan, int64_t* harm_samples, int64_t* harm_terms, int64_t* harm_amp_bytes,
+                         int64_t* fft_frames) {
+  if (!plan) return SG_E_ARG;
+  *harm_samples = plan->B.harm_samples;
+  *harm_terms = plan->B.harm_terms;
+  *harm_amp_bytes = plan->B.harm_amp_bytes;
+  *fft_frames = plan->B.fft_frames;
+  return SG_OK;
+}
+
+int sg_synchronize(sg_ctx* ctx) {
+  return guarded(ctx, [&]() {
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return SG_OK;
+  });
+}
+
+// ---- synchronous single-call helpers --------------------------------------
+static int run_single(sg_ctx* ctx, const sg_call_desc& d, double* out, int64_t cap, int64_t* out_len) {
+  sg_plan* plan = nullptr;
+  int rc = sg_plan_batch(ctx, &d, 1, &plan);
+  if (rc) return rc;
+  std::unique_ptr<sg_plan, void (*)(sg_plan*)> hold(plan, sg_plan_destroy);
+  if (plan->B.call_status[0]) return set_err(ctx, plan->B.call_status[0], plan->B.call_msg[0]);
+  const int64_t L = plan->B.call_len[0];
+  *out_len = L;
+  if (L > cap) return set_err(ctx, SG_E_CAPACITY, "output buffer too small");
+  return guarded(ctx, [&]() {
+    HIPCHK(hipSetDevice(ctx->device));
+    sg::device_upload(plan->B, plan->D, ctx->stream);
+    float* d_out = nullptr;
+    HIPCHK(hipMalloc(&d_out, (size_t)std::max<int64_t>(L, 1) * sizeof(float)));
+    std::unique_ptr<float, hipError_t (*)(void*)> hold_out(d_out, hipFree);
+    sg::device_execute(plan->B, plan->D, d_out, ctx->stream, nullptr, nullptr);
+    std::vector<float> h((size_t)L);
+    HIPCHK(hipMemcpyAsync(h.data(), d_out, (size_t)L * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    for (int64_t i = 0; i < L; ++i) out[i] = h[i];
+    return SG_OK;
+  });
+}
+
+int sg_generate_harmonics(sg_ctx* ctx, const double* pitch, int64_t len, const sg_harm_params* p,
+                          sg_anchors amplAnchors, const sg_random* rnd, double* out, int64_t cap,
+                          int64_t* out_len) {
+  sg_call_desc d{};
+  d.kind = SG_CALL_HARMONICS;
+  d.pitch = pitch;
+  d.pitch_len = len;
+  d.harm = p;
+  d.amplAnchors = amplAnchors;
+  if (rnd) d.random = *rnd;
+  return run_single(ctx, d, out, cap, out_len);
+}
+
+int sg_soundgen(sg_ctx* ctx, const sg_soundgen_args* a, const sg_random* rnd, double* out, int64_t cap,
+                int64_t* out_len) {
+  sg_call_desc d{};
+  d.kind = SG_CALL_SOUNDGEN;
+  d.args = a;
+  if (rnd) d.random = *rnd;
+  return run_single(ctx, d, out, cap, out_len);
+}
+
+int sg_get_rolloff(const double* pitch_per_gc, int32_t n_gc, int32_t nHarmonics, double rolloff, double rolloffOct,
+                   double rolloffParab, double rolloffParabHarm, double rolloffKHz, double baseline,
+                   double throwaway, double samplingRate, double* out, int32_t* out_rows) {
+  return guarded(nullptr, [&]() {
+    sg::vec p(pitch_per_gc, pitch_per_gc + n_gc);
+    int64_t H = 0;
+    sg::vec r = sg::get_rolloff(p, nHarmonics, sg::vec(n_gc, rolloff), sg::vec(n_gc, rolloffOct), rolloffParab,
+                                rolloffParabHarm, sg::vec(n_gc, rolloffKHz), baseline, throwaway, samplingRate, H);
+    std::memcpy(out, r.data(), r.size() * sizeof(double));
+    *out_rows = (int32_t)H;
+    return SG_OK;
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,750 @@
+// sg_plan_harm.cpp — host planner for generateHarmonics() (R/source.R:173-471).
+//
+// The planner reproduces every data-independent step of the reference in
+// fp64 (vibrato, glottal cycles, jitter/drift/random walks from injected
+// draws, getRolloff, shimmer, getVocalFry, upsample) and the two
+// data-dependent bookkeeping steps (zero-crossing trims of crossFade(), the
+// output length) by evaluating the epoch waveform in fp64 only at the few
+// samples the zero-crossing searches visit. The per-sample work — the sine
+// bank, the crossfades, normalisation, fades, envelopes — runs on the GPU.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "sg_plan.h"
+
+namespace sg {
+
+// ------------------------------------------------------------- contours
+bool smooth_contour(const sg_anchors& an, int64_t len, bool thisIsPitch, int method, bool has_floor,
+                    double vfloor, bool has_ceil, double vceil, vec& out) {
+  out.clear();
+  if (an.n <= 0) return false;
+  const int64_t n = an.n;
+  if (n > 10 && method == 0) method = 1;
+  vec t(an.time, an.time + n), v(an.value, an.value + n);
+  if (has_floor) for (auto& x : v) if (x < vfloor) x = vfloor;
+  if (has_ceil) for (auto& x : v) if (x > vceil) x = vceil;
+  if (thisIsPitch) {
+    for (auto& x : v) x = HzToSemitones(x);
+    if (has_floor) vfloor = HzToSemitones(vfloor);
+    if (has_ceil) vceil = HzToSemitones(vceil);
+  }
+  const double tmin = r_min(t);
+  for (auto& x : t) x -= tmin;
+  const double tmax = r_max(t);
+  for (auto& x : t) x /= tmax;
+  if (len == 0) return false;
+  if (n == 1) out.assign(len, v[0]);
+  else if (n == 2) out = r_seq_len(v[0], v[1], len);
+  else {
+    if (method != 1) throw SgError(SG_E_UNSUPPORTED, "getSmoothContour: loess (3-10 anchors) not supported yet");
+    out = r_spline(t, v, len);
+    for (auto& x : out) {
+      if (has_floor && x < vfloor) x = vfloor;
+      if (has_ceil && x > vceil) x = vceil;
+    }
+  }
+  for (auto& x : out) if (std::isnan(x)) x = 0;
+  if (thisIsPitch) for (auto& x : out) x = semitonesToHz(x);
+  return true;
+}
+
+SgContour contour_desc(Batch& B, const sg_anchors& an, int64_t L, bool has_floor, double vfloor,
+                       bool has_ceil, double vceil, bool db) {
+  SgContour c{};
+  c.lo = -INFINITY; c.hi = INFINITY; c.db = db ? 1 : 0;
+  if (an.n <= 0 || L <= 0) { c.kind = 0; return c; }
+  const int64_t n = an.n;
+  vec t(an.time, an.time + n), v(an.value, an.value + n);
+  if (has_floor) for (auto& x : v) if (x < vfloor) x = vfloor;
+  if (has_ceil) for (auto& x : v) if (x > vceil) x = vceil;
+  if (n == 1) { c.kind = 1; c.a = v[0]; return c; }
+  if (n == 2) { c.kind = 2; c.a = v[0]; c.b = v[1]; return c; }
+  if (n <= 10) throw SgError(SG_E_UNSUPPORTED, "getSmoothContour: loess (3-10 anchors) not supported yet");
+  const double tmin = r_min(t);
+  for (auto& x : t) x -= tmin;
+  const double tmax = r_max(t);
+  for (auto& x : t) x /= tmax;
+  Spline s = fmm_spline(t, v);
+  c.kind = 3; c.nk = (int32_t)n; c.k_off = (int64_t)B.cknots.size();
+  c.a = t.front(); c.b = t.back();
+  if (has_floor) c.lo = vfloor;
+  if (has_ceil) c.hi = vceil;
+  for (const vec* a : {&s.x, &s.y, &s.b, &s.c, &s.d}) B.cknots.insert(B.cknots.end(), a->begin(), a->end());
+  return c;
+}
+
+// host evaluation of a device contour (used for the fused-max bookkeeping tests)
+static double contour_eval(const Batch& B, const SgContour& c, int64_t L, int64_t k) {
+  double v;
+  switch (c.kind) {
+    case 0: return 1.0;
+    case 1: v = c.a; break;
+    case 2: {
+      if (k == 0 || c.a == c.b) v = c.a;
+      else if (k == L - 1) v = c.b;
+      else v = c.a + (double)k * ((c.b - c.a) / (double)(L - 1));
+      break;
+    }
+    default: {
+      const double* x = &B.cknots[c.k_off];
+      const double* y = x + c.nk; const double* b = y + c.nk; const double* cc = b + c.nk; const double* d = cc + c.nk;
+      const double u = r_seqint_at(c.a, c.b, L, k);
+      int64_t i = 0, j = c.nk;
+      do { int64_t m = (i + j) / 2; if (u < x[m]) j = m; else i = m; } while (j > i + 1);
+      const double dx = u - x[i];
+      v = y[i] + dx * (b[i] + dx * (cc[i] + dx * d[i]));
+      if (v < c.lo) v = c.lo;
+      if (v > c.hi) v = c.hi;
+    }
+  }
+  return c.db ? std::pow(2.0, v / 10) : v;
+}
+
+// ------------------------------------------------------ random walks
+static void zero_one(vec& x) {
+  const double mn = r_min(x);
+  for (auto& v : x) v -= mn;
+  const double mx = r_max(x);
+  for (auto& v : x) v /= mx;
+}
+
+// getRandomWalk(), R/utilities_math.R:289-326 (method: 0 linear, 1 spline)
+vec get_random_walk(Rng& R, int64_t len, double rw_range, double rw_smoothing, int method,
+                    const vec& trend_in, bool trend_lazy_rnorm) {
+  if (len < 2) return vec{R.rgamma(1.0 / (rw_range * rw_range), 1.0 / (rw_range * rw_range))};
+  vec trend = trend_in;
+  if (trend_lazy_rnorm) trend = vec{R.rnorm(0, 1)};
+  const double p = std::pow(2.0, 1.0 / rw_smoothing);
+  double nd = std::floor(p > 2 ? p : 2);
+  vec tshort;
+  if (trend.size() > 1) {
+    nd = r_round(nd / 2) * 2;
+    const int64_t each = (int64_t)(nd / (double)trend.size());
+    for (double tv : trend) for (int64_t e = 0; e < each; ++e) tshort.push_back(tv);
+  } else tshort = trend;
+  vec rw_long;
+  if (nd > (double)len) {
+    vec z(len);
+    for (int64_t i = 0; i < len; ++i) z[i] = R.rnorm(tshort[i % tshort.size()], 1.0);
+    rw_long = r_cumsum(z);
+  } else {
+    const int64_t n = (int64_t)nd;
+    vec z(n);
+    for (int64_t i = 0; i < n; ++i) z[i] = R.rnorm(tshort[i % tshort.size()], 1.0);
+    vec rs = r_cumsum(z), xs(n);
+    for (int64_t i = 0; i < n; ++i) xs[i] = (double)(i + 1);
+    rw_long = method == 0 ? r_approx_n(xs, rs, len) : r_spline(xs, rs, len);
+  }
+  const double mn = r_min(rw_long);
+  for (auto& v : rw_long) v -= mn;
+  double mx = 0;
+  for (double v : rw_long) { double a = std::fabs(v); if (a > mx || std::isnan(a)) mx = a; }
+  for (auto& v : rw_long) v = v / mx * rw_range;
+  return rw_long;
+}
+
+// clumper(), R/utilities_math.R:555-600
+void clumper(vec& s, const vec& minLen_in) {
+  const int64_t n = (int64_t)s.size();
+  if (r_max(minLen_in) < 2) return;
+  vec ml(minLen_in.size());
+  for (size_t i = 0; i < ml.size(); ++i) ml[i] = r_round(minLen_in[i]);
+  bool uniq2 = false;
+  for (int64_t i = 1; i < n && !uniq2; ++i) if (s[i] != s[0]) uniq2 = true;
+  if (!uniq2 || (ml.size() == 1 && (double)n < ml[0]) || (double)n < ml[0]) {
+    vec tmp = s; std::sort(tmp.begin(), tmp.end());
+    const double med = (n % 2) ? tmp[n / 2] : (tmp[n / 2 - 1] + tmp[n / 2]) / 2.0;
+    for (auto& v : s) v = r_round(med);
+    return;
+  }
+  if (ml.size() == 1 || (int64_t)ml.size() != n) {
+    vec m2(n);
+    for (int64_t i = 0; i < n; ++i) m2[i] = ml[i % ml.size()];
+    ml = m2;
+  }
+  double c = 0;
+  for (int64_t i = 1; i < n; ++i) {
+    if (s[i - 1] == s[i]) c = c + 1;
+    else if (c < ml[i]) { s[i] = s[i - 1]; c = c + 1; }
+    else c = 1;
+  }
+  const double mlast = ml[n - 1];
+  int64_t lo = (int64_t)((double)n - mlast + 1);
+  if (lo < 2) lo = 2;
+  int64_t cnt = 0;
+  for (int64_t k = lo; k <= n; ++k) if (s[k - 1] == s[n - 1]) cnt++;
+  if ((double)cnt < mlast) {
+    const int64_t nidx = n - lo + 1;
+    std::vector<int64_t> idx(nidx);
+    for (int64_t k = 0; k < nidx; ++k) idx[k] = n - k;
+    double cc = 1; int64_t ii = 2;
+    while (ii <= nidx && s[idx[ii - 1] - 1] == s[idx[ii - 1] - 2] && ii < nidx) { cc++; ii++; }
+    if (cc < mlast) { const double v = s[lo - 1]; for (int64_t k = 0; k < nidx; ++k) s[idx[k] - 1] = v; }
+  }
+}
+
+// ------------------------------------------------------------- rolloff
+// getRolloff(), R/sourceSpectrum.R:71-186 with per-gc vector parameters.
+// Returns H x nGC column-major (kept rows compacted, renumbered 1..H).
+vec get_rolloff(const vec& pitch, int64_t nH, const vec& rolloff, const vec& rolloffOct, double rolloffParab,
+                double rolloffParabHarm, const vec& rolloffKHz, double baseline, double throwaway, double sr,
+                int64_t& H) {
+  const int64_t nGC = (int64_t)pitch.size();
+  if (nH < 1) throw SgError(SG_E_DOMAIN, "getRolloff: nHarmonics < 1");
+  vec r(nH * nGC);
+  auto at = [&](int64_t h, int64_t g) -> double& { return r[g * nH + h]; };
+  bool anyOct = false;
+  for (double v : rolloffOct) if (v != 0) anyOct = true;
+  for (int64_t h = 0; h < nH; ++h)
+    for (int64_t g = 0; g < nGC; ++g) {
+      const double hh = (double)(h + 1);
+      const double delta = (anyOct && h >= 1) ? rolloffOct[g] * (pitch[g] * hh - baseline) / 1000 : 0.0;
+      double v = ((rolloff[g] + rolloffKHz[g] * (pitch[g] - baseline) / 1000) * std::log2(hh)) + delta;
+      if (hh * pitch[g] >= sr / 2) v = -INFINITY;
+      at(h, g) = v;
+    }
+  if (rolloffParab != 0) {
+    double rph = r_round(rolloffParabHarm);
+    if (rph == 2) rph = 3;
+    const double a = -4 * rolloffParab / ((rph - 1) * (rph - 1));
+    const double b = -a * (1 + rph), c = a * rph;
+    for (int64_t g = 0; g < nGC; ++g) {
+      if (rph < 3) { if (rph < 2) at(0, g) = at(0, g) + rolloffParab; }
+      else {
+        if (rph > nH) throw SgError(SG_E_DOMAIN, "getRolloff: subscript out of bounds (rolloffParabHarm > nHarmonics)");
+        for (int64_t k = 1; k <= (int64_t)rph; ++k) at(k - 1, g) = at(k - 1, g) + a * k * k + b * k + c;
+      }
+    }
+  }
+  for (auto& v : r) if (v < throwaway) v = -INFINITY;
+  for (int64_t g = 0; g < nGC; ++g) {
+    double mx = -INFINITY;
+    for (int64_t h = 0; h < nH; ++h) if (at(h, g) > mx) mx = at(h, g);
+    for (int64_t h = 0; h < nH; ++h) at(h, g) = at(h, g) - mx;
+  }
+  for (auto& v : r) v = std::pow(2.0, v / 10);
+  std::vector<int64_t> keep;
+  for (int64_t h = 0; h < nH; ++h) {
+    long double s = 0;
+    for (int64_t g = 0; g < nGC; ++g) s += at(h, g);
+    if ((double)s > 0) keep.push_back(h);
+  }
+  H = (int64_t)keep.size();
+  vec o(H * nGC);
+  for (int64_t g = 0; g < nGC; ++g)
+    for (int64_t k = 0; k < H; ++k) o[g * H + k] = at(keep[k], g);
+  return o;
+}
+
+// ---------------------------------------------------------- vocal fry
+struct EpochMat {
+  int64_t g0, g1;     // 0-based gc range (inclusive)
+  int64_t D;          // nSubharm + 1
+  int64_t R;          // max rank
+  vec A;              // [G][R] by rank, fp64 (zero rows for dropped ranks)
+  vec mult;           // [R]: R's times_f0 for ranks present (0 if absent)
+};
+
+static double rowname_num(double x) {
+  char buf[64];
+  snprintf(buf, sizeof buf, "%.15g", x);
+  return strtod(buf, nullptr);
+}
+
+// getVocalFry_per_epoch(), R/subharmonics.R:25-86
+static EpochMat fry_per_epoch(const double* roll, int64_t H, int64_t g0, int64_t g1, const vec& pitch, int64_t nSub,
+                              const vec& sbw, double throwaway01) {
+  EpochMat m;
+  m.g0 = g0; m.g1 = g1;
+  const int64_t ncol = g1 - g0 + 1;
+  if (nSub < 1) {
+    m.D = 1; m.R = H; m.A.assign(roll + g0 * H, roll + (g1 + 1) * H);
+    m.mult.resize(H);
+    for (int64_t h = 0; h < H; ++h) m.mult[h] = (double)(h + 1);
+    return m;
+  }
+  vec gseq = r_seq_by(0, (double)(H + 1), 1.0 / (double)(nSub + 1));
+  const int64_t nr = (int64_t)gseq.size();
+  vec rn(nr * ncol, NAN);
+  auto RN = [&](int64_t i, int64_t g) -> double& { return rn[g * nr + i]; };
+  for (int64_t g = 0; g < ncol; ++g) { RN(0, g) = 0; RN(nr - 1, g) = 0; }
+  char a[64], b[64];
+  for (int64_t h = 0; h < H; ++h) {  // match(rownames(rolloff), rownames(rolloff_new))
+    snprintf(a, sizeof a, "%.15g", (double)(h + 1));
+    for (int64_t i = 0; i < nr; ++i) {
+      snprintf(b, sizeof b, "%.15g", gseq[i]);
+      if (!strcmp(a, b)) { for (int64_t g = 0; g < ncol; ++g) RN(i, g) = roll[(g0 + g) * H + h]; break; }
+    }
+  }
+  vec ml(nSub * ncol);
+  for (int64_t s = 1; s <= nSub; ++s)
+    for (int64_t g = 0; g < ncol; ++g) {
+      const double d = pitch[g0 + g] * (double)s / (double)(nSub + 1), sd = sbw[g0 + g];
+      ml[(s - 1) * ncol + g] = (sd == 0) ? (d == 0 ? NAN : 0.0) : std::exp(-0.5 * (d / sd) * (d / sd));
+    }
+  for (int64_t block = 1; block <= H + 1; ++block) {
+    const int64_t row_lwr = 1 + (block - 1) * (nSub + 1), row_upr = row_lwr + nSub + 1;
+    const double Alin = rn[row_lwr - 1], Blin = rn[row_upr - 1];  // linear index = column 1 (quirk)
+    for (int64_t gg = 1; gg <= nSub; ++gg)
+      for (int64_t g = 0; g < ncol; ++g)
+        RN(row_lwr + gg - 1, g) = Alin * ml[(gg - 1) * ncol + g] + Blin * ml[(nSub - gg) * ncol + g];
+  }
+  for (auto& v : rn) if (v < throwaway01) v = 0;
+  std::vector<int64_t> keep;
+  for (int64_t i = 0; i < nr; ++i) {
+    long double s = 0;
+    for (int64_t g = 0; g < ncol; ++g) s += RN(i, g);
+    if ((double)s > 0) keep.push_back(i);
+  }
+  m.D = nSub + 1;
+  m.R = keep.empty() ? 0 : keep.back();
+  m.A.assign(ncol * std::max<int64_t>(m.R, 1), 0.0);
+  m.mult.assign(std::max<int64_t>(m.R, 1), 0.0);
+  for (int64_t i : keep) {
+    // rank i (0 never survives: row 1 is all zero)
+    for (int64_t g = 0; g < ncol; ++g) m.A[g * m.R + (i - 1)] = RN(i, g);
+    m.mult[i - 1] = rowname_num(gseq[i]);
+  }
+  return m;
+}
+
+// getVocalFry(), R/subharmonics.R:108-163
+static std::vector<EpochMat> get_vocal_fry(const vec& roll, int64_t H, const vec& pitch, const vec& subFreq,
+                                           const vec& subDep, double throwaway, double shortestEpoch) {
+  const int64_t nGC = (int64_t)pitch.size();
+  vec nsub(nGC);
+  double mx = -INFINITY;
+  for (int64_t g = 0; g < nGC; ++g) {
+    double v = r_round(pitch[g] / subFreq[g]) - 1;
+    if (v < 0) v = 0;
+    nsub[g] = v; mx = std::max(mx, v);
+  }
+  std::vector<EpochMat> out;
+  if (mx < 1) { out.push_back(fry_per_epoch(roll.data(), H, 0, nGC - 1, pitch, 0, subDep, 0)); return out; }
+  const double throwaway01 = std::pow(2.0, throwaway / 10);
+  vec minlen(nGC);
+  for (int64_t g = 0; g < nGC; ++g) minlen[g] = r_round(shortestEpoch / (1000 / pitch[g]));
+  if (nGC > 1) clumper(nsub, minlen);
+  int64_t s0 = 0;
+  for (int64_t g = 1; g <= nGC; ++g) {
+    if (g == nGC || nsub[g] != nsub[g - 1]) {
+      out.push_back(fry_per_epoch(roll.data(), H, s0, g - 1, pitch, (int64_t)nsub[g - 1], subDep, throwaway01));
+      s0 = g;
+    }
+  }
+  return out;
+}
+
+// ---------------------------------------------------- host evaluator
+struct HostSyl {
+  std::vector<SgSeg> segs;
+  double sr;
+  double integr(int64_t u) const {  // cumsum(pitch_up)[u] / sr, u 1-based
+    int64_t lo = 0, hi = (int64_t)segs.size() - 1;
+    while (lo < hi) { int64_t m = (lo + hi + 1) / 2; if (segs[m].t0 < (double)u) lo = m; else hi = m - 1; }
+    const SgSeg& s = segs[lo];
+    const double m = (double)u - s.t0;
+    const double S1 = m * (m + 1) / 2, S2 = m * (m + 1) * (2 * m + 1) / 6, S3 = S1 * S1;
+    return (s.prefix + s.y * m + s.b * S1 + s.c * S2 + s.d * S3) / sr;
+  }
+};
+
+struct HostEpoch {
+  const EpochMat* M;
+  const HostSyl* S;
+  int64_t u0, n, G;
+  vec knots;
+  // W(j) in fp64, same formula/row order as R/source.R:396-419
+  double W(int64_t j) const {
+    const double v = r_seqint_at(knots.front(), knots.back(), n, j);
+    int64_t i = 0, jj = G - 1;
+    while (i < jj - 1) { int64_t ij = (i + jj) / 2; if (v < knots[ij]) jj = ij; else i = ij; }
+    const double t = (v - knots[i]) / (knots[jj] - knots[i]);
+    const double integ = S->integr(u0 + j);
+    double acc = 0;
+    for (int64_t r = 0; r < M->R; ++r) {
+      if (M->mult[r] == 0) continue;
+      const double y0 = M->A[i * M->R + r], y1 = M->A[jj * M->R + r];
+      double am;
+      if (v == knots[jj]) am = y1;
+      else if (v == knots[i]) am = y0;
+      else am = y0 + (y1 - y0) * t;
+      acc = acc + std::sin(2 * M_PI * integ * M->mult[r]) * am;
+    }
+    return acc;
+  }
+};
+
+// --------------------------------------------------- crossFade chain
+struct HTerm { int64_t e; int64_t j0; double w0, w1, w2; };
+struct HPiece { int64_t start, len; std::vector<HTerm> t; };
+
+struct Chain {
+  std::vector<HPiece> P;
+  const std::vector<HostEpoch>* E;
+  int64_t L() const { return P.empty() ? 0 : P.back().start + P.back().len; }
+  double at(int64_t k) const {  // 0-based
+    int64_t lo = 0, hi = (int64_t)P.size() - 1;
+    while (lo < hi) { int64_t m = (lo + hi + 1) / 2; if (P[m].start <= k) lo = m; else hi = m - 1; }
+    const HPiece& p = P[lo];
+    const double q = (double)(k - p.start);
+    double v = 0;
+    for (const HTerm& t : p.t) v += (t.w0 + q * (t.w1 + q * t.w2)) * (*E)[t.e].W(t.j0 + (k - p.start));
+    return v;
+  }
+  void truncate(int64_t newL) {
+    while (!P.empty() && P.back().start >= newL) P.pop_back();
+    if (!P.empty() && P.back().start + P.back().len > newL) P.back().len = newL - P.back().start;
+  }
+};
+
+// findZeroCrossing(), R/utilities_soundgen.R:255-295, 1-based, 0 = NA
+template <class F>
+static int64_t find_zero_crossing(F&& a, int64_t len, int64_t location) {
+  if (len < 1 || location < 1 || location > len) return 0;
+  if (len == 1 && location == 1) return location;
+  int64_t zl = 0, zr = 0, i = 0;
+  if (location > 1) {
+    i = location;
+    double cur = a(i - 1);
+    while (i > 1) {
+      const double prev = a(i - 2);
+      if (cur > 0 && prev < 0) { zl = i - 1; break; }
+      cur = prev;
+      i = i - 1;
+    }
+  }
+  if (location < len) i = location;
+  if (i < len - 1) {
+    double cur = a(i - 1);
+    while (i < (len - 1)) {
+      const double nxt = a(i);
+      if (nxt > 0 && cur < 0) { zr = i; break; }
+      cur = nxt;
+      i = i + 1;
+    }
+  }
+  if (!zl && !zr) return 0;
+  if (!zl) return zr;
+  if (!zr) return zl;
+  return (std::llabs(zl - location) <= std::llabs(zr - location)) ? zl : zr;
+}
+
+static HTerm rebase(const HTerm& t, double s) {  // weight polynomial shifted by s samples
+  HTerm o = t;
+  o.j0 = t.j0 + (int64_t)s;
+  o.w0 = t.w0 + t.w1 * s + t.w2 * s * s;
+  o.w1 = t.w1 + 2 * t.w2 * s;
+  o.w2 = t.w2;
+  return o;
+}
+
+// crossFade(A, W_e), R/utilities_soundgen.R:328-375
+static void cross_fade(Chain& A, const HostEpoch& W, int64_t e, double sr, double crossLen) {
+  const int64_t LA = A.L();
+  const int64_t zc1 = find_zero_crossing([&](int64_t k) { return A.at(k); }, LA, LA);
+  if (zc1) {
+    A.truncate(zc1);
+    A.P.push_back(HPiece{zc1, 1, {}});
+  }
+  const int64_t zc2 = find_zero_crossing([&](int64_t j) { return W.W(j); }, W.n, 1);
+  const int64_t w0 = zc2;  // W' = W[zc2 ..] (0-based)
+  const int64_t lenW = W.n - w0;
+  const int64_t L1 = A.L();
+  double cl = std::floor(crossLen * sr / 1000);
+  if ((double)(L1 - 1) < cl) cl = (double)(L1 - 1);
+  if ((double)(lenW - 1) < cl) cl = (double)(lenW - 1);
+  if (cl < 2) {
+    A.P.push_back(HPiece{L1, lenW, {HTerm{e, w0, 1, 0, 0}}});
+    return;
+  }
+  const int64_t c = (int64_t)cl;
+  const int64_t idx1 = L1 - c;
+  const double by = 1.0 / (double)(c - 1);
+  // split A's pieces over [idx1, L1) into crossfade sub-pieces
+  std::vector<HPiece> tail;
+  for (const HPiece& p : A.P) {
+    const int64_t s = std::max(p.start, idx1), en = std::min(p.start + p.len, L1);
+    if (s >= en) continue;
+    HPiece np{s, en - s, {}};
+    const double off = (double)(s - idx1);  // q_global at sub-piece start
+    for (const HTerm& t : p.t) {
+      HTerm r = rebase(t, (double)(s - p.start));
+      // multiply by down(q) = 1 - (off + q) * by
+      const double a0 = 1 - off * by, a1 = -by;
+      if (r.w2 != 0 && a1 != 0) throw SgError(SG_E_UNSUPPORTED, "crossFade: nested crossfades deeper than 2");
+      HTerm m = r;
+      m.w0 = r.w0 * a0;
+      m.w1 = r.w0 * a1 + r.w1 * a0;
+      m.w2 = r.w1 * a1 + r.w2 * a0;
+      np.t.push_back(m);
+    }
+    // + up(q) * W'[off + q]
+    np.t.push_back(HTerm{e, w0 + (int64_t)off, off * by, by, 0});
+    if ((int)np.t.size() > SG_MAX_TERMS) throw SgError(SG_E_UNSUPPORTED, "crossFade: too many overlapping terms");
+    tail.push_back(np);
+  }
+  A.truncate(idx1);
+  for (auto& p : tail) A.P.push_back(p);
+  if (lenW - c > 0) A.P.push_back(HPiece{L1, lenW - c, {HTerm{e, w0 + c, 1, 0, 0}}});
+}
+
+// ----------------------------------------------------------- planner
+int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_harm_params& P,
+                       const sg_anchors& amplAnchors, Rng& R, int64_t out_off, bool dry_run) {
+  const double sr = P.samplingRate;
+  if (len < 2) throw SgError(SG_E_DOMAIN, "generateHarmonics: pitch contour too short");
+  vec pitch(pitch_in, pitch_in + len);
+  if (P.vibratoDep > 0)
+    for (int64_t i = 0; i < len; ++i)
+      pitch[i] *= std::pow(2.0, std::sin(2 * M_PI * (double)(i + 1) * P.vibratoFreq / P.pitchSamplingRate) * P.vibratoDep / 12);
+  // getGlottalCycles()
+  std::vector<int64_t> gc;
+  for (double i = 1; i < (double)len;) {
+    gc.push_back((int64_t)i);
+    const double st = std::floor(P.pitchSamplingRate / pitch[(int64_t)i - 1]);
+    i = i + (st > 2 ? st : 2);
+  }
+  const int64_t nGC = (int64_t)gc.size();
+  vec ppg(nGC);
+  for (int64_t g = 0; g < nGC; ++g) ppg[g] = pitch[gc[g] - 1];
+  bool useAmpl = false;
+  for (int i = 0; i < amplAnchors.n; ++i) if (amplAnchors.value[i] < -P.throwaway) useAmpl = true;
+  vec rolloffAmpl(nGC, 0.0);
+  if (useAmpl) {
+    vec ac;
+    smooth_contour(amplAnchors, nGC, false, 0, true, 0, true, -P.throwaway, ac);
+    for (int64_t g = 0; g < nGC; ++g) rolloffAmpl[g] = (ac[g] / std::fabs(P.throwaway) - 1) * P.rolloff_perAmpl;
+  }
+  vec rw(nGC, 1.0), vf_on(nGC, 1.0), jit_on(nGC, 1.0), drift;
+  if (P.temperature > 0) {
+    rw = get_random_walk(R, nGC, P.temperature, 0.3, 1, vec{P.randomWalk_trendStrength, -P.randomWalk_trendStrength}, false);
+    vec r0100 = rw;
+    zero_one(r0100);
+    for (auto& v : r0100) v *= 100;
+    vec rwbin(nGC, 0.0);
+    if (P.nonlinBalance == 100) rwbin.assign(nGC, 2.0);
+    else if (P.nonlinBalance != 0) {
+      const double k = (double)(int64_t)(P.nonlinBalance + 1) - 1;  // R truncates the index
+      const double q1 = 100 / (1 + std::exp(0.1 * (k - 33))), q2 = 100 / (1 + std::exp(0.1 * (k - 66)));
+      for (int64_t g = 0; g < nGC; ++g) { if (r0100[g] > q1) rwbin[g] = 1; if (r0100[g] > q2) rwbin[g] = 2; }
+      vec ml(nGC);
+      for (int64_t g = 0; g < nGC; ++g) ml[g] = std::ceil(P.shortestEpoch / 1000 * ppg[g]);
+      clumper(rwbin, ml);
+    }
+    const double m = r_mean(rw);
+    for (int64_t g = 0; g < nGC; ++g) { rw[g] = rw[g] - m + 1; vf_on[g] = rwbin[g] > 0; jit_on[g] = rwbin[g] == 2; }
+  }
+  if (P.jitterDep > 0 && P.nonlinBalance > 0) {
+    vec idx{1.0};
+    double i = 1;
+    while (i < (double)nGC) {
+      const double ratio = ppg[(int64_t)i - 1] * P.jitterLen / 1000;
+      i = idx.back() + ratio;
+      idx.push_back(i);
+    }
+    vec idx2;
+    for (double v0 : idx) {
+      const double v = r_round(v0);
+      if (v > (double)nGC) continue;
+      if (std::find(idx2.begin(), idx2.end(), v) == idx2.end()) idx2.push_back(v);
+    }
+    vec jit(idx2.size());
+    for (size_t k = 0; k < idx2.size(); ++k) {
+      const double z = R.rnorm(0, P.jitterDep / 12);
+      const int64_t q = (int64_t)idx2[k] - 1;
+      jit[k] = std::pow(2.0, z * rw[q] * jit_on[q]);
+    }
+    vec jpg = idx2.size() == 1 ? vec(nGC, jit[0]) : r_spline(idx2, jit, nGC);
+    for (int64_t g = 0; g < nGC; ++g) ppg[g] *= jpg[g];
+  }
+  if (P.temperature > 0) {
+    const double rws = .9 - P.temperature * P.pitchDriftFreq - 1.2 / (1 + std::exp(-.008 * ((double)nGC - 10))) + .6;
+    const double rwr = P.temperature * P.pitchDriftDep + (double)nGC / 1000 / 12;
+    drift = get_random_walk(R, nGC, rwr, rws, 1, vec{0.0}, false);
+    const double m = r_mean(drift);
+    for (int64_t g = 0; g < nGC; ++g) { drift[g] = std::pow(2.0, drift[g] - m); ppg[g] *= drift[g]; }
+  }
+  for (auto& v : ppg) { if (v > P.pitchCeiling) v = P.pitchCeiling; if (v < P.pitchFloor) v = P.pitchFloor; }
+  const double pmin = r_min(ppg);
+  const int64_t nH = (int64_t)std::ceil((sr / 2 - pmin) / pmin);
+  vec ro(nGC), roo(nGC), rk(nGC);
+  for (int64_t g = 0; g < nGC; ++g) {
+    const double w = rw[g];
+    ro[g] = (P.rolloff + rolloffAmpl[g]) * w * w * w;
+    roo[g] = P.rolloffOct * w * w * w;
+    rk[g] = P.rolloffKHz * w;
+  }
+  int64_t H = 0;
+  vec roll = get_rolloff(ppg, nH, ro, roo, P.rolloffParab, P.rolloffParabHarm, rk, 200, P.throwaway, sr, H);
+  if (P.shimmerDep > 0 && P.nonlinBalance > 0)
+    for (int64_t g = 0; g < nGC; ++g) {
+      const double z = R.rnorm(0, P.shimmerDep / 100);
+      const double sh = std::pow(2.0, z * rw[g] * jit_on[g]);
+      for (int64_t h = 0; h < H; ++h) roll[g * H + h] *= sh;
+    }
+  std::vector<EpochMat> mats;
+  if (P.subDep > 0 && P.nonlinBalance > 0) {
+    vec sf(nGC), sd(nGC);
+    for (int64_t g = 0; g < nGC; ++g) { const double w4 = std::pow(rw[g], 4); sf[g] = P.subFreq * w4; sd[g] = P.subDep * w4 * vf_on[g]; }
+    mats = get_vocal_fry(roll, H, ppg, sf, sd, P.throwaway, P.shortestEpoch);
+  } else {
+    mats.push_back(fry_per_epoch(roll.data(), H, 0, nGC - 1, ppg, 0, vec(nGC, 0.0), 0));
+  }
+  // upsample(): gcLen, gc_up, cumulative-pitch segments
+  vec gcl(nGC);
+  for (int64_t g = 0; g < nGC; ++g) gcl[g] = r_round(sr / ppg[g]);
+  vec cs = r_cumsum(gcl);
+  vec gc_up(nGC + 1);
+  gc_up[0] = 1;
+  for (int64_t g = 0; g < nGC; ++g) gc_up[g + 1] = cs[g];
+  const int64_t N = (int64_t)cs[nGC - 1];
+  HostSyl HS;
+  HS.sr = sr;
+  if (nGC == 1) {
+    HS.segs.push_back(SgSeg{0, 0, ppg[0], 0, 0, 0});
+  } else if (nGC == 2) {
+    const double by = (ppg[1] - ppg[0]) / (double)(N - 1);
+    HS.segs.push_back(SgSeg{0, 0, ppg[0] - by, by, 0, 0});
+  } else {
+    vec t(nGC);
+    t[0] = 1; t[nGC - 1] = (double)N;
+    for (int64_t i = 2; i <= nGC - 1; ++i) t[i - 1] = cs[i - 2] + r_round(gcl[i - 1] / 2);
+    Spline s = fmm_spline(t, ppg);
+    long double pre = s.y[0];
+    for (int64_t k = 0; k + 1 < nGC; ++k) {
+      HS.segs.push_back(SgSeg{t[k], (double)pre, s.y[k], s.b[k], s.c[k], s.d[k]});
+      const long double M = (long double)(t[k + 1] - t[k]);
+      const long double S1 = M * (M + 1) / 2, S2 = M * (M + 1) * (2 * M + 1) / 6, S3 = S1 * S1;
+      pre += s.y[k] * M + s.b[k] * S1 + s.c[k] * S2 + s.d[k] * S3;
+    }
+  }
+  // epochs
+  std::vector<HostEpoch> HE(mats.size());
+  for (size_t e = 0; e < mats.size(); ++e) {
+    HostEpoch& he = HE[e];
+    he.M = &mats[e]; he.S = &HS;
+    he.u0 = (int64_t)gc_up[mats[e].g0];
+    const int64_t u1 = (int64_t)gc_up[mats[e].g1 + 1];
+    he.n = u1 - he.u0 + 1;
+    he.G = mats[e].g1 - mats[e].g0 + 1;
+    if (he.G < 2) throw SgError(SG_E_DOMAIN, "approx: need at least two non-NA values to interpolate");
+    he.knots.assign(gc_up.begin() + mats[e].g0, gc_up.begin() + mats[e].g1 + 1);
+  }
+  // crossFade chain → pieces (host fp64 decisions)
+  Chain A;
+  A.E = &HE;
+  A.P.push_back(HPiece{0, 1, {}});  // waveform = 0
+  for (size_t e = 0; e < mats.size(); ++e) cross_fade(A, HE[e], (int64_t)e, sr, 15);
+  const int64_t Lsyl = A.L();
+  if (dry_run) return Lsyl;
+
+  // ------------------------------------------------ emit device arrays
+  const int32_t syl_idx = (int32_t)B.syls.size();
+  SgSyllable sy{};
+  sy.L = Lsyl;
+  sy.out_off = out_off;
+  sy.max_slot = syl_idx;
+  const double lf = P.attackLen > 0 ? std::floor(P.attackLen * sr / 1000) : 0;
+  sy.fade = (int32_t)(lf >= 2 ? std::min<double>(lf, (double)Lsyl) : 0);
+  sy.env = useAmpl ? contour_desc(B, amplAnchors, Lsyl, true, 0, false, 0, true) : SgContour{};
+  if (!useAmpl) { sy.env.kind = 0; sy.env.lo = -INFINITY; sy.env.hi = INFINITY; }
+  if (P.temperature > 0) {
+    sy.drift.nk = (int32_t)nGC;
+    sy.drift.k_off = (int64_t)B.cknots.size();
+    sy.drift.x0 = gc_up[0];
+    sy.drift.x1 = gc_up[nGC - 1];
+    B.cknots.insert(B.cknots.end(), gc_up.begin(), gc_up.begin() + nGC);
+    B.cknots.insert(B.cknots.end(), drift.begin(), drift.end());
+  }
+  const int32_t seg_off = (int32_t)B.segs.size();
+  B.segs.insert(B.segs.end(), HS.segs.begin(), HS.segs.end());
+  std::vector<int32_t> ep_index(mats.size());
+  for (size_t e = 0; e < mats.size(); ++e) {
+    const EpochMat& m = mats[e];
+    const HostEpoch& he = HE[e];
+    SgEpoch d{};
+    d.w_off = B.w_total;
+    B.w_total += he.n;
+    d.n = (int32_t)he.n;
+    d.G = (int32_t)he.G;
+    d.R = (int32_t)((m.R + 7) / 8 * 8);
+    d.u0 = (int32_t)he.u0;
+    d.seg_off = seg_off;
+    d.nseg = (int32_t)HS.segs.size();
+    d.x1 = he.knots.front();
+    d.xG = he.knots.back();
+    d.inv_srD = 1.0 / (sr * (double)m.D);
+    d.knot_off = (int64_t)B.knots.size();
+    B.knots.insert(B.knots.end(), he.knots.begin(), he.knots.end());
+    d.amp_off = (int64_t)B.amps.size();
+    B.amps.resize(B.amps.size() + (size_t)d.G * d.R, 0.0f);
+    for (int64_t g = 0; g < he.G; ++g)
+      for (int64_t r = 0; r < m.R; ++r) B.amps[d.amp_off + g * d.R + r] = (float)m.A[g * m.R + r];
+    d.syl = syl_idx;
+    d.dj0 = d.dj1 = 0;
+    d.dk0 = 0;
+    ep_index[e] = (int32_t)B.epochs.size();
+    B.epochs.push_back(d);
+    B.harm_samples += he.n;
+    B.harm_terms += he.n * (int64_t)d.R;
+    B.harm_amp_bytes += (int64_t)d.G * d.R * 4;
+  }
+  // pieces; the single full-weight piece of each epoch becomes its direct window
+  sy.piece0 = (int32_t)B.pieces.size();
+  for (const HPiece& p : A.P) {
+    SgPiece d{};
+    d.start = p.start;
+    d.len = (int32_t)p.len;
+    d.nterms = (int32_t)p.t.size();
+    for (size_t k = 0; k < p.t.size(); ++k) {
+      const HTerm& t = p.t[k];
+      const SgEpoch& ep = B.epochs[ep_index[t.e]];
+      d.t[k].src = ep.w_off + t.j0;
+      d.t[k].w0 = (float)t.w0; d.t[k].w1 = (float)t.w1; d.t[k].w2 = (float)t.w2;
+    }
+    if (p.t.size() == 1 && p.t[0].w0 == 1 && p.t[0].w1 == 0 && p.t[0].w2 == 0) {
+      SgEpoch& ep = B.epochs[ep_index[p.t[0].e]];
+      ep.dj0 = (int32_t)p.t[0].j0;
+      ep.dj1 = (int32_t)(p.t[0].j0 + p.len);
+      ep.dk0 = p.start - p.t[0].j0;
+      d.nterms = -1;  // marks a direct piece (max handled by the sine-bank kernel)
+      d.t[0].src = ep.w_off + p.t[0].j0;
+      d.t[0].w0 = 1;
+    }
+    B.pieces.push_back(d);
+  }
+  sy.npiece = (int32_t)(B.pieces.size() - sy.piece0);
+  B.syls.push_back(sy);
+  // sine-bank tiles: 256 samples each
+  constexpr int TILE = 256;
+  for (size_t e = 0; e < mats.size(); ++e) {
+    const HostEpoch& he = HE[e];
+    int64_t i = 0;
+    int64_t k = 0;
+    for (int64_t j0 = 0; j0 < he.n; j0 += TILE) {
+      const double v = r_seqint_at(he.knots.front(), he.knots.back(), he.n, j0);
+      while (i < he.G - 2 && he.knots[i + 1] <= v) ++i;
+      const double u = (double)(he.u0 + j0);
+      while (k + 1 < (int64_t)HS.segs.size() && HS.segs[k + 1].t0 < u) ++k;
+      B.tiles.push_back(SgTile{ep_index[e], (int32_t)j0, (int32_t)i, (int32_t)k});
+    }
+  }
+  return Lsyl;
+}
+
+void tile_syllables(Batch& B, int first_syl) {
+  constexpr int64_t STILE = 1024;
+  for (int s = first_syl; s < (int)B.syls.size(); ++s) {
+    const SgSyllable& sy = B.syls[s];
+    int32_t p = sy.piece0;
+    for (int64_t k0 = 0; k0 < sy.L; k0 += STILE) {
+      while (p + 1 < sy.piece0 + sy.npiece && B.pieces[p + 1].start <= k0) ++p;
+      B.syl_tiles.push_back(SgSylTile{s, p, k0});
+    }
+  }
+}
+
+}  // namespace sg

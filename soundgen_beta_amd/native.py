@@ -1,0 +1,117 @@
+"""Loader of the in-tree HIP library soundgen_beta_amd/lib/libsoundgen_hip.so.
+
+There is no CPU fallback: if the library is missing or the GPU is not
+usable, calls raise. (The planner entry points work without a GPU so host
+bookkeeping can be tested on CPU; every synthesis call needs the device.)
+"""
+import ctypes as C
+import os
+import re
+
+from . import _abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libsoundgen_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "soundgen_hip.h")
+
+_lib = None
+
+
+class SoundgenError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s: %s" % (_abi.SG_ERR_NAMES.get(code, code), msg))
+        self.code = code
+
+
+def declared_symbols():
+    """Function names declared in include/soundgen_hip.h."""
+    txt = open(HEADER_PATH).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(sg_[a-z_0-9]+)\s*\(", txt)))
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    # Share torch's HIP runtime when torch is present: torch/lib/libamdhip64.so
+    # has the same SONAME as /opt/rocm's, so importing torch first makes our
+    # NEEDED entry resolve to that copy (one runtime, valid device pointers).
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libsoundgen_hip.so not built (run __graft_entry__.build()): %s" % LIB_PATH)
+    L = C.CDLL(LIB_PATH)
+    vp = C.c_void_p
+    dp = C.POINTER(C.c_double)
+    i64 = C.c_int64
+    i64p = C.POINTER(C.c_int64)
+    L.sg_ctx_create.argtypes = [C.c_int, C.POINTER(vp)]
+    L.sg_ctx_destroy.argtypes = [vp]
+    L.sg_last_error.argtypes = [vp]
+    L.sg_last_error.restype = C.c_char_p
+    L.sg_plan_batch.argtypes = [vp, C.POINTER(_abi.sg_call_desc), i64, C.POINTER(vp)]
+    L.sg_plan_destroy.argtypes = [vp]
+    L.sg_plan_n_calls.argtypes = [vp]
+    L.sg_plan_n_calls.restype = i64
+    L.sg_plan_total_samples.argtypes = [vp]
+    L.sg_plan_total_samples.restype = i64
+    L.sg_plan_lengths.argtypes = [vp, i64p, i64p]
+    L.sg_plan_status.argtypes = [vp, C.POINTER(C.c_int32)]
+    L.sg_plan_call_message.argtypes = [vp, i64]
+    L.sg_plan_call_message.restype = C.c_char_p
+    L.sg_plan_device_bytes.argtypes = [vp]
+    L.sg_plan_device_bytes.restype = i64
+    L.sg_plan_upload.argtypes = [vp, vp]
+    L.sg_execute.argtypes = [vp, vp, vp, vp]
+    L.sg_set_profiling.argtypes = [vp, C.c_int]
+    L.sg_profile_read.argtypes = [vp, dp, i64p]
+    L.sg_plan_kernel_stats.argtypes = [vp, i64p, i64p, i64p, i64p]
+    L.sg_synchronize.argtypes = [vp]
+    L.sg_generate_harmonics.argtypes = [vp, dp, i64, C.POINTER(_abi.sg_harm_params), _abi.sg_anchors,
+                                        C.POINTER(_abi.sg_random), dp, i64, i64p]
+    L.sg_soundgen.argtypes = [vp, C.POINTER(_abi.sg_soundgen_args), C.POINTER(_abi.sg_random), dp, i64, i64p]
+    L.sg_get_rolloff.argtypes = [dp, C.c_int32, C.c_int32] + [C.c_double] * 8 + [dp, C.POINTER(C.c_int32)]
+    L.sg_abi_version.restype = C.c_int
+    _lib = L
+    return L
+
+
+def check(rc, ctx=None):
+    if rc < 0:
+        msg = lib().sg_last_error(ctx).decode() if ctx is not None else ""
+        raise SoundgenError(rc, msg)
+    return rc
+
+
+class Context:
+    """A device context (one HIP stream on one GPU)."""
+
+    def __init__(self, device=0):
+        self.device = device
+        self.ptr = C.c_void_p()
+        rc = lib().sg_ctx_create(device, C.byref(self.ptr))
+        if rc < 0:
+            raise SoundgenError(rc, "sg_ctx_create(%d) failed (no usable GPU?)" % device)
+
+    def close(self):
+        if self.ptr:
+            lib().sg_ctx_destroy(self.ptr)
+            self.ptr = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_default_ctx = {}
+
+
+def default_context(device=0):
+    if device not in _default_ctx:
+        _default_ctx[device] = Context(device)
+    return _default_ctx[device]

@@ -1,0 +1,286 @@
+"""R-level argument semantics of soundgen()/generateHarmonics(), marshalled
+into the plain C structs of include/soundgen_hip.h.
+
+Mirrors the reference's formals and defaults:
+  soundgen()          R/soundgen.R:208-277
+  generateHarmonics() R/source.R:173-205
+  permittedValues     R/presets.R:22-79
+and the argument coercions done at the top of soundgen():
+  numeric anchors -> data.frame(time = seq(0, 1, ...), value)   R/soundgen.R:305-315
+  list formants   -> lapply(formants, as.data.frame)            R/soundgen.R:384-389
+  vowel strings   -> convertStringToFormants()                  R/utilities_soundgen.R:135-222
+"""
+import math
+
+import numpy as np
+
+from . import _abi
+
+NA = None  # R's NA / NULL for anchors and formants
+
+# permittedValues rows used by soundgen(): name -> (default, low, high, step)
+PERMITTED_VALUES = {
+    "repeatBout": (1, 1, 20, 1), "nSyl": (1, 1, 10, 1), "sylLen": (300, 20, 5000, 10),
+    "pauseLen": (200, 20, 1000, 10), "temperature": (.025, 0, 1, .025),
+    "maleFemale": (0, -1, 1, .1), "creakyBreathy": (0, -1, 1, .1),
+    "nonlinBalance": (0, 0, 100, 1), "nonlinDep": (50, 0, 100, 1), "jitterDep": (3, 0, 24, .1),
+    "jitterLen": (1, 1, 100, 1), "vibratoFreq": (5, 3, 10, .5), "vibratoDep": (0, 0, 3, .125),
+    "shimmerDep": (0, 0, 100, 1), "attackLen": (50, 0, 200, 10), "rolloff": (-12, -60, 0, 1),
+    "rolloffOct": (-12, -30, 10, 1), "rolloffParab": (0, -50, 50, 5),
+    "rolloffParabHarm": (3, 1, 20, 1), "rolloffKHz": (-6, -20, 0, 1), "rolloffLip": (6, 0, 20, 1),
+    "formantDep": (1, 0, 5, .1), "formantDepStoch": (30, 0, 60, 10), "vocalTract": (15.5, 2, 100, .5),
+    "subFreq": (100, 10, 1000, 10), "subDep": (100, 0, 500, 10), "shortestEpoch": (300, 50, 500, 25),
+    "amDep": (0, 0, 100, 5), "amFreq": (30, 10, 100, 5), "amShape": (0, -1, 1, .025),
+    "samplingRate": (16000, 8000, 44100, 100), "windowLength": (40, 5, 100, 2.5),
+    "rolloffNoise": (-14, -20, 20, 1), "overlap": (50, 0, 99, 1), "addSilence": (100, 0, 1000, 50),
+    "pitchFloor": (50, 1, 1000, 1), "pitchCeiling": (3500, 10, 100000, 10),
+    "pitchSamplingRate": (3500, 10, 100000, 10), "throwaway": (-120, -200, -10, 10),
+    "mouthOpening": (.5, 0, 1, .05), "pitch": (100, 25, 3500, 1), "noiseAmpl": (0, -120, 40, 1),
+}
+
+TEMP_EFFECTS_ORDER = ["sylLenDep", "formDrift", "formDisp", "pitchDriftDep", "pitchDriftFreq",
+                      "pitchAnchorsDep", "noiseAnchorsDep", "amplAnchorsDep"]
+TEMP_EFFECTS_DEFAULT = {"sylLenDep": .02, "formDrift": .3, "formDisp": .2, "pitchDriftDep": .5,
+                        "pitchDriftFreq": .125, "pitchAnchorsDep": .05, "noiseAnchorsDep": .1,
+                        "amplAnchorsDep": .1}
+
+# soundgen() formals, R/soundgen.R:208-277
+SOUNDGEN_DEFAULTS = dict(
+    repeatBout=1, nSyl=1, sylLen=300, pauseLen=200,
+    pitchAnchors={"time": [0, .1, .9, 1], "value": [100, 150, 135, 100]},
+    pitchAnchorsGlobal=NA, temperature=0.025, tempEffects=None,
+    maleFemale=0, creakyBreathy=0, nonlinBalance=0, nonlinDep=50, jitterLen=1, jitterDep=3,
+    vibratoFreq=5, vibratoDep=0, shimmerDep=0, attackLen=50, rolloff=-12, rolloffOct=-12,
+    rolloffKHz=-6, rolloffParab=0, rolloffParabHarm=3, rolloffLip=6,
+    formants={"f1": {"time": 0, "freq": 860, "amp": 30, "width": 120},
+              "f2": {"time": 0, "freq": 1280, "amp": 40, "width": 120},
+              "f3": {"time": 0, "freq": 2900, "amp": 25, "width": 200}},
+    formantDep=1, formantDepStoch=30, vocalTract=15.5, subFreq=100, subDep=100,
+    shortestEpoch=300, amDep=0, amFreq=30, amShape=0,
+    noiseAnchors={"time": [0, 300], "value": [-120, -120]}, formantsNoise=NA,
+    rolloffNoise=-14, mouthAnchors={"time": [0, 1], "value": [.5, .5]}, amplAnchors=NA,
+    amplAnchorsGlobal=NA, samplingRate=16000, windowLength=50, overlap=75, addSilence=100,
+    pitchFloor=50, pitchCeiling=3500, pitchSamplingRate=3500, throwaway=-120,
+    invalidArgAction="adjust",
+)
+
+# generateHarmonics() formals, R/source.R:173-205
+HARM_DEFAULTS = dict(
+    attackLen=50, nonlinBalance=0, nonlinDep=0, jitterDep=0, jitterLen=1, vibratoFreq=100,
+    vibratoDep=0, shimmerDep=0, creakyBreathy=0, rolloff=-18, rolloffOct=-2, rolloffKHz=-6,
+    rolloffParab=0, rolloffParabHarm=3, rolloffLip=6, rolloff_perAmpl=12, temperature=0,
+    pitchDriftDep=.5, pitchDriftFreq=.125, randomWalk_trendStrength=.5, shortestEpoch=300,
+    subFreq=100, subDep=0, amDep=0, amFreq=30, overlap=75, samplingRate=16000,
+    pitchFloor=75, pitchCeiling=3500, pitchSamplingRate=3500, throwaway=-120,
+)
+
+# Vowel dictionaries of presets$<speaker>$Formants$vowels (R/presets.R:176-212,
+# :268-305) as {vowel: [(name, freq, amp, width), ...]} (time is always 0).
+VOWELS = {
+    "M1": {
+        "a": [("f1", 860, 30, 120), ("f2", 1280, 40, 120), ("f3", 2900, 25, 200)],
+        "o": [("f1", 630, 35, 100), ("f2", 900, 35, 100), ("f3", 3000, 30, 200), ("f4", 3960, 30, 200)],
+        "i": [("f1", 300, 25, 80), ("f2", 2700, 30, 100), ("f3", 3400, 40, 350), ("f4", 4200, 40, 350)],
+        "e": [("f1", 530, 30, 50), ("f1.4", 1100, -20, 100), ("f1.6", 1400, 20, 100),
+              ("f2", 2400, 40, 300), ("f3", 4000, 30, 300)],
+        "u": [("f1", 375, 25, 80), ("f2", 550, 35, 120), ("f3", 2100, 25, 300), ("f4", 4200, 45, 250)],
+        "0": [("f1", 640, 30, 100), ("f2", 1670, 30, 100), ("f3", 2700, 30, 100), ("f4", 3880, 30, 100)],
+    },
+    "F1": {
+        "a": [("f1", 900, 30, 80), ("f2", 1300, 30, 160), ("f3", 3300, 25, 130), ("f4", 4340, 20, 370)],
+        "o": [("f1", 800, 30, 80), ("f2", 1100, 30, 80), ("f3", 3560, 40, 200), ("f4", 5830, 50, 200)],
+        "i": [("f1", 330, 30, 120), ("f2", 2700, 40, 120), ("f3", 3580, 30, 200), ("f4", 4710, 30, 200),
+              ("f5", 5800, 30, 200)],
+        "e": [("f1", 930, 30, 100), ("f2", 2470, 30, 100), ("f3", 3300, 25, 120), ("f4", 4200, 30, 200)],
+        "u": [("f1", 450, 30, 80), ("f2", 850, 40, 120), ("f3", 2900, 30, 200), ("f4", 4100, 30, 275)],
+        "0": [("f1", 790, 30, 100), ("f2", 1600, 30, 100), ("f3", 3100, 30, 100), ("f4", 3900, 30, 100)],
+    },
+}
+
+
+def convertStringToFormants(phonemeString, speaker="M1"):
+    """R/utilities_soundgen.R:135-222. Returns an ordered dict name -> columns."""
+    if speaker not in VOWELS:
+        speaker = "M1"
+    dic = VOWELS[speaker]
+    valid = [p for p in phonemeString if p in dic]
+    if not valid:
+        return NA
+    uniq = list(dict.fromkeys(valid))
+    vowels = {v: {n: (fr, a, w) for (n, fr, a, w) in dic[v]} for v in uniq}
+    names = sorted({n for v in uniq for n in vowels[v]})
+    for v in uniq:  # fill absent formants with amp 0, width 100, freq of the first vowel having it
+        for f in names:
+            if f not in vowels[v]:
+                fr = next(vowels[u][f][0] for u in uniq if f in vowels[u])
+                vowels[v][f] = (fr, 0, 100)
+    stamps = _seq_len(0.0, 1.0, len(valid))
+    out = {}
+    for f in names:
+        rows = [vowels[v][f] for v in valid]
+        out[f] = {"time": list(stamps), "freq": [r[0] for r in rows],
+                  "amp": [r[1] for r in rows], "width": [r[2] for r in rows]}
+    # R removes a formant when sum(f$amp == 0) == length(f); length() of a
+    # data.frame is its column count (4), so only formants with exactly four
+    # zero-amplitude rows are dropped (reference quirk, kept).
+    out = {f: out[f] for f in names if sum(a == 0 for a in out[f]["amp"]) != 4}
+    return out
+
+
+def _seq_len(a, b, n):
+    """R seq(a, b, length.out = n)."""
+    if n == 1:
+        return np.array([a], dtype=np.float64)
+    by = (b - a) / (n - 1)
+    v = a + np.arange(n, dtype=np.float64) * by
+    v[-1] = b
+    return v
+
+
+def _is_na(x):
+    if x is None:
+        return True
+    if isinstance(x, float) and math.isnan(x):
+        return True
+    if isinstance(x, str) and x == "NA":
+        return True
+    return False
+
+
+def as_anchors(x, time_to=1.0):
+    """Anchors -> (time, value) float64 arrays, or None for NA.
+    Numeric vectors become data.frame(time = seq(0, time_to, len), value)."""
+    if _is_na(x):
+        return None
+    if isinstance(x, dict):
+        t = np.atleast_1d(np.asarray(x["time"], dtype=np.float64))
+        v = np.atleast_1d(np.asarray(x["value"], dtype=np.float64))
+        n = max(len(t), len(v))
+        if len(t) < n:
+            t = np.resize(t, n)
+        if len(v) < n:
+            v = np.resize(v, n)
+        return np.ascontiguousarray(t), np.ascontiguousarray(v)
+    v = np.atleast_1d(np.asarray(x, dtype=np.float64))
+    if len(v) == 0:
+        return None
+    return _seq_len(0.0, float(time_to), len(v)), np.ascontiguousarray(v)
+
+
+def as_formants(x, speaker="M1"):
+    """formants -> ordered list of (name, time, freq, amp, width) or None."""
+    if _is_na(x):
+        return None
+    if isinstance(x, str):
+        x = convertStringToFormants(x, speaker)
+        if x is None:
+            return None
+    out = []
+    for name, f in x.items():
+        cols = [np.atleast_1d(np.asarray(f[k], dtype=np.float64)) for k in ("time", "freq", "amp", "width")]
+        n = max(len(c) for c in cols)
+        cols = [np.resize(c, n) for c in cols]  # as.data.frame recycling
+        out.append((name,) + tuple(cols))
+    return out
+
+
+class Holder:
+    """Keeps the numpy buffers behind a filled C struct alive."""
+
+    def __init__(self):
+        self.keep = []
+
+    def arr(self, a, dtype=np.float64):
+        a = np.ascontiguousarray(np.asarray(a, dtype=dtype))
+        self.keep.append(a)
+        return a
+
+    def anchors(self, an):
+        s = _abi.sg_anchors()
+        if an is None:
+            s.n = 0
+            return s
+        t, v = self.arr(an[0]), self.arr(an[1])
+        s.n = len(t)
+        s.time, s.value = _abi.dptr(t), _abi.dptr(v)
+        return s
+
+    def formants(self, fl):
+        s = _abi.sg_formants()
+        if not fl:
+            s.n_formants = 0
+            s.f1_index = -1
+            return s
+        s.n_formants = len(fl)
+        names = [f[0] for f in fl]
+        s.f1_index = names.index("f1") if "f1" in names else -1
+        npnt = self.arr([len(f[1]) for f in fl], np.int32)
+        cat = [self.arr(np.concatenate([f[k] for f in fl])) for k in (1, 2, 3, 4)]
+        s.n_points = _abi.iptr(npnt)
+        s.time, s.freq, s.amp, s.width = (_abi.dptr(c) for c in cat)
+        return s
+
+    def random(self, normals=None, uniforms=None):
+        r = _abi.sg_random()
+        if normals is not None:
+            n = self.arr(normals)
+            r.normals, r.n_normals = _abi.dptr(n), len(n)
+        if uniforms is not None:
+            u = self.arr(uniforms)
+            r.uniforms, r.n_uniforms = _abi.dptr(u), len(u)
+        return r
+
+
+def resolve_soundgen_kwargs(kw):
+    """Fill soundgen() defaults for missing args; returns a plain dict."""
+    unknown = set(kw) - set(SOUNDGEN_DEFAULTS)
+    if unknown:
+        raise TypeError("soundgen(): unused argument(s) %s" % sorted(unknown))
+    a = dict(SOUNDGEN_DEFAULTS)
+    a.update(kw)
+    te = dict(TEMP_EFFECTS_DEFAULT)
+    if a.get("tempEffects"):
+        te.update(a["tempEffects"])
+    a["tempEffects"] = te
+    return a
+
+
+def fill_soundgen_args(h, kw):
+    """kwargs (R names) -> sg_soundgen_args (buffers kept alive by h)."""
+    a = resolve_soundgen_kwargs(kw)
+    s = _abi.sg_soundgen_args()
+    for f, _ in _abi.sg_soundgen_args._fields_:
+        if f in ("pitchAnchors", "pitchAnchorsGlobal", "noiseAnchors", "mouthAnchors",
+                 "amplAnchors", "amplAnchorsGlobal", "formants", "formantsNoise",
+                 "tempEffects", "invalidArgAction"):
+            continue
+        v = a[f]
+        setattr(s, f, float("nan") if _is_na(v) else float(v))
+    s.tempEffects = (C_double8())(*[float(a["tempEffects"][k]) for k in TEMP_EFFECTS_ORDER])
+    s.pitchAnchors = h.anchors(as_anchors(a["pitchAnchors"]))
+    s.pitchAnchorsGlobal = h.anchors(as_anchors(a["pitchAnchorsGlobal"]))
+    s.amplAnchors = h.anchors(as_anchors(a["amplAnchors"]))
+    s.amplAnchorsGlobal = h.anchors(as_anchors(a["amplAnchorsGlobal"]))
+    s.mouthAnchors = h.anchors(as_anchors(a["mouthAnchors"]))
+    s.noiseAnchors = h.anchors(as_anchors(a["noiseAnchors"], time_to=a["sylLen"]))
+    s.formants = h.formants(as_formants(a["formants"]))
+    s.formantsNoise = h.formants(as_formants(a["formantsNoise"]))
+    s.invalidArgAction = {"adjust": 0, "abort": 1, "ignore": 2}[a["invalidArgAction"]]
+    return s
+
+
+def C_double8():
+    import ctypes
+    return ctypes.c_double * 8
+
+
+def fill_harm_params(kw):
+    unknown = set(kw) - set(HARM_DEFAULTS)
+    if unknown:
+        raise TypeError("generateHarmonics(): unused argument(s) %s" % sorted(unknown))
+    p = dict(HARM_DEFAULTS)
+    p.update(kw)
+    s = _abi.sg_harm_params()
+    for f in _abi.HARM_FIELDS:
+        setattr(s, f, float(p[f]))
+    return s
