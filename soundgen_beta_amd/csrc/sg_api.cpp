@@ -132,7 +132,7 @@ int sg_plan_batch(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, sg_pl
         }
         B.call_off[c] = off;
         B.call_len[c] = L;
-        off += L;
+        off += (L + 63) / 64 * 64;  // 256-B aligned call slots
       } catch (const sg::SgError& e) {
         cp.restore(B);
         sg::restore_soundgen_tail(B, first_syl);

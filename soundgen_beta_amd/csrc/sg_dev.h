@@ -28,6 +28,7 @@ struct SgEpoch {
   int32_t R;         // rows (multiple of 8, zero padded)
   int32_t u0;        // first sample, 1-based within the syllable
   double x1, xG;     // xout range
+  double xby;        // (xG - x1) / (n - 1), as R's seq.int computes it
   double inv_srD;    // 1 / (samplingRate * D), D = nSubharm + 1
   // direct-copy window used for the fused max: W[j] lands at syllable
   // sample k = dk0 + j for j in [dj0, dj1) with weight 1.
@@ -36,6 +37,8 @@ struct SgEpoch {
   int32_t syl;       // syllable index
   int32_t pad;
 };
+
+constexpr int SG_SINE_TILE = 2048;  // samples per sine-bank workgroup (256 threads x 8)
 
 struct SgTile {
   int32_t epoch;

@@ -134,67 +134,84 @@ __device__ __forceinline__ float wave_max(float v) {
 
 }  // namespace
 
+// sin(pi*x), cos(pi*x) for |x| <= 1/4 (|pi*x| <= pi/4): Taylor to x^9 / x^10,
+// truncation < 2e-9, i.e. below fp32 rounding.
+__device__ __forceinline__ void sincospi_q(float x, float& s, float& c) {
+  const float a = 3.14159265358979f * x;
+  const float a2 = a * a;
+  s = a * fmaf(a2, fmaf(a2, fmaf(a2, fmaf(a2, 2.75573192e-6f, -1.98412698e-4f), 8.33333333e-3f), -1.66666667e-1f), 1.f);
+  c = fmaf(a2, fmaf(a2, fmaf(a2, fmaf(a2, fmaf(a2, -2.75573192e-7f, 2.48015873e-5f), -1.38888889e-3f),
+                          4.16666667e-2f), -0.5f), 1.f);
+}
+
 extern "C" __global__ __launch_bounds__(256) void sg_sine_bank(
     const SgTile* __restrict__ tiles, const SgEpoch* __restrict__ epochs, const SgSeg* __restrict__ segs,
     const double* __restrict__ knots, const float* __restrict__ amps, const SgSyllable* __restrict__ syls,
     const double* __restrict__ cknots, float* __restrict__ W, unsigned* __restrict__ maxes) {
   const SgTile tl = tiles[blockIdx.x];
   const SgEpoch ep = epochs[tl.epoch];
-  const int j = tl.j0 + (int)threadIdx.x;
-  const bool valid = j < ep.n;
-  const int jc = valid ? j : ep.n - 1;
-
-  // --- amplitude interval: approx() on xo = seq.int(x1, xG, n)[j]
   const double* __restrict__ kn = knots + ep.knot_off;
-  const double xo = seqint_at(ep.x1, ep.xG, ep.n, jc);
-  int i = tl.i0;
-  while (i < ep.G - 2 && kn[i + 1] <= xo) ++i;
-  const double xa = kn[i], xb = kn[i + 1];
-  const float t = (xo == xb) ? 1.f : ((xo == xa) ? 0.f : (float)((xo - xa) / (xb - xa)));
-
-  // --- phase: integr(u) = cumsum(pitch_up)[u] / sr, closed form per segment
   const SgSeg* __restrict__ sg = segs + ep.seg_off;
-  const double u = (double)(ep.u0 + jc);
-  int k = tl.k0;
-  while (k + 1 < ep.nseg && sg[k + 1].t0 < u) ++k;
-  const SgSeg S = sg[k];
-  const double m = u - S.t0;
-  const double S1 = m * (m + 1.0) * 0.5;
-  const double S2 = S1 * (2.0 * m + 1.0) * (1.0 / 3.0);
-  const double P = S.prefix + S.y * m + S.b * S1 + S.c * S2 + S.d * (S1 * S1);
-  const double v = P * ep.inv_srD;
-  double ph = v - floor(v);
-  if (ph >= 0.5) ph -= 1.0;
-  float sigma = 1.f;
-  if (ph > 0.25) { ph -= 0.5; sigma = -1.f; }
-  else if (ph < -0.25) { ph += 0.5; sigma = -1.f; }
-  float sh, ch;
-  sincospif((float)ph, &sh, &ch);
-  const float s1 = 2.f * sh * ch;  // sin(2*pi*psi)
-  const float lam = -4.f * sh * sh;  // 2cos(2*pi*psi) - 2, cancellation-free
-
-  // --- wave-uniform knot columns
-  const int ia = __builtin_amdgcn_readfirstlane(i);
-  const int ib = __builtin_amdgcn_readfirstlane(__shfl(i, 63));
-  const int ncol = ib - ia + 2;
   const float* __restrict__ A = amps + ep.amp_off;
-  float y;
-  if (ncol == 2) y = rows_uniform<2>(A, ep.R, ia, i - ia, t, s1, lam, sigma);
-  else if (ncol == 3) y = rows_uniform<3>(A, ep.R, ia, i - ia, t, s1, lam, sigma);
-  else y = rows_gather(A, ep.R, i, t, s1, lam, sigma);
-
-  if (valid) W[ep.w_off + j] = y;
-
-  // --- fused normalisation max over the direct-copy window
-  if (ep.dj1 > ep.dj0) {
-    float cand = 0.f;
-    if (valid && j >= ep.dj0 && j < ep.dj1) {
-      cand = y;
-      const SgSyllable& sy = syls[ep.syl];
-      if (sy.env.kind != 0) cand = (float)((double)y * contour_at(sy.env, cknots, sy.L, ep.dk0 + j));
+  const int half = ep.n >> 1;
+  int i = tl.i0, k = tl.k0;
+  float tmax = 0.f;
+  const bool env = ep.dj1 > ep.dj0 && syls[ep.syl].env.kind != 0;
+#pragma unroll 1
+  for (int q = 0; q < SG_SINE_TILE / 256; ++q) {
+    const int jw = tl.j0 + q * 256;  // wave-group base (uniform)
+    if (jw >= ep.n) break;
+    const int j = jw + (int)threadIdx.x;
+    const bool valid = j < ep.n;
+    const int jc = valid ? j : ep.n - 1;
+    // amplitude interval: approx() at xo = seq.int(x1, xG, n)[j]
+    const double xo = (jc == ep.n - 1) ? ep.xG
+                      : (jc < half ? fma((double)jc, ep.xby, ep.x1) : fma(-(double)(ep.n - 1 - jc), ep.xby, ep.xG));
+    while (i < ep.G - 2 && kn[i + 1] <= xo) ++i;
+    const double xa = kn[i], xb = kn[i + 1];
+    const float t = (xo == xb) ? 1.f : ((xo == xa) ? 0.f : (float)(xo - xa) / (float)(xb - xa));
+    // phase: integr(u) = cumsum(pitch_up)[u] / sr in closed form per segment
+    const double u = (double)(ep.u0 + jc);
+    while (k + 1 < ep.nseg && sg[k + 1].t0 < u) ++k;
+    const SgSeg S = sg[k];
+    const double m = u - S.t0;
+    const double S1 = m * (m + 1.0) * 0.5;
+    const double S2 = S1 * fma(2.0, m, 1.0) * (1.0 / 3.0);
+    const double P = fma(S.d, S1 * S1, fma(S.c, S2, fma(S.b, S1, fma(S.y, m, S.prefix))));
+    const double v = P * ep.inv_srD;
+    double ph = v - floor(v);
+    if (ph >= 0.5) ph -= 1.0;
+    float sigma = 1.f;
+    if (ph > 0.25) { ph -= 0.5; sigma = -1.f; }
+    else if (ph < -0.25) { ph += 0.5; sigma = -1.f; }
+    float sh, ch;
+    sincospi_q((float)ph, sh, ch);
+    const float s1 = 2.f * sh * ch;    // sin(2*pi*psi)
+    const float lam = -4.f * sh * sh;  // 2cos(2*pi*psi) - 2 without cancellation
+    // wave-uniform knot columns
+    const int ia = __builtin_amdgcn_readfirstlane(i);
+    const int ib = __builtin_amdgcn_readfirstlane(__shfl(i, 63));
+    const int ncol = ib - ia + 2;
+    float y;
+    if (ncol == 2) y = rows_uniform<2>(A, ep.R, ia, i - ia, t, s1, lam, sigma);
+    else if (ncol == 3) y = rows_uniform<3>(A, ep.R, ia, i - ia, t, s1, lam, sigma);
+    else y = rows_gather(A, ep.R, i, t, s1, lam, sigma);
+    if (valid) {
+      W[ep.w_off + j] = y;
+      if (j >= ep.dj0 && j < ep.dj1) {
+        float cand = y;
+        if (env) {
+          const SgSyllable& sy = syls[ep.syl];
+          cand = (float)((double)y * contour_at(sy.env, cknots, sy.L, ep.dk0 + j));
+        }
+        tmax = fmaxf(tmax, cand);
+      }
     }
+  }
+  // fused normalisation max over the direct-copy window
+  if (ep.dj1 > ep.dj0) {
     __shared__ float red[4];
-    const float wm = wave_max(cand);
+    const float wm = wave_max(tmax);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = wm;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -220,7 +237,7 @@ extern "C" __global__ __launch_bounds__(256) void sg_piece_max(
     const SgSylTile* __restrict__ ptiles, const SgPiece* __restrict__ pieces, const SgSyllable* __restrict__ syls,
     const double* __restrict__ cknots, const float* __restrict__ W, unsigned* __restrict__ maxes) {
   const SgSylTile tl = ptiles[blockIdx.x];
-  const SgPiece p = pieces[tl.piece];
+  const SgPiece& p = pieces[tl.piece];
   const SgSyllable& sy = syls[tl.syl];
   const int64_t q = tl.k0 + threadIdx.x;
   float cand = 0.f;
@@ -239,6 +256,17 @@ extern "C" __global__ __launch_bounds__(256) void sg_piece_max(
 }
 
 // out[k] = assembled[k] * env[k] / max * fade[k] * drift[k]   (R/source.R:436-467)
+// Each thread owns 4 consecutive samples; a tile lying inside one direct
+// piece with a 16-B aligned source and destination moves float4s.
+__device__ __forceinline__ float fade_at(int lf, int64_t L, int64_t k) {
+  float f = 1.f;
+  const float by = 1.f / (float)(lf - 1);
+  if (k < lf) f *= (k == lf - 1) ? 1.f : (float)k * by;
+  const int64_t kb = L - 1 - k;
+  if (kb < lf) f *= (kb == lf - 1) ? 1.f : (float)kb * by;
+  return f;
+}
+
 extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize(
     const SgSylTile* __restrict__ stiles, const SgPiece* __restrict__ pieces, const SgSyllable* __restrict__ syls,
     const double* __restrict__ cknots, const float* __restrict__ W, const unsigned* __restrict__ maxes,
@@ -247,23 +275,43 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize(
   const SgSyllable& sy = syls[tl.syl];
   const float inv_max = 1.f / __uint_as_float(maxes[sy.max_slot]);
   const int pend = sy.piece0 + sy.npiece;
+  const int64_t kt = tl.k0 + 4 * (int64_t)threadIdx.x;
+  const int64_t tile_end = tl.k0 + 1024 < sy.L ? tl.k0 + 1024 : sy.L;
+  const SgPiece& p0 = pieces[tl.piece];
+  const bool simple = sy.env.kind == 0 && sy.drift.nk == 0;
+  // fast path: whole tile inside one direct piece, aligned, no env/drift
+  if (simple && p0.nterms < 0 && p0.start <= tl.k0 && p0.start + p0.len >= tile_end &&
+      ((sy.out_off + tl.k0) & 3) == 0 && ((p0.t[0].src + (tl.k0 - p0.start)) & 3) == 0) {
+    if (kt >= tile_end) return;
+    const float* src = W + p0.t[0].src + (kt - p0.start);
+    float* dst = out + sy.out_off + kt;
+    if (kt + 4 <= tile_end) {
+      float4 v = *reinterpret_cast<const float4*>(src);
+      v.x *= inv_max; v.y *= inv_max; v.z *= inv_max; v.w *= inv_max;
+      if (sy.fade >= 2 && (kt < sy.fade || kt + 4 > sy.L - sy.fade)) {
+        v.x *= fade_at(sy.fade, sy.L, kt); v.y *= fade_at(sy.fade, sy.L, kt + 1);
+        v.z *= fade_at(sy.fade, sy.L, kt + 2); v.w *= fade_at(sy.fade, sy.L, kt + 3);
+      }
+      *reinterpret_cast<float4*>(dst) = v;
+    } else {
+      for (int64_t k = kt; k < tile_end; ++k) {
+        float v = src[k - kt] * inv_max;
+        if (sy.fade >= 2) v *= fade_at(sy.fade, sy.L, k);
+        dst[k - kt] = v;
+      }
+    }
+    return;
+  }
   int p = tl.piece;
-#pragma unroll
-  for (int q4 = 0; q4 < 4; ++q4) {
-    const int64_t k = tl.k0 + q4 * 256 + threadIdx.x;
-    if (k >= sy.L) break;
+  for (int e = 0; e < 4; ++e) {
+    const int64_t k = kt + e;
+    if (k >= tile_end) break;
     while (p + 1 < pend && pieces[p + 1].start <= k) ++p;
     const SgPiece& pc = pieces[p];
     float v = pc.nterms == 0 ? 0.f : piece_value(pc, W, k - pc.start);
     if (sy.env.kind != 0) v = (float)((double)v * contour_at(sy.env, cknots, sy.L, k));
     v *= inv_max;
-    if (sy.fade >= 2) {
-      const int lf = sy.fade;
-      const float by = 1.f / (float)(lf - 1);
-      if (k < lf) v *= (k == lf - 1) ? 1.f : (float)k * by;
-      const int64_t kb = sy.L - 1 - k;
-      if (kb < lf) v *= (kb == lf - 1) ? 1.f : (float)kb * by;
-    }
+    if (sy.fade >= 2) v *= fade_at(sy.fade, sy.L, k);
     if (sy.drift.nk > 0) v = (float)((double)v * linear_at(sy.drift, cknots, sy.L, k));
     out[sy.out_off + k] = v;
   }

@@ -662,10 +662,17 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
   const int32_t seg_off = (int32_t)B.segs.size();
   B.segs.insert(B.segs.end(), HS.segs.begin(), HS.segs.end());
   std::vector<int32_t> ep_index(mats.size());
+  // destination offset of each epoch's direct piece, to keep the fp32 copy
+  // in the finalize kernel 16-byte aligned on both sides
+  std::vector<int64_t> dk(mats.size(), 0);
+  for (const HPiece& p : A.P)
+    if (p.t.size() == 1 && p.t[0].w0 == 1 && p.t[0].w1 == 0 && p.t[0].w2 == 0) dk[p.t[0].e] = p.start - p.t[0].j0;
   for (size_t e = 0; e < mats.size(); ++e) {
     const EpochMat& m = mats[e];
     const HostEpoch& he = HE[e];
     SgEpoch d{};
+    const int64_t want = (((out_off + dk[e]) % 4) + 4) % 4;
+    B.w_total += ((want - B.w_total % 4) + 4) % 4;
     d.w_off = B.w_total;
     B.w_total += he.n;
     d.n = (int32_t)he.n;
@@ -676,6 +683,7 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
     d.nseg = (int32_t)HS.segs.size();
     d.x1 = he.knots.front();
     d.xG = he.knots.back();
+    d.xby = he.n > 1 ? (d.xG - d.x1) / (double)(he.n - 1) : 0.0;
     d.inv_srD = 1.0 / (sr * (double)m.D);
     d.knot_off = (int64_t)B.knots.size();
     B.knots.insert(B.knots.end(), he.knots.begin(), he.knots.end());
@@ -719,7 +727,7 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
   sy.npiece = (int32_t)(B.pieces.size() - sy.piece0);
   B.syls.push_back(sy);
   // sine-bank tiles: 256 samples each
-  constexpr int TILE = 256;
+  constexpr int TILE = SG_SINE_TILE;
   for (size_t e = 0; e < mats.size(); ++e) {
     const HostEpoch& he = HE[e];
     int64_t i = 0;
