@@ -121,11 +121,12 @@ def main():
         # algorithmic bytes of one sine-bank launch: fp32 epoch
         # waveform write + amplitude matrices + pitch segments/knots
         n_gc = sum(int(np.ceil(c["pitch"].size)) for c in calls[:0])
-        alg_bytes = 4 * st["harm_samples"] + st["harm_amp_bytes"]
+        launches = max(1, nprof.value // args.steps)  # sine-bank launches per step (batch slices)
+        alg_bytes = (4 * st["harm_samples"] + st["harm_amp_bytes"]) / launches
         sine_s = sine_ms.value / 1e3
         achieved = alg_bytes / sine_s / 1e9 if sine_s > 0 else 0.0
         # VALU: per (sample, row) the kernel issues 3 instructions (ISA, C=2 path)
-        valu_ops = 3.0 * st["harm_terms"]
+        valu_ops = 2.0 * st["harm_terms"] / launches
         host = out[: min(plan.total, 4 * 50000)].cpu().numpy()
         from oracle import oracle as O
         rms = []

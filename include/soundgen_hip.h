@@ -154,9 +154,10 @@ int sg_plan_upload(sg_ctx* ctx, sg_plan* plan);
  * writing fp32 samples into device buffer d_out (packed, offsets as above).
  * No host synchronisation inside; graph-capturable. */
 int sg_execute(sg_ctx* ctx, sg_plan* plan, float* d_out, void* stream);
-/* Profiling: when enabled, sg_execute brackets the sine-bank launch with
- * HIP events on the launch stream; sg_profile_read returns the average
- * duration (ms) over the recorded executes and clears them. */
+/* Profiling: when enabled, sg_execute brackets every sine-bank launch (one
+ * per batch slice) with HIP events on the launch stream; sg_profile_read
+ * returns the average launch duration (ms) and the number of launches
+ * recorded, and clears them. */
 int sg_set_profiling(sg_ctx* ctx, int on);
 int sg_profile_read(sg_ctx* ctx, double* sine_ms_avg, int64_t* n);
 int sg_synchronize(sg_ctx* ctx);

@@ -14,6 +14,7 @@
 struct sg_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t aux = nullptr;  // finalize stream of the slice pipeline
   std::string err;
   bool profiling = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
@@ -53,17 +54,17 @@ int guarded(sg_ctx* ctx, F&& f) {
 
 // Rolls a Batch back to a checkpoint when planning one call fails.
 struct Checkpoint {
-  size_t segs, epochs, knots, amps, tiles, pieces, syls, syl_tiles, cknots, noise, filt, mixes, bouts, frames;
+  size_t segs, epochs, knots, amps, tasks, pieces, syls, syl_tiles, cknots, noise, filt, mixes, bouts, frames;
   int64_t w_total, harm_samples, harm_terms, harm_amp_bytes, fft_frames, scratch;
   explicit Checkpoint(const sg::Batch& B)
       : segs(B.segs.size()), epochs(B.epochs.size()), knots(B.knots.size()), amps(B.amps.size()),
-        tiles(B.tiles.size()), pieces(B.pieces.size()), syls(B.syls.size()), syl_tiles(B.syl_tiles.size()),
+        tasks(B.tasks.size()), pieces(B.pieces.size()), syls(B.syls.size()), syl_tiles(B.syl_tiles.size()),
         cknots(B.cknots.size()), noise(0), filt(0), mixes(0), bouts(0), frames(0), w_total(B.w_total),
         harm_samples(B.harm_samples), harm_terms(B.harm_terms), harm_amp_bytes(B.harm_amp_bytes),
         fft_frames(B.fft_frames), scratch(0) {}
   void restore(sg::Batch& B) const {
     B.segs.resize(segs); B.epochs.resize(epochs); B.knots.resize(knots); B.amps.resize(amps);
-    B.tiles.resize(tiles); B.pieces.resize(pieces); B.syls.resize(syls); B.syl_tiles.resize(syl_tiles);
+    B.tasks.resize(tasks); B.pieces.resize(pieces); B.syls.resize(syls); B.syl_tiles.resize(syl_tiles);
     B.cknots.resize(cknots); B.w_total = w_total; B.harm_samples = harm_samples; B.harm_terms = harm_terms;
     B.harm_amp_bytes = harm_amp_bytes; B.fft_frames = fft_frames;
   }
@@ -85,7 +86,8 @@ int sg_ctx_create(int device, sg_ctx** out) {
   auto* c = new (std::nothrow) sg_ctx();
   if (!c) return SG_E_NOMEM;
   c->device = device;
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return SG_E_DEVICE;
   }
@@ -95,9 +97,10 @@ int sg_ctx_create(int device, sg_ctx** out) {
 
 void sg_ctx_destroy(sg_ctx* ctx) {
   if (!ctx) return;
-  hipSetDevice(ctx->device);
-  for (auto& ev : ctx->prof_events) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
-  if (ctx->stream) hipStreamDestroy(ctx->stream);
+  (void)hipSetDevice(ctx->device);
+  for (auto& ev : ctx->prof_events) { (void)hipEventDestroy(ev.first); (void)hipEventDestroy(ev.second); }
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
   delete ctx;
 }
 
@@ -191,13 +194,7 @@ int sg_execute(sg_ctx* ctx, sg_plan* plan, float* d_out, void* stream) {
   return guarded(ctx, [&]() {
     if (!plan->D.uploaded) throw sg::SgError(SG_E_ARG, "sg_execute: plan not uploaded");
     hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (ctx->profiling) {
-      HIPCHK(hipEventCreate(&e0));
-      HIPCHK(hipEventCreate(&e1));
-    }
-    sg::device_execute(plan->B, plan->D, d_out, s, e0, e1);
-    if (ctx->profiling) ctx->prof_events.emplace_back(e0, e1);
+    sg::device_execute(plan->B, plan->D, d_out, s, ctx->aux, ctx->profiling ? &ctx->prof_events : nullptr);
     return SG_OK;
   });
 }
@@ -219,8 +216,8 @@ int sg_profile_read(sg_ctx* ctx, double* sine_ms_avg, int64_t* n) {
       HIPCHK(hipEventElapsedTime(&ms, ev.first, ev.second));
       tot += ms;
       ++cnt;
-      hipEventDestroy(ev.first);
-      hipEventDestroy(ev.second);
+      (void)hipEventDestroy(ev.first);
+      (void)hipEventDestroy(ev.second);
     }
     ctx->prof_events.clear();
     *sine_ms_avg = cnt ? tot / cnt : 0;
@@ -262,7 +259,7 @@ static int run_single(sg_ctx* ctx, const sg_call_desc& d, double* out, int64_t c
     float* d_out = nullptr;
     HIPCHK(hipMalloc(&d_out, (size_t)std::max<int64_t>(L, 1) * sizeof(float)));
     std::unique_ptr<float, hipError_t (*)(void*)> hold_out(d_out, hipFree);
-    sg::device_execute(plan->B, plan->D, d_out, ctx->stream, nullptr, nullptr);
+    sg::device_execute(plan->B, plan->D, d_out, ctx->stream, ctx->aux, nullptr);
     std::vector<float> h((size_t)L);
     HIPCHK(hipMemcpyAsync(h.data(), d_out, (size_t)L * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));

@@ -3,14 +3,15 @@
 #pragma once
 #include <stdint.h>
 
-// Cumulative-pitch segment: pitch_up[u] for u in (t0, t1] is the cubic
-// y + dx*(b + dx*(c + dx*d)), dx = u - t0 (R's spline_eval keeps the left
-// segment at an exact knot, R/utilities_soundgen.R:410 via stats splines.c).
-// prefix = sum_{u' <= t0} pitch_up[u'] (long-double accumulated on host).
+// Phase segment of a syllable: for u in (t0, t1] (1-based samples)
+//   integr(u) = cumsum(pitch_up)[u] / samplingRate = c0 + m(c1 + m(c2 + m(c3 + m c4))),  m = u - t0
+// i.e. the closed-form prefix sum of the FMM pitch spline piece y + dx(b + dx(c + dx d))
+// (R's spline_eval keeps the left piece at an exact knot, R/utilities_soundgen.R:410 via
+// stats splines.c; R/source.R:385 cumsum in long double). Coefficients are built in long
+// double on the host, divided by samplingRate.
 struct SgSeg {
   double t0;
-  double prefix;
-  double y, b, c, d;
+  double c0, c1, c2, c3, c4;
 };
 
 // One subharmonic epoch of one syllable (R/source.R:389-427).
@@ -20,16 +21,17 @@ struct SgSeg {
 struct SgEpoch {
   int64_t w_off;     // scratch offset of W[0]
   int64_t amp_off;   // float offset of the [G][R] amplitude block
+  int64_t da_off;    // float offset of the [G-1][R] block dA[i] = A[i+1] - A[i]
   int64_t knot_off;  // double offset of the G knots
   int32_t seg_off;   // first SgSeg of the syllable
   int32_t nseg;
   int32_t n;         // N_e samples
   int32_t G;         // knots / amplitude columns (>= 2)
-  int32_t R;         // rows (multiple of 8, zero padded)
+  int32_t R;         // rows (multiple of SG_ROW_CHUNK, zero padded)
   int32_t u0;        // first sample, 1-based within the syllable
   double x1, xG;     // xout range
   double xby;        // (xG - x1) / (n - 1), as R's seq.int computes it
-  double inv_srD;    // 1 / (samplingRate * D), D = nSubharm + 1
+  double invD;       // 1 / D, D = nSubharm + 1
   // direct-copy window used for the fused max: W[j] lands at syllable
   // sample k = dk0 + j for j in [dj0, dj1) with weight 1.
   int32_t dj0, dj1;
@@ -38,14 +40,39 @@ struct SgEpoch {
   int32_t pad;
 };
 
-constexpr int SG_SINE_TILE = 2048;  // samples per sine-bank workgroup (256 threads x 8)
+constexpr int SG_ROW_CHUNK = 16;  // amplitude rows per scalar load (s_load_dwordx16)
 
-struct SgTile {
-  int32_t epoch;
-  int32_t j0;  // first sample of the tile
-  int32_t i0;  // amplitude interval of sample j0
-  int32_t k0;  // pitch segment of sample j0
+// One wave task of the sine bank: `len` (<= SG_TASK_MAX) consecutive samples
+// j0.. of one epoch that lie in ONE phase segment and whose approx() xout all
+// fall in one amplitude interval [knot i, knot i+1] (or in a run of intervals
+// whose columns are equal, flag CONST). Everything the wave needs is in this
+// record (wave-uniform scalar loads):
+//   sample l = j - j0:  m = mbase + l,  integr/D = (c0 + m(c1 + m(c2 + m(c3 + m c4)))) * invD
+//                       t = (tc0 + l * xby) * rdx   (approx() weight inside the interval)
+constexpr int SG_TASK_CONST = 1;  // columns equal over the task: A chain only
+constexpr int SG_TASK_MAX = 512;  // samples per task (8 slots of 64 lanes)
+struct SgWTask {
+  int64_t w_off;       // W offset of epoch sample 0
+  int64_t a_off;       // float offset of A[i][0..R)
+  int64_t d_off;       // float offset of dA[i][0..R) = A[i+1] - A[i]
+  int64_t dk0;         // syllable sample (0-based) of epoch sample 0
+  double c0, c1, c2, c3, c4;  // phase segment, see SgSeg
+  double invD;         // 1 / (nSubharm + 1)
+  float rdx, tc0, xby;
+  int32_t mbase;       // u(j0) - t0 of the segment
+  int32_t R;           // rows (multiple of 16)
+  int32_t j0, len;
+  int32_t dj0, dj1;    // direct-copy window (fused max)
+  int32_t syl;
+  int32_t flags;
+  int32_t pad;
 };
+static_assert(sizeof(SgWTask) == 128, "SgWTask layout");
+constexpr int SG_TASKS_PER_BLOCK = 8;  // 4 waves x 2 tasks
+// batch slices of the sine-bank / finalize pipeline; measured on MI355X (C2): 4 slices
+// on two streams ran 0.41 ms/step against 0.32 for one (both kernels slowed when
+// co-resident), so the default is a single slice
+constexpr int SG_SLICES = 1;
 
 // A piece of an assembled syllable (crossFade() chain, R/utilities_soundgen.R:328-375):
 // value(k) = sum_t (w0 + w1*q + w2*q^2) * W[src_t + q], q = k - start.
@@ -88,6 +115,10 @@ struct SgSyllable {
   int32_t piece0, npiece;
   int32_t fade;      // fade length (0/1 = none)
   int32_t max_slot;  // index into the per-syllable max array
+  int32_t ntask;     // sine-bank tasks of the syllable: per-task max slots [task0, task0+ntask)
+  int64_t task0;
+  int32_t ptile0;    // crossfade-piece tiles: per-tile max slots [ptile0, ptile0+nptile)
+  int32_t nptile;
   SgContour env;     // amplEnvelope (kind 0 = none)
   SgLinear drift;
 };

@@ -1,6 +1,7 @@
 // sg_exec.cpp — HBM arena for a plan and the per-batch launch sequence.
 #include "sg_exec.h"
 
+#include <algorithm>
 #include <cstring>
 #include <string>
 
@@ -18,7 +19,7 @@ constexpr size_t ALIGN = 256;
 size_t up(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
 struct Layout {
-  size_t segs, epochs, knots, amps, tiles, pieces, syls, syl_tiles, ptiles, cknots, W, maxes, total;
+  size_t segs, epochs, knots, amps, tasks, pieces, syls, syl_tiles, ptiles, cknots, W, taskmax, ptilemax, maxes, total;
   explicit Layout(const Batch& B) {
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o += up(bytes > 0 ? bytes : 1); return r; };
@@ -26,14 +27,16 @@ struct Layout {
     epochs = take(B.epochs.size() * sizeof(SgEpoch));
     knots = take(B.knots.size() * sizeof(double));
     amps = take(B.amps.size() * sizeof(float) + 64 * sizeof(float));
-    tiles = take(B.tiles.size() * sizeof(SgTile));
+    tasks = take(B.tasks.size() * sizeof(SgWTask));
     pieces = take(B.pieces.size() * sizeof(SgPiece));
     syls = take(B.syls.size() * sizeof(SgSyllable));
     syl_tiles = take(B.syl_tiles.size() * sizeof(SgSylTile));
     ptiles = take(B.ptiles.size() * sizeof(SgSylTile));
     cknots = take(B.cknots.size() * sizeof(double));
     W = take((size_t)B.w_total * sizeof(float));
-    maxes = take(B.syls.size() * sizeof(unsigned));
+    taskmax = take(B.tasks.size() * sizeof(float));
+    ptilemax = take(B.ptiles.size() * sizeof(float));
+    maxes = take(B.syls.size() * sizeof(float));
     total = o;
   }
 };
@@ -42,17 +45,47 @@ struct Layout {
 void finalize_plan(Batch& B) {
   B.ptiles.clear();
   for (size_t s = 0; s < B.syls.size(); ++s) {
-    const SgSyllable& sy = B.syls[s];
+    SgSyllable& sy = B.syls[s];
+    sy.ptile0 = (int32_t)B.ptiles.size();
     for (int32_t p = sy.piece0; p < sy.piece0 + sy.npiece; ++p)
       if (B.pieces[p].nterms > 0)
         for (int64_t q0 = 0; q0 < B.pieces[p].len; q0 += 256) B.ptiles.push_back(SgSylTile{(int32_t)s, p, q0});
+    sy.nptile = (int32_t)B.ptiles.size() - sy.ptile0;
+  }
+  // slices of whole syllables with about equal sample counts
+  B.slices.clear();
+  const int64_t nsyl = (int64_t)B.syls.size();
+  if (nsyl == 0) return;
+  int64_t total = 0;
+  for (const SgSyllable& sy : B.syls) total += sy.L;
+  const int K = (int)std::min<int64_t>(SG_SLICES, nsyl);
+  int64_t acc = 0, ft = 0;
+  int32_t s0 = 0;
+  for (int32_t s = 0; s < nsyl; ++s) {
+    acc += B.syls[s].L;
+    const bool cut = s == nsyl - 1 || acc * K >= total * ((int64_t)B.slices.size() + 1);
+    if (!cut) continue;
+    Slice c{};
+    c.s0 = s0; c.s1 = s + 1;
+    c.t0 = B.syls[s0].task0;
+    c.t1 = B.syls[s].task0 + B.syls[s].ntask;
+    c.p0 = B.syls[s0].ptile0;
+    c.p1 = B.syls[s].ptile0 + B.syls[s].nptile;
+    c.f0 = ft;
+    while (ft < (int64_t)B.syl_tiles.size() && B.syl_tiles[ft].syl <= s) ++ft;
+    c.f1 = ft;
+    B.slices.push_back(c);
+    s0 = s + 1;
   }
 }
 
 int64_t device_bytes(const Batch& B) { return (int64_t)Layout(B).total; }
 
 void device_free(DevicePlan& D) {
-  if (D.arena) hipFree(D.arena);
+  if (D.arena) (void)hipFree(D.arena);
+  for (hipEvent_t e : D.ev_slice) (void)hipEventDestroy(e);
+  if (D.ev_fork) (void)hipEventDestroy(D.ev_fork);
+  if (D.ev_join) (void)hipEventDestroy(D.ev_join);
   D = DevicePlan{};
 }
 
@@ -68,14 +101,16 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   D.epochs = (SgEpoch*)(a + L.epochs);
   D.knots = (double*)(a + L.knots);
   D.amps = (float*)(a + L.amps);
-  D.tiles = (SgTile*)(a + L.tiles);
+  D.tasks = (SgWTask*)(a + L.tasks);
   D.pieces = (SgPiece*)(a + L.pieces);
   D.syls = (SgSyllable*)(a + L.syls);
   D.syl_tiles = (SgSylTile*)(a + L.syl_tiles);
   D.ptiles = (SgSylTile*)(a + L.ptiles);
   D.cknots = (double*)(a + L.cknots);
   D.W = (float*)(a + L.W);
-  D.maxes = (unsigned*)(a + L.maxes);
+  D.taskmax = (float*)(a + L.taskmax);
+  D.ptilemax = (float*)(a + L.ptilemax);
+  D.maxes = (float*)(a + L.maxes);
   auto cp = [&](void* dst, const void* src, size_t bytes) {
     if (bytes) HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
   };
@@ -83,23 +118,58 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   cp(D.epochs, B.epochs.data(), B.epochs.size() * sizeof(SgEpoch));
   cp(D.knots, B.knots.data(), B.knots.size() * sizeof(double));
   cp(D.amps, B.amps.data(), B.amps.size() * sizeof(float));
-  cp(D.tiles, B.tiles.data(), B.tiles.size() * sizeof(SgTile));
+  cp(D.tasks, B.tasks.data(), B.tasks.size() * sizeof(SgWTask));
   cp(D.pieces, B.pieces.data(), B.pieces.size() * sizeof(SgPiece));
   cp(D.syls, B.syls.data(), B.syls.size() * sizeof(SgSyllable));
   cp(D.syl_tiles, B.syl_tiles.data(), B.syl_tiles.size() * sizeof(SgSylTile));
   cp(D.ptiles, B.ptiles.data(), B.ptiles.size() * sizeof(SgSylTile));
   cp(D.cknots, B.cknots.data(), B.cknots.size() * sizeof(double));
   HIPCHK(hipStreamSynchronize(s));
+  while (D.ev_slice.size() < B.slices.size()) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    D.ev_slice.push_back(e);
+  }
+  if (!D.ev_fork) HIPCHK(hipEventCreateWithFlags(&D.ev_fork, hipEventDisableTiming));
+  if (!D.ev_join) HIPCHK(hipEventCreateWithFlags(&D.ev_join, hipEventDisableTiming));
   D.uploaded = true;
 }
 
-void device_execute(const Batch& B, const DevicePlan& D, float* d_out, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-  if (!B.syls.empty()) HIPCHK(hipMemsetAsync(D.maxes, 0, B.syls.size() * sizeof(unsigned), s));
-  if (e0) HIPCHK(hipEventRecord(e0, s));
-  launch_sine_bank(D, (int64_t)B.tiles.size(), s);
-  if (e1) HIPCHK(hipEventRecord(e1, s));
-  launch_piece_max(D, (int64_t)B.ptiles.size(), s);
-  launch_harm_finalize(D, (int64_t)B.syl_tiles.size(), d_out, s);
+void device_execute(const Batch& B, DevicePlan& D, float* d_out, hipStream_t s, hipStream_t s2,
+                    std::vector<std::pair<hipEvent_t, hipEvent_t>>* prof) {
+  if (B.slices.empty()) return;
+  const bool two = B.slices.size() > 1;
+  if (!two) s2 = s;
+  // fork: s2 starts after everything already queued on s
+  if (two) {
+    HIPCHK(hipEventRecord(D.ev_fork, s));
+    HIPCHK(hipStreamWaitEvent(s2, D.ev_fork, 0));
+  }
+  for (size_t c = 0; c < B.slices.size(); ++c) {
+    const Slice& sl = B.slices[c];
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (prof) {
+      HIPCHK(hipEventCreate(&e0));
+      HIPCHK(hipEventCreate(&e1));
+      HIPCHK(hipEventRecord(e0, s));
+    }
+    launch_sine_bank(D, sl.t0, sl.t1 - sl.t0, s);
+    if (prof) {
+      HIPCHK(hipEventRecord(e1, s));
+      prof->emplace_back(e0, e1);
+    }
+    launch_piece_max(D, sl.p0, sl.p1 - sl.p0, s);
+    launch_syl_max(D, sl.s0, sl.s1 - sl.s0, s);
+    if (two) {
+      HIPCHK(hipEventRecord(D.ev_slice[c], s));
+      HIPCHK(hipStreamWaitEvent(s2, D.ev_slice[c], 0));
+    }
+    launch_harm_finalize(D, sl.f0, sl.f1 - sl.f0, d_out, s2);
+  }
+  if (two) {  // join
+    HIPCHK(hipEventRecord(D.ev_join, s2));
+    HIPCHK(hipStreamWaitEvent(s, D.ev_join, 0));
+  }
   HIPCHK(hipGetLastError());
 }
 

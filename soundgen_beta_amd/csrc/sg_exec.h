@@ -2,6 +2,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <utility>
+#include <vector>
+
 #include "sg_plan.h"
 
 namespace sg {
@@ -14,25 +17,33 @@ struct DevicePlan {
   SgEpoch* epochs = nullptr;
   double* knots = nullptr;
   float* amps = nullptr;
-  SgTile* tiles = nullptr;
+  SgWTask* tasks = nullptr;
   SgPiece* pieces = nullptr;
   SgSyllable* syls = nullptr;
   SgSylTile* syl_tiles = nullptr;
   SgSylTile* ptiles = nullptr;
   double* cknots = nullptr;
   float* W = nullptr;
-  unsigned* maxes = nullptr;
+  float* taskmax = nullptr;
+  float* ptilemax = nullptr;
+  float* maxes = nullptr;
+  std::vector<hipEvent_t> ev_slice;  // slice c's maxes are ready (s -> s2)
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 int64_t device_bytes(const Batch& B);
 void device_upload(const Batch& B, DevicePlan& D, hipStream_t s);
 void device_free(DevicePlan& D);
-// e0/e1 (optional) bracket the sine-bank launch for profiling
-void device_execute(const Batch& B, const DevicePlan& D, float* d_out, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
+// Slice pipeline: sine bank + maxes of slice c on s, finalize of slice c on
+// s2 (overlapping the sine bank of c+1); s waits for s2 at the end. prof
+// (optional) receives one event pair per sine-bank launch.
+void device_execute(const Batch& B, DevicePlan& D, float* d_out, hipStream_t s, hipStream_t s2,
+                    std::vector<std::pair<hipEvent_t, hipEvent_t>>* prof);
 
 // launchers (sg_harm.hip)
-void launch_sine_bank(const DevicePlan& D, int64_t n_tiles, hipStream_t s);
-void launch_piece_max(const DevicePlan& D, int64_t n_ptiles, hipStream_t s);
-void launch_harm_finalize(const DevicePlan& D, int64_t n_stiles, float* out, hipStream_t s);
+void launch_sine_bank(const DevicePlan& D, int64_t t0, int64_t n_tasks, hipStream_t s);
+void launch_syl_max(const DevicePlan& D, int64_t s0, int64_t n_syls, hipStream_t s);
+void launch_piece_max(const DevicePlan& D, int64_t p0, int64_t n_ptiles, hipStream_t s);
+void launch_harm_finalize(const DevicePlan& D, int64_t f0, int64_t n_stiles, float* out, hipStream_t s);
 
 }  // namespace sg

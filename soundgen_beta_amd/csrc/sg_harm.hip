@@ -1,16 +1,19 @@
 // sg_harm.hip — gfx950 kernels of the additive harmonic source
 // (generateHarmonics(), R/source.R:377-467).
 //
-// sg_sine_bank: one 256-sample tile per workgroup (4 wave64s). Per sample:
-//   integr(u)  = closed-form prefix sum of the FMM pitch spline (fp64)
-//   phi        = frac(integr / D) folded to |psi| <= 1/4 (sign sigma)
-//   sin(r*phi) via Reinsch's stable 2-term recurrence (2 VALU ops/row)
-//   amplitude  = approx() hat weights over the wave's 2-3 knot columns; the
-//                columns are wave-uniform so every amplitude is a scalar
-//                (SGPR) operand loaded by s_load: no LDS, no per-lane gathers
-//   => 2 + C VALU ops per (sample, harmonic row), C = columns (2 or 3)
-// It also produces the signed max of the syllable over its direct-copy
-// window (the R normalisation waveform / max(waveform)).
+// sg_sine_bank: one wave task = up to 64 consecutive samples of one epoch
+// inside ONE amplitude interval (the approx() knots x_i, x_{i+1}, R/source.R:403-405),
+// so both amplitude columns A[i][.], dA[i][.] = A[i+1][.] - A[i][.] are wave-uniform
+// and stream through the scalar cache (s_load_dwordx16, prefetched one chunk ahead):
+//   integr(u)  closed-form quartic prefix sum of the FMM pitch spline (fp64, Horner)
+//   theta      = 2*pi*frac(integr / D)
+//   W(j)       = sum_r (A_r + t_j dA_r) sin(r theta)             (R/source.R:396-419)
+//              = (b_1 + t_j e_1) sin(theta)  by Clenshaw's recurrence
+//                b_r = A_r + 2cos(theta) b_{r+1} - b_{r+2}  (2 VALU ops per row and chain)
+//   a task whose two columns are equal runs the A chain only.
+// Each task also writes the signed max of its samples that land 1:1 in the
+// assembled syllable (R's waveform / max(waveform), R/source.R:449); a small
+// kernel reduces those per syllable — no atomics, deterministic.
 #include <hip/hip_runtime.h>
 
 #include "sg_dev.h"
@@ -71,61 +74,6 @@ __device__ __forceinline__ double linear_at(const SgLinear& l, const double* __r
   return y[i] + (y[j] - y[i]) * ((u - x[i]) / (x[j] - x[i]));
 }
 
-// Sum over rows with wave-uniform columns ia..ia+C-1 (amplitudes in SGPRs).
-template <int C>
-__device__ __forceinline__ float rows_uniform(const float* __restrict__ A, int R, int ia, int rel, float t,
-                                              float s1, float lam, float sigma) {
-  float acc_o[C], acc_e[C];
-#pragma unroll
-  for (int c = 0; c < C; ++c) { acc_o[c] = 0.f; acc_e[c] = 0.f; }
-  float s = s1, d = s1;
-  const float* __restrict__ col = A + (size_t)ia * R;
-  for (int r0 = 0; r0 < R; r0 += 8) {
-    float a[C][8];
-#pragma unroll
-    for (int c = 0; c < C; ++c)
-#pragma unroll
-      for (int q = 0; q < 8; ++q) a[c][q] = col[c * R + r0 + q];
-#pragma unroll
-    for (int q = 0; q < 8; q += 2) {
-#pragma unroll
-      for (int c = 0; c < C; ++c) acc_o[c] = fmaf(a[c][q], s, acc_o[c]);
-      d = fmaf(lam, s, d);
-      s = s + d;
-#pragma unroll
-      for (int c = 0; c < C; ++c) acc_e[c] = fmaf(a[c][q + 1], s, acc_e[c]);
-      d = fmaf(lam, s, d);
-      s = s + d;
-    }
-  }
-  float y = 0.f;
-#pragma unroll
-  for (int c = 0; c < C; ++c) {
-    const float w = (c == rel) ? 1.f - t : ((c == rel + 1) ? t : 0.f);
-    y = fmaf(w, fmaf(sigma, acc_o[c], acc_e[c]), y);
-  }
-  return y;
-}
-
-// Fallback when a wave spans > 3 knot columns (f0 near pitchCeiling):
-// per-lane amplitude gathers.
-__device__ __forceinline__ float rows_gather(const float* __restrict__ A, int R, int i, float t, float s1,
-                                             float lam, float sigma) {
-  const float* __restrict__ c0 = A + (size_t)i * R;
-  const float* __restrict__ c1 = c0 + R;
-  float ao = 0.f, ae = 0.f, s = s1, d = s1;
-  for (int r = 0; r < R; r += 2) {
-    const float a0 = c0[r], a1 = c1[r], b0 = c0[r + 1], b1 = c1[r + 1];
-    ao = fmaf(fmaf(t, a1 - a0, a0), s, ao);
-    d = fmaf(lam, s, d);
-    s = s + d;
-    ae = fmaf(fmaf(t, b1 - b0, b0), s, ae);
-    d = fmaf(lam, s, d);
-    s = s + d;
-  }
-  return fmaf(sigma, ao, ae);
-}
-
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
@@ -144,81 +92,166 @@ __device__ __forceinline__ void sincospi_q(float x, float& s, float& c) {
                           4.16666667e-2f), -0.5f), 1.f);
 }
 
-extern "C" __global__ __launch_bounds__(256) void sg_sine_bank(
-    const SgTile* __restrict__ tiles, const SgEpoch* __restrict__ epochs, const SgSeg* __restrict__ segs,
-    const double* __restrict__ knots, const float* __restrict__ amps, const SgSyllable* __restrict__ syls,
-    const double* __restrict__ cknots, float* __restrict__ W, unsigned* __restrict__ maxes) {
-  const SgTile tl = tiles[blockIdx.x];
-  const SgEpoch ep = epochs[tl.epoch];
-  const double* __restrict__ kn = knots + ep.knot_off;
-  const SgSeg* __restrict__ sg = segs + ep.seg_off;
-  const float* __restrict__ A = amps + ep.amp_off;
-  const int half = ep.n >> 1;
-  int i = tl.i0, k = tl.k0;
-  float tmax = 0.f;
-  const bool env = ep.dj1 > ep.dj0 && syls[ep.syl].env.kind != 0;
-#pragma unroll 1
-  for (int q = 0; q < SG_SINE_TILE / 256; ++q) {
-    const int jw = tl.j0 + q * 256;  // wave-group base (uniform)
-    if (jw >= ep.n) break;
-    const int j = jw + (int)threadIdx.x;
-    const bool valid = j < ep.n;
-    const int jc = valid ? j : ep.n - 1;
-    // amplitude interval: approx() at xo = seq.int(x1, xG, n)[j]
-    const double xo = (jc == ep.n - 1) ? ep.xG
-                      : (jc < half ? fma((double)jc, ep.xby, ep.x1) : fma(-(double)(ep.n - 1 - jc), ep.xby, ep.xG));
-    while (i < ep.G - 2 && kn[i + 1] <= xo) ++i;
-    const double xa = kn[i], xb = kn[i + 1];
-    const float t = (xo == xb) ? 1.f : ((xo == xa) ? 0.f : (float)(xo - xa) / (float)(xb - xa));
-    // phase: integr(u) = cumsum(pitch_up)[u] / sr in closed form per segment
-    const double u = (double)(ep.u0 + jc);
-    while (k + 1 < ep.nseg && sg[k + 1].t0 < u) ++k;
-    const SgSeg S = sg[k];
-    const double m = u - S.t0;
-    const double S1 = m * (m + 1.0) * 0.5;
-    const double S2 = S1 * fma(2.0, m, 1.0) * (1.0 / 3.0);
-    const double P = fma(S.d, S1 * S1, fma(S.c, S2, fma(S.b, S1, fma(S.y, m, S.prefix))));
-    const double v = P * ep.inv_srD;
-    double ph = v - floor(v);
-    if (ph >= 0.5) ph -= 1.0;
-    float sigma = 1.f;
-    if (ph > 0.25) { ph -= 0.5; sigma = -1.f; }
-    else if (ph < -0.25) { ph += 0.5; sigma = -1.f; }
-    float sh, ch;
-    sincospi_q((float)ph, sh, ch);
-    const float s1 = 2.f * sh * ch;    // sin(2*pi*psi)
-    const float lam = -4.f * sh * sh;  // 2cos(2*pi*psi) - 2 without cancellation
-    // wave-uniform knot columns
-    const int ia = __builtin_amdgcn_readfirstlane(i);
-    const int ib = __builtin_amdgcn_readfirstlane(__shfl(i, 63));
-    const int ncol = ib - ia + 2;
-    float y;
-    if (ncol == 2) y = rows_uniform<2>(A, ep.R, ia, i - ia, t, s1, lam, sigma);
-    else if (ncol == 3) y = rows_uniform<3>(A, ep.R, ia, i - ia, t, s1, lam, sigma);
-    else y = rows_gather(A, ep.R, i, t, s1, lam, sigma);
-    if (valid) {
-      W[ep.w_off + j] = y;
-      if (j >= ep.dj0 && j < ep.dj1) {
+// row_newbcast:K — every 16-lane row reads its lane K (gfx950 DPP): with
+// amplitude rows r0..r0+15 held in lanes 0..15 of every row, lane L gets row r0+K.
+#define SG_BC(v, K) \
+  __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, (v)), 0x150 + (K), 0xf, 0xf, true))
+
+// Clenshaw rows g*16+K of group g: b = A_r + al*b1 - b2 (and the dA chain when TWO)
+#define SG_ROW(g, K)                                                    \
+  {                                                                     \
+    _Pragma("unroll") for (int s = 0; s < NS; ++s) {                    \
+      const float b = fmaf(al[s], b1[s], SG_BC(va[g], K) - b2[s]);      \
+      b2[s] = b1[s];                                                    \
+      b1[s] = b;                                                        \
+      if (TWO) {                                                        \
+        const float e = fmaf(al[s], e1[s], SG_BC(vd[g], K) - e2[s]);    \
+        e2[s] = e1[s];                                                  \
+        e1[s] = e;                                                      \
+      }                                                                 \
+    }                                                                   \
+  }
+#define SG_GROUP(g)                                                                                    \
+  if ((g) < ng) {                                                                                      \
+    SG_ROW(g, 15) SG_ROW(g, 14) SG_ROW(g, 13) SG_ROW(g, 12) SG_ROW(g, 11) SG_ROW(g, 10) SG_ROW(g, 9) \
+    SG_ROW(g, 8) SG_ROW(g, 7) SG_ROW(g, 6) SG_ROW(g, 5) SG_ROW(g, 4) SG_ROW(g, 3) SG_ROW(g, 2)       \
+    SG_ROW(g, 1) SG_ROW(g, 0)                                                                          \
+  }
+
+// Amplitude rows of one 64-row chunk, register resident: group g (rows
+// 16g..16g+15 of the chunk) is ONE coalesced 64-B vector load replicated into
+// the four 16-lane rows of va[g]; each row reaches every lane through a DPP
+// broadcast folded into the v_sub.
+struct AmpChunk {
+  float va[4], vd[4];
+  int ng;
+};
+
+template <bool TWO>
+__device__ __forceinline__ void load_chunk(AmpChunk& c, const float* __restrict__ A, const float* __restrict__ D,
+                                           int r0, int R, int lane) {
+  const int r = lane & 15;
+  c.ng = (R - r0) >= 64 ? 4 : (R - r0) >> 4;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    c.va[g] = (g < c.ng) ? A[r0 + 16 * g + r] : 0.f;
+    c.vd[g] = (TWO && g < c.ng) ? D[r0 + 16 * g + r] : 0.f;
+  }
+}
+
+// Clenshaw over one chunk (top row first) continuing the recurrences b, e.
+template <int NS, bool TWO>
+__device__ __forceinline__ void clenshaw_chunk(const AmpChunk& c, const float (&al)[NS], float (&b1)[NS],
+                                               float (&b2)[NS], float (&e1)[NS], float (&e2)[NS]) {
+  const int ng = c.ng;
+  const float(&va)[4] = c.va;
+  const float(&vd)[4] = c.vd;
+  SG_GROUP(3) SG_GROUP(2) SG_GROUP(1) SG_GROUP(0)
+}
+
+// Per-sample set-up for task sample l: approx() weight t, 2cos(theta), sin(theta).
+template <bool TWO>
+__device__ __forceinline__ void sample_setup(const SgWTask& T, int l, float& t, float& al, float& sn) {
+  t = TWO ? fmaf((float)l, T.xby, T.tc0) * T.rdx : 0.f;
+  const double m = (double)(T.mbase + l);
+  const double P = fma(m, fma(m, fma(m, fma(m, T.c4, T.c3), T.c2), T.c1), T.c0);
+  const double v = P * T.invD;
+  float x = (float)(v - rint(v));  // frac in [-1/2, 1/2] cycles
+  float sigma = 1.f;
+  if (x > 0.25f) { x -= 0.5f; sigma = -1.f; }
+  else if (x < -0.25f) { x += 0.5f; sigma = -1.f; }
+  float sh, ch;
+  sincospi_q(x, sh, ch);
+  sn = sigma * (2.f * sh * ch);            // sin(theta)
+  al = sigma * fmaf(-4.f * sh, sh, 2.f);   // 2 cos(theta)
+}
+
+template <int NS, bool TWO>
+__device__ __forceinline__ void run_slots(const SgWTask& T, const AmpChunk& c0, const float* __restrict__ amps,
+                                          const SgSyllable* __restrict__ syls, const double* __restrict__ cknots,
+                                          float* __restrict__ W, int l0, int lane, float& tmax) {
+  float t[NS], al[NS], sn[NS], b1[NS], b2[NS], e1[NS], e2[NS];
+  int l[NS];
+  bool valid[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    l[s] = l0 + 64 * s + lane;
+    valid[s] = l[s] < T.len;
+    sample_setup<TWO>(T, valid[s] ? l[s] : 0, t[s], al[s], sn[s]);
+    b1[s] = b2[s] = e1[s] = e2[s] = 0.f;
+  }
+  if (T.R <= 64) {
+    clenshaw_chunk<NS, TWO>(c0, al, b1, b2, e1, e2);
+  } else {  // rare (subharmonic epochs with many rows): stream 64-row chunks, top first
+    for (int r0 = (T.R - 1) / 64 * 64; r0 >= 0; r0 -= 64) {
+      AmpChunk c;
+      load_chunk<TWO>(c, amps + T.a_off, amps + T.d_off, r0, T.R, lane);
+      clenshaw_chunk<NS, TWO>(c, al, b1, b2, e1, e2);
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const float y = (TWO ? fmaf(t[s], e1[s], b1[s]) : b1[s]) * sn[s];
+    if (valid[s]) {
+      const int j = T.j0 + l[s];
+      W[T.w_off + j] = y;
+      if (j >= T.dj0 && j < T.dj1) {
         float cand = y;
-        if (env) {
-          const SgSyllable& sy = syls[ep.syl];
-          cand = (float)((double)y * contour_at(sy.env, cknots, sy.L, ep.dk0 + j));
-        }
+        const SgSyllable& sy = syls[T.syl];
+        if (sy.env.kind != 0) cand = (float)((double)y * contour_at(sy.env, cknots, sy.L, T.dk0 + j));
         tmax = fmaxf(tmax, cand);
       }
     }
   }
-  // fused normalisation max over the direct-copy window
-  if (ep.dj1 > ep.dj0) {
-    __shared__ float red[4];
+}
+
+template <bool TWO>
+__device__ __forceinline__ float run_task(const SgWTask& T, const float* __restrict__ amps,
+                                          const SgSyllable* __restrict__ syls, const double* __restrict__ cknots,
+                                          float* __restrict__ W, int lane) {
+  AmpChunk c0;  // rows [0, 64) stay in registers for every slot of the task
+  if (T.R <= 64) load_chunk<TWO>(c0, amps + T.a_off, amps + T.d_off, 0, T.R, lane);
+  float tmax = 0.f;
+  int l0 = 0;
+#pragma unroll 1
+  for (; l0 + 64 < T.len; l0 += 128) run_slots<2, TWO>(T, c0, amps, syls, cknots, W, l0, lane, tmax);
+  if (l0 < T.len) run_slots<1, TWO>(T, c0, amps, syls, cknots, W, l0, lane, tmax);
+  return tmax;
+}
+
+extern "C" __global__ __launch_bounds__(256) void sg_sine_bank(
+    const SgWTask* __restrict__ tasks, int64_t ntasks, const float* __restrict__ amps,
+    const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, float* __restrict__ W,
+    float* __restrict__ taskmax) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t tbase = (int64_t)blockIdx.x * SG_TASKS_PER_BLOCK;
+#pragma unroll 1
+  for (int q = wave; q < SG_TASKS_PER_BLOCK; q += 4) {
+    const int64_t ti = tbase + q;
+    if (ti >= ntasks) break;
+    const SgWTask T = tasks[ti];
+    const float tmax = (T.flags & SG_TASK_CONST) ? run_task<false>(T, amps, syls, cknots, W, lane)
+                                                 : run_task<true>(T, amps, syls, cknots, W, lane);
     const float wm = wave_max(tmax);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = wm;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const float bm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-      if (bm > 0.f) atomicMax(maxes + syls[ep.syl].max_slot, __float_as_uint(bm));
-    }
+    if (lane == 0) taskmax[ti] = wm;
   }
+}
+
+// per-syllable max over its task slots and crossfade-piece slots
+extern "C" __global__ __launch_bounds__(256) void sg_syl_max(const SgSyllable* __restrict__ syls,
+                                                             const float* __restrict__ taskmax,
+                                                             const float* __restrict__ ptilemax,
+                                                             float* __restrict__ maxes) {
+  const SgSyllable& sy = syls[blockIdx.x];
+  float m = 0.f;
+  for (int64_t i = threadIdx.x; i < sy.ntask; i += 256) m = fmaxf(m, taskmax[sy.task0 + i]);
+  for (int i = threadIdx.x; i < sy.nptile; i += 256) m = fmaxf(m, ptilemax[sy.ptile0 + i]);
+  __shared__ float red[4];
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) maxes[sy.max_slot] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 
 namespace {
@@ -235,7 +268,7 @@ __device__ __forceinline__ float piece_value(const SgPiece& p, const float* __re
 // max over crossfade pieces (multi-term); tiles list (syl, piece, q0)
 extern "C" __global__ __launch_bounds__(256) void sg_piece_max(
     const SgSylTile* __restrict__ ptiles, const SgPiece* __restrict__ pieces, const SgSyllable* __restrict__ syls,
-    const double* __restrict__ cknots, const float* __restrict__ W, unsigned* __restrict__ maxes) {
+    const double* __restrict__ cknots, const float* __restrict__ W, float* __restrict__ ptilemax) {
   const SgSylTile tl = ptiles[blockIdx.x];
   const SgPiece& p = pieces[tl.piece];
   const SgSyllable& sy = syls[tl.syl];
@@ -250,8 +283,7 @@ extern "C" __global__ __launch_bounds__(256) void sg_piece_max(
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = wm;
   __syncthreads();
   if (threadIdx.x == 0) {
-    const float bm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    if (bm > 0.f) atomicMax(maxes + sy.max_slot, __float_as_uint(bm));
+    ptilemax[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   }
 }
 
@@ -269,11 +301,11 @@ __device__ __forceinline__ float fade_at(int lf, int64_t L, int64_t k) {
 
 extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize(
     const SgSylTile* __restrict__ stiles, const SgPiece* __restrict__ pieces, const SgSyllable* __restrict__ syls,
-    const double* __restrict__ cknots, const float* __restrict__ W, const unsigned* __restrict__ maxes,
+    const double* __restrict__ cknots, const float* __restrict__ W, const float* __restrict__ maxes,
     float* __restrict__ out) {
   const SgSylTile tl = stiles[blockIdx.x];
   const SgSyllable& sy = syls[tl.syl];
-  const float inv_max = 1.f / __uint_as_float(maxes[sy.max_slot]);
+  const float inv_max = 1.f / maxes[sy.max_slot];
   const int pend = sy.piece0 + sy.npiece;
   const int64_t kt = tl.k0 + 4 * (int64_t)threadIdx.x;
   const int64_t tile_end = tl.k0 + 1024 < sy.L ? tl.k0 + 1024 : sy.L;
@@ -320,19 +352,25 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize(
 // ---------------------------------------------------------------- launchers
 #include "sg_exec.h"
 namespace sg {
-void launch_sine_bank(const DevicePlan& D, int64_t n_tiles, hipStream_t s) {
-  if (n_tiles <= 0) return;
-  hipLaunchKernelGGL(sg_sine_bank, dim3((unsigned)n_tiles), dim3(256), 0, s, D.tiles, D.epochs, D.segs, D.knots,
-                     D.amps, D.syls, D.cknots, D.W, D.maxes);
+void launch_sine_bank(const DevicePlan& D, int64_t t0, int64_t n_tasks, hipStream_t s) {
+  if (n_tasks <= 0) return;
+  const int64_t blocks = (n_tasks + SG_TASKS_PER_BLOCK - 1) / SG_TASKS_PER_BLOCK;
+  hipLaunchKernelGGL(sg_sine_bank, dim3((unsigned)blocks), dim3(256), 0, s, D.tasks + t0, n_tasks, D.amps, D.syls,
+                     D.cknots, D.W, D.taskmax + t0);
 }
-void launch_piece_max(const DevicePlan& D, int64_t n_ptiles, hipStream_t s) {
+void launch_piece_max(const DevicePlan& D, int64_t p0, int64_t n_ptiles, hipStream_t s) {
   if (n_ptiles <= 0) return;
-  hipLaunchKernelGGL(sg_piece_max, dim3((unsigned)n_ptiles), dim3(256), 0, s, D.ptiles, D.pieces, D.syls, D.cknots,
-                     D.W, D.maxes);
+  hipLaunchKernelGGL(sg_piece_max, dim3((unsigned)n_ptiles), dim3(256), 0, s, D.ptiles + p0, D.pieces, D.syls,
+                     D.cknots, D.W, D.ptilemax + p0);
 }
-void launch_harm_finalize(const DevicePlan& D, int64_t n_stiles, float* out, hipStream_t s) {
+void launch_syl_max(const DevicePlan& D, int64_t s0, int64_t n_syls, hipStream_t s) {
+  if (n_syls <= 0) return;
+  hipLaunchKernelGGL(sg_syl_max, dim3((unsigned)n_syls), dim3(256), 0, s, D.syls + s0, D.taskmax, D.ptilemax,
+                     D.maxes);
+}
+void launch_harm_finalize(const DevicePlan& D, int64_t f0, int64_t n_stiles, float* out, hipStream_t s) {
   if (n_stiles <= 0) return;
-  hipLaunchKernelGGL(sg_harm_finalize, dim3((unsigned)n_stiles), dim3(256), 0, s, D.syl_tiles, D.pieces, D.syls,
+  hipLaunchKernelGGL(sg_harm_finalize, dim3((unsigned)n_stiles), dim3(256), 0, s, D.syl_tiles + f0, D.pieces, D.syls,
                      D.cknots, D.W, D.maxes, out);
 }
 }  // namespace sg

@@ -16,17 +16,27 @@ struct DeviceArrays;  // sg_api.cpp
 // FFT/OLA job of the noise source or the formant filter (seewave istft/stft)
 struct SgFftJob;
 
+// A slice of the batch (whole syllables) launched as one unit so that the
+// HBM-bound finalize of slice c overlaps the VALU-bound sine bank of c+1.
+struct Slice {
+  int64_t t0, t1;    // sine-bank tasks
+  int32_t p0, p1;    // crossfade-piece max tiles
+  int32_t s0, s1;    // syllables
+  int64_t f0, f1;    // finalize tiles
+};
+
 struct Batch {
   // ---- harmonic source ----
   std::vector<SgSeg> segs;
   std::vector<SgEpoch> epochs;
   std::vector<double> knots;
   std::vector<float> amps;
-  std::vector<SgTile> tiles;
+  std::vector<SgWTask> tasks;
   std::vector<SgPiece> pieces;
   std::vector<SgSyllable> syls;
   std::vector<SgSylTile> syl_tiles;
   std::vector<SgSylTile> ptiles;   // tiles over multi-term (crossfade) pieces
+  std::vector<Slice> slices;
   std::vector<double> cknots;   // contour / linear knot data
   int64_t w_total = 0;          // epoch-waveform scratch (floats)
   // ---- per call ----

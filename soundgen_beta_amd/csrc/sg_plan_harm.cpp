@@ -338,13 +338,20 @@ static std::vector<EpochMat> get_vocal_fry(const vec& roll, int64_t H, const vec
 }
 
 // ---------------------------------------------------- host evaluator
+// cubic piece of the upsampled pitch (host fp64 evaluator for the bookkeeping)
+struct HSeg {
+  double t0;
+  double prefix;
+  double y, b, c, d;
+};
+
 struct HostSyl {
-  std::vector<SgSeg> segs;
+  std::vector<HSeg> segs;
   double sr;
   double integr(int64_t u) const {  // cumsum(pitch_up)[u] / sr, u 1-based
     int64_t lo = 0, hi = (int64_t)segs.size() - 1;
     while (lo < hi) { int64_t m = (lo + hi + 1) / 2; if (segs[m].t0 < (double)u) lo = m; else hi = m - 1; }
-    const SgSeg& s = segs[lo];
+    const HSeg& s = segs[lo];
     const double m = (double)u - s.t0;
     const double S1 = m * (m + 1) / 2, S2 = m * (m + 1) * (2 * m + 1) / 6, S3 = S1 * S1;
     return (s.prefix + s.y * m + s.b * S1 + s.c * S2 + s.d * S3) / sr;
@@ -604,10 +611,10 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
   HostSyl HS;
   HS.sr = sr;
   if (nGC == 1) {
-    HS.segs.push_back(SgSeg{0, 0, ppg[0], 0, 0, 0});
+    HS.segs.push_back(HSeg{0, 0, ppg[0], 0, 0, 0});
   } else if (nGC == 2) {
     const double by = (ppg[1] - ppg[0]) / (double)(N - 1);
-    HS.segs.push_back(SgSeg{0, 0, ppg[0] - by, by, 0, 0});
+    HS.segs.push_back(HSeg{0, 0, ppg[0] - by, by, 0, 0});
   } else {
     vec t(nGC);
     t[0] = 1; t[nGC - 1] = (double)N;
@@ -615,7 +622,7 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
     Spline s = fmm_spline(t, ppg);
     long double pre = s.y[0];
     for (int64_t k = 0; k + 1 < nGC; ++k) {
-      HS.segs.push_back(SgSeg{t[k], (double)pre, s.y[k], s.b[k], s.c[k], s.d[k]});
+      HS.segs.push_back(HSeg{t[k], (double)pre, s.y[k], s.b[k], s.c[k], s.d[k]});
       const long double M = (long double)(t[k + 1] - t[k]);
       const long double S1 = M * (M + 1) / 2, S2 = M * (M + 1) * (2 * M + 1) / 6, S3 = S1 * S1;
       pre += s.y[k] * M + s.b[k] * S1 + s.c[k] * S2 + s.d[k] * S3;
@@ -660,7 +667,18 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
     B.cknots.insert(B.cknots.end(), drift.begin(), drift.end());
   }
   const int32_t seg_off = (int32_t)B.segs.size();
-  B.segs.insert(B.segs.end(), HS.segs.begin(), HS.segs.end());
+  for (const HSeg& h : HS.segs) {
+    // sum_{x=1..m} (y + b x + c x^2 + d x^3) = y m + b S1 + c S2 + d S3 expanded in powers of m
+    const long double y = h.y, b = h.b, c = h.c, d = h.d, isr = 1.0L / (long double)sr;
+    SgSeg g;
+    g.t0 = h.t0;
+    g.c0 = (double)((long double)h.prefix * isr);
+    g.c1 = (double)((y + b / 2 + c / 6) * isr);
+    g.c2 = (double)((b / 2 + c / 2 + d / 4) * isr);
+    g.c3 = (double)((c / 3 + d / 2) * isr);
+    g.c4 = (double)((d / 4) * isr);
+    B.segs.push_back(g);
+  }
   std::vector<int32_t> ep_index(mats.size());
   // destination offset of each epoch's direct piece, to keep the fp32 copy
   // in the finalize kernel 16-byte aligned on both sides
@@ -677,20 +695,25 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
     B.w_total += he.n;
     d.n = (int32_t)he.n;
     d.G = (int32_t)he.G;
-    d.R = (int32_t)((m.R + 7) / 8 * 8);
+    d.R = (int32_t)((m.R + SG_ROW_CHUNK - 1) / SG_ROW_CHUNK * SG_ROW_CHUNK);
     d.u0 = (int32_t)he.u0;
     d.seg_off = seg_off;
     d.nseg = (int32_t)HS.segs.size();
     d.x1 = he.knots.front();
     d.xG = he.knots.back();
     d.xby = he.n > 1 ? (d.xG - d.x1) / (double)(he.n - 1) : 0.0;
-    d.inv_srD = 1.0 / (sr * (double)m.D);
+    d.invD = 1.0 / (double)m.D;
     d.knot_off = (int64_t)B.knots.size();
     B.knots.insert(B.knots.end(), he.knots.begin(), he.knots.end());
+    // [G][R] amplitudes then [G-1][R] column differences, 64-B aligned rows
     d.amp_off = (int64_t)B.amps.size();
-    B.amps.resize(B.amps.size() + (size_t)d.G * d.R, 0.0f);
+    d.da_off = d.amp_off + (int64_t)d.G * d.R;
+    B.amps.resize(B.amps.size() + (size_t)(2 * d.G - 1) * d.R, 0.0f);
     for (int64_t g = 0; g < he.G; ++g)
       for (int64_t r = 0; r < m.R; ++r) B.amps[d.amp_off + g * d.R + r] = (float)m.A[g * m.R + r];
+    for (int64_t g = 0; g + 1 < he.G; ++g)
+      for (int64_t r = 0; r < m.R; ++r)
+        B.amps[d.da_off + g * d.R + r] = B.amps[d.amp_off + (g + 1) * d.R + r] - B.amps[d.amp_off + g * d.R + r];
     d.syl = syl_idx;
     d.dj0 = d.dj1 = 0;
     d.dk0 = 0;
@@ -698,7 +721,7 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
     B.epochs.push_back(d);
     B.harm_samples += he.n;
     B.harm_terms += he.n * (int64_t)d.R;
-    B.harm_amp_bytes += (int64_t)d.G * d.R * 4;
+    B.harm_amp_bytes += (int64_t)(2 * d.G - 1) * d.R * 4;
   }
   // pieces; the single full-weight piece of each epoch becomes its direct window
   sy.piece0 = (int32_t)B.pieces.size();
@@ -726,20 +749,73 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
   }
   sy.npiece = (int32_t)(B.pieces.size() - sy.piece0);
   B.syls.push_back(sy);
-  // sine-bank tiles: 256 samples each
-  constexpr int TILE = SG_SINE_TILE;
+  // sine-bank wave tasks: <= SG_TASK_MAX samples inside one amplitude
+  // interval, or inside a run of intervals with equal columns
+  B.syls.back().task0 = (int64_t)B.tasks.size();
+  const int64_t nseg = (int64_t)HS.segs.size();
   for (size_t e = 0; e < mats.size(); ++e) {
     const HostEpoch& he = HE[e];
-    int64_t i = 0;
+    const SgEpoch& ep = B.epochs[ep_index[e]];
+    // sample boundaries of the intervals: jb[i] = first j with xout_j >= knot i+1
+    std::vector<int64_t> jb(he.G - 1);
+    std::vector<char> cst(he.G - 1);
+    int64_t ja = 0;
+    for (int64_t i = 0; i + 1 < he.G; ++i) {
+      int64_t g = he.n;
+      if (i + 2 < he.G) {
+        const double xb = he.knots[i + 1];
+        g = (int64_t)std::floor((xb - he.knots.front()) / ep.xby);
+        if (g < ja) g = ja;
+        if (g > he.n) g = he.n;
+        while (g > ja && r_seqint_at(he.knots.front(), he.knots.back(), he.n, g - 1) >= xb) --g;
+        while (g < he.n && r_seqint_at(he.knots.front(), he.knots.back(), he.n, g) < xb) ++g;
+      }
+      jb[i] = g;
+      ja = g;
+      bool c = true;
+      for (int64_t r = 0; r < ep.R && c; ++r) c = B.amps[ep.da_off + i * ep.R + r] == 0.0f;
+      cst[i] = c;
+    }
     int64_t k = 0;
-    for (int64_t j0 = 0; j0 < he.n; j0 += TILE) {
-      const double v = r_seqint_at(he.knots.front(), he.knots.back(), he.n, j0);
-      while (i < he.G - 2 && he.knots[i + 1] <= v) ++i;
-      const double u = (double)(he.u0 + j0);
-      while (k + 1 < (int64_t)HS.segs.size() && HS.segs[k + 1].t0 < u) ++k;
-      B.tiles.push_back(SgTile{ep_index[e], (int32_t)j0, (int32_t)i, (int32_t)k});
+    ja = 0;
+    for (int64_t i = 0; i + 1 < he.G;) {
+      int64_t i1 = i + 1;  // span [i, i1) of intervals
+      if (cst[i])
+        while (i1 + 1 < he.G && cst[i1]) ++i1;
+      const int64_t jend = jb[i1 - 1];
+      for (int64_t j0 = ja; j0 < jend;) {
+        const double u = (double)(he.u0 + j0);
+        while (k + 1 < nseg && HS.segs[k + 1].t0 < u) ++k;
+        int64_t len = std::min<int64_t>(SG_TASK_MAX, jend - j0);
+        if (k + 1 < nseg) {  // stay inside segment k: u <= t0[k+1]
+          const int64_t jmax = (int64_t)HS.segs[k + 1].t0 - he.u0 + 1;
+          if (j0 + len > jmax) len = jmax - j0;
+        }
+        const SgSeg& S = B.segs[seg_off + k];
+        SgWTask T{};
+        T.w_off = ep.w_off;
+        T.a_off = ep.amp_off + i * ep.R;
+        T.d_off = ep.da_off + i * ep.R;
+        T.dk0 = ep.dk0;
+        T.c0 = S.c0; T.c1 = S.c1; T.c2 = S.c2; T.c3 = S.c3; T.c4 = S.c4;
+        T.invD = ep.invD;
+        T.rdx = (float)(1.0 / (he.knots[i + 1] - he.knots[i]));
+        T.tc0 = (float)(r_seqint_at(he.knots.front(), he.knots.back(), he.n, j0) - he.knots[i]);
+        T.xby = (float)ep.xby;
+        T.mbase = (int32_t)((double)(he.u0 + j0) - S.t0);
+        T.R = ep.R;
+        T.j0 = (int32_t)j0; T.len = (int32_t)len;
+        T.dj0 = ep.dj0; T.dj1 = ep.dj1;
+        T.syl = ep.syl;
+        T.flags = cst[i] ? SG_TASK_CONST : 0;
+        B.tasks.push_back(T);
+        j0 += len;
+      }
+      ja = jend;
+      i = i1;
     }
   }
+  B.syls.back().ntask = (int32_t)((int64_t)B.tasks.size() - B.syls.back().task0);
   return Lsyl;
 }
 
