@@ -1,0 +1,291 @@
+"""TEST INFRASTRUCTURE — an independent NumPy restatement of the simple
+(temperature = 0, nonlinBalance = 0) generateHarmonics() path and of the R /
+seewave numerics it relies on, written from the reference R sources, used to
+cross-check the C oracle (oracle/sg_oracle.c) inside this container where R
+itself is absent (parity vs R is unpinned).
+
+Reference lines followed:
+  getGlottalCycles   R/utilities_soundgen.R:477-486
+  upsample           R/utilities_soundgen.R:392-416
+  findZeroCrossing   R/utilities_soundgen.R:255-295
+  crossFade          R/utilities_soundgen.R:328-375
+  fadeInOut          R/utilities_soundgen.R:440-459
+  getRolloff         R/sourceSpectrum.R:71-186
+  generateHarmonics  R/source.R:173-471 (the deterministic branch)
+  seewave stft/istft seewave_2.0.5.tar.gz::seewave/R/seewave.r:7782-7819, :3447-3486
+"""
+import numpy as np
+
+
+def seq_len(a, b, n):
+    """seq(a, b, length.out = n) — R seq.default."""
+    if n <= 0:
+        return np.zeros(0)
+    if n == 1:
+        return np.array([float(a)])
+    if a == b:
+        return np.full(n, float(a))
+    by = (b - a) / (n - 1)
+    out = a + np.arange(n) * by
+    out[-1] = b
+    return out
+
+
+def seqint_len(a, b, n):
+    """seq.int(a, b, length.out = n) — R's C seq.int (symmetric interior)."""
+    i = np.arange(n, dtype=np.float64)
+    if n == 1:
+        return np.array([float(a)])
+    by = (b - a) / (n - 1)
+    out = np.where(i < n // 2, a + i * by, b - (n - 1 - i) * by)
+    out[0], out[-1] = a, b
+    return out
+
+
+def r_round(x):
+    return np.rint(x)  # half to even, as R's round(x, 0)
+
+
+def glottal_cycles(pitch, sr):
+    gc, i = [], 1
+    while i < len(pitch):
+        gc.append(i)
+        i = i + max(2, int(np.floor(sr / pitch[i - 1])))
+    return np.array(gc, dtype=np.int64)
+
+
+def fmm_coef(x, y):
+    """Forsythe-Malcolm-Moler cubic spline (end conditions from cubics through
+    the first / last four points), tridiagonal solve."""
+    n = len(x)
+    x = np.asarray(x, float)
+    y = np.asarray(y, float)
+    b, c, d = np.zeros(n), np.zeros(n), np.zeros(n)
+    if n < 3:
+        t = (y[1] - y[0]) / (x[1] - x[0])
+        b[:] = t
+        return b, c, d
+    h = np.diff(x)
+    dy = np.diff(y) / h
+    diag = np.zeros(n)
+    rhs = np.zeros(n)
+    diag[0], diag[-1] = -h[0], -h[-1]
+    diag[1:-1] = 2 * (h[:-1] + h[1:])
+    rhs[1:-1] = dy[1:] - dy[:-1]
+    if n > 3:
+        rhs[0] = (dy[2] - dy[1]) / (x[3] - x[1]) - (dy[1] - dy[0]) / (x[2] - x[0])
+        rhs[0] = rhs[0] * h[0] ** 2 / (x[3] - x[0])
+        rhs[-1] = (dy[-1] - dy[-2]) / (x[-1] - x[-3]) - (dy[-2] - dy[-3]) / (x[-2] - x[-4])
+        rhs[-1] = -rhs[-1] * h[-1] ** 2 / (x[-1] - x[-4])
+    # forward elimination (sub = super = h)
+    dd = diag.copy()
+    r = rhs.copy()
+    for i in range(1, n):
+        t = h[i - 1] / dd[i - 1]
+        dd[i] -= t * h[i - 1]
+        r[i] -= t * r[i - 1]
+    sig = np.zeros(n)
+    sig[-1] = r[-1] / dd[-1]
+    for i in range(n - 2, -1, -1):
+        sig[i] = (r[i] - h[i] * sig[i + 1]) / dd[i]
+    b[-1] = dy[-1] + h[-1] * (sig[-2] + 2 * sig[-1])
+    b[:-1] = dy - h * (sig[1:] + 2 * sig[:-1])
+    d[:-1] = (sig[1:] - sig[:-1]) / h
+    c = 3 * sig
+    d[-1] = d[-2]
+    return b, c, d
+
+
+def spline(x, y, n):
+    """spline(x, y, n = n)$y with method 'fmm'."""
+    x = np.asarray(x, float)
+    y = np.asarray(y, float)
+    b, c, d = fmm_coef(x, y)
+    u = seqint_len(x[0], x[-1], n)
+    i = np.clip(np.searchsorted(x, u, side="right") - 1, 0, len(x) - 1)
+    dx = u - x[i]
+    return y[i] + dx * (b[i] + dx * (c[i] + dx * d[i]))
+
+
+def approx(x, y, n):
+    """approx(x, y, n = n)$y, linear, rule = 1."""
+    x = np.asarray(x, float)
+    y = np.asarray(y, float)
+    v = seqint_len(x[0], x[-1], n)
+    j = np.clip(np.searchsorted(x, v, side="right"), 1, len(x) - 1)
+    i = j - 1
+    out = y[i] + (y[j] - y[i]) * ((v - x[i]) / (x[j] - x[i]))
+    out = np.where(v == x[j], y[j], out)
+    out = np.where(v == x[i], y[i], out)
+    return out
+
+
+def upsample(ppg, sr):
+    gcl = r_round(sr / np.asarray(ppg, float))
+    c = np.cumsum(gcl)
+    gc_up = np.concatenate([[1.0], c])
+    l = len(ppg)
+    if l == 1:
+        pu = np.repeat(ppg, gcl.astype(int))
+    elif l == 2:
+        pu = seq_len(ppg[0], ppg[1], int(c[-1]))
+    else:
+        t = np.ones(l)
+        t[-1] = c[-1]
+        for i in range(2, l):
+            t[i - 1] = c[i - 2] + r_round(gcl[i - 1] / 2)
+        pu = spline(t, ppg, int(c[-1]))
+    return pu, gc_up
+
+
+def get_rolloff(pitch, nH, rolloff=-12, rolloffOct=-2, rolloffKHz=-6, baseline=200, throwaway=-120, sr=16000,
+                rolloffParab=0, rolloffParabHarm=2):
+    pitch = np.atleast_1d(np.asarray(pitch, float))
+    h = np.arange(1, nH + 1)[:, None]
+    r = (rolloff + rolloffKHz * (pitch[None, :] - baseline) / 1000) * np.log2(h)
+    if rolloffOct != 0:
+        r = r + np.where(h >= 2, rolloffOct * (pitch[None, :] * h - baseline) / 1000, 0.0)
+    r = np.where(h * pitch[None, :] >= sr / 2, -np.inf, r)
+    if rolloffParab != 0:
+        rph = r_round(rolloffParabHarm)
+        if rph == 2:
+            rph = 3
+        with np.errstate(divide="ignore"):
+            a = -4 * rolloffParab / (rph - 1) ** 2
+        b = -a * (1 + rph)
+        c = a * rph
+        if rph < 3:
+            if rph < 2:
+                r[0] = r[0] + rolloffParab
+        else:
+            k = np.arange(1, int(rph) + 1)[:, None]
+            r[:int(rph)] = r[:int(rph)] + a * k ** 2 + b * k + c
+    r = np.where(r < throwaway, -np.inf, r)
+    r = r - r.max(axis=0, keepdims=True)
+    r = 2.0 ** (r / 10)
+    keep = r.sum(axis=1) > 0
+    return r[keep]
+
+
+def find_zero_crossing(a, location):
+    n = len(a)
+    if n < 1 or location < 1 or location > n:
+        return None
+    if n == 1 and location == 1:
+        return location
+    zl = zr = None
+    i = 0
+    if location > 1:
+        i = location
+        while i > 1:
+            if a[i - 1] > 0 and a[i - 2] < 0:
+                zl = i - 1
+                break
+            i -= 1
+    if location < n:
+        i = location
+    while i < n - 1:
+        if a[i] > 0 and a[i - 1] < 0:
+            zr = i
+            break
+        i += 1
+    if zl is None and zr is None:
+        return None
+    if zl is None:
+        return zr
+    if zr is None:
+        return zl
+    return zl if abs(zl - location) <= abs(zr - location) else zr
+
+
+def cross_fade(a1, a2, sr, crossLen=15):
+    a1 = np.asarray(a1, float)
+    a2 = np.asarray(a2, float)
+    z1 = find_zero_crossing(a1, len(a1))
+    if z1 is not None:
+        a1 = np.concatenate([a1[:z1], [0.0]])
+    z2 = find_zero_crossing(a2, 1)
+    if z2 is not None:
+        a2 = a2[z2:]
+    cl = int(min(np.floor(crossLen * sr / 1000), len(a1) - 1, len(a2) - 1))
+    if cl < 2:
+        return np.concatenate([a1, a2])
+    m = seq_len(0, 1, cl)
+    idx1 = len(a1) - cl
+    cross = m[::-1] * a1[idx1:] + m * a2[:cl]
+    return np.concatenate([a1[:idx1], cross, a2[cl:]])
+
+
+def fade_in_out(a, length_fade):
+    a = np.array(a, float)
+    if length_fade < 2:
+        return a
+    lf = int(min(length_fade, len(a)))
+    f = seq_len(0, 1, lf)
+    a[:lf] *= f
+    a[len(a) - lf:] *= f[::-1]
+    return a
+
+
+def generate_harmonics_simple(pitch, sr=16000, attackLen=50, rolloff=-18, rolloffOct=-2, rolloffKHz=-6,
+                              pitchFloor=75, pitchCeiling=3500, psr=3500, throwaway=-120, **_):
+    """generateHarmonics() with temperature = 0, nonlinBalance = 0, no vibrato,
+    no amplAnchors: one epoch, sine bank, crossFade onto 0, /max, fade."""
+    pitch = np.asarray(pitch, float)
+    gc = glottal_cycles(pitch, psr)
+    ppg = np.clip(pitch[gc - 1], pitchFloor, pitchCeiling)
+    nH = int(np.ceil((sr / 2 - ppg.min()) / ppg.min()))
+    A = get_rolloff(ppg, nH, rolloff, rolloffOct, rolloffKHz, 200, throwaway, sr)
+    pu, gc_up = upsample(ppg, sr)
+    acc, s = np.zeros(len(pu)), 0.0
+    # cumsum in extended precision, as R's cumsum (long double accumulator)
+    acc = np.cumsum(pu.astype(np.longdouble)).astype(np.float64)
+    integr = acc / sr
+    idx = gc_up  # epoch = all gcs: idx_gc_up = gc_up[1:(nGC+1)]
+    lo, hi = int(idx.min()), int(idx.max())
+    ie = integr[lo - 1:hi]
+    n = len(ie)
+    w = np.zeros(n)
+    for h in range(A.shape[0]):
+        am = approx(idx[:-1], A[h], n)
+        w = w + np.sin(2 * np.pi * ie * (h + 1)) * am
+    wave = cross_fade(np.array([0.0]), w, sr, 15)
+    wave = wave / wave.max()
+    if attackLen > 0:
+        wave = fade_in_out(wave, np.floor(attackLen * sr / 1000))
+    return wave
+
+
+def hamming(n):
+    return 0.54 - 0.46 * np.cos(2 * np.pi * np.arange(n) / (n - 1))
+
+
+def hanning(n):
+    return 0.5 - 0.5 * np.cos(2 * np.pi * np.arange(n) / (n - 1))
+
+
+def stft(wave, wl, step):
+    """seewave::stft(wave, wl, step, wn = 'hamming', complex = TRUE): nr x nc."""
+    w = hamming(wl)
+    cols = []
+    for x0 in step:
+        i0 = int(x0) - 1
+        cols.append(np.fft.fft(wave[i0:i0 + wl] * w)[: wl // 2] / wl)
+    return np.array(cols).T
+
+
+def istft(z, ovlp, wl):
+    """seewave::istft(z, ovlp, wl, wn = 'hanning') incl. the Nyquist quirk."""
+    nr, nc = z.shape
+    h = wl * (100 - ovlp) / 100
+    x = np.zeros(int(wl + (nc - 1) * h))
+    win = hanning(wl)
+    for f in range(nc):
+        X = np.concatenate([z[:, f], [np.real(z[nr - 1, f])], np.conj(z[1:, f][::-1])])
+        y = np.real(np.fft.ifft(X)) * wl / wl  # R: Re(fft(X, inverse = TRUE)) / wl
+        b = f * h
+        i0 = int(b)
+        seg = y * win
+        end = min(len(x), i0 + wl)
+        x[i0:end] += seg[: end - i0]
+    return x * h / np.sum(win ** 2)
