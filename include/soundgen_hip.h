@@ -62,12 +62,21 @@ typedef struct sg_formants {
   const double* width;
 } sg_formants;
 
-/* Injected random streams (R's rnorm()/runif() draw order). */
+/* Random draws, consumed in the reference's draw order: standard normals
+ * (rnorm), standard uniforms (runif) and gamma variates (rgamma). The arrays
+ * are used first; once one is exhausted (or NULL) the matching callback is
+ * called if set, else the call fails with SG_E_RANDOM. The R shim binds the
+ * callbacks to R's own norm_rand()/unif_rand()/rgamma() so that draws follow
+ * set.seed() exactly; tests inject arrays. */
 typedef struct sg_random {
   const double* normals;
   int64_t n_normals;
   const double* uniforms;
   int64_t n_uniforms;
+  double (*norm_cb)(void* user);
+  double (*unif_cb)(void* user);
+  double (*gamma_cb)(void* user, double shape, double rate);
+  void* user;
 } sg_random;
 
 /* Formals of generateHarmonics(), R/source.R:173-205 (pitch and amplAnchors
@@ -161,6 +170,12 @@ int sg_execute(sg_ctx* ctx, sg_plan* plan, float* d_out, void* stream);
 int sg_set_profiling(sg_ctx* ctx, int on);
 int sg_profile_read(sg_ctx* ctx, double* sine_ms_avg, int64_t* n);
 int sg_synchronize(sg_ctx* ctx);
+/* Synchronous convenience: upload (if needed), execute and copy the packed
+ * output to host doubles: call i's samples land at out_host + offset[i]
+ * (sg_plan_lengths), sg_plan_total_samples(plan) doubles in all. Random draws
+ * happen only in sg_plan_batch, so a caller can size its buffer from the plan
+ * before any sample is produced. */
+int sg_execute_to_host(sg_ctx* ctx, sg_plan* plan, double* out_host);
 /* Message of a failed call (status != 0). */
 const char* sg_plan_call_message(const sg_plan* plan, int64_t i);
 /* Per-kernel launch statistics of the last sg_execute (for roofline). */

@@ -85,11 +85,11 @@ def _f64(a):
     return np.ascontiguousarray(np.asarray(a, dtype=np.float64))
 
 
-def generate_harmonics(pitch, amplAnchors=None, normals=None, uniforms=None, **kw):
+def generate_harmonics(pitch, amplAnchors=None, normals=None, uniforms=None, rng=None, **kw):
     h = rargs.Holder()
     p = rargs.fill_harm_params(kw)
     pitch = h.arr(pitch)
-    rnd = h.random(normals, uniforms)
+    rnd = h.random(normals, uniforms, rng)
     out = C.POINTER(C.c_double)()
     n = C.c_int64()
     _check(lib().or_generate_harmonics(_abi.dptr(pitch), len(pitch), C.byref(p),
@@ -98,10 +98,10 @@ def generate_harmonics(pitch, amplAnchors=None, normals=None, uniforms=None, **k
     return _take(out, n.value)
 
 
-def soundgen(normals=None, uniforms=None, **kw):
+def soundgen(normals=None, uniforms=None, rng=None, **kw):
     h = rargs.Holder()
     a = rargs.fill_soundgen_args(h, kw)
-    rnd = h.random(normals, uniforms)
+    rnd = h.random(normals, uniforms, rng)
     out = C.POINTER(C.c_double)()
     n = C.c_int64()
     _check(lib().or_soundgen(C.byref(a), C.byref(rnd), C.byref(out), C.byref(n)))

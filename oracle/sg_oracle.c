@@ -67,12 +67,14 @@ static void dv_append_zeros(dv* a, int64_t n) {
 /* ------------------------------------------------------------------ random */
 typedef struct { const sg_random* s; int64_t in, iu; } rng_t;
 static int rng_norm(rng_t* r, double* z) {
-  if (!r || !r->s || r->in >= r->s->n_normals) return fail(SG_E_RANDOM, "normal stream exhausted");
-  *z = r->s->normals[r->in++]; return 0;
+  if (r && r->s && r->in < r->s->n_normals) { *z = r->s->normals[r->in++]; return 0; }
+  if (r && r->s && r->s->norm_cb) { *z = r->s->norm_cb(r->s->user); return 0; }
+  return fail(SG_E_RANDOM, "normal stream exhausted");
 }
 static int rng_unif(rng_t* r, double* u) {
-  if (!r || !r->s || r->iu >= r->s->n_uniforms) return fail(SG_E_RANDOM, "uniform stream exhausted");
-  *u = r->s->uniforms[r->iu++]; return 0;
+  if (r && r->s && r->iu < r->s->n_uniforms) { *u = r->s->uniforms[r->iu++]; return 0; }
+  if (r && r->s && r->s->unif_cb) { *u = r->s->unif_cb(r->s->user); return 0; }
+  return fail(SG_E_RANDOM, "uniform stream exhausted");
 }
 /* R rnorm(1, mu, sd): no draw when sd == 0 (nmath/rnorm.c) */
 static int r_rnorm1(rng_t* r, double mu, double sd, double* out) {
@@ -83,6 +85,7 @@ static int r_rnorm1(rng_t* r, double mu, double sd, double* out) {
 /* rgamma(1, shape, rate): Marsaglia-Tsang on the injected streams. */
 static int r_rgamma1(rng_t* r, double shape, double rate, double* out) {
   if (!(shape > 0) || !(rate > 0)) { *out = NAN; return 0; }
+  if (r && r->s && r->s->gamma_cb) { *out = r->s->gamma_cb(r->s->user, shape, rate); return 0; }
   double boost = 1.0, a = shape;
   if (a < 1.0) {
     double u; int rc = rng_unif(r, &u); if (rc) return rc;

@@ -1,0 +1,50 @@
+# soundgen_hip.R — R-side wrappers a maintainer drops into the reference
+# package (nemochina2008/soundgen_beta) to route its hot path through
+# libsoundgen_hip.so. Formals and defaults are the reference's own; only the
+# bodies change (see INTEGRATION.md). Not run in this repository (no R).
+
+# R/source.R:173-205
+generateHarmonics = function(pitch, attackLen = 50, nonlinBalance = 0, nonlinDep = 0, jitterDep = 0,
+                             jitterLen = 1, vibratoFreq = 100, vibratoDep = 0, shimmerDep = 0,
+                             creakyBreathy = 0, rolloff = -18, rolloffOct = -2, rolloffKHz = -6,
+                             rolloffParab = 0, rolloffParabHarm = 3, rolloffLip = 6, rolloff_perAmpl = 12,
+                             temperature = 0, pitchDriftDep = .5, pitchDriftFreq = .125,
+                             randomWalk_trendStrength = .5, shortestEpoch = 300, subFreq = 100,
+                             subDep = 0, amDep = 0, amFreq = 30, amplAnchors = NA, overlap = 75,
+                             samplingRate = 16000, pitchFloor = 75, pitchCeiling = 3500,
+                             pitchSamplingRate = 3500, throwaway = -120) {
+  pars = as.list(environment())
+  pars$pitch = NULL
+  pars$amplAnchors = NULL
+  aa = if (is.data.frame(amplAnchors)) amplAnchors[, c('time', 'value')] else NULL
+  .Call(C_sg_generate_harmonics, as.double(pitch), pars, aa)
+}
+
+# formants list(f1 = data.frame(time, freq, amp, width), ...) -> flat arrays
+.sg_flatten_formants = function(formants) {
+  if (!is.list(formants) || length(formants) == 0) return(NULL)
+  fs = lapply(formants, as.data.frame)
+  list(n_points = as.integer(sapply(fs, nrow)),
+       f1_index = if ('f1' %in% names(fs)) match('f1', names(fs)) - 1L else -1L,
+       time = as.double(unlist(lapply(fs, function(f) f$time))),
+       freq = as.double(unlist(lapply(fs, function(f) f$freq))),
+       amp = as.double(unlist(lapply(fs, function(f) f$amp))),
+       width = as.double(unlist(lapply(fs, function(f) f$width))))
+}
+
+# R/soundgen.R:208: same formals; the body keeps the reference's argument
+# coercions (R/soundgen.R:305-315, :384-389) and hands the call to the device.
+soundgen_hip = function(...) {
+  a = list(...)
+  if (is.character(a$formants)) a$formants = convertStringToFormants(a$formants)
+  if (is.character(a$formantsNoise)) a$formantsNoise = convertStringToFormants(a$formantsNoise)
+  for (nm in c('pitchAnchors', 'pitchAnchorsGlobal', 'noiseAnchors', 'mouthAnchors', 'amplAnchors',
+               'amplAnchorsGlobal')) {
+    v = a[[nm]]
+    if (is.numeric(v)) a[[nm]] = data.frame(time = seq(0, 1, length.out = length(v)), value = v)
+  }
+  a$formants_flat = .sg_flatten_formants(a$formants)
+  a$formantsNoise_flat = .sg_flatten_formants(a$formantsNoise)
+  a$formants = a$formantsNoise = NULL
+  .Call(C_sg_soundgen, a)
+}

@@ -1,0 +1,226 @@
+/*
+ * sg_r_shim.c — the thin .Call shim a maintainer adds to the reference R
+ * package (nemochina2008/soundgen_beta, soundgen 1.0.0) so that its hot path
+ * runs in libsoundgen_hip.so. Compiled only where R headers exist (R CMD
+ * INSTALL with r/src/Makevars); it is not built in this repository's CI
+ * (R is absent from the build image).
+ *
+ * Entry points (reference call sites they replace):
+ *   C_sg_generate_harmonics  R/source.R:173-471     (do.call(generateHarmonics, ...) at R/soundgen.R:616-620)
+ *   C_sg_soundgen            R/soundgen.R:208-862
+ *   C_sg_generate_noise      R/source.R:57-138      (R/soundgen.R:686-696)
+ *   C_sg_formant_filter      R/soundgen.R:743-807   (seewave::stft x env -> seewave::istft)
+ *
+ * Randomness: the sg_random callbacks are bound to R's own norm_rand(),
+ * unif_rand() and rgamma() between GetRNGstate()/PutRNGstate(), so a
+ * set.seed() before the call reproduces the reference's draws in its order.
+ * Errors: a negative SG_E_* status becomes Rf_error(sg_last_error()) after
+ * every device buffer of the call has been released (the library frees them
+ * before returning); no C++ exception crosses the C ABI.
+ */
+#include <R.h>
+#include <Rinternals.h>
+#include <R_ext/Random.h>
+#include <R_ext/Rdynload.h>
+#include <Rmath.h>
+#include <string.h>
+
+#include "soundgen_hip.h"
+
+static sg_ctx* g_ctx = NULL;
+
+static sg_ctx* ctx(void) {
+  if (!g_ctx && sg_ctx_create(0, &g_ctx) != SG_OK) Rf_error("soundgen_hip: no usable MI355X (sg_ctx_create failed)");
+  return g_ctx;
+}
+
+static double cb_norm(void* u) { (void)u; return norm_rand(); }
+static double cb_unif(void* u) { (void)u; return unif_rand(); }
+static double cb_gamma(void* u, double shape, double rate) { (void)u; return rgamma(shape, 1.0 / rate); }
+
+static sg_random r_rng(void) {
+  sg_random r;
+  memset(&r, 0, sizeof r);
+  r.norm_cb = cb_norm;
+  r.unif_cb = cb_unif;
+  r.gamma_cb = cb_gamma;
+  return r;
+}
+
+static double num(SEXP list, const char* name, double dflt) {
+  SEXP nms = Rf_getAttrib(list, R_NamesSymbol);
+  for (R_xlen_t i = 0; i < Rf_xlength(list); ++i)
+    if (!strcmp(CHAR(STRING_ELT(nms, i)), name)) {
+      SEXP v = VECTOR_ELT(list, i);
+      return (Rf_isNull(v) || Rf_xlength(v) < 1) ? NA_REAL : Rf_asReal(v);
+    }
+  return dflt;
+}
+
+/* data.frame(time, value) or NULL/NA -> sg_anchors (views into R memory) */
+static sg_anchors anchors(SEXP df) {
+  sg_anchors a = {0, NULL, NULL};
+  if (!Rf_isNewList(df) || Rf_xlength(df) < 2) return a;
+  SEXP t = VECTOR_ELT(df, 0), v = VECTOR_ELT(df, 1);
+  if (TYPEOF(t) != REALSXP || TYPEOF(v) != REALSXP) Rf_error("anchors must be numeric data.frame(time, value)");
+  a.n = (int32_t)Rf_xlength(t);
+  a.time = REAL(t);
+  a.value = REAL(v);
+  return a;
+}
+
+static void check(int rc) {
+  if (rc < 0) Rf_error("soundgen_hip: %s", sg_last_error(g_ctx));
+}
+
+/* plan (every random draw happens here, once, on R's RNG), size the R
+ * vector from the plan, then run the device path */
+static SEXP run_planned(const sg_call_desc* d) {
+  sg_plan* plan = NULL;
+  GetRNGstate();
+  int rc = sg_plan_batch(ctx(), d, 1, &plan);
+  PutRNGstate();
+  check(rc);
+  int32_t st = 0;
+  sg_plan_status(plan, &st);
+  if (st) {
+    char msg[512];
+    snprintf(msg, sizeof msg, "%s", sg_plan_call_message(plan, 0));
+    sg_plan_destroy(plan);
+    Rf_error("soundgen_hip: %s", msg);
+  }
+  int64_t len = 0, off = 0;
+  sg_plan_lengths(plan, &len, &off);
+  SEXP out = PROTECT(Rf_allocVector(REALSXP, sg_plan_total_samples(plan) > 0 ? sg_plan_total_samples(plan) : 1));
+  rc = sg_execute_to_host(ctx(), plan, REAL(out));
+  sg_plan_destroy(plan);
+  check(rc);
+  out = Rf_xlengthgets(out, len);
+  UNPROTECT(1);
+  return out;
+}
+
+/* generateHarmonics(pitch, <formals as a named list>, amplAnchors) */
+SEXP C_sg_generate_harmonics(SEXP pitch, SEXP pars, SEXP amplAnchors) {
+  if (TYPEOF(pitch) != REALSXP) Rf_error("pitch must be double");
+  sg_harm_params p;
+  sg_default_harm_params(&p);
+#define F(nm) p.nm = num(pars, #nm, p.nm)
+  F(attackLen); F(nonlinBalance); F(nonlinDep); F(jitterDep); F(jitterLen); F(vibratoFreq); F(vibratoDep);
+  F(shimmerDep); F(creakyBreathy); F(rolloff); F(rolloffOct); F(rolloffKHz); F(rolloffParab);
+  F(rolloffParabHarm); F(rolloffLip); F(rolloff_perAmpl); F(temperature); F(pitchDriftDep); F(pitchDriftFreq);
+  F(randomWalk_trendStrength); F(shortestEpoch); F(subFreq); F(subDep); F(amDep); F(amFreq); F(overlap);
+  F(samplingRate); F(pitchFloor); F(pitchCeiling); F(pitchSamplingRate); F(throwaway);
+#undef F
+  sg_call_desc d;
+  memset(&d, 0, sizeof d);
+  d.kind = SG_CALL_HARMONICS;
+  d.pitch = REAL(pitch);
+  d.pitch_len = Rf_xlength(pitch);
+  d.harm = &p;
+  d.amplAnchors = anchors(amplAnchors);
+  d.random = r_rng();
+  return run_planned(&d);
+}
+
+/* soundgen(...) with the formals of R/soundgen.R:208-277 already resolved by
+ * the R wrapper (anchors as data.frames, formants as lists of data.frames) */
+SEXP C_sg_soundgen(SEXP args) {
+  sg_soundgen_args a;
+  sg_default_soundgen_args(&a);
+#define F(nm) a.nm = num(args, #nm, a.nm)
+  F(repeatBout); F(nSyl); F(sylLen); F(pauseLen); F(temperature); F(maleFemale); F(creakyBreathy);
+  F(nonlinBalance); F(nonlinDep); F(jitterLen); F(jitterDep); F(vibratoFreq); F(vibratoDep); F(shimmerDep);
+  F(attackLen); F(rolloff); F(rolloffOct); F(rolloffKHz); F(rolloffParab); F(rolloffParabHarm); F(rolloffLip);
+  F(formantDep); F(formantDepStoch); F(vocalTract); F(subFreq); F(subDep); F(shortestEpoch); F(amDep);
+  F(amFreq); F(amShape); F(rolloffNoise); F(samplingRate); F(windowLength); F(overlap); F(addSilence);
+  F(pitchFloor); F(pitchCeiling); F(pitchSamplingRate); F(throwaway);
+#undef F
+  SEXP nms = Rf_getAttrib(args, R_NamesSymbol);
+  for (R_xlen_t i = 0; i < Rf_xlength(args); ++i) {
+    const char* k = CHAR(STRING_ELT(nms, i));
+    SEXP v = VECTOR_ELT(args, i);
+    if (!strcmp(k, "pitchAnchors")) a.pitchAnchors = anchors(v);
+    else if (!strcmp(k, "pitchAnchorsGlobal")) a.pitchAnchorsGlobal = anchors(v);
+    else if (!strcmp(k, "noiseAnchors")) a.noiseAnchors = anchors(v);
+    else if (!strcmp(k, "mouthAnchors")) a.mouthAnchors = anchors(v);
+    else if (!strcmp(k, "amplAnchors")) a.amplAnchors = anchors(v);
+    else if (!strcmp(k, "amplAnchorsGlobal")) a.amplAnchorsGlobal = anchors(v);
+    else if (!strcmp(k, "tempEffects") && TYPEOF(v) == REALSXP && Rf_xlength(v) == 8)
+      memcpy(a.tempEffects, REAL(v), sizeof a.tempEffects);
+  }
+  /* formants / formantsNoise arrive flattened by the R wrapper as
+   * list(n_points = integer, f1_index = integer, time, freq, amp, width) */
+  sg_formants* fs[2] = {&a.formants, &a.formantsNoise};
+  const char* fk[2] = {"formants_flat", "formantsNoise_flat"};
+  for (int f = 0; f < 2; ++f) {
+    for (R_xlen_t i = 0; i < Rf_xlength(args); ++i) {
+      if (strcmp(CHAR(STRING_ELT(nms, i)), fk[f])) continue;
+      SEXP v = VECTOR_ELT(args, i);
+      fs[f]->n_formants = (int32_t)Rf_xlength(VECTOR_ELT(v, 0));
+      fs[f]->n_points = INTEGER(VECTOR_ELT(v, 0));
+      fs[f]->f1_index = Rf_asInteger(VECTOR_ELT(v, 1));
+      fs[f]->time = REAL(VECTOR_ELT(v, 2));
+      fs[f]->freq = REAL(VECTOR_ELT(v, 3));
+      fs[f]->amp = REAL(VECTOR_ELT(v, 4));
+      fs[f]->width = REAL(VECTOR_ELT(v, 5));
+    }
+  }
+  sg_call_desc d;
+  memset(&d, 0, sizeof d);
+  d.kind = SG_CALL_SOUNDGEN;
+  d.args = &a;
+  d.random = r_rng();
+  return run_planned(&d);
+}
+
+/* istft-based filtered noise, R/source.R:57-138 */
+SEXP C_sg_generate_noise(SEXP len, SEXP noiseAnchors, SEXP pars, SEXP filterNoise) {
+  const int64_t L = (int64_t)Rf_asReal(len);
+  SEXP out = PROTECT(Rf_allocVector(REALSXP, L));
+  const double* fn = NULL;
+  int32_t fnc = 0;
+  if (TYPEOF(filterNoise) == REALSXP && Rf_isMatrix(filterNoise)) {
+    fn = REAL(filterNoise);
+    fnc = Rf_ncols(filterNoise);
+  }
+  sg_random rnd = r_rng();
+  GetRNGstate();
+  int rc = sg_generate_noise(ctx(), L, anchors(noiseAnchors), num(pars, "rolloffNoise", -6),
+                             num(pars, "attackLen", 10), (int32_t)num(pars, "windowLength_points", 1024),
+                             num(pars, "samplingRate", 16000), num(pars, "overlap", 75), num(pars, "throwaway", -120),
+                             fn, fnc, &rnd, REAL(out));
+  PutRNGstate();
+  check(rc);
+  UNPROTECT(1);
+  return out;
+}
+
+SEXP C_sg_formant_filter(SEXP sound, SEXP env, SEXP wl, SEXP overlap) {
+  const int64_t L = Rf_xlength(sound);
+  int64_t cap = L + 2 * (int64_t)Rf_asInteger(wl), n = 0;
+  SEXP out = PROTECT(Rf_allocVector(REALSXP, cap));
+  check(sg_formant_filter(ctx(), REAL(sound), L, REAL(env), Rf_isMatrix(env) ? Rf_ncols(env) : 1,
+                          Rf_asInteger(wl), Rf_asReal(overlap), REAL(out), cap, &n));
+  out = Rf_xlengthgets(out, n);
+  UNPROTECT(1);
+  return out;
+}
+
+static const R_CallMethodDef CALLS[] = {
+    {"C_sg_generate_harmonics", (DL_FUNC)&C_sg_generate_harmonics, 3},
+    {"C_sg_soundgen", (DL_FUNC)&C_sg_soundgen, 1},
+    {"C_sg_generate_noise", (DL_FUNC)&C_sg_generate_noise, 4},
+    {"C_sg_formant_filter", (DL_FUNC)&C_sg_formant_filter, 4},
+    {NULL, NULL, 0}};
+
+void R_init_soundgen(DllInfo* dll) {
+  R_registerRoutines(dll, NULL, CALLS, NULL, NULL);
+  R_useDynamicSymbols(dll, FALSE);
+}
+
+void R_unload_soundgen(DllInfo* dll) {
+  (void)dll;
+  if (g_ctx) sg_ctx_destroy(g_ctx);
+  g_ctx = NULL;
+}

@@ -36,9 +36,16 @@ class sg_formants(C.Structure):
                 ("amp", _dp), ("width", _dp)]
 
 
+NORM_CB = C.CFUNCTYPE(C.c_double, C.c_void_p)
+UNIF_CB = C.CFUNCTYPE(C.c_double, C.c_void_p)
+GAMMA_CB = C.CFUNCTYPE(C.c_double, C.c_void_p, C.c_double, C.c_double)
+
+
 class sg_random(C.Structure):
     _fields_ = [("normals", _dp), ("n_normals", C.c_int64),
-                ("uniforms", _dp), ("n_uniforms", C.c_int64)]
+                ("uniforms", _dp), ("n_uniforms", C.c_int64),
+                ("norm_cb", NORM_CB), ("unif_cb", UNIF_CB), ("gamma_cb", GAMMA_CB),
+                ("user", C.c_void_p)]
 
 
 HARM_FIELDS = ["attackLen", "nonlinBalance", "nonlinDep", "jitterDep", "jitterLen",

@@ -24,7 +24,7 @@ class Plan:
         for i, c in enumerate(calls):
             d = descs[i]
             kind = c.get("kind", "soundgen")
-            d.random = self.holder.random(c.get("normals"), c.get("uniforms"))
+            d.random = self.holder.random(c.get("normals"), c.get("uniforms"), c.get("rng"))
             if kind == "harmonics":
                 d.kind = _abi.SG_CALL_HARMONICS
                 p = self.holder.arr(c["pitch"])

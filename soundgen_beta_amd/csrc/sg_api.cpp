@@ -243,6 +243,25 @@ int sg_synchronize(sg_ctx* ctx) {
   });
 }
 
+int sg_execute_to_host(sg_ctx* ctx, sg_plan* plan, double* out_host) {
+  return guarded(ctx, [&]() {
+    HIPCHK(hipSetDevice(ctx->device));
+    if (!plan->D.uploaded) sg::device_upload(plan->B, plan->D, ctx->stream);
+    const int64_t T = plan->B.total_out;
+    float* d_out = nullptr;
+    HIPCHK(hipMalloc(&d_out, (size_t)std::max<int64_t>(T, 1) * sizeof(float)));
+    std::unique_ptr<void, hipError_t (*)(void*)> hold_out(d_out, hipFree);
+    sg::device_execute(plan->B, plan->D, d_out, ctx->stream, ctx->aux, nullptr);
+    std::vector<float> h((size_t)T);
+    if (T) HIPCHK(hipMemcpyAsync(h.data(), d_out, (size_t)T * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    for (size_t c = 0; c < plan->B.call_len.size(); ++c)
+      for (int64_t i = 0; i < plan->B.call_len[c]; ++i)
+        out_host[plan->B.call_off[c] + i] = h[plan->B.call_off[c] + i];
+    return SG_OK;
+  });
+}
+
 // ---- synchronous single-call helpers --------------------------------------
 static int run_single(sg_ctx* ctx, const sg_call_desc& d, double* out, int64_t cap, int64_t* out_len) {
   sg_plan* plan = nullptr;
@@ -253,19 +272,7 @@ static int run_single(sg_ctx* ctx, const sg_call_desc& d, double* out, int64_t c
   const int64_t L = plan->B.call_len[0];
   *out_len = L;
   if (L > cap) return set_err(ctx, SG_E_CAPACITY, "output buffer too small");
-  return guarded(ctx, [&]() {
-    HIPCHK(hipSetDevice(ctx->device));
-    sg::device_upload(plan->B, plan->D, ctx->stream);
-    float* d_out = nullptr;
-    HIPCHK(hipMalloc(&d_out, (size_t)std::max<int64_t>(L, 1) * sizeof(float)));
-    std::unique_ptr<float, hipError_t (*)(void*)> hold_out(d_out, hipFree);
-    sg::device_execute(plan->B, plan->D, d_out, ctx->stream, ctx->aux, nullptr);
-    std::vector<float> h((size_t)L);
-    HIPCHK(hipMemcpyAsync(h.data(), d_out, (size_t)L * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    for (int64_t i = 0; i < L; ++i) out[i] = h[i];
-    return SG_OK;
-  });
+  return sg_execute_to_host(ctx, plan, out);  // single call: offset 0
 }
 
 int sg_generate_harmonics(sg_ctx* ctx, const double* pitch, int64_t len, const sg_harm_params* p,

@@ -189,21 +189,25 @@ struct Rng {
   const sg_random* s = nullptr;
   int64_t in = 0, iu = 0;
   double norm() {
-    if (!s || in >= s->n_normals) throw SgError(SG_E_RANDOM, "normal stream exhausted");
-    return s->normals[in++];
+    if (s && in < s->n_normals) return s->normals[in++];
+    if (s && s->norm_cb) return s->norm_cb(s->user);
+    throw SgError(SG_E_RANDOM, "normal stream exhausted");
   }
   double unif() {
-    if (!s || iu >= s->n_uniforms) throw SgError(SG_E_RANDOM, "uniform stream exhausted");
-    return s->uniforms[iu++];
+    if (s && iu < s->n_uniforms) return s->uniforms[iu++];
+    if (s && s->unif_cb) return s->unif_cb(s->user);
+    throw SgError(SG_E_RANDOM, "uniform stream exhausted");
   }
   // rnorm(1, mu, sd): no draw when sd == 0 (nmath/rnorm.c)
   double rnorm(double mu, double sd) {
     if (sd == 0.0 || !std::isfinite(mu)) return mu;
     return mu + sd * norm();
   }
-  // rgamma(1, shape, rate) — Marsaglia-Tsang on the injected streams
+  // rgamma(1, shape, rate): the gamma callback (R's own rgamma) when bound,
+  // else Marsaglia-Tsang on the injected streams
   double rgamma(double shape, double rate) {
     if (!(shape > 0) || !(rate > 0)) return NAN;
+    if (s && s->gamma_cb) return s->gamma_cb(s->user, shape, rate);
     double boost = 1.0, a = shape;
     if (a < 1.0) { boost = std::pow(unif(), 1.0 / a); a += 1.0; }
     const double d = a - 1.0 / 3.0, c = 1.0 / std::sqrt(9.0 * d);

@@ -70,6 +70,7 @@ def lib():
     L.sg_profile_read.argtypes = [vp, dp, i64p]
     L.sg_plan_kernel_stats.argtypes = [vp, i64p, i64p, i64p, i64p]
     L.sg_synchronize.argtypes = [vp]
+    L.sg_execute_to_host.argtypes = [vp, vp, dp]
     L.sg_generate_harmonics.argtypes = [vp, dp, i64, C.POINTER(_abi.sg_harm_params), _abi.sg_anchors,
                                         C.POINTER(_abi.sg_random), dp, i64, i64p]
     L.sg_soundgen.argtypes = [vp, C.POINTER(_abi.sg_soundgen_args), C.POINTER(_abi.sg_random), dp, i64, i64p]

@@ -220,7 +220,10 @@ class Holder:
         s.time, s.freq, s.amp, s.width = (_abi.dptr(c) for c in cat)
         return s
 
-    def random(self, normals=None, uniforms=None):
+    def random(self, normals=None, uniforms=None, rng=None):
+        """sg_random from injected arrays and/or a draw source `rng` (an object
+        with standard_normal(), random() and gamma(shape, scale), e.g. a
+        numpy Generator) bound to the norm/unif/gamma callbacks."""
         r = _abi.sg_random()
         if normals is not None:
             n = self.arr(normals)
@@ -228,6 +231,12 @@ class Holder:
         if uniforms is not None:
             u = self.arr(uniforms)
             r.uniforms, r.n_uniforms = _abi.dptr(u), len(u)
+        if rng is not None:
+            cbs = (_abi.NORM_CB(lambda _u: float(rng.standard_normal())),
+                   _abi.UNIF_CB(lambda _u: float(rng.random())),
+                   _abi.GAMMA_CB(lambda _u, shape, rate: float(rng.gamma(shape, 1.0 / rate))))
+            self.keep.extend(cbs)
+            r.norm_cb, r.unif_cb, r.gamma_cb = cbs
         return r
 
 

@@ -78,3 +78,13 @@ def test_plan_stats_and_device_bytes():
     assert st["harm_samples"] >= sum(plan.lengths)
     assert st["harm_terms"] >= st["harm_samples"]
     assert plan.device_bytes() > 4 * st["harm_samples"]
+
+
+def test_rng_callbacks_follow_the_same_draw_order(oracle):
+    """With draws from callbacks (how the R shim binds norm_rand/unif_rand/
+    rgamma), planner and oracle consume identical sequences."""
+    p = 200 + 60 * t3500
+    prm = dict(C2, temperature=0.1, nonlinBalance=100, subFreq=120, subDep=60, jitterDep=1, shimmerDep=8)
+    plan = batch.Plan([{"kind": "harmonics", "pitch": p, "params": prm, "rng": np.random.default_rng(5)}], None)
+    ref = oracle.generate_harmonics(p, rng=np.random.default_rng(5), **prm)
+    assert plan.status[0] == 0 and plan.lengths[0] == len(ref)
