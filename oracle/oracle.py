@@ -109,9 +109,9 @@ def soundgen(normals=None, uniforms=None, rng=None, **kw):
 
 
 def generate_noise(len, noiseAnchors, rolloffNoise=-6, attackLen=10, windowLength_points=1024,
-                   samplingRate=16000, overlap=75, throwaway=-120, filterNoise=None, uniforms=None):
+                   samplingRate=16000, overlap=75, throwaway=-120, filterNoise=None, uniforms=None, rng=None):
     h = rargs.Holder()
-    rnd = h.random(None, uniforms)
+    rnd = h.random(None, uniforms, rng)
     fn, fnc = None, 0
     if filterNoise is not None:
         filterNoise = np.asarray(filterNoise, dtype=np.float64)
@@ -129,10 +129,10 @@ def generate_noise(len, noiseAnchors, rolloffNoise=-6, attackLen=10, windowLengt
 def spectral_envelope(nr, nc, formants=None, formantDep=1, rolloffLip=6, mouthAnchors=None,
                       mouthOpenThres=0, openMouthBoost=0, vocalTract=None, temperature=0, formDrift=.3,
                       formDisp=.2, formantDepStoch=30, smoothLinearFactor=1, samplingRate=16000,
-                      speedSound=35400, normals=None, uniforms=None):
+                      speedSound=35400, normals=None, uniforms=None, rng=None):
     h = rargs.Holder()
     F = h.formants(rargs.as_formants(formants))
-    rnd = h.random(normals, uniforms)
+    rnd = h.random(normals, uniforms, rng)
     out = np.zeros(nr * nc)
     vt = float("nan") if vocalTract is None else float(vocalTract)
     _check(lib().or_spectral_envelope(nr, nc, C.byref(F), formantDep, rolloffLip,

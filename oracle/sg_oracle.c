@@ -1473,8 +1473,9 @@ OR_API int or_soundgen(const sg_soundgen_args* A_in, const sg_random* rnd, doubl
   sg_formants Fm = A.formants; Fm.freq = ffreq;
   /* nSyl / repeatBout stochastic rounding: rbinom(1, 1, p) — no draw when p == 0 */
   double nSyl = A.nSyl, repeatBout = A.repeatBout;
-  if (nSyl - floor(nSyl) != 0) { double u; TRY(rng_unif(&R, &u)); nSyl = floor(nSyl) + (u < nSyl - floor(nSyl)); }
-  if (repeatBout - floor(repeatBout) != 0) { double u; TRY(rng_unif(&R, &u)); repeatBout = floor(repeatBout) + (u < repeatBout - floor(repeatBout)); }
+  /* rbinom(1, 1, p): R's inversion for size 1 (nmath/rbinom.c) -> (u >= 1 - p) for p <= .5, (u < p) above */
+  { double p = nSyl - floor(nSyl); if (p != 0) { double u; TRY(rng_unif(&R, &u)); nSyl = floor(nSyl) + (p <= .5 ? (u >= 1 - p) : (u < p)); } }
+  { double p = repeatBout - floor(repeatBout); if (p != 0) { double u; TRY(rng_unif(&R, &u)); repeatBout = floor(repeatBout) + (p <= .5 ? (u >= 1 - p) : (u < p)); } }
   int64_t nS = (int64_t)nSyl, nB = (int64_t)repeatBout;
   pitchDeltas = (double*)malloc((nS > 0 ? nS : 1) * sizeof(double));
   {

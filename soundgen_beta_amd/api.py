@@ -40,11 +40,11 @@ def generateHarmonics(pitch, amplAnchors=rargs.NA, normals=None, uniforms=None, 
     return out[:n.value].copy()
 
 
-def soundgen(normals=None, uniforms=None, device=0, **kw):
+def soundgen(normals=None, uniforms=None, rng=None, device=0, **kw):
     """soundgen(...) — R/soundgen.R:208-862. Returns the waveform (float64)."""
     h = rargs.Holder()
     a = rargs.fill_soundgen_args(h, kw)
-    rnd = h.random(normals, uniforms)
+    rnd = h.random(normals, uniforms, rng)
     ctx = _ctx(device)
     L = native.lib()
     n = C.c_int64()
@@ -57,6 +57,68 @@ def soundgen(normals=None, uniforms=None, device=0, **kw):
             continue
         native.check(rc, ctx.ptr)
         return out[:n.value].copy()
+
+
+def generateNoise(len, noiseAnchors=None, rolloffNoise=-6, attackLen=10, windowLength_points=1024,
+                  samplingRate=16000, overlap=75, throwaway=-120, filterNoise=None, uniforms=None, rng=None,
+                  device=0):
+    """generateNoise() — R/source.R:57-138 (runif draws injected or from `rng`)."""
+    if noiseAnchors is None:
+        noiseAnchors = {"time": [0, 300], "value": [-120, -120]}
+    h = rargs.Holder()
+    rnd = h.random(None, uniforms, rng)
+    fn, fnc = None, 0
+    if filterNoise is not None:
+        filterNoise = np.asarray(filterNoise, dtype=np.float64)
+        if filterNoise.ndim == 1:
+            filterNoise = filterNoise[:, None]
+        fnc = filterNoise.shape[1]
+        fn = h.arr(filterNoise.T.ravel())  # column-major nr x nc
+    out = np.zeros(int(len))
+    ctx = _ctx(device)
+    native.check(native.lib().sg_generate_noise(ctx.ptr, int(len), h.anchors(rargs.as_anchors(noiseAnchors)),
+                                                rolloffNoise, attackLen, int(windowLength_points), samplingRate,
+                                                overlap, throwaway, _abi.dptr(fn), fnc, C.byref(rnd),
+                                                _abi.dptr(out)), ctx.ptr)
+    return out
+
+
+def getSpectralEnvelope(nr, nc, formants=None, formantDep=1, rolloffLip=6, mouthAnchors=None, mouthOpenThres=0,
+                        openMouthBoost=0, vocalTract=None, temperature=0, formDrift=.3, formDisp=.2,
+                        formantDepStoch=30, smoothLinearFactor=1, samplingRate=16000, speedSound=35400,
+                        normals=None, uniforms=None, rng=None, device=0):
+    """getSpectralEnvelope() — R/sourceSpectrum.R:261-566; returns nr x nc."""
+    h = rargs.Holder()
+    F = h.formants(rargs.as_formants(formants))
+    rnd = h.random(normals, uniforms, rng)
+    out = np.zeros(int(nr) * int(nc))
+    vt = float("nan") if vocalTract is None else float(vocalTract)
+    # host-side computation in the library (no device context needed)
+    native.check(native.lib().sg_spectral_envelope(None, int(nr), int(nc), C.byref(F), formantDep, rolloffLip,
+                                                   h.anchors(rargs.as_anchors(mouthAnchors)), mouthOpenThres,
+                                                   openMouthBoost, vt, temperature, formDrift, formDisp,
+                                                   formantDepStoch, smoothLinearFactor, samplingRate, speedSound,
+                                                   C.byref(rnd), _abi.dptr(out)))
+    return out.reshape(int(nc), int(nr)).T
+
+
+def formantFilter(sound, env, windowLength_points, overlap=75, device=0):
+    """The formant filter of soundgen(): seewave::stft x env -> istft -> /max
+    (R/soundgen.R:743-807). env: nr x nc (nc == 1: stationary)."""
+    h = rargs.Holder()
+    sound = h.arr(sound)
+    env = np.asarray(env, dtype=np.float64)
+    if env.ndim == 1:
+        env = env[:, None]
+    envc = h.arr(env.T.ravel())
+    wl = int(windowLength_points)
+    cap = len(sound) + 2 * wl
+    out = np.zeros(cap)
+    n = C.c_int64()
+    ctx = _ctx(device)
+    native.check(native.lib().sg_formant_filter(ctx.ptr, _abi.dptr(sound), len(sound), _abi.dptr(envc), env.shape[1],
+                                                wl, overlap, _abi.dptr(out), cap, C.byref(n)), ctx.ptr)
+    return out[:n.value].copy()
 
 
 def getRolloff(pitch_per_gc=(440,), nHarmonics=100, rolloff=-12, rolloffOct=-2, rolloffParab=0,

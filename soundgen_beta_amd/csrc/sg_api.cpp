@@ -54,19 +54,27 @@ int guarded(sg_ctx* ctx, F&& f) {
 
 // Rolls a Batch back to a checkpoint when planning one call fails.
 struct Checkpoint {
-  size_t segs, epochs, knots, amps, tasks, pieces, syls, syl_tiles, cknots, noise, filt, mixes, bouts, frames;
-  int64_t w_total, harm_samples, harm_terms, harm_amp_bytes, fft_frames, scratch;
+  size_t segs, epochs, knots, amps, tasks, pieces, syls, syl_tiles, cknots, fl, items;
+  size_t frames[2], olas[2], mixes[2], copies;
+  int64_t w_total, harm_samples, harm_terms, harm_amp_bytes, fft_frames, fs_total;
   explicit Checkpoint(const sg::Batch& B)
       : segs(B.segs.size()), epochs(B.epochs.size()), knots(B.knots.size()), amps(B.amps.size()),
         tasks(B.tasks.size()), pieces(B.pieces.size()), syls(B.syls.size()), syl_tiles(B.syl_tiles.size()),
-        cknots(B.cknots.size()), noise(0), filt(0), mixes(0), bouts(0), frames(0), w_total(B.w_total),
-        harm_samples(B.harm_samples), harm_terms(B.harm_terms), harm_amp_bytes(B.harm_amp_bytes),
-        fft_frames(B.fft_frames), scratch(0) {}
+        cknots(B.cknots.size()), fl(B.fl.size()), items(B.items.size()), copies(B.copies.size()),
+        w_total(B.w_total), harm_samples(B.harm_samples), harm_terms(B.harm_terms),
+        harm_amp_bytes(B.harm_amp_bytes), fft_frames(B.fft_frames), fs_total(B.fs_total) {
+    for (int p = 0; p < 2; ++p) { frames[p] = B.frames[p].size(); olas[p] = B.olas[p].size(); mixes[p] = B.mixes[p].size(); }
+  }
   void restore(sg::Batch& B) const {
     B.segs.resize(segs); B.epochs.resize(epochs); B.knots.resize(knots); B.amps.resize(amps);
     B.tasks.resize(tasks); B.pieces.resize(pieces); B.syls.resize(syls); B.syl_tiles.resize(syl_tiles);
-    B.cknots.resize(cknots); B.w_total = w_total; B.harm_samples = harm_samples; B.harm_terms = harm_terms;
-    B.harm_amp_bytes = harm_amp_bytes; B.fft_frames = fft_frames;
+    B.cknots.resize(cknots); B.fl.resize(fl); B.items.resize(items); B.copies.resize(copies);
+    for (int p = 0; p < 2; ++p) {
+      B.frames[p].resize(frames[p]); B.frame_geom[p].resize(frames[p]);
+      B.olas[p].resize(olas[p]); B.mixes[p].resize(mixes[p]);
+    }
+    B.w_total = w_total; B.harm_samples = harm_samples; B.harm_terms = harm_terms;
+    B.harm_amp_bytes = harm_amp_bytes; B.fft_frames = fft_frames; B.fs_total = fs_total;
   }
 };
 
@@ -130,6 +138,7 @@ int sg_plan_batch(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, sg_pl
         } else if (d.kind == SG_CALL_SOUNDGEN) {
           if (!d.args) throw sg::SgError(SG_E_ARG, "soundgen call without args");
           L = sg::plan_soundgen(B, *d.args, R, off, first_syl);
+          sg::tile_syllables(B, first_syl);
         } else {
           throw sg::SgError(SG_E_ARG, "unknown call kind");
         }
@@ -147,6 +156,7 @@ int sg_plan_batch(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, sg_pl
     }
     B.total_out = off;
     sg::finalize_plan(B);
+    sg::finalize_spec(B);
     *out = P.release();
     return SG_OK;
   });
@@ -295,6 +305,85 @@ int sg_soundgen(sg_ctx* ctx, const sg_soundgen_args* a, const sg_random* rnd, do
   d.args = a;
   if (rnd) d.random = *rnd;
   return run_single(ctx, d, out, cap, out_len);
+}
+
+// ---- function-level spectral entries (single-item batches) -----------------
+static int run_plan_to_host(sg_ctx* ctx, sg_plan* P, double* out, int64_t n) {
+  P->B.call_len.assign(1, n);
+  P->B.call_off.assign(1, 0);
+  P->B.call_status.assign(1, 0);
+  P->B.call_msg.assign(1, "");
+  P->B.total_out = n;
+  sg::finalize_plan(P->B);
+  sg::finalize_spec(P->B);
+  return sg_execute_to_host(ctx, P, out);
+}
+
+int sg_formant_filter(sg_ctx* ctx, const double* sound, int64_t len, const double* env, int32_t env_nc,
+                      int32_t windowLength_points, double overlap, double* out, int64_t cap, int64_t* out_len) {
+  return guarded(ctx, [&]() {
+    auto P = std::make_unique<sg_plan>();
+    sg::Batch& B = P->B;
+    const int wl = windowLength_points;
+    if (len < wl) throw sg::SgError(SG_E_ARG, "formant filter: sound shorter than the window");
+    const int64_t src = sg::fl_push(B, sound, len);
+    const int64_t snd = sg::fs_alloc(B, len);
+    B.copies.push_back(sg::Batch::Copy{src, snd, len});
+    const sg::vec e(env, env + (int64_t)(wl / 2) * env_nc);
+    int64_t Lf = 0, filt = 0;
+    const int ola = sg::plan_filter(B, snd, len, wl, overlap, e, env_nc, &Lf, &filt);
+    *out_len = Lf;
+    if (Lf > cap) throw sg::SgError(SG_E_CAPACITY, "output buffer too small");
+    SgNoiseItem it{};
+    it.raw = filt;
+    it.len = Lf;
+    it.ola = ola;
+    it.flags = SG_ITEM_FILTER_OLA;
+    B.items.push_back(it);
+    SgMix m{};
+    m.len = Lf;
+    m.nitems = 1;
+    B.mixes[1].push_back(m);
+    return run_plan_to_host(ctx, P.get(), out, Lf);
+  });
+}
+
+int sg_generate_noise(sg_ctx* ctx, int64_t len, sg_anchors noiseAnchors, double rolloffNoise, double attackLen,
+                      int32_t windowLength_points, double samplingRate, double overlap, double throwaway,
+                      const double* filterNoise, int32_t filter_nc, const sg_random* rnd, double* out) {
+  (void)throwaway;
+  return guarded(ctx, [&]() {
+    auto P = std::make_unique<sg_plan>();
+    sg::Batch& B = P->B;
+    sg::Rng R;
+    R.s = rnd;
+    SgNoiseItem it{};
+    SgMix m{};
+    m.len = len;
+    if (sg::plan_noise(B, R, len, noiseAnchors, rolloffNoise, attackLen, windowLength_points, samplingRate, overlap,
+                       filterNoise, filter_nc, &it)) {
+      B.items.push_back(it);
+      m.nitems = 1;
+    }
+    B.mixes[1].push_back(m);
+    return run_plan_to_host(ctx, P.get(), out, len);
+  });
+}
+
+int sg_spectral_envelope(sg_ctx* ctx, int32_t nr, int32_t nc, const sg_formants* formants, double formantDep,
+                         double rolloffLip, sg_anchors mouthAnchors, double mouthOpenThres, double openMouthBoost,
+                         double vocalTract, double temperature, double formDrift, double formDisp,
+                         double formantDepStoch, double smoothLinearFactor, double samplingRate, double speedSound,
+                         const sg_random* rnd, double* out) {
+  return guarded(ctx, [&]() {
+    sg::Rng R;
+    R.s = rnd;
+    const sg::vec e = sg::spectral_envelope(R, nr, nc, formants, formantDep, rolloffLip, mouthAnchors, mouthOpenThres,
+                                            openMouthBoost, vocalTract, temperature, formDrift, formDisp,
+                                            formantDepStoch, smoothLinearFactor, samplingRate, speedSound);
+    std::memcpy(out, e.data(), e.size() * sizeof(double));
+    return SG_OK;
+  });
 }
 
 int sg_get_rolloff(const double* pitch_per_gc, int32_t n_gc, int32_t nHarmonics, double rolloff, double rolloffOct,

@@ -119,6 +119,8 @@ struct SgSyllable {
   int64_t task0;
   int32_t ptile0;    // crossfade-piece tiles: per-tile max slots [ptile0, ptile0+nptile)
   int32_t nptile;
+  int32_t dst_fs;    // 1: out_off is in the spectral scratch (voiced part of a soundgen() bout)
+  int32_t pad2;
   SgContour env;     // amplEnvelope (kind 0 = none)
   SgLinear drift;
 };
@@ -127,5 +129,87 @@ struct SgSyllable {
 struct SgSylTile {
   int32_t syl;
   int32_t piece;     // piece containing k0
+  int64_t k0;
+};
+
+// ------------------------------------------------------------------------
+// Spectral part: seewave::stft / istft frames, OLA, noise, formant filter.
+// Float data (inputs, windows, twiddles, envelopes) live in one fp32 arena
+// `fl`; intermediate buffers (frame scratch, sound, raw noise) in `fs`.
+
+constexpr int SG_FFT_MAX_STAGES = 12;
+// FFT geometry of one window length wl = N (even), computed as a complex
+// FFT of M = N/2 points (real-input / Hermitian-output packing).
+struct SgFftGeom {
+  int32_t wl, M, nstages, fb;      // fb: frames per workgroup
+  int32_t radix[SG_FFT_MAX_STAGES];
+  int64_t tw;                      // fl offset: M pairs W_M^t, then M pairs W_N^k (interleaved re, im)
+  int64_t win;                     // fl offset: hamming[wl] then hanning[wl] (seewave ftwindow)
+  int32_t lds_bytes, pad;
+};
+
+constexpr int SG_FRAME_FILTER = 0;  // fs sound -> hamming -> FFT/wl -> x env -> ISTFT/wl -> x hann
+constexpr int SG_FRAME_NOISE = 1;   // fl uniforms x fl filter (real spectrum)  -> ISTFT/wl -> x hann
+struct SgFrame {
+  int64_t src;  // FILTER: fs offset of the frame's first sound sample; NOISE: fl offset of nr uniforms
+  int64_t env;  // fl offset of the nr envelope (FILTER) / filter (NOISE) values
+  int64_t dst;  // fs offset of the wl windowed ISTFT outputs
+};
+struct SgFrameGroup {  // frames of one workgroup: same geometry and mode
+  int32_t geom, mode;
+  int32_t f0, nf;
+};
+
+// Overlap-add of nframes windowed frames (seewave istft, seewave.r:3462-3484)
+// into samples [first, first + len) of the full istft output of length xlen
+// (samples outside [0, xlen) are the zero padding of matchLengths()).
+struct SgOla {
+  int64_t frames;  // fs offset of frame 0 (frames contiguous, wl floats each)
+  int64_t out;     // fs offset of output sample `first`
+  int64_t first, len, xlen;
+  double h;        // hop wl * (100 - overlap) / 100
+  int32_t nframes, wl;
+  float scale;     // h / sum(hann^2)
+  int32_t tile0;   // first per-tile max slot
+};
+constexpr int SG_OLA_TILE = 1024;
+struct SgOlaTile {
+  int32_t ola, pad;
+  int64_t q0;  // first sample of the tile (relative to `first`)
+};
+
+// Noise of one syllable, as generateNoise() returns it (R/source.R:124-131):
+// matchLengths()-trimmed OLA output / its max * 2^(dB/10) contour, faded.
+struct SgNoiseItem {
+  int64_t raw;        // fs offset of the trimmed OLA output (len samples)
+  int64_t len;
+  int64_t off;        // insertion offset inside the mix (addVectors, R/utilities_math.R:500-526)
+  int32_t ola;        // its OLA (max slot); < 0: raw samples (no normalisation)
+  int32_t fade;       // fadeInOut length (0/1: none)
+  int32_t flags;      // host bookkeeping: SG_ITEM_*
+  int32_t pad;
+  SgContour strength;
+};
+constexpr int SG_ITEM_FILTER_OLA = 1;  // ola indexes the filter-phase OLAs (shifted at finalize)
+constexpr int SG_ITEM_ZERO = 2;        // all-zero content (R's rep(0, len)): layout only
+// One output range: v = base + sum(noise items), * mult contour, * AM trill.
+constexpr int SG_BASE_NONE = 0;  // zeros
+constexpr int SG_BASE_RAW = 1;   // fs[base + k]
+constexpr int SG_BASE_NORM = 2;  // fs[base + k] / olamax[base_ola]  (soundFiltered / max)
+struct SgMix {
+  int64_t dst;        // destination offset (fs when to_fs, else the output buffer)
+  int64_t len;
+  int64_t base, base_len;
+  int32_t base_kind, base_ola;
+  int32_t item0, nitems;
+  int32_t to_fs;
+  int32_t am_lo;      // AM trill: half period of the sigmoid table (0: none)
+  int64_t am_tab;     // fl offset of the sigmoid half period
+  float am_dep, pad;
+  SgContour mult;     // amplAnchorsGlobal envelope (kind 0: none)
+};
+constexpr int SG_MIX_TILE = 1024;
+struct SgMixTile {
+  int32_t mix, pad;
   int64_t k0;
 };

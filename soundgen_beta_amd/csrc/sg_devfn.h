@@ -1,0 +1,70 @@
+// sg_devfn.h — device helpers shared by the HIP kernels (contours, approx, reductions).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "sg_dev.h"
+
+namespace sgd {
+
+__device__ __forceinline__ double seqint_at(double from, double to, int n, int i) {
+  if (i == 0) return from;
+  if (i == n - 1) return to;
+  const double by = (to - from) / (double)(n - 1);
+  return (i < n / 2) ? from + (double)i * by : to - (double)(n - 1 - i) * by;
+}
+
+__device__ __forceinline__ double contour_at(const SgContour& c, const double* __restrict__ ck, int64_t L, int64_t k) {
+  double v;
+  if (c.kind == 1) v = c.a;
+  else if (c.kind == 2) {
+    if (k == 0 || c.a == c.b) v = c.a;
+    else if (k == L - 1) v = c.b;
+    else v = c.a + (double)k * ((c.b - c.a) / (double)(L - 1));
+  } else {
+    const double* x = ck + c.k_off;
+    const double* y = x + c.nk;
+    const double* b = y + c.nk;
+    const double* cc = b + c.nk;
+    const double* d = cc + c.nk;
+    double u;
+    if (k == 0) u = c.a;
+    else if (k == L - 1) u = c.b;
+    else {
+      const double by = (c.b - c.a) / (double)(L - 1);
+      u = (k < L / 2) ? c.a + (double)k * by : c.b - (double)(L - 1 - k) * by;
+    }
+    int i = 0, j = c.nk;
+    do { int m = (i + j) >> 1; if (u < x[m]) j = m; else i = m; } while (j > i + 1);
+    const double dx = u - x[i];
+    v = y[i] + dx * (b[i] + dx * (cc[i] + dx * d[i]));
+    v = v < c.lo ? c.lo : v;
+    v = v > c.hi ? c.hi : v;
+  }
+  return c.db ? exp2(v * 0.1) : v;
+}
+
+__device__ __forceinline__ double linear_at(const SgLinear& l, const double* __restrict__ ck, int64_t L, int64_t k) {
+  const double* x = ck + l.k_off;
+  const double* y = x + l.nk;
+  double u;
+  if (k == 0) u = l.x0;
+  else if (k == L - 1) u = l.x1;
+  else {
+    const double by = (l.x1 - l.x0) / (double)(L - 1);
+    u = (k < L / 2) ? l.x0 + (double)k * by : l.x1 - (double)(L - 1 - k) * by;
+  }
+  int i = 0, j = l.nk - 1;
+  while (i < j - 1) { int ij = (i + j) >> 1; if (u < x[ij]) j = ij; else i = ij; }
+  if (u == x[j]) return y[j];
+  if (u == x[i]) return y[i];
+  return y[i] + (y[j] - y[i]) * ((u - x[i]) / (x[j] - x[i]));
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+}  // namespace sgd
+

@@ -20,6 +20,7 @@ size_t up(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
 struct Layout {
   size_t segs, epochs, knots, amps, tasks, pieces, syls, syl_tiles, ptiles, cknots, W, taskmax, ptilemax, maxes, total;
+  size_t geoms, frames, fgroups, olas, olatiles, olatilemax, olamax, items, mixes, mixtiles, fl, fs;
   explicit Layout(const Batch& B) {
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o += up(bytes > 0 ? bytes : 1); return r; };
@@ -37,6 +38,18 @@ struct Layout {
     taskmax = take(B.tasks.size() * sizeof(float));
     ptilemax = take(B.ptiles.size() * sizeof(float));
     maxes = take(B.syls.size() * sizeof(float));
+    geoms = take(B.geoms.size() * sizeof(SgFftGeom));
+    frames = take((B.frames[0].size() + B.frames[1].size()) * sizeof(SgFrame));
+    fgroups = take(B.fgroups.size() * sizeof(SgFrameGroup));
+    olas = take(B.olas_dev.size() * sizeof(SgOla));
+    olatiles = take(B.olatiles.size() * sizeof(SgOlaTile));
+    olatilemax = take(B.olatiles.size() * sizeof(float));
+    olamax = take(B.olas_dev.size() * sizeof(float));
+    items = take(B.items.size() * sizeof(SgNoiseItem));
+    mixes = take(B.mixes_dev.size() * sizeof(SgMix));
+    mixtiles = take(B.mixtiles.size() * sizeof(SgMixTile));
+    fl = take(B.fl.size() * sizeof(float));
+    fs = take((size_t)B.fs_total * sizeof(float) + 256);
     total = o;
   }
 };
@@ -111,6 +124,18 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   D.taskmax = (float*)(a + L.taskmax);
   D.ptilemax = (float*)(a + L.ptilemax);
   D.maxes = (float*)(a + L.maxes);
+  D.geoms = (SgFftGeom*)(a + L.geoms);
+  D.frames = (SgFrame*)(a + L.frames);
+  D.fgroups = (SgFrameGroup*)(a + L.fgroups);
+  D.olas = (SgOla*)(a + L.olas);
+  D.olatiles = (SgOlaTile*)(a + L.olatiles);
+  D.olatilemax = (float*)(a + L.olatilemax);
+  D.olamax = (float*)(a + L.olamax);
+  D.items = (SgNoiseItem*)(a + L.items);
+  D.mixes = (SgMix*)(a + L.mixes);
+  D.mixtiles = (SgMixTile*)(a + L.mixtiles);
+  D.fl = (float*)(a + L.fl);
+  D.fs = (float*)(a + L.fs);
   auto cp = [&](void* dst, const void* src, size_t bytes) {
     if (bytes) HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
   };
@@ -124,6 +149,16 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   cp(D.syl_tiles, B.syl_tiles.data(), B.syl_tiles.size() * sizeof(SgSylTile));
   cp(D.ptiles, B.ptiles.data(), B.ptiles.size() * sizeof(SgSylTile));
   cp(D.cknots, B.cknots.data(), B.cknots.size() * sizeof(double));
+  cp(D.geoms, B.geoms.data(), B.geoms.size() * sizeof(SgFftGeom));
+  cp(D.frames, B.frames[0].data(), B.frames[0].size() * sizeof(SgFrame));
+  cp(D.frames + B.frames[0].size(), B.frames[1].data(), B.frames[1].size() * sizeof(SgFrame));
+  cp(D.fgroups, B.fgroups.data(), B.fgroups.size() * sizeof(SgFrameGroup));
+  cp(D.olas, B.olas_dev.data(), B.olas_dev.size() * sizeof(SgOla));
+  cp(D.olatiles, B.olatiles.data(), B.olatiles.size() * sizeof(SgOlaTile));
+  cp(D.items, B.items.data(), B.items.size() * sizeof(SgNoiseItem));
+  cp(D.mixes, B.mixes_dev.data(), B.mixes_dev.size() * sizeof(SgMix));
+  cp(D.mixtiles, B.mixtiles.data(), B.mixtiles.size() * sizeof(SgMixTile));
+  cp(D.fl, B.fl.data(), B.fl.size() * sizeof(float));
   HIPCHK(hipStreamSynchronize(s));
   while (D.ev_slice.size() < B.slices.size()) {
     hipEvent_t e;
@@ -137,7 +172,10 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
 
 void device_execute(const Batch& B, DevicePlan& D, float* d_out, hipStream_t s, hipStream_t s2,
                     std::vector<std::pair<hipEvent_t, hipEvent_t>>* prof) {
-  if (B.slices.empty()) return;
+  if (B.slices.empty()) {  // no harmonic syllables: spectral phases only
+    device_execute_spec(B, D, d_out, s);
+    return;
+  }
   const bool two = B.slices.size() > 1;
   if (!two) s2 = s;
   // fork: s2 starts after everything already queued on s
@@ -170,6 +208,23 @@ void device_execute(const Batch& B, DevicePlan& D, float* d_out, hipStream_t s, 
     HIPCHK(hipEventRecord(D.ev_join, s2));
     HIPCHK(hipStreamWaitEvent(s, D.ev_join, 0));
   }
+  device_execute_spec(B, D, d_out, s);
+  HIPCHK(hipGetLastError());
+}
+
+// Spectral phases after the harmonic syllables: noise frames -> noise OLA,
+// pre-filter mixes (sounds), filter frames -> filter OLA, final mixes.
+void device_execute_spec(const Batch& B, const DevicePlan& D, float* d_out, hipStream_t s) {
+  const int64_t ng = (int64_t)B.fgroups.size();
+  launch_fft_frames(D, 0, B.fgroup_split, B.fgroup_lds[0], s);
+  launch_ola(D, 0, B.olatile_split, 0, B.ola_split, s);
+  for (const Batch::Copy& c : B.copies)
+    HIPCHK(hipMemcpyAsync(D.fs + c.fs_off, D.fl + c.fl_off, (size_t)c.n * sizeof(float), hipMemcpyDeviceToDevice, s));
+  launch_mix(D, 0, B.mixtile_split, d_out, s);
+  launch_fft_frames(D, B.fgroup_split, ng - B.fgroup_split, B.fgroup_lds[1], s);
+  launch_ola(D, B.olatile_split, (int64_t)B.olatiles.size() - B.olatile_split, B.ola_split,
+             (int64_t)B.olas_dev.size() - B.ola_split, s);
+  launch_mix(D, B.mixtile_split, (int64_t)B.mixtiles.size() - B.mixtile_split, d_out, s);
   HIPCHK(hipGetLastError());
 }
 

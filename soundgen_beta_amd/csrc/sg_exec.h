@@ -27,6 +27,18 @@ struct DevicePlan {
   float* taskmax = nullptr;
   float* ptilemax = nullptr;
   float* maxes = nullptr;
+  SgFftGeom* geoms = nullptr;
+  SgFrame* frames = nullptr;
+  SgFrameGroup* fgroups = nullptr;
+  SgOla* olas = nullptr;
+  SgOlaTile* olatiles = nullptr;
+  float* olatilemax = nullptr;
+  float* olamax = nullptr;
+  SgNoiseItem* items = nullptr;
+  SgMix* mixes = nullptr;
+  SgMixTile* mixtiles = nullptr;
+  float* fl = nullptr;
+  float* fs = nullptr;
   std::vector<hipEvent_t> ev_slice;  // slice c's maxes are ready (s -> s2)
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
@@ -39,11 +51,16 @@ void device_free(DevicePlan& D);
 // (optional) receives one event pair per sine-bank launch.
 void device_execute(const Batch& B, DevicePlan& D, float* d_out, hipStream_t s, hipStream_t s2,
                     std::vector<std::pair<hipEvent_t, hipEvent_t>>* prof);
+void device_execute_spec(const Batch& B, const DevicePlan& D, float* d_out, hipStream_t s);
 
 // launchers (sg_harm.hip)
 void launch_sine_bank(const DevicePlan& D, int64_t t0, int64_t n_tasks, hipStream_t s);
 void launch_syl_max(const DevicePlan& D, int64_t s0, int64_t n_syls, hipStream_t s);
 void launch_piece_max(const DevicePlan& D, int64_t p0, int64_t n_ptiles, hipStream_t s);
 void launch_harm_finalize(const DevicePlan& D, int64_t f0, int64_t n_stiles, float* out, hipStream_t s);
+// sg_fft.hip
+void launch_fft_frames(const DevicePlan& D, int64_t g0, int64_t n_groups, int lds_bytes, hipStream_t s);
+void launch_ola(const DevicePlan& D, int64_t t0, int64_t n_tiles, int64_t o0, int64_t n_olas, hipStream_t s);
+void launch_mix(const DevicePlan& D, int64_t t0, int64_t n_tiles, float* out, hipStream_t s);
 
 }  // namespace sg

@@ -18,69 +18,11 @@
 
 #include "sg_dev.h"
 
-namespace {
+#include "sg_devfn.h"
 
-__device__ __forceinline__ double seqint_at(double from, double to, int n, int i) {
-  if (i == 0) return from;
-  if (i == n - 1) return to;
-  const double by = (to - from) / (double)(n - 1);
-  return (i < n / 2) ? from + (double)i * by : to - (double)(n - 1 - i) * by;
-}
-
-__device__ __forceinline__ double contour_at(const SgContour& c, const double* __restrict__ ck, int64_t L, int64_t k) {
-  double v;
-  if (c.kind == 1) v = c.a;
-  else if (c.kind == 2) {
-    if (k == 0 || c.a == c.b) v = c.a;
-    else if (k == L - 1) v = c.b;
-    else v = c.a + (double)k * ((c.b - c.a) / (double)(L - 1));
-  } else {
-    const double* x = ck + c.k_off;
-    const double* y = x + c.nk;
-    const double* b = y + c.nk;
-    const double* cc = b + c.nk;
-    const double* d = cc + c.nk;
-    double u;
-    if (k == 0) u = c.a;
-    else if (k == L - 1) u = c.b;
-    else {
-      const double by = (c.b - c.a) / (double)(L - 1);
-      u = (k < L / 2) ? c.a + (double)k * by : c.b - (double)(L - 1 - k) * by;
-    }
-    int i = 0, j = c.nk;
-    do { int m = (i + j) >> 1; if (u < x[m]) j = m; else i = m; } while (j > i + 1);
-    const double dx = u - x[i];
-    v = y[i] + dx * (b[i] + dx * (cc[i] + dx * d[i]));
-    v = v < c.lo ? c.lo : v;
-    v = v > c.hi ? c.hi : v;
-  }
-  return c.db ? exp2(v * 0.1) : v;
-}
-
-__device__ __forceinline__ double linear_at(const SgLinear& l, const double* __restrict__ ck, int64_t L, int64_t k) {
-  const double* x = ck + l.k_off;
-  const double* y = x + l.nk;
-  double u;
-  if (k == 0) u = l.x0;
-  else if (k == L - 1) u = l.x1;
-  else {
-    const double by = (l.x1 - l.x0) / (double)(L - 1);
-    u = (k < L / 2) ? l.x0 + (double)k * by : l.x1 - (double)(L - 1 - k) * by;
-  }
-  int i = 0, j = l.nk - 1;
-  while (i < j - 1) { int ij = (i + j) >> 1; if (u < x[ij]) j = ij; else i = ij; }
-  if (u == x[j]) return y[j];
-  if (u == x[i]) return y[i];
-  return y[i] + (y[j] - y[i]) * ((u - x[i]) / (x[j] - x[i]));
-}
-
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-  return v;
-}
-
-}  // namespace
+using sgd::contour_at;
+using sgd::linear_at;
+using sgd::wave_max;
 
 // sin(pi*x), cos(pi*x) for |x| <= 1/4 (|pi*x| <= pi/4): Taylor to x^9 / x^10,
 // truncation < 2e-9, i.e. below fp32 rounding.
@@ -302,9 +244,10 @@ __device__ __forceinline__ float fade_at(int lf, int64_t L, int64_t k) {
 extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize(
     const SgSylTile* __restrict__ stiles, const SgPiece* __restrict__ pieces, const SgSyllable* __restrict__ syls,
     const double* __restrict__ cknots, const float* __restrict__ W, const float* __restrict__ maxes,
-    float* __restrict__ out) {
+    float* __restrict__ out_buf, float* __restrict__ fs) {
   const SgSylTile tl = stiles[blockIdx.x];
   const SgSyllable& sy = syls[tl.syl];
+  float* __restrict__ out = sy.dst_fs ? fs : out_buf;
   const float inv_max = 1.f / maxes[sy.max_slot];
   const int pend = sy.piece0 + sy.npiece;
   const int64_t kt = tl.k0 + 4 * (int64_t)threadIdx.x;
@@ -371,6 +314,6 @@ void launch_syl_max(const DevicePlan& D, int64_t s0, int64_t n_syls, hipStream_t
 void launch_harm_finalize(const DevicePlan& D, int64_t f0, int64_t n_stiles, float* out, hipStream_t s) {
   if (n_stiles <= 0) return;
   hipLaunchKernelGGL(sg_harm_finalize, dim3((unsigned)n_stiles), dim3(256), 0, s, D.syl_tiles + f0, D.pieces, D.syls,
-                     D.cknots, D.W, D.maxes, out);
+                     D.cknots, D.W, D.maxes, out, D.fs);
 }
 }  // namespace sg

@@ -37,6 +37,27 @@ struct Batch {
   std::vector<SgSylTile> syl_tiles;
   std::vector<SgSylTile> ptiles;   // tiles over multi-term (crossfade) pieces
   std::vector<Slice> slices;
+  // ---- spectral part (noise, formant filter, assembly) ----
+  std::vector<float> fl;                 // host-initialised floats (windows, twiddles, uniforms, envelopes, ...)
+  int64_t fs_total = 0;                  // scratch floats (frames, sounds, raw noise)
+  std::vector<SgFftGeom> geoms;
+  std::vector<SgFrame> frames[2];        // [0] noise frames, [1] filter frames
+  std::vector<int32_t> frame_geom[2];
+  std::vector<SgOla> olas[2];            // [0] noise OLAs, [1] filter OLAs (device: [0] then [1])
+  std::vector<SgNoiseItem> items;        // items[].ola indexes the device OLA table
+  std::vector<SgMix> mixes[2];           // [0] pre-filter sounds (fs), [1] final output
+  struct Copy { int64_t fl_off, fs_off, n; };
+  std::vector<Copy> copies;              // fl -> fs before the filter phase
+  // derived (finalize_spec)
+  std::vector<SgFrameGroup> fgroups;
+  int64_t fgroup_split = 0;              // groups [0, split) noise, [split, end) filter
+  int fgroup_lds[2] = {0, 0};            // max dynamic LDS per phase
+  std::vector<SgOla> olas_dev;
+  std::vector<SgOlaTile> olatiles;
+  int64_t olatile_split = 0, ola_split = 0;
+  std::vector<SgMix> mixes_dev;
+  std::vector<SgMixTile> mixtiles;
+  int64_t mixtile_split = 0;
   std::vector<double> cknots;   // contour / linear knot data
   int64_t w_total = 0;          // epoch-waveform scratch (floats)
   // ---- per call ----
@@ -50,8 +71,11 @@ struct Batch {
 
 // Plan one generateHarmonics() call; the finalized syllable is written at
 // `out_off` of the output buffer. Returns the syllable length.
+// to_fs: the syllable goes to a fresh spectral-scratch region (*fs_off), the
+// voiced part of a soundgen() bout, instead of the output buffer.
 int64_t plan_harmonics(Batch& B, const double* pitch, int64_t len, const sg_harm_params& P,
-                       const sg_anchors& amplAnchors, Rng& R, int64_t out_off, bool dry_run);
+                       const sg_anchors& amplAnchors, Rng& R, int64_t out_off, bool dry_run, bool to_fs = false,
+                       int64_t* fs_off = nullptr);
 
 // getSmoothContour() for the lengths/values the planner needs on the host.
 // method: 0 loess (default; only 1, 2 or >10 anchors supported), 1 spline.
@@ -70,6 +94,30 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a, Rng& R, int64_t out_o
 void restore_soundgen_tail(Batch& B, int first_syl);
 // Build derived tables (piece tiles) once all calls are planned.
 void finalize_plan(Batch& B);
+void finalize_spec(Batch& B);
+
+// ---- spectral planning (sg_plan_spec.cpp) ----
+// FFT geometry of window length wl (cached per wl); SG_E_UNSUPPORTED if
+// wl/2 has a prime factor > 31.
+int geometry(Batch& B, int wl);
+int64_t fs_alloc(Batch& B, int64_t n);
+int64_t fl_push(Batch& B, const double* v, int64_t n);
+// STFT(hamming) x env -> ISTFT(hann) of the fs sound [sound, sound + L)
+// (R/soundgen.R:743-806). env: nr x env_nc (column-major); returns the
+// filter OLA index (phase 1); *out_len = istft length.
+int plan_filter(Batch& B, int64_t sound, int64_t L, int wl, double overlap, const vec& env, int64_t env_nc,
+                int64_t* out_len, int64_t* out_fs);
+// generateNoise(), R/source.R:57-138: returns a noise item (off = 0);
+// ok == false when the noise contour is NA (R returns zeros).
+bool plan_noise(Batch& B, Rng& R, int64_t len, const sg_anchors& noiseAnchors, double rolloffNoise,
+                double attackLen, int wl, double sr, double overlap, const double* filterNoise, int64_t fnc,
+                SgNoiseItem* item);
+// getSpectralEnvelope(), R/sourceSpectrum.R:261-566 (host, fp64), nr x nc column-major
+vec spectral_envelope(Rng& R, int64_t nr, int64_t nc, const sg_formants* F, double formantDep, double rolloffLip,
+                      const sg_anchors& mouthAnchors, double mouthOpenThres, double openMouthBoost,
+                      double vocalTract, double temperature, double formDrift, double formDisp,
+                      double formantDepStoch, double smoothLinearFactor, double sr, double speedSound);
+vec sigmoid_half(double sr, double freq, double shape, double spikiness);
 
 // getRolloff() with per-gc vector parameters (R/sourceSpectrum.R:71-186)
 vec get_rolloff(const vec& pitch, int64_t nH, const vec& rolloff, const vec& rolloffOct, double rolloffParab,

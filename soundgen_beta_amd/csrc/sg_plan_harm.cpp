@@ -500,7 +500,8 @@ static void cross_fade(Chain& A, const HostEpoch& W, int64_t e, double sr, doubl
 
 // ----------------------------------------------------------- planner
 int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_harm_params& P,
-                       const sg_anchors& amplAnchors, Rng& R, int64_t out_off, bool dry_run) {
+                       const sg_anchors& amplAnchors, Rng& R, int64_t out_off, bool dry_run, bool to_fs,
+                       int64_t* fs_off) {
   const double sr = P.samplingRate;
   if (len < 2) throw SgError(SG_E_DOMAIN, "generateHarmonics: pitch contour too short");
   vec pitch(pitch_in, pitch_in + len);
@@ -647,12 +648,17 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
   for (size_t e = 0; e < mats.size(); ++e) cross_fade(A, HE[e], (int64_t)e, sr, 15);
   const int64_t Lsyl = A.L();
   if (dry_run) return Lsyl;
+  if (to_fs) {
+    out_off = fs_alloc(B, Lsyl);
+    if (fs_off) *fs_off = out_off;
+  }
 
   // ------------------------------------------------ emit device arrays
   const int32_t syl_idx = (int32_t)B.syls.size();
   SgSyllable sy{};
   sy.L = Lsyl;
   sy.out_off = out_off;
+  sy.dst_fs = to_fs ? 1 : 0;
   sy.max_slot = syl_idx;
   const double lf = P.attackLen > 0 ? std::floor(P.attackLen * sr / 1000) : 0;
   sy.fade = (int32_t)(lf >= 2 ? std::min<double>(lf, (double)Lsyl) : 0);

@@ -1,0 +1,484 @@
+// sg_plan_spec.cpp — host planner of the spectral part: FFT geometries,
+// noise (generateNoise(), R/source.R:57-138), formant filter
+// (R/soundgen.R:743-807, seewave stft/istft), getSpectralEnvelope()
+// (R/sourceSpectrum.R:261-566) and getSigmoid() (R/utilities_math.R:639-653).
+// Lengths, frame starts and trims are integers computed here in fp64 with
+// R's operation order; per-sample work runs in sg_fft.hip.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "sg_plan.h"
+
+namespace sg {
+
+namespace {
+constexpr int kRadices[] = {4, 2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31};
+constexpr int kLdsBudget = 72 * 1024;  // two workgroups per CU
+}  // namespace
+
+int64_t fs_alloc(Batch& B, int64_t n) {
+  const int64_t o = B.fs_total;
+  B.fs_total += (n + 63) / 64 * 64;
+  return o;
+}
+
+int64_t fl_push(Batch& B, const double* v, int64_t n) {
+  const int64_t o = (int64_t)B.fl.size();
+  for (int64_t i = 0; i < n; ++i) B.fl.push_back((float)v[i]);
+  while (B.fl.size() % 4) B.fl.push_back(0.f);  // 16-B aligned blocks
+  return o;
+}
+
+int geometry(Batch& B, int wl) {
+  for (size_t i = 0; i < B.geoms.size(); ++i)
+    if (B.geoms[i].wl == wl) return (int)i;
+  if (wl < 4 || wl % 2) throw SgError(SG_E_UNSUPPORTED, "FFT: window length must be even and >= 4");
+  SgFftGeom g{};
+  g.wl = wl;
+  g.M = wl / 2;
+  int m = g.M;
+  for (int r : kRadices) {
+    while (m % r == 0) {
+      if (g.nstages >= SG_FFT_MAX_STAGES) throw SgError(SG_E_UNSUPPORTED, "FFT: too many stages");
+      g.radix[g.nstages++] = r;
+      m /= r;
+    }
+  }
+  if (m != 1)
+    throw SgError(SG_E_UNSUPPORTED, "FFT: window length " + std::to_string(wl) + " has a prime factor > 31");
+  // twiddles W_M^t (t < M), W_N^k (k < M), fp64 -> fp32
+  vec tw(4 * (size_t)g.M);
+  for (int t = 0; t < g.M; ++t) {
+    const double a = -2.0 * M_PI * (double)t / (double)g.M;
+    tw[2 * t] = std::cos(a);
+    tw[2 * t + 1] = std::sin(a);
+    const double b = -2.0 * M_PI * (double)t / (double)wl;
+    tw[2 * g.M + 2 * t] = std::cos(b);
+    tw[2 * g.M + 2 * t + 1] = std::sin(b);
+  }
+  g.tw = fl_push(B, tw.data(), (int64_t)tw.size());
+  // seewave ftwindow: hamming.w (seewave.r:7431-7437), hanning.w (:7444-7450)
+  vec win(2 * (size_t)wl);
+  for (int i = 0; i < wl; ++i) {
+    win[i] = 0.54 - 0.46 * std::cos(2 * M_PI * (double)i / (double)(wl - 1));
+    win[wl + i] = 0.5 - 0.5 * std::cos(2 * M_PI * (double)i / (double)(wl - 1));
+  }
+  g.win = fl_push(B, win.data(), (int64_t)win.size());
+  // frames per workgroup: twiddles 2M + two ping-pong buffers fb*M (float2)
+  const int per_frame = 2 * g.M * 8;
+  g.fb = std::max(1, std::min(8, (kLdsBudget - 2 * g.M * 8) / per_frame));
+  g.lds_bytes = (2 * g.M + 2 * g.fb * g.M) * 8;
+  if (g.lds_bytes > 160 * 1024) throw SgError(SG_E_UNSUPPORTED, "FFT: window too long for LDS");
+  B.geoms.push_back(g);
+  return (int)B.geoms.size() - 1;
+}
+
+// istft() frame bookkeeping shared by noise and filter: hop, xlen, W0 scale
+struct IstftGeom {
+  double h;
+  int64_t xlen;
+  float scale;
+};
+static IstftGeom istft_geom(int wl, int64_t nc, double ovlp) {
+  IstftGeom g;
+  g.h = (double)wl * (100 - ovlp) / 100;
+  g.xlen = (int64_t)((double)wl + (double)(nc - 1) * g.h);  // numeric(xlen) truncates
+  long double W0 = 0;
+  for (int i = 0; i < wl; ++i) {
+    const double w = 0.5 - 0.5 * std::cos(2 * M_PI * (double)i / (double)(wl - 1));
+    W0 += w * w;
+  }
+  g.scale = (float)(g.h / (double)W0);
+  return g;
+}
+
+static int push_ola(Batch& B, int phase, int64_t frames, int64_t nframes, int wl, const IstftGeom& ig, int64_t first,
+                    int64_t len, int64_t out) {
+  SgOla o{};
+  o.frames = frames;
+  o.out = out;
+  o.first = first;
+  o.len = len;
+  o.xlen = ig.xlen;
+  o.h = ig.h;
+  o.nframes = (int32_t)nframes;
+  o.wl = wl;
+  o.scale = ig.scale;
+  B.olas[phase].push_back(o);
+  return (int)B.olas[phase].size() - 1;
+}
+
+int plan_filter(Batch& B, int64_t sound, int64_t L, int wl, double overlap, const vec& env, int64_t env_nc,
+                int64_t* out_len, int64_t* out_fs) {
+  const int gi = geometry(B, wl);
+  const int64_t nr = wl / 2;
+  // step = seq(1, max(1, L - wl), by = wl - overlap * wl / 100)   R/soundgen.R:744-748
+  const double by = (double)wl - overlap * (double)wl / 100;
+  const vec step = r_seq_by(1, (double)std::max<int64_t>(1, L - wl), by);
+  const int64_t nc = (int64_t)step.size();
+  if (env_nc != 1 && env_nc != nc) throw SgError(SG_E_ARG, "formant filter: envelope columns != frames");
+  for (double x0 : step)
+    if ((int64_t)x0 - 1 + wl > L) throw SgError(SG_E_DOMAIN, "stft: frame beyond the sound");
+  const int64_t env_off = fl_push(B, env.data(), (int64_t)env.size());
+  const int64_t fr = fs_alloc(B, nc * wl);
+  for (int64_t c = 0; c < nc; ++c) {
+    SgFrame f{};
+    f.src = sound + (int64_t)step[c] - 1;  // wave[x:(x + wl - 1)], x truncated
+    f.env = env_off + (env_nc == 1 ? 0 : c * nr);
+    f.dst = fr + c * wl;
+    B.frames[1].push_back(f);
+    B.frame_geom[1].push_back(gi);
+  }
+  const IstftGeom ig = istft_geom(wl, nc, overlap);
+  const int64_t out = fs_alloc(B, ig.xlen);
+  B.fft_frames += nc;
+  *out_len = ig.xlen;
+  *out_fs = out;
+  return push_ola(B, 1, fr, nc, wl, ig, 0, ig.xlen, out);
+}
+
+bool plan_noise(Batch& B, Rng& R, int64_t len, const sg_anchors& noiseAnchors, double rolloffNoise,
+                double attackLen, int wl, double sr, double overlap, const double* filterNoise, int64_t fnc,
+                SgNoiseItem* item) {
+  // breathingStrength = getSmoothContour(noiseAnchors, len, valueFloor = -120, valueCeiling = 40)
+  //   R/source.R:70-81 (NA when len == 0 or anchors NA)
+  if (noiseAnchors.n <= 0 || len <= 0) return false;
+  SgContour strength = contour_desc(B, noiseAnchors, len, true, -120, true, 40, true);
+  // step = seq(1, len + wl, by = hop); nr = wl / 2; nc = length(step)   R/source.R:88-94
+  const int gi = geometry(B, wl);
+  const double hop = (double)wl - overlap * (double)wl / 100;
+  const int64_t nc = (int64_t)r_seq_by(1, (double)(len + wl), hop).size();
+  const int64_t nr = wl / 2;
+  // filter = [filterNoise or 1] * 2^(rolloffNoise / 10 * log2(1:nr)); column index per frame
+  //   round(seq(1, ncol(filter), length.out = nc))   R/source.R:95-114
+  const int64_t ncolF = filterNoise ? fnc : 1;
+  vec filt((size_t)(nr * ncolF));
+  for (int64_t c = 0; c < ncolF; ++c)
+    for (int64_t k = 0; k < nr; ++k)
+      filt[c * nr + k] = (filterNoise ? filterNoise[c * nr + k] : 1.0) *
+                         std::pow(2.0, rolloffNoise / 10 * std::log2((double)(k + 1)));
+  const int64_t filt_off = fl_push(B, filt.data(), (int64_t)filt.size());
+  vec fri((size_t)nc, 1.0);
+  if (filterNoise) {
+    const vec s = r_seq_len(1, (double)ncolF, nc);
+    for (int64_t c = 0; c < nc; ++c) fri[c] = r_round(s[c]);
+  }
+  // z1 = complex(real = runif(nr * nc)), column-major: bin fastest   R/source.R:111
+  vec u((size_t)(nr * nc));
+  for (auto& x : u) x = R.unif();
+  const int64_t u_off = fl_push(B, u.data(), (int64_t)u.size());
+  const int64_t fr = fs_alloc(B, nc * wl);
+  for (int64_t c = 0; c < nc; ++c) {
+    SgFrame f{};
+    f.src = u_off + c * nr;
+    f.env = filt_off + ((int64_t)fri[c] - 1) * nr;
+    f.dst = fr + c * wl;
+    B.frames[0].push_back(f);
+    B.frame_geom[0].push_back(gi);
+  }
+  // istft, then matchLengths(breathing, len, 'central')   R/utilities_math.R:413-444
+  const IstftGeom ig = istft_geom(wl, nc, overlap);
+  int64_t first = 0;
+  if (ig.xlen != len) {
+    const int64_t padded = ig.xlen < len ? ig.xlen + 2 * len : ig.xlen;
+    const double halflen = (double)len / 2, center = (1 + (double)padded) / 2;
+    const int64_t start = (int64_t)std::ceil(center - halflen);  // 1-based in the padded vector
+    first = start - 1 - (ig.xlen < len ? len : 0);
+  }
+  const int64_t raw = fs_alloc(B, len);
+  const int ola = push_ola(B, 0, fr, nc, wl, ig, first, len, raw);
+  B.fft_frames += nc;
+  item->raw = raw;
+  item->len = len;
+  item->off = 0;
+  item->ola = ola;  // phase-0 index == device index (noise OLAs come first)
+  const double lf = std::floor(attackLen * sr / 1000);
+  item->fade = (int32_t)(lf >= 2 ? std::min<double>(lf, (double)len) : 0);
+  item->strength = strength;
+  return true;
+}
+
+vec sigmoid_half(double sr, double freq, double shape, double spikiness) {
+  // getSigmoid(), R/utilities_math.R:639-653: seq(from, to, length.out = sr / freq / 2)
+  // (length.out rounded up), logistic, zeroOne
+  const double from = -std::exp(-shape * spikiness), to = std::exp(shape * spikiness);
+  const double slope = std::exp(std::fabs(shape)) * 5;
+  const int64_t lo = (int64_t)std::ceil(sr / freq / 2);
+  vec a = r_seq_len(from, to, lo);
+  for (auto& v : a) v = 1 / (1 + std::exp(-v * slope));
+  const double mn = r_min(a);
+  for (auto& v : a) v -= mn;
+  const double mx = r_max(a);
+  for (auto& v : a) v /= mx;
+  return a;
+}
+
+// ------------------------------------------------------------ envelope
+namespace {
+struct Track {
+  vec time, freq, amp, width;
+};
+vec col_upsample(const double* t, const double* y, int64_t np, int64_t nPoints, double slf, int64_t nc) {
+  // spline(approx(y, n = nPoints + 2^slf, x = time)$y, n = nc)   R/sourceSpectrum.R:326-335
+  if (np <= 1) return vec((size_t)nc, y[0]);
+  const vec xt(t, t + np), yt(y, y + np);
+  const vec a = r_approx_n(xt, yt, (int64_t)((double)nPoints + std::pow(2.0, slf)));
+  vec xs(a.size());
+  for (size_t i = 0; i < xs.size(); ++i) xs[i] = (double)(i + 1);
+  return r_spline(xs, a, nc);
+}
+}  // namespace
+
+vec spectral_envelope(Rng& R, int64_t nr, int64_t nc, const sg_formants* F, double formantDep, double rolloffLip,
+                      const sg_anchors& mouthAnchors, double mouthOpenThres, double openMouthBoost,
+                      double vocalTract, double temperature, double formDrift, double formDisp,
+                      double formantDepStoch, double slf, double sr, double speedSound) {
+  int nF = F ? F->n_formants : 0;
+  bool vtNull = std::isnan(vocalTract);
+  double VT = vocalTract;
+  std::vector<int32_t> np;
+  vec t0, f0, a0, w0;  // concatenated input formants
+  int f1_index = F ? F->f1_index : -1;
+  if (nF > 0) {
+    int64_t tot = 0;
+    for (int f = 0; f < nF; ++f) { np.push_back(F->n_points[f]); tot += F->n_points[f]; }
+    t0.assign(F->time, F->time + tot);
+    f0.assign(F->freq, F->freq + tot);
+    a0.assign(F->amp, F->amp + tot);
+    w0.assign(F->width, F->width + tot);
+  }
+  // vocalTract guessed from formant dispersion when NULL   R/sourceSpectrum.R:293-307
+  if (vtNull && nF > 0) {
+    double fd = NAN;
+    if (f0.size() >= 2) {
+      vec d(f0.size() - 1);
+      for (size_t i = 0; i + 1 < f0.size(); ++i) d[i] = f0[i + 1] - f0[i];
+      fd = r_mean(d);
+    }
+    VT = speedSound / 2 / fd;
+    vtNull = false;
+  }
+  // schwa from vocalTract when formants are NA   R/sourceSpectrum.R:309-322
+  if (nF == 0 && !vtNull) {
+    const double fr = speedSound / 4 / VT;
+    np = {1};
+    t0 = {0};
+    f0 = {fr};
+    a0 = {30};
+    w0 = {50 * (1 + fr * fr / 6 / 1e6)};
+    nF = 1;
+    f1_index = 0;
+  }
+  vec env((size_t)(nr * nc), 0.0);
+  vec mouth((size_t)nc, 0.5), mbin((size_t)nc, 1.0);
+  if (nF > 0) {
+    int64_t nPoints = 0;
+    for (int f = 0; f < nF; ++f) nPoints = std::max<int64_t>(nPoints, np[f]);
+    std::vector<Track> fu(nF);
+    int64_t off = 0;
+    for (int f = 0; f < nF; ++f) {
+      fu[f].time = col_upsample(&t0[off], &t0[off], np[f], nPoints, slf, nc);
+      fu[f].freq = col_upsample(&t0[off], &f0[off], np[f], nPoints, slf, nc);
+      fu[f].amp = col_upsample(&t0[off], &a0[off], np[f], nPoints, slf, nc);
+      fu[f].width = col_upsample(&t0[off], &w0[off], np[f], nPoints, slf, nc);
+      off += np[f];
+    }
+    if (temperature > 0) {  // stochastic formants   R/sourceSpectrum.R:347-415
+      double fdisp;
+      if (vtNull && nF > 1) {
+        vec c2(nF);
+        int64_t o2 = 0;
+        for (int f = 0; f < nF; ++f) { c2[f] = f0[o2] - (f ? f0[o2 - np[f - 1]] : 0); o2 += np[f]; }
+        fdisp = r_mean(c2);
+      } else if (!vtNull) {
+        fdisp = 2 * speedSound / (4 * VT);
+      } else {
+        fdisp = NAN;
+      }
+      const double sdG = fdisp * temperature * formDisp;
+      double fmax = r_max(fu.back().freq);
+      if (!std::isnan(sdG) && formantDepStoch > 0) {
+        while (fmax < (sr / 2 - 1000)) {
+          vec rw = get_random_walk(R, nc, temperature * formDrift, 0, 1, vec{0.0}, false);
+          if (rw.size() > 1) { const double m = r_mean(rw); for (auto& v : rw) v = v - m + 1; }
+          const double g1 = R.rgamma(fdisp * fdisp / (sdG * sdG), fdisp / (sdG * sdG));
+          Track t;
+          t.time = fu[0].time;
+          t.freq.resize(nc);
+          for (int64_t c = 0; c < nc; ++c) t.freq[c] = fu.back().freq[c] + r_round(g1 * rw[rw.size() > 1 ? c : 0]);
+          const double sh = (formantDep / temperature) * (formantDep / temperature);
+          const double rt = formantDepStoch * formantDep / ((formantDepStoch * temperature) * (formantDepStoch * temperature));
+          const double g2 = R.rgamma(sh, rt);
+          t.amp.resize(nc);
+          t.width.resize(nc);
+          for (int64_t c = 0; c < nc; ++c) {
+            t.amp[c] = r_round(g2 * rw[rw.size() > 1 ? c : 0]);
+            t.width[c] = 50 + (std::log2(t.freq[c]) - 5) * 20;
+          }
+          fu.push_back(t);
+          fmax = r_max(fu.back().freq);
+        }
+      }
+      for (auto& tr : fu)
+        for (int cc = 0; cc < 3; ++cc) {
+          vec rw = get_random_walk(R, nc, temperature * formDrift, 0.3, 1, vec{}, true);
+          if (rw.size() > 1) { const double m = r_mean(rw); for (auto& v : rw) v = v - m + 1; }
+          vec& col = cc == 0 ? tr.freq : cc == 1 ? tr.amp : tr.width;
+          for (int64_t c = 0; c < nc; ++c) col[c] *= rw[rw.size() > 1 ? c : 0];
+        }
+    }
+    // Hz -> bins   R/sourceSpectrum.R:417-424
+    const double bw = sr / 2 / (double)nr;
+    for (auto& tr : fu)
+      for (int64_t c = 0; c < nc; ++c) {
+        tr.freq[c] = (tr.freq[c] - bw / 2) / bw + 1;
+        tr.width[c] = tr.width[c] / bw;
+      }
+    // mouth opening   R/sourceSpectrum.R:426-456
+    bool mouthNA = mouthAnchors.n < 1;
+    for (int i = 0; i < mouthAnchors.n; ++i)
+      if (std::isnan(mouthAnchors.value[i]) || std::isnan(mouthAnchors.time[i])) mouthNA = true;
+    if (!mouthNA) {
+      vec mo;
+      if (!smooth_contour(mouthAnchors, nc, false, 0, true, 0, true, 1, mo)) mo.assign(nc, 0.5);
+      for (int64_t c = 0; c < nc; ++c) {
+        double v = mo[c];
+        if (v < mouthOpenThres) v = 0;
+        mouth[c] = v;
+        mbin[c] = v > 0 ? 1 : 0;
+      }
+    }
+    const bool adj = !vtNull && std::isfinite(VT);
+    for (auto& tr : fu)
+      for (int64_t c = 0; c < nc; ++c) {
+        double ab = 0;
+        if (adj) {
+          const double ah = (mouth[c] - 0.5) * speedSound / (4 * VT);
+          ab = (ah - bw / 2) / bw + 1;
+        }
+        tr.freq[c] += ab;
+        if (tr.freq[c] < 1) tr.freq[c] = 1;
+      }
+    // nasalization when the mouth is closed   R/sourceSpectrum.R:469-504
+    bool anyClosed = false;
+    for (int64_t c = 0; c < nc; ++c) if (mbin[c] == 0) anyClosed = true;
+    if (anyClosed && f1_index >= 0) {
+      Track p = fu[f1_index], z = fu[f1_index];
+      Track& f1 = fu[f1_index];
+      for (int64_t c = 0; c < nc; ++c) {
+        p.amp[c] = 0;
+        if (mbin[c] == 0) {
+          p.amp[c] = f1.amp[c] * 2 / 3;
+          p.width[c] = f1.width[c] * 2 / 3;
+          p.freq[c] = (f1.freq[c] > 550 / bw) ? f1.freq[c] - 250 / bw : f1.freq[c] + 250 / bw;
+        }
+      }
+      for (int64_t c = 0; c < nc; ++c) {
+        z.amp[c] = 0;
+        if (mbin[c] == 0) {
+          z.amp[c] = -f1.amp[c] * 2 / 3;
+          z.freq[c] = (p.freq[c] + f1.freq[c]) / 2;
+          z.width[c] = p.width[c];
+        }
+      }
+      for (int64_t c = 0; c < nc; ++c)
+        if (mbin[c] == 0) { f1.amp[c] = f1.amp[c] * 4 / 5; f1.width[c] = f1.width[c] * 5 / 4; }
+      fu.push_back(p);
+      fu.push_back(z);
+    }
+    // dgamma(1:nr, shape = mu^2/sd^2, rate = mu/sd^2), normalised by its max   R/sourceSpectrum.R:507-522
+    vec col((size_t)nr);
+    for (const auto& tr : fu)
+      for (int64_t c = 0; c < nc; ++c) {
+        const double mg = tr.freq[c];
+        double sdg = tr.width[c];
+        if (sdg == 0) sdg = 1;
+        const double shape = mg * mg / (sdg * sdg), rate = mg / (sdg * sdg);
+        double lmax = -INFINITY;
+        for (int64_t k = 0; k < nr; ++k) {
+          const double x = (double)(k + 1);
+          const double l = (shape == 1) ? -rate * x : (shape - 1) * std::log(x) - rate * x;
+          col[k] = l;
+          if (l > lmax) lmax = l;
+        }
+        for (int64_t k = 0; k < nr; ++k) env[c * nr + k] += std::exp(col[k] - lmax) * tr.amp[c];
+      }
+    for (auto& v : env) v *= formantDep;
+  }
+  // lip radiation, open-mouth boost, dB -> linear (2^(x/10))   R/sourceSpectrum.R:524-541
+  for (int64_t c = 0; c < nc; ++c)
+    for (int64_t k = 0; k < nr; ++k) {
+      const double lip = rolloffLip * std::log2((double)(k + 1));
+      env[c * nr + k] = (env[c * nr + k] + lip * mbin[c]) * std::pow(2.0, mouth[c] * openMouthBoost / 10);
+    }
+  for (auto& v : env) v = std::pow(2.0, v / 10);
+  return env;
+}
+
+// ------------------------------------------------------------ finalize
+void finalize_spec(Batch& B) {
+  // frame groups: per phase, frames of one geometry in runs of g.fb
+  B.fgroups.clear();
+  for (int ph = 0; ph < 2; ++ph) {
+    if (ph == 1) B.fgroup_split = (int64_t)B.fgroups.size();
+    // frames are emitted per call; sort them by geometry keeping order
+    std::vector<int64_t> idx(B.frames[ph].size());
+    for (size_t i = 0; i < idx.size(); ++i) idx[i] = (int64_t)i;
+    std::stable_sort(idx.begin(), idx.end(),
+                     [&](int64_t a, int64_t b) { return B.frame_geom[ph][a] < B.frame_geom[ph][b]; });
+    std::vector<SgFrame> fr(idx.size());
+    std::vector<int32_t> fg(idx.size());
+    for (size_t i = 0; i < idx.size(); ++i) { fr[i] = B.frames[ph][idx[i]]; fg[i] = B.frame_geom[ph][idx[i]]; }
+    B.frames[ph] = fr;
+    B.frame_geom[ph] = fg;
+    const int32_t base = ph == 0 ? 0 : (int32_t)B.frames[0].size();
+    int lds = 0;
+    for (size_t i = 0; i < fr.size();) {
+      const int gi = fg[i];
+      const SgFftGeom& g = B.geoms[gi];
+      size_t j = i;
+      while (j < fr.size() && fg[j] == gi && (int)(j - i) < g.fb) ++j;
+      B.fgroups.push_back(SgFrameGroup{gi, ph == 0 ? SG_FRAME_NOISE : SG_FRAME_FILTER, base + (int32_t)i,
+                                       (int32_t)(j - i)});
+      lds = std::max(lds, g.lds_bytes);
+      i = j;
+    }
+    B.fgroup_lds[ph] = lds;
+  }
+  // OLAs: device table [noise..., filter...]; tiles per phase
+  B.olas_dev.clear();
+  B.olatiles.clear();
+  B.ola_split = (int64_t)B.olas[0].size();
+  for (int ph = 0; ph < 2; ++ph) {
+    if (ph == 1) B.olatile_split = (int64_t)B.olatiles.size();
+    for (const SgOla& o0 : B.olas[ph]) {
+      SgOla o = o0;
+      o.tile0 = (int32_t)B.olatiles.size();
+      const int32_t oi = (int32_t)B.olas_dev.size();
+      for (int64_t q0 = 0; q0 < o.len; q0 += SG_OLA_TILE) B.olatiles.push_back(SgOlaTile{oi, 0, q0});
+      B.olas_dev.push_back(o);
+    }
+  }
+  // items and mixes referring to filter-phase OLAs: device index = ola_split + i
+  for (SgNoiseItem& it : B.items)
+    if (it.flags & SG_ITEM_FILTER_OLA) {
+      it.ola += (int32_t)B.ola_split;
+      it.flags &= ~SG_ITEM_FILTER_OLA;
+    }
+  // mixes: [pre-filter..., final...]
+  B.mixes_dev.clear();
+  B.mixtiles.clear();
+  for (int ph = 0; ph < 2; ++ph) {
+    if (ph == 1) B.mixtile_split = (int64_t)B.mixtiles.size();
+    for (const SgMix& m0 : B.mixes[ph]) {
+      const int32_t mi = (int32_t)B.mixes_dev.size();
+      for (int64_t k0 = 0; k0 < m0.len; k0 += SG_MIX_TILE) B.mixtiles.push_back(SgMixTile{mi, 0, k0});
+      SgMix m = m0;
+      if (m.base_kind == SG_BASE_NORM) m.base_ola += (int32_t)B.ola_split;
+      B.mixes_dev.push_back(m);
+    }
+  }
+}
+
+}  // namespace sg

@@ -74,6 +74,13 @@ def lib():
     L.sg_generate_harmonics.argtypes = [vp, dp, i64, C.POINTER(_abi.sg_harm_params), _abi.sg_anchors,
                                         C.POINTER(_abi.sg_random), dp, i64, i64p]
     L.sg_soundgen.argtypes = [vp, C.POINTER(_abi.sg_soundgen_args), C.POINTER(_abi.sg_random), dp, i64, i64p]
+    L.sg_formant_filter.argtypes = [vp, dp, i64, dp, C.c_int32, C.c_int32, C.c_double, dp, i64, i64p]
+    L.sg_generate_noise.argtypes = [vp, i64, _abi.sg_anchors, C.c_double, C.c_double, C.c_int32, C.c_double,
+                                    C.c_double, C.c_double, dp, C.c_int32, C.POINTER(_abi.sg_random), dp]
+    L.sg_spectral_envelope.argtypes = [vp, C.c_int32, C.c_int32, C.POINTER(_abi.sg_formants), C.c_double,
+                                       C.c_double, _abi.sg_anchors, C.c_double, C.c_double, C.c_double,
+                                       C.c_double, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double,
+                                       C.c_double, C.POINTER(_abi.sg_random), dp]
     L.sg_get_rolloff.argtypes = [dp, C.c_int32, C.c_int32] + [C.c_double] * 8 + [dp, C.POINTER(C.c_int32)]
     L.sg_abi_version.restype = C.c_int
     _lib = L

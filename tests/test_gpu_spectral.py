@@ -1,0 +1,54 @@
+"""GPU parity of the spectral path (sg_fft.hip) and of whole soundgen() calls
+against the oracle, same inputs and draws. Tolerance: RMS <= 1e-5 on the
+normalised waveform (north star); lengths bit-exact."""
+import numpy as np
+import pytest
+
+from test_spectral_cpu import FORMANTS_A, MOVING, N, SOUNDGEN_CASES, U
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+
+def _rms(a, b):
+    return float(np.sqrt(np.mean((np.asarray(a, np.float64) - b) ** 2)))
+
+
+@pytest.mark.parametrize("wl", [440, 800, 1764, 2204])
+def test_formant_filter_vs_oracle(oracle, wl):
+    from soundgen_beta_amd import api
+    rng = np.random.default_rng(wl)
+    sound = np.sin(np.cumsum(rng.uniform(0.01, 0.2, 20 * wl))) + 0.1 * rng.normal(size=20 * wl)
+    nr = wl // 2
+    step = np.arange(1, max(1, len(sound) - wl) + 1, wl // 4)
+    for env in (np.abs(rng.normal(1, 0.3, size=(nr, 1))), np.abs(rng.normal(1, 0.3, size=(nr, len(step))))):
+        got = api.formantFilter(sound, env, wl, 75)
+        want = oracle.formant_filter(sound, env, wl, 75)
+        assert len(got) == len(want)
+        assert _rms(got, want) <= TOL
+
+
+@pytest.mark.parametrize("wl,sr", [(800, 16000), (2204, 44100), (440, 44100)])
+def test_generate_noise_vs_oracle(oracle, wl, sr):
+    from soundgen_beta_amd import api
+    na = {"time": [0, 1000], "value": [-30, -10]}
+    for L, filt in ((sr, None), (sr // 3, np.abs(np.random.default_rng(3).normal(1, .5, size=(wl // 2, 5))))):
+        got = api.generateNoise(L, na, rolloffNoise=-6, attackLen=20, windowLength_points=wl, samplingRate=sr,
+                                filterNoise=filt, uniforms=U)
+        want = oracle.generate_noise(L, na, rolloffNoise=-6, attackLen=20, windowLength_points=wl, samplingRate=sr,
+                                     filterNoise=filt, uniforms=U)
+        assert len(got) == len(want)
+        assert _rms(got, want) <= TOL
+
+
+def test_soundgen_cases_one_batch(oracle):
+    from soundgen_beta_amd import batch
+    names = sorted(SOUNDGEN_CASES)
+    calls = [{"kind": "soundgen", "args": SOUNDGEN_CASES[n], "normals": N, "uniforms": U} for n in names]
+    outs = batch.synthesize(calls)
+    for n, y in zip(names, outs):
+        ref = oracle.soundgen(normals=N, uniforms=U, **SOUNDGEN_CASES[n])
+        assert len(y) == len(ref), n
+        r = _rms(y, ref)
+        print(n, "rms", r)
+        assert r <= TOL, (n, r)

@@ -1,0 +1,67 @@
+"""CPU: host parts of the spectral path — getSpectralEnvelope (host, fp64)
+against the oracle, and soundgen() planning: every output length (syllables,
+pauses, noise trims, istft lengths, bouts, silence) bit-exact with the oracle."""
+import numpy as np
+import pytest
+
+from soundgen_beta_amd import api, batch
+
+U = np.random.default_rng(1).uniform(size=3_000_000)
+N = np.random.default_rng(2).standard_normal(200_000)
+
+FORMANTS_A = {"f1": {"time": 0, "freq": 860, "amp": 30, "width": 120},
+              "f2": {"time": 0, "freq": 1280, "amp": 40, "width": 120},
+              "f3": {"time": 0, "freq": 2900, "amp": 25, "width": 200}}
+MOVING = {"f1": {"time": [0, 1], "freq": [700, 300], "amp": [30, 30], "width": [100, 100]},
+          "f2": {"time": [0, .5, 1], "freq": [1200, 1800, 2400], "amp": [40, 40, 40], "width": [120, 120, 150]}}
+
+
+@pytest.mark.parametrize("fm,nc,extra", [
+    (FORMANTS_A, 1, {}),
+    (MOVING, 37, {}),
+    ("a", 1, dict(vocalTract=15.5)),
+    ("u", 25, dict(mouthAnchors={"time": [0, 1], "value": [0, 0.8]}, mouthOpenThres=0.2, openMouthBoost=5)),
+    (None, 1, dict(vocalTract=17)),  # schwa from vocalTract
+])
+def test_spectral_envelope_matches_oracle(oracle, fm, nc, extra):
+    kw = dict(formants=fm, samplingRate=44100, **extra)
+    got = api.getSpectralEnvelope(1102, nc, **kw)
+    want = oracle.spectral_envelope(1102, nc, **kw)
+    np.testing.assert_allclose(got, want, rtol=1e-12, atol=0)
+
+
+def test_spectral_envelope_stochastic_same_draws(oracle):
+    kw = dict(formants=FORMANTS_A, samplingRate=16000, temperature=0.1, vocalTract=15)
+    got = api.getSpectralEnvelope(400, 9, rng=np.random.default_rng(9), **kw)
+    want = oracle.spectral_envelope(400, 9, rng=np.random.default_rng(9), **kw)
+    np.testing.assert_allclose(got, want, rtol=1e-12)
+
+
+SOUNDGEN_CASES = {
+    # C1 parity pin: presets$M1$Vowel1 defaults, sylLen 1000 @16 kHz, 2-anchor pitch
+    "c1_pin": dict(sylLen=1000, samplingRate=16000, temperature=0, addSilence=0, pitchAnchors=[100, 150]),
+    "c3_vowel_breathing": dict(sylLen=2000, samplingRate=44100, temperature=0, addSilence=0, windowLength=50,
+                               overlap=75, formants="a", pitchAnchors=[120, 200],
+                               noiseAnchors={"time": [0, 2000], "value": [-25, -25]}, formantsNoise=None),
+    "multi_syl_bouts": dict(sylLen=500, samplingRate=16000, temperature=0, pitchAnchors=[300, 250], nSyl=3,
+                            repeatBout=2, pauseLen=100),
+    "post_noise_am": dict(sylLen=700, samplingRate=22050, temperature=0, pitchAnchors=[180, 140],
+                          noiseAnchors={"time": [-50, 700], "value": [-10, -30]}, formantsNoise="s",
+                          amDep=40, amFreq=25, amShape=0.3),
+    "moving_formants_global_ampl": dict(sylLen=800, samplingRate=16000, temperature=0, pitchAnchors=[150, 220],
+                                        formants=MOVING, amplAnchorsGlobal={"time": [0, 1], "value": [110, 80]},
+                                        nSyl=2, pauseLen=150),
+    "stochastic": dict(sylLen=400, samplingRate=16000, temperature=0.1, pitchAnchors=[200, 260], nSyl=2,
+                       nonlinBalance=60, subDep=80, jitterDep=1, shimmerDep=5),
+    "noise_only": dict(sylLen=300, samplingRate=16000, temperature=0, pitchAnchors=None,
+                       noiseAnchors={"time": [0, 300], "value": [-20, -20]}),
+}
+
+
+@pytest.mark.parametrize("name", sorted(SOUNDGEN_CASES))
+def test_soundgen_plan_lengths_match_oracle(oracle, name):
+    kw = SOUNDGEN_CASES[name]
+    p = batch.Plan([{"kind": "soundgen", "args": kw, "normals": N, "uniforms": U}], None)
+    assert p.status[0] == 0, p.message(0)
+    y = oracle.soundgen(normals=N, uniforms=U, **kw)
+    assert p.lengths[0] == len(y)
