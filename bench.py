@@ -1,17 +1,21 @@
 """bench.py — synthesized audio samples/s of the soundgen hot path on MI355X.
 
-Workload (BASELINE.json configs[1], the config the metric is quoted on, fits
-one GPU): C2 = 1024 x generateHarmonics(pitch = rep(f0, 3500),
+Default workload (BASELINE.json configs[1], the config the metric is quoted
+on, fits one GPU): C2 = 1024 x generateHarmonics(pitch = rep(f0, 3500),
 samplingRate = 44100, temperature = 0, nonlinBalance = 0, rolloff = -12,
 rolloffOct = -12, rolloffKHz = -6, pitchFloor = 50), f0 log-uniform in
 [80, 400] Hz, numpy PCG64 seed 20261015.
+--config c3 / c4 run the other single-GPU configs:
+  C3 1024 x 2 s vowels, formant filter + breathing noise (uniform draws injected)
+  C4 512 x 3 s, subharmonics + jitter/shimmer, temperature 0.05 (draws injected)
 
-A "step" = one pass of the hot path over the whole batch (plan/upload happen
-before the timed region; inputs are resident in HBM). With N ranks each rank
-synthesizes its own 1024-call shard (weak scaling, no data-path collective);
+A "step" = one pass of the hot path over the whole batch (planning and upload
+happen before the timed region; inputs are resident in HBM). With N ranks each
+rank synthesizes its own shard (weak scaling, no data-path collective);
 time = max over ranks, value = samples of all ranks / time.
 """
 import argparse
+import ctypes as C
 import json
 import os
 import sys
@@ -27,14 +31,71 @@ METRIC = "synthesized audio samples/sec (whole node) @44.1 kHz; RMS error vs R r
 C2_PARAMS = dict(samplingRate=44100, pitchSamplingRate=3500, temperature=0, nonlinBalance=0, attackLen=50,
                  rolloff=-12, rolloffOct=-12, rolloffKHz=-6, rolloffParab=0, rolloffParabHarm=3, pitchFloor=50,
                  pitchCeiling=3500, throwaway=-120)
-HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
-VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9  # wave64 VALU lane-ops/s (78.6e12)
+HBM_PEAK_GBS = 8000.0                 # MI355X_MICROARCH.md chip table (spec)
+VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9  # lane-ops/s: 256 CU x 4 SIMD-32 x 2.4 GHz (one op per lane per cycle)
+
+
+def _rng(rank, salt):
+    return np.random.Generator(np.random.PCG64(SEED + 7919 * rank + salt))
 
 
 def c2_calls(n_calls, rank=0):
-    rng = np.random.Generator(np.random.PCG64(SEED + 7919 * rank))
+    rng = _rng(rank, 0)
     f0 = np.exp(rng.uniform(np.log(80.0), np.log(400.0), n_calls))
     return [{"kind": "harmonics", "pitch": np.full(3500, f), "params": C2_PARAMS} for f in f0]
+
+
+def c3_calls(n_calls, rank=0):
+    rng = _rng(rank, 3)
+    vowels = np.array(list("aoieu0"))
+    v = rng.choice(vowels, n_calls)
+    a = np.exp(rng.uniform(np.log(90), np.log(250), n_calls))
+    b = np.exp(rng.uniform(np.log(90), np.log(250), n_calls))
+    n = rng.uniform(-40, -10, n_calls)
+    per = 1102 * 170  # noise spectrum uniforms per call (1102 bins x ~165 frames)
+    U = rng.uniform(size=per * n_calls)
+    calls = []
+    for i in range(n_calls):
+        args = dict(sylLen=2000, samplingRate=44100, temperature=0, addSilence=0, windowLength=50, overlap=75,
+                    formants=str(v[i]), pitchAnchors=[float(a[i]), float(b[i])],
+                    noiseAnchors={"time": [0, 2000], "value": [float(n[i]), float(n[i])]}, formantsNoise=None)
+        calls.append({"kind": "soundgen", "args": args, "uniforms": U[i * per:(i + 1) * per]})
+    return calls
+
+
+def c4_calls(n_calls, rank=0):
+    rng = _rng(rank, 4)
+    s = rng.uniform(60, 200, n_calls)
+    d = rng.uniform(40, 150, n_calls)
+    j = rng.uniform(0.3, 2, n_calls)
+    l = rng.uniform(1, 20, n_calls)
+    h = rng.uniform(5, 20, n_calls)
+    a = np.exp(rng.uniform(np.log(150), np.log(600), n_calls))
+    b = np.exp(rng.uniform(np.log(150), np.log(600), n_calls))
+    pn, pu = 40000, 20000
+    Z = rng.standard_normal(pn * n_calls)
+    U = rng.uniform(size=pu * n_calls)
+    calls = []
+    for i in range(n_calls):
+        args = dict(sylLen=3000, samplingRate=44100, nonlinBalance=100, temperature=0.05, subFreq=float(s[i]),
+                    subDep=float(d[i]), jitterDep=float(j[i]), jitterLen=float(l[i]), shimmerDep=float(h[i]),
+                    shortestEpoch=300, pitchAnchors=[float(a[i]), float(b[i])], addSilence=0)
+        calls.append({"kind": "soundgen", "args": args, "normals": Z[i * pn:(i + 1) * pn],
+                      "uniforms": U[i * pu:(i + 1) * pu]})
+    return calls
+
+
+CONFIGS = {
+    "c2": (c2_calls, 1024, "C2: %d x 1 s static-f0 tones, generateHarmonics, 44.1 kHz, harmonics only"),
+    "c3": (c3_calls, 1024, "C3: %d x 2 s vowels, soundgen() with formant filter + breathing noise, 44.1 kHz"),
+    "c4": (c4_calls, 512, "C4: %d x 3 s soundgen() with subharmonics, jitter, shimmer, temperature 0.05, 44.1 kHz"),
+}
+
+
+def oracle_call(O, c):
+    if c["kind"] == "harmonics":
+        return O.generate_harmonics(c["pitch"], normals=c.get("normals"), uniforms=c.get("uniforms"), **c["params"])
+    return O.soundgen(normals=c.get("normals"), uniforms=c.get("uniforms"), **c["args"])
 
 
 def cpu_baseline(calls, budget_s):
@@ -44,13 +105,17 @@ def cpu_baseline(calls, budget_s):
     t0 = time.perf_counter()
     n_samples = n = 0
     for c in calls:
-        n_samples += len(O.generate_harmonics(c["pitch"], **c["params"]))
+        try:
+            n_samples += len(oracle_call(O, c))
+        except Exception:  # same unsupported calls as the GPU path
+            continue
         n += 1
         if time.perf_counter() - t0 > budget_s:
             break
     dt = time.perf_counter() - t0
     return {"value": n_samples / dt, "unit": "samples/s", "cores": 1, "kind": "port",
-            "sample": "%d of the C2 calls (%d samples) through oracle/sg_oracle.c, single thread" % (n, n_samples)}
+            "sample": "%d of the workload's calls (%d samples) through oracle/sg_oracle.c, single thread"
+                      % (n, n_samples)}
 
 
 def main():
@@ -58,7 +123,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--calls", type=int, default=1024)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--calls", type=int, default=0, help="calls per GPU (default: the config's)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -75,12 +141,19 @@ def main():
     dev = torch.device("cuda", local)
 
     from soundgen_beta_amd import batch, native
-    calls = c2_calls(args.calls, rank)
+    make, n_default, desc = CONFIGS[args.config]
+    n_calls = args.calls or n_default
+    calls = make(n_calls, rank)
     ctx = native.Context(local)
+    t_plan = time.perf_counter()
     plan = batch.Plan(calls, ctx)
-    assert (plan.status == 0).all(), [plan.message(i) for i in np.nonzero(plan.status)[0][:3]]
+    t_plan = time.perf_counter() - t_plan
+    failed = int((plan.status != 0).sum())
+    if failed:  # e.g. loess-smoothed contours (3-10 anchors) are SG_E_UNSUPPORTED; their slots stay empty
+        print("bench: %d of %d calls not synthesized: %s" % (failed, plan.n, plan.message(int(np.nonzero(plan.status)[0][0]))),
+              file=sys.stderr)
     plan.upload()
-    out = torch.empty(plan.total, dtype=torch.float32, device=dev)
+    out = torch.empty(max(plan.total, 1), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
 
@@ -100,11 +173,10 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     L.sg_set_profiling(ctx.ptr, 0)
-    import ctypes as C
     sine_ms, nprof = C.c_double(), C.c_int64()
     native.check(L.sg_profile_read(ctx.ptr, C.byref(sine_ms), C.byref(nprof)), ctx.ptr)
 
-    samples_rank = plan.total
+    samples_rank = int(plan.lengths.sum())  # synthesized samples (slot padding excluded)
     if dist:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -119,30 +191,28 @@ def main():
     if rank == 0:
         st = plan.stats()
         # algorithmic bytes of one sine-bank launch: fp32 epoch
-        # waveform write + amplitude matrices + pitch segments/knots
-        n_gc = sum(int(np.ceil(c["pitch"].size)) for c in calls[:0])
+        # waveform write + the amplitude blocks it reads (A and dA columns)
         launches = max(1, nprof.value // args.steps)  # sine-bank launches per step (batch slices)
         alg_bytes = (4 * st["harm_samples"] + st["harm_amp_bytes"]) / launches
         sine_s = sine_ms.value / 1e3
         achieved = alg_bytes / sine_s / 1e9 if sine_s > 0 else 0.0
-        # VALU: per (sample, row) the kernel issues 3 instructions (ISA, C=2 path)
+        # VALU: Clenshaw rows cost 2 lane-ops per (sample, row, chain)
         valu_ops = 2.0 * st["harm_terms"] / launches
-        host = out[: min(plan.total, 4 * 50000)].cpu().numpy()
         from oracle import oracle as O
         rms = []
-        for i in range(min(4, plan.n)):
-            y = host[plan.offsets[i]:plan.offsets[i] + plan.lengths[i]].astype(np.float64)
-            if plan.offsets[i] + plan.lengths[i] > host.size:
-                break
-            ref = O.generate_harmonics(calls[i]["pitch"], **calls[i]["params"])
+        host = None
+        for i in [k for k in range(plan.n) if plan.status[k] == 0][:3]:
+            lo, n = int(plan.offsets[i]), int(plan.lengths[i])
+            y = out[lo:lo + n].double().cpu().numpy()
+            ref = oracle_call(O, calls[i])
             rms.append(float(np.sqrt(np.mean((y - ref) ** 2))) if len(ref) == len(y) else float("inf"))
         res = {
             "metric": METRIC, "value": value, "unit": "samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32 (fp64 phase)", "data": "synthetic",
-            "config": {"workload": "C2: %d x 1 s static-f0 tones, generateHarmonics, 44.1 kHz, harmonics only"
-                       % args.calls, "calls_per_gpu": args.calls, "samples_per_gpu": samples_rank,
-                       "sampling_rate": 44100, "parallelism": "dp%d (independent shards)" % world},
+            "config": {"workload": desc % n_calls, "calls_per_gpu": n_calls, "samples_per_gpu": samples_rank,
+                       "sampling_rate": 44100, "parallelism": "dp%d (independent shards)" % world,
+                       "plan_s": t_plan, "failed_calls": failed},
             "rms_error_vs_oracle": max(rms) if rms else None,
             "roofline": {"bound": "hbm", "kernel": "sg_sine_bank", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
