@@ -100,67 +100,6 @@ struct Dft<4, INV> {
   }
 };
 
-// One Stockham pass (radix R, Ns = product of earlier radices) over fb frames
-// of M points: X -> Y. Twiddle exp(-+2 pi i r (j mod Ns) / (Ns R)) = W_M^(r (j mod Ns) M/(Ns R)).
-template <int R, bool INV>
-__device__ __forceinline__ void stage(const float2* X, float2* Y, int M, int Ns, const float2* twM, int fb) {
-  const int MR = M / R;
-  const int tstep = M / (Ns * R);
-  for (int idx = threadIdx.x; idx < fb * MR; idx += blockDim.x) {
-    const int f = idx / MR;
-    const int j = idx - f * MR;
-    const float2* x = X + f * M;
-    float2* y = Y + f * M;
-    float2 v[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) v[r] = x[j + r * MR];
-    const int jm = j % Ns;
-    if (Ns > 1) {
-#pragma unroll
-      for (int r = 1; r < R; ++r) {
-        const float2 w = twM[r * jm * tstep];
-        v[r] = INV ? cmulc(v[r], w) : cmul(v[r], w);
-      }
-    }
-    Dft<R, INV>::run(v);
-    const int o = (j - jm) * R + jm;
-#pragma unroll
-    for (int r = 0; r < R; ++r) y[o + r * Ns] = v[r];
-  }
-}
-
-// Full complex FFT over fb frames; returns the buffer holding the result.
-template <bool INV>
-__device__ float2* fft_frames(float2* A, float2* B, const SgFftGeom& g, const float2* twM, int fb) {
-  float2* X = A;
-  float2* Y = B;
-  int Ns = 1;
-  for (int s = 0; s < g.nstages; ++s) {
-    const int R = g.radix[s];
-    switch (R) {
-      case 2: stage<2, INV>(X, Y, g.M, Ns, twM, fb); break;
-      case 3: stage<3, INV>(X, Y, g.M, Ns, twM, fb); break;
-      case 4: stage<4, INV>(X, Y, g.M, Ns, twM, fb); break;
-      case 5: stage<5, INV>(X, Y, g.M, Ns, twM, fb); break;
-      case 7: stage<7, INV>(X, Y, g.M, Ns, twM, fb); break;
-      case 11: stage<11, INV>(X, Y, g.M, Ns, twM, fb); break;
-      case 13: stage<13, INV>(X, Y, g.M, Ns, twM, fb); break;
-      case 17: stage<17, INV>(X, Y, g.M, Ns, twM, fb); break;
-      case 19: stage<19, INV>(X, Y, g.M, Ns, twM, fb); break;
-      case 23: stage<23, INV>(X, Y, g.M, Ns, twM, fb); break;
-      case 29: stage<29, INV>(X, Y, g.M, Ns, twM, fb); break;
-      case 31: stage<31, INV>(X, Y, g.M, Ns, twM, fb); break;
-      default: break;  // the planner only emits the radices above
-    }
-    __syncthreads();
-    float2* t = X;
-    X = Y;
-    Y = t;
-    Ns *= R;
-  }
-  return X;
-}
-
 // ISTFT input packing: from the one-sided spectrum Y[0..M) (seewave's mirror:
 // Xf[k] = Y[k], Xf[M] = Re(Y[M-1]), Xf[N-k] = conj(Y[k])) build
 // Z'[k] = (Xf[k] + Xf[k+M]) + i (Xf[k] - Xf[k+M]) e^{2 pi i k / N}
@@ -177,81 +116,211 @@ __device__ __forceinline__ void pack_pair(float2 yk, float2 ymk, float2 wNk, flo
   zmk = make_float2(e2.x - o2.y, e2.y + o2.x);
 }
 
+// ---------------------------------------------------------------- FFT v2
+// In-place Stockham pass over fb frames of M points held in ONE LDS buffer:
+// phase 1 reads each butterfly (twiddled) into registers and reduces it to
+// its state (odd primes: x0 and the symmetric sums a_m, b_m; radix 2/4: the
+// outputs), barrier, phase 2 produces the outputs and writes them. With
+// fb*M <= SG_FFT_SLOTS complex points and SG_FFT_THREADS threads, a thread
+// owns at most NB = ceil(SG_FFT_SLOTS / (R * SG_FFT_THREADS)) butterflies.
+constexpr int SG_FFT_THREADS = 512;
+constexpr int SG_FFT_SLOTS = 8192;  // complex points per workgroup (64 KB of LDS)
+
+template <int R>
+struct NbOf {
+  static constexpr int value = (SG_FFT_SLOTS / SG_FFT_THREADS + R - 1) / R;
+};
+
+template <int R, bool INV>
+__device__ __forceinline__ void stage_ip(float2* X, int M, int Ns, const float2* __restrict__ twM, int fb) {
+  constexpr int NB = NbOf<R>::value;
+  constexpr bool ODD = (R % 2) == 1;
+  constexpr int H = ODD ? (R - 1) / 2 : 1;
+  const int MR = M / R;
+  const int tstep = M / (Ns * R);
+  const int total = fb * MR;
+  float2 st[NB][ODD ? (2 * H + 1) : R];  // odd: [x0, a_1..a_H, b_1..b_H]; even radix: outputs
+  int base_o[NB];
+  bool live[NB];
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    const int idx = threadIdx.x + q * SG_FFT_THREADS;
+    live[q] = idx < total;
+    base_o[q] = 0;
+    if (!live[q]) continue;
+    const int f = idx / MR;
+    const int j = idx - f * MR;
+    const float2* x = X + f * M;
+    float2 v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = x[j + r * MR];
+    const int jm = j % Ns;
+    if (Ns > 1) {
+#pragma unroll
+      for (int r = 1; r < R; ++r) {
+        const float2 w = twM[r * jm * tstep];
+        v[r] = INV ? cmulc(v[r], w) : cmul(v[r], w);
+      }
+    }
+    base_o[q] = f * M + (j - jm) * R + jm;
+    if constexpr (ODD) {
+      st[q][0] = v[0];
+#pragma unroll
+      for (int m = 1; m <= H; ++m) {
+        st[q][m] = cadd(v[m], v[R - m]);
+        st[q][H + m] = csub(v[m], v[R - m]);
+      }
+    } else {
+      Dft<R, INV>::run(v);
+#pragma unroll
+      for (int r = 0; r < R; ++r) st[q][r] = v[r];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    if (!live[q]) continue;
+    float2* y = X + base_o[q];
+    if constexpr (ODD) {
+      const float2 x0 = st[q][0];
+      float2 y0 = x0;
+#pragma unroll
+      for (int m = 1; m <= H; ++m) y0 = cadd(y0, st[q][m]);
+      y[0] = y0;
+#pragma unroll
+      for (int k = 1; k <= H; ++k) {
+        float2 P = x0, Q = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int m = 1; m <= H; ++m) {
+          const int id = (m * k) % R;
+          const float c = SgRoots<R>::c(id), s = SgRoots<R>::s(id);
+          P.x = fmaf(st[q][m].x, c, P.x);
+          P.y = fmaf(st[q][m].y, c, P.y);
+          Q.x = fmaf(st[q][H + m].x, s, Q.x);
+          Q.y = fmaf(st[q][H + m].y, s, Q.y);
+        }
+        if (!INV) {
+          y[k * Ns] = make_float2(P.x + Q.y, P.y - Q.x);
+          y[(R - k) * Ns] = make_float2(P.x - Q.y, P.y + Q.x);
+        } else {
+          y[k * Ns] = make_float2(P.x - Q.y, P.y + Q.x);
+          y[(R - k) * Ns] = make_float2(P.x + Q.y, P.y - Q.x);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) y[r * Ns] = st[q][r];
+    }
+  }
+  __syncthreads();
+}
+
+template <bool INV>
+__device__ void fft_ip(float2* X, const SgFftGeom& g, const float2* __restrict__ twM, int fb) {
+  int Ns = 1;
+  for (int s = 0; s < g.nstages; ++s) {
+    const int R = g.radix[s];
+    switch (R) {
+      case 2: stage_ip<2, INV>(X, g.M, Ns, twM, fb); break;
+      case 3: stage_ip<3, INV>(X, g.M, Ns, twM, fb); break;
+      case 4: stage_ip<4, INV>(X, g.M, Ns, twM, fb); break;
+      case 5: stage_ip<5, INV>(X, g.M, Ns, twM, fb); break;
+      case 7: stage_ip<7, INV>(X, g.M, Ns, twM, fb); break;
+      case 11: stage_ip<11, INV>(X, g.M, Ns, twM, fb); break;
+      case 13: stage_ip<13, INV>(X, g.M, Ns, twM, fb); break;
+      case 17: stage_ip<17, INV>(X, g.M, Ns, twM, fb); break;
+      case 19: stage_ip<19, INV>(X, g.M, Ns, twM, fb); break;
+      case 23: stage_ip<23, INV>(X, g.M, Ns, twM, fb); break;
+      case 29: stage_ip<29, INV>(X, g.M, Ns, twM, fb); break;
+      case 31: stage_ip<31, INV>(X, g.M, Ns, twM, fb); break;
+      default: break;  // the planner only emits the radices above
+    }
+    Ns *= R;
+  }
+}
+
 }  // namespace
 
-extern "C" __global__ __launch_bounds__(256) void sg_fft_frames(const SgFrameGroup* __restrict__ groups,
-                                                                const SgFrame* __restrict__ frames,
-                                                                const SgFftGeom* __restrict__ geoms,
-                                                                const float* __restrict__ fl, float* __restrict__ fs) {
+extern "C" __global__ __launch_bounds__(SG_FFT_THREADS) void sg_fft_frames(
+    const SgFrameGroup* __restrict__ groups, const SgFrame* __restrict__ frames, const SgFftGeom* __restrict__ geoms,
+    const float* __restrict__ fl, float* __restrict__ fs) {
   extern __shared__ float4 lds4[];
-  float2* lds = reinterpret_cast<float2*>(lds4);
+  float2* A = reinterpret_cast<float2*>(lds4);
   const SgFrameGroup G = groups[blockIdx.x];
   const SgFftGeom& g = geoms[G.geom];
   const int M = g.M, N = g.wl, fb = G.nf;
-  float2* twM = lds;
-  float2* twN = twM + M;
-  float2* A = twN + M;
-  float2* B = A + g.fb * M;
-  const float2* tw = reinterpret_cast<const float2*>(fl + g.tw);
-  for (int i = threadIdx.x; i < 2 * M; i += blockDim.x) twM[i] = tw[i];
+  const float2* twM = reinterpret_cast<const float2*>(fl + g.tw);  // L1/L2 resident
+  const float2* twN = twM + M;
   const float* ham = fl + g.win;
   const float* han = ham + N;
   const float invN = 1.f / (float)N;
-  float2* Zp;  // packed ISTFT input
-  float2* other;
+  const int half = M / 2;
+  const int npairs = fb * (half + 1);
+  constexpr int NP = SG_FFT_SLOTS / 2 / SG_FFT_THREADS + 1;  // pairs per thread
   if (G.mode == SG_FRAME_FILTER) {
-    for (int idx = threadIdx.x; idx < fb * M; idx += blockDim.x) {
+    for (int idx = threadIdx.x; idx < fb * M; idx += SG_FFT_THREADS) {
       const int f = idx / M, n = idx - f * M;
       const float* s = fs + frames[G.f0 + f].src;
-      A[f * M + n] = make_float2(s[2 * n] * ham[2 * n], s[2 * n + 1] * ham[2 * n + 1]);
+      A[idx] = make_float2(s[2 * n] * ham[2 * n], s[2 * n + 1] * ham[2 * n + 1]);
     }
     __syncthreads();
-    float2* Z = fft_frames<false>(A, B, g, twM, fb);
-    other = (Z == A) ? B : A;
+    fft_ip<false>(A, g, twM, fb);
     // untangle the real transform: X[k] = E + W_N^k O, E = (Z_k + conj Z_{M-k})/2,
-    // O = -i (Z_k - conj Z_{M-k}) / 2; Y = X / N * env; then pack for the inverse
-    const int half = M / 2;
-    for (int idx = threadIdx.x; idx < fb * (half + 1); idx += blockDim.x) {
+    // O = -i (Z_k - conj Z_{M-k}) / 2; Y = X / N * env; pack for the inverse
+    float2 zk[NP], zm[NP], zh[NP];
+    int pk[NP], pf[NP];
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const int idx = threadIdx.x + q * SG_FFT_THREADS;
+      pk[q] = -1;
+      if (idx >= npairs) continue;
       const int f = idx / (half + 1), k = idx - f * (half + 1);
-      const float2* z = Z + f * M;
+      if (k != 0 && k >= M - k) continue;
+      pk[q] = k;
+      pf[q] = f;
+      const float2* z = A + f * M;
       const float* env = fl + frames[G.f0 + f].env;
-      float2* out = other + f * M;
-      auto X_at = [&](int kk) -> float2 {  // kk in [0, M)
-        const float2 zk = z[kk], zm = z[(M - kk) % M];
-        const float2 e = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
-        const float2 dd = make_float2(zk.x - zm.x, zk.y + zm.y);  // Z_k - conj Z_{M-k}
-        const float2 o = make_float2(0.5f * dd.y, -0.5f * dd.x);  // -i dd / 2
+      auto X_at = [&](int kk) -> float2 {
+        const float2 a = z[kk], b = z[(M - kk) % M];
+        const float2 e = make_float2(0.5f * (a.x + b.x), 0.5f * (a.y - b.y));
+        const float2 dd = make_float2(a.x - b.x, a.y + b.y);
+        const float2 o = make_float2(0.5f * dd.y, -0.5f * dd.x);
         return cadd(e, cmul(o, twN[kk]));
       };
       if (k == 0) {
         const float2 x0 = X_at(0), xl = X_at(M - 1);
-        const float y0 = x0.x * invN * env[0];  // bin 0 of a real frame is real
-        const float nyq = xl.x * invN * env[M - 1];  // Re(Y[M-1]) (seewave's Nyquist)
-        out[0] = make_float2(y0 + nyq, y0 - nyq);  // E' = Xf0 + XfM, O' = Xf0 - XfM (times e^0)
-        if (M % 2 == 0 && M >= 2) {  // k = M/2 pairs with itself
-          const int km = M / 2;
-          const float2 xk = X_at(km);
-          const float2 yk = make_float2(xk.x * invN * env[km], xk.y * invN * env[km]);
-          float2 zk, zmk;
-          pack_pair(yk, yk, twN[km], zk, zmk);
-          out[km] = zk;
+        const float y0 = x0.x * invN * env[0];
+        const float nyq = xl.x * invN * env[M - 1];
+        zk[q] = make_float2(y0 + nyq, y0 - nyq);
+        if (M % 2 == 0) {
+          const float2 xk = X_at(half);
+          const float2 yk = make_float2(xk.x * invN * env[half], xk.y * invN * env[half]);
+          float2 t2;
+          pack_pair(yk, yk, twN[half], zh[q], t2);
         }
-      } else if (k < M - k) {
+      } else {
         const float2 xk = X_at(k), xm = X_at(M - k);
         const float2 yk = make_float2(xk.x * invN * env[k], xk.y * invN * env[k]);
         const float2 ym = make_float2(xm.x * invN * env[M - k], xm.y * invN * env[M - k]);
-        float2 zk, zmk;
-        pack_pair(yk, ym, twN[k], zk, zmk);
-        out[k] = zk;
-        out[M - k] = zmk;
+        pack_pair(yk, ym, twN[k], zk[q], zm[q]);
       }
     }
     __syncthreads();
-    Zp = other;
-    other = Z;
-  } else {  // SG_FRAME_NOISE: real spectrum u * filter
-    const int half = M / 2;
-    for (int idx = threadIdx.x; idx < fb * (half + 1); idx += blockDim.x) {
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      if (pk[q] < 0) continue;
+      float2* out = A + pf[q] * M;
+      const int k = pk[q];
+      out[k] = zk[q];
+      if (k == 0) {
+        if (M % 2 == 0) out[half] = zh[q];
+      } else {
+        out[M - k] = zm[q];
+      }
+    }
+    __syncthreads();
+  } else {  // SG_FRAME_NOISE: real spectrum u * filter, packed straight into LDS
+    for (int idx = threadIdx.x; idx < npairs; idx += SG_FFT_THREADS) {
       const int f = idx / (half + 1), k = idx - f * (half + 1);
       const SgFrame& F = frames[G.f0 + f];
       const float* u = fl + F.src;
@@ -260,30 +329,27 @@ extern "C" __global__ __launch_bounds__(256) void sg_fft_frames(const SgFrameGro
       if (k == 0) {
         const float y0 = u[0] * flt[0], nyq = u[M - 1] * flt[M - 1];
         out[0] = make_float2(y0 + nyq, y0 - nyq);
-        if (M % 2 == 0 && M >= 2) {
-          const int km = M / 2;
-          const float2 yk = make_float2(u[km] * flt[km], 0.f);
-          float2 zk, zmk;
-          pack_pair(yk, yk, twN[km], zk, zmk);
-          out[km] = zk;
+        if (M % 2 == 0) {
+          const float2 yk = make_float2(u[half] * flt[half], 0.f);
+          float2 a, b;
+          pack_pair(yk, yk, twN[half], a, b);
+          out[half] = a;
         }
       } else if (k < M - k) {
         const float2 yk = make_float2(u[k] * flt[k], 0.f), ym = make_float2(u[M - k] * flt[M - k], 0.f);
-        float2 zk, zmk;
-        pack_pair(yk, ym, twN[k], zk, zmk);
-        out[k] = zk;
-        out[M - k] = zmk;
+        float2 a, b;
+        pack_pair(yk, ym, twN[k], a, b);
+        out[k] = a;
+        out[M - k] = b;
       }
     }
     __syncthreads();
-    Zp = A;
-    other = B;
   }
-  float2* y = fft_frames<true>(Zp, other, g, twM, fb);
+  fft_ip<true>(A, g, twM, fb);
   // windowed frame: Re(ifft)/N x hann, y[2n] = Re z[n], y[2n+1] = Im z[n]
-  for (int idx = threadIdx.x; idx < fb * M; idx += blockDim.x) {
+  for (int idx = threadIdx.x; idx < fb * M; idx += SG_FFT_THREADS) {
     const int f = idx / M, n = idx - f * M;
-    const float2 v = y[f * M + n];
+    const float2 v = A[idx];
     float* d = fs + frames[G.f0 + f].dst;
     d[2 * n] = v.x * invN * han[2 * n];
     d[2 * n + 1] = v.y * invN * han[2 * n + 1];
@@ -399,7 +465,8 @@ extern "C" __global__ __launch_bounds__(256) void sg_mix(const SgMixTile* __rest
 namespace sg {
 void launch_fft_frames(const DevicePlan& D, int64_t g0, int64_t n_groups, int lds_bytes, hipStream_t s) {
   if (n_groups <= 0) return;
-  hipLaunchKernelGGL(sg_fft_frames, dim3((unsigned)n_groups), dim3(256), lds_bytes, s, D.fgroups + g0, D.frames,
+  hipLaunchKernelGGL(sg_fft_frames, dim3((unsigned)n_groups), dim3(SG_FFT_THREADS), lds_bytes, s, D.fgroups + g0,
+                     D.frames,
                      D.geoms, D.fl, D.fs);
 }
 void launch_ola(const DevicePlan& D, int64_t t0, int64_t n_tiles, int64_t o0, int64_t n_olas, hipStream_t s) {

@@ -14,7 +14,7 @@ namespace sg {
 
 namespace {
 constexpr int kRadices[] = {4, 2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31};
-constexpr int kLdsBudget = 72 * 1024;  // two workgroups per CU
+constexpr int kFftSlots = 8192;  // complex points per FFT workgroup (sg_fft.hip SG_FFT_SLOTS)
 }  // namespace
 
 int64_t fs_alloc(Batch& B, int64_t n) {
@@ -65,11 +65,11 @@ int geometry(Batch& B, int wl) {
     win[wl + i] = 0.5 - 0.5 * std::cos(2 * M_PI * (double)i / (double)(wl - 1));
   }
   g.win = fl_push(B, win.data(), (int64_t)win.size());
-  // frames per workgroup: twiddles 2M + two ping-pong buffers fb*M (float2)
-  const int per_frame = 2 * g.M * 8;
-  g.fb = std::max(1, std::min(8, (kLdsBudget - 2 * g.M * 8) / per_frame));
-  g.lds_bytes = (2 * g.M + 2 * g.fb * g.M) * 8;
-  if (g.lds_bytes > 160 * 1024) throw SgError(SG_E_UNSUPPORTED, "FFT: window too long for LDS");
+  // frames per workgroup: one in-place LDS buffer of fb * M complex points,
+  // fb * M <= 8192 (64 KB: two workgroups per CU; sg_fft.hip SG_FFT_SLOTS)
+  g.fb = std::max(1, std::min(16, kFftSlots / g.M));
+  if (g.fb * g.M > kFftSlots) throw SgError(SG_E_UNSUPPORTED, "FFT: window too long for LDS (wl > 16384)");
+  g.lds_bytes = g.fb * g.M * 8;
   B.geoms.push_back(g);
   return (int)B.geoms.size() - 1;
 }
