@@ -225,6 +225,13 @@ int sg_get_rolloff(const double* pitch_per_gc, int32_t n_gc,
                    double rolloffKHz, double baseline, double throwaway,
                    double samplingRate, double* out, int32_t* out_rows);
 
+/* Test hook, no reference counterpart: the wavefront FFT stages used inside
+ * the fused STFT/ISTFT kernel, on nframes frames of wl/2 complex points
+ * (interleaved re, im, in place semantics: out = DFT(in), unscaled; inverse
+ * uses exp(+2 pi i nk / M)). SG_E_UNSUPPORTED if wl is not on that path. */
+int sg_debug_wave_fft(sg_ctx* ctx, int32_t wl, int32_t inverse, int32_t nframes,
+                      const float* in, float* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -96,7 +96,9 @@ def synthesize(calls, device=0):
     out = torch.empty(max(plan.total, 1), dtype=torch.float32, device="cuda:%d" % device)
     stream = torch.cuda.current_stream(device)
     plan.execute(out.data_ptr(), stream.cuda_stream)
-    stream.synchronize()
+    # torch's default stream has handle 0, which sg_execute reads as "the
+    # context's own stream" (non-blocking): wait for the device, not the stream
+    torch.cuda.synchronize(device)
     host = out.cpu().numpy()
     res = []
     for i in range(plan.n):

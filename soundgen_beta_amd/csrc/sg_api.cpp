@@ -319,6 +319,32 @@ static int run_plan_to_host(sg_ctx* ctx, sg_plan* P, double* out, int64_t n) {
   return sg_execute_to_host(ctx, P, out);
 }
 
+// Test hook (not part of the reference surface): the wavefront FFT stages of
+// sg_stft_ola on nframes frames of M = wl / 2 complex points (interleaved re, im).
+int sg_debug_wave_fft(sg_ctx* ctx, int32_t wl, int32_t inverse, int32_t nframes, const float* in, float* out) {
+  return guarded(ctx, [&]() {
+    sg::Batch B;
+    const int gi = sg::geometry(B, wl);
+    const SgFftGeom g = B.geoms[gi];
+    if (g.kind != SG_FFT_WAVE) throw sg::SgError(SG_E_UNSUPPORTED, "window length not on the wavefront FFT path");
+    const size_t nd = (size_t)nframes * g.M * 2;
+    void *dg = nullptr, *dfl = nullptr, *dd = nullptr;
+    HIPCHK(hipMalloc(&dg, sizeof(SgFftGeom)));
+    HIPCHK(hipMalloc(&dfl, B.fl.size() * sizeof(float)));
+    HIPCHK(hipMalloc(&dd, nd * sizeof(float)));
+    HIPCHK(hipMemcpy(dg, &g, sizeof(SgFftGeom), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(dfl, B.fl.data(), B.fl.size() * sizeof(float), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(dd, in, nd * sizeof(float), hipMemcpyHostToDevice));
+    sg::launch_fft_probe((const SgFftGeom*)dg, (const float*)dfl, (float*)dd, g.M, nframes, inverse, ctx->stream);
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipMemcpy(out, dd, nd * sizeof(float), hipMemcpyDeviceToHost));
+    (void)hipFree(dg);
+    (void)hipFree(dfl);
+    (void)hipFree(dd);
+    return SG_OK;
+  });
+}
+
 int sg_formant_filter(sg_ctx* ctx, const double* sound, int64_t len, const double* env, int32_t env_nc,
                       int32_t windowLength_points, double overlap, double* out, int64_t cap, int64_t* out_len) {
   return guarded(ctx, [&]() {

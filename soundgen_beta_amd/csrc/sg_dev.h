@@ -145,8 +145,22 @@ struct SgFftGeom {
   int32_t radix[SG_FFT_MAX_STAGES];
   int64_t tw;                      // fl offset: M pairs W_M^t, then M pairs W_N^k (interleaved re, im)
   int64_t win;                     // fl offset: hamming[wl] then hanning[wl] (seewave ftwindow)
-  int32_t lds_bytes, pad;
+  int32_t lds_bytes;
+  int32_t kind;                    // SG_FFT_WAVE: one wavefront per frame (sg_fft_wave); SG_FFT_WG: sg_fft_frames
+  // n / d == __umulhi(n, ceil(2^32 / d)) exactly for n * d < 2^32 (d > 1);
+  // per stage s: d = M / radix[s] and d = Ns (product of the earlier radices)
+  uint32_t mr_magic[SG_FFT_MAX_STAGES], ns_magic[SG_FFT_MAX_STAGES];
+  uint32_t m_magic, hp_magic;      // d = M, d = M / 2 + 1
+  int64_t tws;                     // fl offset: stage-ordered twiddles for sg_fft_wave, (M - 1) pairs:
+                                   // stage s at Ns - 1, entry (r - 1) Ns + jm = W_M^(r jm M / (Ns R))
 };
+
+constexpr int SG_FFT_WG = 0;
+constexpr int SG_FFT_WAVE = 1;
+constexpr int SG_WAVE_STATE = 24;  // complex butterfly points a lane holds per stage in sg_stft_ola
+constexpr int SG_FFT_WAVES = 8;    // wavefronts (segments) per sg_stft_ola workgroup: one workgroup per CU
+constexpr int SG_PF_SRC = 20;      // sg_stft_ola register prefetch: sound pairs per lane (M <= 1280)
+constexpr int SG_PF_PAIR = 10;     // bin pairs per lane (M / 2 + 1 <= 640)
 
 constexpr int SG_FRAME_FILTER = 0;  // fs sound -> hamming -> FFT/wl -> x env -> ISTFT/wl -> x hann
 constexpr int SG_FRAME_NOISE = 1;   // fl uniforms x fl filter (real spectrum)  -> ISTFT/wl -> x hann
@@ -171,8 +185,28 @@ struct SgOla {
   int32_t nframes, wl;
   float scale;     // h / sum(hann^2)
   int32_t tile0;   // first per-tile max slot
+  int32_t hi;      // h when it is a whole number of samples (integer gather path), else 0
+  int32_t nslot;   // max slots [tile0, tile0 + nslot): sg_ola tiles or sg_stft_ola segments
+  int32_t fidx;    // index of frame 0 (planner: within its phase; device: in the frame table)
+  int32_t fused;   // 1: frames transformed and overlap-added by sg_stft_ola (no frame scratch)
 };
 constexpr int SG_OLA_TILE = 1024;
+
+// sg_stft_ola work unit: frames [f0, f0 + nf) of one OLA (OLA-relative;
+// f0 may start before the segment's own frames to rebuild the overlap
+// carried in from earlier frames), owning istft samples [pa, pb).
+struct SgSegment {
+  int32_t ola, geom, mode;
+  int32_t fdev;    // frame-table index of frame f0
+  int32_t f0, nf;
+  int32_t pa, pb;
+  int32_t slot;    // per-segment max slot
+  int32_t flags;   // SG_SEG_FIRST: writes the leading zero padding; SG_SEG_LAST: the trailing one
+};
+constexpr int SG_SEG_FIRST = 1;
+constexpr int SG_SEG_LAST = 2;
+constexpr int SG_SEG_FRAMES = 48;   // target frames owned per segment (one wavefront each)
+constexpr int SG_CARRY_PAIRS = 16;  // sg_stft_ola carry registers: wl - floor(hop) <= 128 * 16 samples
 struct SgOlaTile {
   int32_t ola, pad;
   int64_t q0;  // first sample of the tile (relative to `first`)

@@ -20,7 +20,7 @@ size_t up(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
 struct Layout {
   size_t segs, epochs, knots, amps, tasks, pieces, syls, syl_tiles, ptiles, cknots, W, taskmax, ptilemax, maxes, total;
-  size_t geoms, frames, fgroups, olas, olatiles, olatilemax, olamax, items, mixes, mixtiles, fl, fs;
+  size_t geoms, frames, fgroups, olas, olatiles, olasegs, olatilemax, olamax, items, mixes, mixtiles, fl, fs;
   explicit Layout(const Batch& B) {
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o += up(bytes > 0 ? bytes : 1); return r; };
@@ -43,7 +43,8 @@ struct Layout {
     fgroups = take(B.fgroups.size() * sizeof(SgFrameGroup));
     olas = take(B.olas_dev.size() * sizeof(SgOla));
     olatiles = take(B.olatiles.size() * sizeof(SgOlaTile));
-    olatilemax = take(B.olatiles.size() * sizeof(float));
+    olasegs = take(B.olasegs.size() * sizeof(SgSegment));
+    olatilemax = take((B.olatiles.size() + (size_t)B.n_segslots) * sizeof(float));  // tile slots, then segment slots
     olamax = take(B.olas_dev.size() * sizeof(float));
     items = take(B.items.size() * sizeof(SgNoiseItem));
     mixes = take(B.mixes_dev.size() * sizeof(SgMix));
@@ -129,6 +130,7 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   D.fgroups = (SgFrameGroup*)(a + L.fgroups);
   D.olas = (SgOla*)(a + L.olas);
   D.olatiles = (SgOlaTile*)(a + L.olatiles);
+  D.olasegs = (SgSegment*)(a + L.olasegs);
   D.olatilemax = (float*)(a + L.olatilemax);
   D.olamax = (float*)(a + L.olamax);
   D.items = (SgNoiseItem*)(a + L.items);
@@ -155,6 +157,7 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   cp(D.fgroups, B.fgroups.data(), B.fgroups.size() * sizeof(SgFrameGroup));
   cp(D.olas, B.olas_dev.data(), B.olas_dev.size() * sizeof(SgOla));
   cp(D.olatiles, B.olatiles.data(), B.olatiles.size() * sizeof(SgOlaTile));
+  cp(D.olasegs, B.olasegs.data(), B.olasegs.size() * sizeof(SgSegment));
   cp(D.items, B.items.data(), B.items.size() * sizeof(SgNoiseItem));
   cp(D.mixes, B.mixes_dev.data(), B.mixes_dev.size() * sizeof(SgMix));
   cp(D.mixtiles, B.mixtiles.data(), B.mixtiles.size() * sizeof(SgMixTile));
@@ -215,15 +218,21 @@ void device_execute(const Batch& B, DevicePlan& D, float* d_out, hipStream_t s, 
 // Spectral phases after the harmonic syllables: noise frames -> noise OLA,
 // pre-filter mixes (sounds), filter frames -> filter OLA, final mixes.
 void device_execute_spec(const Batch& B, const DevicePlan& D, float* d_out, hipStream_t s) {
-  const int64_t ng = (int64_t)B.fgroups.size();
-  launch_fft_frames(D, 0, B.fgroup_split, B.fgroup_lds[0], s);
-  launch_ola(D, 0, B.olatile_split, 0, B.ola_split, s);
+  // phase: fused STFT/ISTFT/OLA segments, unfused frame groups + OLA tiles, per-OLA maxima
+  auto phase = [&](int ph) {
+    const int64_t* r = B.fgroup_range[ph];
+    launch_stft_ola(D, B.seg_range[ph][0], B.seg_range[ph][1] - B.seg_range[ph][0], B.fgroup_lds[ph][0], s);
+    launch_fft_frames(D, r[1], r[2] - r[1], B.fgroup_lds[ph][1], s);
+    const int64_t t0 = ph == 0 ? 0 : B.olatile_split, t1 = ph == 0 ? B.olatile_split : (int64_t)B.olatiles.size();
+    const int64_t o0 = ph == 0 ? 0 : B.ola_split, o1 = ph == 0 ? B.ola_split : (int64_t)B.olas_dev.size();
+    launch_ola(D, t0, t1 - t0, s);
+    launch_ola_max(D, o0, o1 - o0, s);
+  };
+  phase(0);
   for (const Batch::Copy& c : B.copies)
     HIPCHK(hipMemcpyAsync(D.fs + c.fs_off, D.fl + c.fl_off, (size_t)c.n * sizeof(float), hipMemcpyDeviceToDevice, s));
   launch_mix(D, 0, B.mixtile_split, d_out, s);
-  launch_fft_frames(D, B.fgroup_split, ng - B.fgroup_split, B.fgroup_lds[1], s);
-  launch_ola(D, B.olatile_split, (int64_t)B.olatiles.size() - B.olatile_split, B.ola_split,
-             (int64_t)B.olas_dev.size() - B.ola_split, s);
+  phase(1);
   launch_mix(D, B.mixtile_split, (int64_t)B.mixtiles.size() - B.mixtile_split, d_out, s);
   HIPCHK(hipGetLastError());
 }

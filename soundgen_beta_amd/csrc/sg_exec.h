@@ -32,6 +32,7 @@ struct DevicePlan {
   SgFrameGroup* fgroups = nullptr;
   SgOla* olas = nullptr;
   SgOlaTile* olatiles = nullptr;
+  SgSegment* olasegs = nullptr;
   float* olatilemax = nullptr;
   float* olamax = nullptr;
   SgNoiseItem* items = nullptr;
@@ -60,7 +61,11 @@ void launch_piece_max(const DevicePlan& D, int64_t p0, int64_t n_ptiles, hipStre
 void launch_harm_finalize(const DevicePlan& D, int64_t f0, int64_t n_stiles, float* out, hipStream_t s);
 // sg_fft.hip
 void launch_fft_frames(const DevicePlan& D, int64_t g0, int64_t n_groups, int lds_bytes, hipStream_t s);
-void launch_ola(const DevicePlan& D, int64_t t0, int64_t n_tiles, int64_t o0, int64_t n_olas, hipStream_t s);
+void launch_stft_ola(const DevicePlan& D, int64_t s0, int64_t n_segs, int lds_bytes, hipStream_t s);
+void launch_ola(const DevicePlan& D, int64_t t0, int64_t n_tiles, hipStream_t s);
+void launch_ola_max(const DevicePlan& D, int64_t o0, int64_t n_olas, hipStream_t s);
+void launch_fft_probe(const SgFftGeom* geom, const float* fl, float* data, int M, int nframes, int inverse,
+                      hipStream_t s);
 void launch_mix(const DevicePlan& D, int64_t t0, int64_t n_tiles, float* out, hipStream_t s);
 
 }  // namespace sg

@@ -131,13 +131,18 @@ struct NbOf {
   static constexpr int value = (SG_FFT_SLOTS / SG_FFT_THREADS + R - 1) / R;
 };
 
+// exact n / d for n * d < 2^32 with magic = ceil(2^32 / d) (planner), magic 0 <=> d == 1
+__device__ __forceinline__ int udiv(int n, uint32_t magic) {
+  return magic ? (int)__umulhi((uint32_t)n, magic) : n;
+}
+
 template <int R, bool INV>
-__device__ __forceinline__ void stage_ip(float2* X, int M, int Ns, const float2* __restrict__ twM, int fb) {
+__device__ __forceinline__ void stage_ip(float2* X, int M, int Ns, const float2* twM, int fb, uint32_t mr_magic,
+                                         uint32_t ns_magic, int tstep) {
   constexpr int NB = NbOf<R>::value;
   constexpr bool ODD = (R % 2) == 1;
   constexpr int H = ODD ? (R - 1) / 2 : 1;
   const int MR = M / R;
-  const int tstep = M / (Ns * R);
   const int total = fb * MR;
   float2 st[NB][ODD ? (2 * H + 1) : R];  // odd: [x0, a_1..a_H, b_1..b_H]; even radix: outputs
   int base_o[NB];
@@ -148,13 +153,13 @@ __device__ __forceinline__ void stage_ip(float2* X, int M, int Ns, const float2*
     live[q] = idx < total;
     base_o[q] = 0;
     if (!live[q]) continue;
-    const int f = idx / MR;
+    const int f = udiv(idx, mr_magic);
     const int j = idx - f * MR;
     const float2* x = X + f * M;
     float2 v[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) v[r] = x[j + r * MR];
-    const int jm = j % Ns;
+    const int jm = j - udiv(j, ns_magic) * Ns;
     if (Ns > 1) {
 #pragma unroll
       for (int r = 1; r < R; ++r) {
@@ -216,24 +221,145 @@ __device__ __forceinline__ void stage_ip(float2* X, int M, int Ns, const float2*
 }
 
 template <bool INV>
-__device__ void fft_ip(float2* X, const SgFftGeom& g, const float2* __restrict__ twM, int fb) {
+__device__ void fft_ip(float2* X, const SgFftGeom& g, const float2* twM, int fb) {
   int Ns = 1;
   for (int s = 0; s < g.nstages; ++s) {
     const int R = g.radix[s];
+    const uint32_t mm = g.mr_magic[s], nm = g.ns_magic[s];
+    int Ms = g.M;
+    __asm__ __volatile__("" : "+s"(Ms));  // keep M / R and its multiples inside the stage (no hoisted SGPRs)
+    const int ts = udiv(Ms / R, nm);      // M / (Ns R)
     switch (R) {
-      case 2: stage_ip<2, INV>(X, g.M, Ns, twM, fb); break;
-      case 3: stage_ip<3, INV>(X, g.M, Ns, twM, fb); break;
-      case 4: stage_ip<4, INV>(X, g.M, Ns, twM, fb); break;
-      case 5: stage_ip<5, INV>(X, g.M, Ns, twM, fb); break;
-      case 7: stage_ip<7, INV>(X, g.M, Ns, twM, fb); break;
-      case 11: stage_ip<11, INV>(X, g.M, Ns, twM, fb); break;
-      case 13: stage_ip<13, INV>(X, g.M, Ns, twM, fb); break;
-      case 17: stage_ip<17, INV>(X, g.M, Ns, twM, fb); break;
-      case 19: stage_ip<19, INV>(X, g.M, Ns, twM, fb); break;
-      case 23: stage_ip<23, INV>(X, g.M, Ns, twM, fb); break;
-      case 29: stage_ip<29, INV>(X, g.M, Ns, twM, fb); break;
-      case 31: stage_ip<31, INV>(X, g.M, Ns, twM, fb); break;
+#define SG_STAGE(RR) \
+      case RR: stage_ip<RR, INV>(X, Ms, Ns, twM, fb, mm, nm, ts); break;
+      SG_STAGE(2) SG_STAGE(3) SG_STAGE(4) SG_STAGE(5) SG_STAGE(7) SG_STAGE(11) SG_STAGE(13) SG_STAGE(17)
+      SG_STAGE(19) SG_STAGE(23) SG_STAGE(29) SG_STAGE(31)
+#undef SG_STAGE
       default: break;  // the planner only emits the radices above
+    }
+    Ns *= R;
+  }
+}
+
+// ---------------------------------------------------------------- FFT v3
+// One wavefront transforms one frame: no workgroup barriers between stages.
+// A wavefront's LDS operations complete in issue order, so the in-place pass
+// only has to keep the compiler from moving the phase-2 writes above the
+// phase-1 reads (sg_wave_fence). A lane owns ceil(M / R / 64) <= 32 / R
+// butterflies of a stage (planner: SG_FFT_WAVE geometries).
+__device__ __forceinline__ void sg_wave_fence() { __asm__ __volatile__("" ::: "memory"); }
+
+template <int R>
+struct NbW {
+  static constexpr int value = SG_WAVE_STATE / R > 0 ? SG_WAVE_STATE / R : 1;
+};
+
+template <int R, bool INV>
+__device__ __forceinline__ void stage_w(float2* X, int M, int Ns, const float2* twS, uint32_t ns_magic, int lane) {
+  constexpr int NB = NbW<R>::value;
+  constexpr bool ODD = (R % 2) == 1;
+  constexpr int H = ODD ? (R - 1) / 2 : 1;
+  const int MR = M / R;
+  float2 st[NB][ODD ? (2 * H + 1) : R];
+  int base_o[NB];
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    if (q * 64 >= MR) break;
+    const int j = lane + q * 64;
+    base_o[q] = 0;
+    if (j >= MR) continue;
+    const int jm = j - udiv(j, ns_magic) * Ns;
+    base_o[q] = (j - jm) * R + jm;
+    if constexpr (ODD) {
+      // pairs (m, R - m) one at a time: inputs, twiddles and the symmetric
+      // sums of one pair live at once (register budget of the fused kernel)
+      st[q][0] = X[j];
+      const float2* tw = twS + (Ns - 1) + jm;
+#pragma unroll
+      for (int m = 1; m <= H; ++m) {
+        float2 a = X[j + m * MR], b = X[j + (R - m) * MR];
+        if (Ns > 1) {
+          const float2 wa = tw[(m - 1) * Ns], wb = tw[(R - m - 1) * Ns];
+          a = INV ? cmulc(a, wa) : cmul(a, wa);
+          b = INV ? cmulc(b, wb) : cmul(b, wb);
+        }
+        st[q][m] = cadd(a, b);
+        st[q][H + m] = csub(a, b);
+      }
+      continue;
+    }
+    float2 v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = X[j + r * MR];
+    if (Ns > 1) {
+      const float2* tw = twS + (Ns - 1) + jm;  // consecutive lanes, consecutive entries
+#pragma unroll
+      for (int r = 1; r < R; ++r) {
+        const float2 w = tw[(r - 1) * Ns];
+        v[r] = INV ? cmulc(v[r], w) : cmul(v[r], w);
+      }
+    }
+    {
+      Dft<R, INV>::run(v);
+#pragma unroll
+      for (int r = 0; r < R; ++r) st[q][r] = v[r];
+    }
+  }
+  sg_wave_fence();
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    if (q * 64 >= MR) break;
+    if (lane + q * 64 >= MR) continue;
+    float2* y = X + base_o[q];
+    if constexpr (ODD) {
+      const float2 x0 = st[q][0];
+      float2 y0 = x0;
+#pragma unroll
+      for (int m = 1; m <= H; ++m) y0 = cadd(y0, st[q][m]);
+      y[0] = y0;
+#pragma unroll
+      for (int k = 1; k <= H; ++k) {
+        float2 P = x0, Q = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int m = 1; m <= H; ++m) {
+          const int id = (m * k) % R;
+          const float c = SgRoots<R>::c(id), s = SgRoots<R>::s(id);
+          P.x = fmaf(st[q][m].x, c, P.x);
+          P.y = fmaf(st[q][m].y, c, P.y);
+          Q.x = fmaf(st[q][H + m].x, s, Q.x);
+          Q.y = fmaf(st[q][H + m].y, s, Q.y);
+        }
+        if (!INV) {
+          y[k * Ns] = make_float2(P.x + Q.y, P.y - Q.x);
+          y[(R - k) * Ns] = make_float2(P.x - Q.y, P.y + Q.x);
+        } else {
+          y[k * Ns] = make_float2(P.x - Q.y, P.y + Q.x);
+          y[(R - k) * Ns] = make_float2(P.x + Q.y, P.y - Q.x);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) y[r * Ns] = st[q][r];
+    }
+  }
+  sg_wave_fence();
+}
+
+template <bool INV>
+__device__ __forceinline__ void fft_w(float2* X, const SgFftGeom& g, const float2* twS, int lane) {
+  int Ns = 1;
+  for (int s = 0; s < g.nstages; ++s) {
+    const int R = g.radix[s];
+    const uint32_t nm = g.ns_magic[s];
+    int Ms = g.M;
+    __asm__ __volatile__("" : "+s"(Ms));  // keep M / R and its multiples inside the stage (no hoisted SGPRs)
+    switch (R) {
+#define SG_STAGE(RR) \
+      case RR: stage_w<RR, INV>(X, Ms, Ns, twS, nm, lane); break;
+      SG_STAGE(2) SG_STAGE(3) SG_STAGE(4) SG_STAGE(5) SG_STAGE(7) SG_STAGE(11) SG_STAGE(13) SG_STAGE(17)
+      SG_STAGE(19) SG_STAGE(23) SG_STAGE(29) SG_STAGE(31)
+#undef SG_STAGE
+      default: break;
     }
     Ns *= R;
   }
@@ -246,11 +372,16 @@ extern "C" __global__ __launch_bounds__(SG_FFT_THREADS) void sg_fft_frames(
     const float* __restrict__ fl, float* __restrict__ fs) {
   extern __shared__ float4 lds4[];
   float2* A = reinterpret_cast<float2*>(lds4);
+  __shared__ SgFrame fr[16];
   const SgFrameGroup G = groups[blockIdx.x];
   const SgFftGeom& g = geoms[G.geom];
   const int M = g.M, N = g.wl, fb = G.nf;
-  const float2* twM = reinterpret_cast<const float2*>(fl + g.tw);  // L1/L2 resident
-  const float2* twN = twM + M;
+  const float2* twg = reinterpret_cast<const float2*>(fl + g.tw);
+  const float2* twN = twg + M;  // L1/L2 resident (one read per bin pair)
+  float2* twM = A + fb * M;     // W_M table in LDS behind the frames
+  for (int t = threadIdx.x; t < M; t += SG_FFT_THREADS) twM[t] = twg[t];
+  if (threadIdx.x < fb) fr[threadIdx.x] = frames[G.f0 + threadIdx.x];
+  __syncthreads();
   const float* ham = fl + g.win;
   const float* han = ham + N;
   const float invN = 1.f / (float)N;
@@ -259,8 +390,8 @@ extern "C" __global__ __launch_bounds__(SG_FFT_THREADS) void sg_fft_frames(
   constexpr int NP = SG_FFT_SLOTS / 2 / SG_FFT_THREADS + 1;  // pairs per thread
   if (G.mode == SG_FRAME_FILTER) {
     for (int idx = threadIdx.x; idx < fb * M; idx += SG_FFT_THREADS) {
-      const int f = idx / M, n = idx - f * M;
-      const float* s = fs + frames[G.f0 + f].src;
+      const int f = udiv(idx, g.m_magic), n = idx - f * M;
+      const float* s = fs + fr[f].src;
       A[idx] = make_float2(s[2 * n] * ham[2 * n], s[2 * n + 1] * ham[2 * n + 1]);
     }
     __syncthreads();
@@ -274,12 +405,12 @@ extern "C" __global__ __launch_bounds__(SG_FFT_THREADS) void sg_fft_frames(
       const int idx = threadIdx.x + q * SG_FFT_THREADS;
       pk[q] = -1;
       if (idx >= npairs) continue;
-      const int f = idx / (half + 1), k = idx - f * (half + 1);
+      const int f = udiv(idx, g.hp_magic), k = idx - f * (half + 1);
       if (k != 0 && k >= M - k) continue;
       pk[q] = k;
       pf[q] = f;
       const float2* z = A + f * M;
-      const float* env = fl + frames[G.f0 + f].env;
+      const float* env = fl + fr[f].env;
       auto X_at = [&](int kk) -> float2 {
         const float2 a = z[kk], b = z[(M - kk) % M];
         const float2 e = make_float2(0.5f * (a.x + b.x), 0.5f * (a.y - b.y));
@@ -321,8 +452,8 @@ extern "C" __global__ __launch_bounds__(SG_FFT_THREADS) void sg_fft_frames(
     __syncthreads();
   } else {  // SG_FRAME_NOISE: real spectrum u * filter, packed straight into LDS
     for (int idx = threadIdx.x; idx < npairs; idx += SG_FFT_THREADS) {
-      const int f = idx / (half + 1), k = idx - f * (half + 1);
-      const SgFrame& F = frames[G.f0 + f];
+      const int f = udiv(idx, g.hp_magic), k = idx - f * (half + 1);
+      const SgFrame& F = fr[f];
       const float* u = fl + F.src;
       const float* flt = fl + F.env;
       float2* out = A + f * M;
@@ -348,12 +479,291 @@ extern "C" __global__ __launch_bounds__(SG_FFT_THREADS) void sg_fft_frames(
   fft_ip<true>(A, g, twM, fb);
   // windowed frame: Re(ifft)/N x hann, y[2n] = Re z[n], y[2n+1] = Im z[n]
   for (int idx = threadIdx.x; idx < fb * M; idx += SG_FFT_THREADS) {
-    const int f = idx / M, n = idx - f * M;
+    const int f = udiv(idx, g.m_magic), n = idx - f * M;
     const float2 v = A[idx];
-    float* d = fs + frames[G.f0 + f].dst;
+    float* d = fs + fr[f].dst;
     d[2 * n] = v.x * invN * han[2 * n];
     d[2 * n + 1] = v.y * invN * han[2 * n + 1];
   }
+}
+
+// ------------------------------------------------ fused frame pipeline
+// Inputs of one frame, prefetched into registers one frame ahead (their HBM
+// latency overlaps the previous frame's inverse FFT and overlap-add):
+//   FILTER: s[i] = sound (y[2n], y[2n+1]), n = 64 i + lane; a[i] = envelope
+//           (env[k], env[M - k]) with k = 64 i + lane (k = 0: env[0], env[M-1]); xh = env[half]
+//   NOISE:  a[i] = uniforms (u[k], u[M - k]), b[i] = filter (f[k], f[M - k]) (k = 0: M - 1); xh, xh2 at half
+struct FramePf {
+  float2 s[SG_PF_SRC];
+  float2 a[SG_PF_PAIR], b[SG_PF_PAIR];
+  float xh, xh2;
+};
+
+__device__ __forceinline__ void frame_prefetch(FramePf& P, const SgFrame& F, int mode, int M,
+                                               const float* __restrict__ fl, const float* __restrict__ fs, int lane) {
+  const int half = M / 2;
+  if (mode == SG_FRAME_FILTER) {
+    const float* src = fs + F.src;
+    const float* env = fl + F.env;
+#pragma unroll
+    for (int i = 0; i < SG_PF_SRC; ++i) {
+      const int n = 64 * i + lane;
+      if (n < M) P.s[i] = make_float2(src[2 * n], src[2 * n + 1]);
+    }
+#pragma unroll
+    for (int i = 0; i < SG_PF_PAIR; ++i) {
+      const int k = 64 * i + lane;
+      if (k <= half) P.a[i] = make_float2(env[k], env[k == 0 ? M - 1 : M - k]);
+    }
+    P.xh = env[half];
+  } else {
+    const float* u = fl + F.src;
+    const float* flt = fl + F.env;
+#pragma unroll
+    for (int i = 0; i < SG_PF_PAIR; ++i) {
+      const int k = 64 * i + lane;
+      if (k <= half) {
+        const int km = k == 0 ? M - 1 : M - k;
+        P.a[i] = make_float2(u[k], u[km]);
+        P.b[i] = make_float2(flt[k], flt[km]);
+      }
+    }
+    P.xh = u[half];
+    P.xh2 = flt[half];
+  }
+}
+
+// Consume P: the frame's packed inverse-FFT input lands in A (FILTER: sound x
+// hamming -> forward FFT -> untangle, /wl x envelope, seewave's Hermitian
+// mirror; NOISE: uniforms x filter). Tables in LDS: ham (wl floats), twN (M pairs).
+__device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mode, const SgFftGeom& g,
+                                            const float2* twS, const float2* twN, const float* ham, int lane) {
+  int M = g.M, N = g.wl;
+  __asm__ __volatile__("" : "+s"(M), "+s"(N));  // opaque: no hoisting across the caller's frame loop
+  const float invN = 1.f / (float)N;
+  const int half = M / 2;
+  if (mode == SG_FRAME_FILTER) {
+#pragma unroll
+    for (int i = 0; i < SG_PF_SRC; ++i) {
+      const int n = 64 * i + lane;
+      if (n < M) A[n] = make_float2(P.s[i].x * ham[2 * n], P.s[i].y * ham[2 * n + 1]);
+    }
+    sg_wave_fence();
+    fft_w<false>(A, g, twS, lane);
+    // untangle X[k] = E + W_N^k O (E, O from Z_k, conj Z_{M-k}), Y = X / wl x env,
+    // pack for the inverse; pair k owns slots k and M - k, the k = 0 lane also
+    // reads slots 1, M - 1 and half; every read of an iteration precedes its writes
+#pragma unroll
+    for (int i = 0; i < SG_PF_PAIR; ++i) {
+      const int k0 = 64 * i;
+      if (k0 > half) break;
+      const int k = k0 + lane;
+      const bool act = k <= half && (k == 0 || k < M - k);
+      const int kk = act ? k : 0;
+      const int km = kk == 0 ? 0 : M - kk;
+      const float2 za = A[kk], zb = A[km];
+      float2 z1 = za, zM1 = za, zh = za;
+      if (i == 0) {
+        z1 = A[1];
+        zM1 = A[M - 1];
+        zh = A[half];
+      }
+      // lane 0's reads of slots 1 and M - 1 must precede lane 1's writes: per
+      // thread the compiler may sink them into the k = 0 branch, which the
+      // SIMT code runs after the other branch
+      sg_wave_fence();
+      if (!act) continue;
+      auto X_at = [&](float2 a, float2 b, int t) -> float2 {
+        const float2 e = make_float2(0.5f * (a.x + b.x), 0.5f * (a.y - b.y));
+        const float2 dd = make_float2(a.x - b.x, a.y + b.y);
+        const float2 o = make_float2(0.5f * dd.y, -0.5f * dd.x);
+        return cadd(e, cmul(o, twN[t]));
+      };
+      const float ek = P.a[i].x * invN, em = P.a[i].y * invN;  // k = 0: env[0], env[M - 1]
+      if (kk == 0) {
+        const float2 x0 = X_at(za, za, 0), xl = X_at(zM1, z1, M - 1);
+        const float y0 = x0.x * ek;
+        const float nyq = xl.x * em;
+        A[0] = make_float2(y0 + nyq, y0 - nyq);
+        if (M % 2 == 0) {
+          const float2 xk = X_at(zh, zh, half);
+          const float eh = P.xh * invN;
+          const float2 yk = make_float2(xk.x * eh, xk.y * eh);
+          float2 a, b;
+          pack_pair(yk, yk, twN[half], a, b);
+          A[half] = a;
+        }
+      } else {
+        const float2 xk = X_at(za, zb, kk), xm = X_at(zb, za, km);
+        const float2 yk = make_float2(xk.x * ek, xk.y * ek);
+        const float2 ym = make_float2(xm.x * em, xm.y * em);
+        float2 a, b;
+        pack_pair(yk, ym, twN[kk], a, b);
+        A[kk] = a;
+        A[km] = b;
+      }
+    }
+  } else {  // SG_FRAME_NOISE: real spectrum u x filter, packed
+#pragma unroll
+    for (int i = 0; i < SG_PF_PAIR; ++i) {
+      const int k = 64 * i + lane;
+      if (k > half) continue;
+      if (k == 0) {
+        const float y0 = P.a[i].x * P.b[i].x, nyq = P.a[i].y * P.b[i].y;
+        A[0] = make_float2(y0 + nyq, y0 - nyq);
+        if (M % 2 == 0) {
+          const float2 yk = make_float2(P.xh * P.xh2, 0.f);
+          float2 a, b;
+          pack_pair(yk, yk, twN[half], a, b);
+          A[half] = a;
+        }
+      } else if (k < M - k) {
+        const float2 yk = make_float2(P.a[i].x * P.b[i].x, 0.f), ym = make_float2(P.a[i].y * P.b[i].y, 0.f);
+        float2 a, b;
+        pack_pair(yk, ym, twN[k], a, b);
+        A[k] = a;
+        A[M - k] = b;
+      }
+    }
+  }
+  sg_wave_fence();
+}
+
+// Fused STFT x envelope -> ISTFT -> overlap-add (seewave istft,
+// seewave.r:3462-3484) -> matchLengths trim. Each wavefront owns one segment
+// (a run of consecutive frames of one OLA) and walks it frame by frame with
+// no workgroup barrier: the frame is transformed in its LDS slice, windowed
+// (/wl x hanning) and added to the carried partial sums of earlier frames,
+// which live in registers (pair layout: lane l, register r <-> samples
+// 2(64r + l), +1 of the frame). The samples before the next frame's start are
+// final (scaled, trimmed, written, max-reduced); the rest, shifted by the
+// hop, is the next carry. The next frame's inputs are prefetched into
+// registers while this frame's inverse FFT runs. Frames never leave LDS;
+// summation is in frame order, so results are deterministic.
+// LDS: twS (M pairs), twN (M pairs), ham + han (M pairs each), SG_FFT_WAVES slices (M pairs each).
+extern "C" __global__ __launch_bounds__(SG_FFT_WAVES * 64) __attribute__((amdgpu_waves_per_eu(2))) void sg_stft_ola(
+    const SgSegment* __restrict__ segs, const SgOla* __restrict__ olas, const SgFrame* __restrict__ frames,
+    const SgFftGeom* __restrict__ geoms, const float* __restrict__ fl, float* __restrict__ fs,
+    float* __restrict__ slotmax) {
+  constexpr int W = SG_FFT_WAVES, NT = W * 64;
+  extern __shared__ float4 lds4[];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // w wave-uniform
+  const SgFftGeom& g = geoms[segs[blockIdx.x * W].geom];  // the planner groups segments by geometry
+  const int M = g.M, N = g.wl;
+  float2* twS = reinterpret_cast<float2*>(lds4);
+  float2* twN = twS + M;
+  float* ham = reinterpret_cast<float*>(twN + M);
+  float* han = ham + N;
+  {
+    const float2* tsg = reinterpret_cast<const float2*>(fl + g.tws);
+    const float2* tng = reinterpret_cast<const float2*>(fl + g.tw) + M;
+    const float* wg = fl + g.win;
+    for (int t = threadIdx.x; t < M; t += NT) {
+      if (t < M - 1) twS[t] = tsg[t];
+      twN[t] = tng[t];
+    }
+    for (int t = threadIdx.x; t < 2 * N; t += NT) ham[t] = wg[t];  // hamming then hanning
+  }
+  __syncthreads();
+  const SgSegment S = segs[blockIdx.x * W + w];
+  if (S.nf <= 0) return;  // padding segment
+  const SgOla& O = olas[S.ola];
+  float2* A = twS + M * (4 + w);
+  const float* Af = reinterpret_cast<const float*>(A);
+  const float invN = 1.f / (float)N;
+  const int hi = O.hi;
+  const double h = O.h;
+  auto bstart = [&](int f) -> int { return hi > 0 ? f * hi : (int)floor((double)f * h); };
+  const int first = (int)O.first, len = (int)O.len;
+  const float scale = O.scale;
+  float* out = fs + O.out;
+  float m = -INFINITY;
+  float2 C[SG_CARRY_PAIRS];
+#pragma unroll
+  for (int r = 0; r < SG_CARRY_PAIRS; ++r) C[r] = make_float2(0.f, 0.f);
+  FramePf P;
+  int bf = bstart(S.f0);
+  for (int k = 0; k < S.nf; ++k) {
+    {
+      int Mk = M;
+      __asm__ __volatile__("" : "+s"(Mk));
+      frame_prefetch(P, frames[S.fdev + k], S.mode, Mk, fl, fs, lane);
+    }
+    frame_front(A, P, S.mode, g, twS, twN, ham, lane);
+    fft_w<true>(A, g, twS, lane);
+    int Mk = M, Nk = N;
+    __asm__ __volatile__("" : "+s"(Mk), "+s"(Nk));
+    // window (/wl x hanning) and add the carry (pairs n = 64 r + lane)
+#pragma unroll
+    for (int r = 0; r < SG_CARRY_PAIRS; ++r) {
+      const int n = 64 * r + lane;
+      if (n < Mk) {
+        const float2 v = A[n];
+        A[n] = make_float2(fmaf(v.x * invN, han[2 * n], C[r].x), fmaf(v.y * invN, han[2 * n + 1], C[r].y));
+      }
+    }
+    for (int n = 64 * SG_CARRY_PAIRS + lane; n < Mk; n += 64) {
+      const float2 v = A[n];
+      A[n] = make_float2(v.x * invN * han[2 * n], v.y * invN * han[2 * n + 1]);
+    }
+    sg_wave_fence();
+    const bool lastf = k == S.nf - 1;
+    const int bn = lastf ? S.pb : bstart(S.f0 + k + 1);
+    const int D = bn - bf;  // samples [bf, bn) are final
+    for (int i = lane; i < D; i += 64) {
+      const int p = bf + i;
+      const int q = p - first;
+      if (p >= S.pa && q >= 0 && q < len) {
+        const float v = (i < Nk ? Af[i] : 0.f) * scale;
+        out[q] = v;
+        m = fmaxf(m, v);
+      }
+    }
+    if (!lastf) {
+#pragma unroll
+      for (int r = 0; r < SG_CARRY_PAIRS; ++r) {
+        const int i0 = 2 * (64 * r + lane) + D;
+        C[r] = make_float2(i0 < Nk ? Af[i0] : 0.f, i0 + 1 < Nk ? Af[i0 + 1] : 0.f);
+      }
+    }
+    sg_wave_fence();  // the next frame overwrites the slice
+    bf = bn;
+  }
+  // matchLengths padding (zeros) outside the istft output
+  if (S.flags & SG_SEG_FIRST)
+    for (int q = lane; q < min(len, -first); q += 64) {
+      out[q] = 0.f;
+      m = fmaxf(m, 0.f);
+    }
+  if (S.flags & SG_SEG_LAST)
+    for (int p = max((int)O.xlen, first) + lane; p < first + len; p += 64) {
+      out[p - first] = 0.f;
+      m = fmaxf(m, 0.f);
+    }
+  m = sgd::wave_max(m);
+  if (lane == 0) slotmax[S.slot] = m;
+}
+
+// Test probe: wavefront w transforms frame w (M complex points, in place) with
+// the stage kernel of sg_stft_ola; inverse = conjugate twiddles, no scaling.
+extern "C" __global__ __launch_bounds__(64) void sg_fft_probe(const SgFftGeom* __restrict__ geom,
+                                                              const float* __restrict__ fl, float2* __restrict__ data,
+                                                              int inverse) {
+  extern __shared__ float4 lds4[];
+  const SgFftGeom& g = geom[0];
+  const int M = g.M, lane = threadIdx.x;
+  float2* twS = reinterpret_cast<float2*>(lds4);
+  float2* A = twS + M;
+  const float2* tsg = reinterpret_cast<const float2*>(fl + g.tws);
+  float2* d = data + (int64_t)blockIdx.x * M;
+  for (int t = lane; t < M; t += 64) {
+    if (t < M - 1) twS[t] = tsg[t];
+    A[t] = d[t];
+  }
+  sg_wave_fence();
+  if (inverse) fft_w<true>(A, g, twS, lane);
+  else fft_w<false>(A, g, twS, lane);
+  for (int t = lane; t < M; t += 64) d[t] = A[t];
 }
 
 using sgd::contour_at;
@@ -372,7 +782,16 @@ extern "C" __global__ __launch_bounds__(256) void sg_ola(const SgOlaTile* __rest
     if (q >= O.len) break;
     const int64_t p = O.first + q;
     float acc = 0.f;
-    if (p >= 0 && p < O.xlen) {
+    if (p >= 0 && p < O.xlen && O.hi > 0) {
+      // whole-sample hop: frames f with f hi <= p < f hi + wl
+      const int pi = (int)p;
+      int f = pi / O.hi;
+      if (f > O.nframes - 1) f = O.nframes - 1;
+      int i = pi - f * O.hi;
+      const float* fr0 = fs + O.frames;
+      for (; f >= 0 && i < O.wl; --f, i += O.hi) acc += fr0[(int64_t)f * O.wl + i];
+      acc *= O.scale;
+    } else if (p >= 0 && p < O.xlen) {
       // frames f with floor(f h) <= p < floor(f h) + wl
       int64_t fhi = (int64_t)floor((double)p / O.h);
       if (fhi > O.nframes - 1) fhi = O.nframes - 1;
@@ -402,7 +821,7 @@ extern "C" __global__ __launch_bounds__(64) void sg_ola_max(const SgOla* __restr
   const int o = blockIdx.x;
   if (o >= n_olas) return;
   const SgOla& O = olas[o];
-  const int nt = (int)((O.len + SG_OLA_TILE - 1) / SG_OLA_TILE);
+  const int nt = O.nslot;
   float m = -INFINITY;
   for (int i = threadIdx.x; i < nt; i += 64) m = fmaxf(m, tilemax[O.tile0 + i]);
   m = wave_max_f(m);
@@ -463,22 +882,63 @@ extern "C" __global__ __launch_bounds__(256) void sg_mix(const SgMixTile* __rest
 // ---------------------------------------------------------------- launchers
 #include "sg_exec.h"
 namespace sg {
+// launch failures (bad configuration, LDS over the opted-in size) are loud
+#define SG_LAUNCHED(name)                                                                       \
+  do {                                                                                          \
+    const hipError_t _e = hipGetLastError();                                                    \
+    if (_e != hipSuccess) throw SgError(SG_E_DEVICE, std::string("launch " name ": ") + hipGetErrorString(_e)); \
+  } while (0)
+
 void launch_fft_frames(const DevicePlan& D, int64_t g0, int64_t n_groups, int lds_bytes, hipStream_t s) {
   if (n_groups <= 0) return;
+  static int lds_max = 0;
+  if (lds_bytes > lds_max) {  // dynamic LDS above 64 KB must be opted into (160 KB per CU on gfx950)
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&sg_fft_frames), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            lds_bytes) != hipSuccess)
+      throw SgError(SG_E_DEVICE, "sg_fft_frames: dynamic LDS " + std::to_string(lds_bytes) + " B refused");
+    lds_max = lds_bytes;
+  }
   hipLaunchKernelGGL(sg_fft_frames, dim3((unsigned)n_groups), dim3(SG_FFT_THREADS), lds_bytes, s, D.fgroups + g0,
                      D.frames,
                      D.geoms, D.fl, D.fs);
+  SG_LAUNCHED("sg_fft_frames");
 }
-void launch_ola(const DevicePlan& D, int64_t t0, int64_t n_tiles, int64_t o0, int64_t n_olas, hipStream_t s) {
+void launch_stft_ola(const DevicePlan& D, int64_t s0, int64_t n_segs, int lds_bytes, hipStream_t s) {
+  if (n_segs <= 0) return;
+  static int lds_max = 0;
+  if (lds_bytes > lds_max) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&sg_stft_ola), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            lds_bytes) != hipSuccess)
+      throw SgError(SG_E_DEVICE, "sg_stft_ola: dynamic LDS " + std::to_string(lds_bytes) + " B refused");
+    lds_max = lds_bytes;
+  }
+  hipLaunchKernelGGL(sg_stft_ola, dim3((unsigned)(n_segs / SG_FFT_WAVES)), dim3(SG_FFT_WAVES * 64), lds_bytes, s,
+                     D.olasegs + s0,
+                     D.olas, D.frames, D.geoms, D.fl, D.fs, D.olatilemax);
+  SG_LAUNCHED("sg_stft_ola");
+}
+void launch_fft_probe(const SgFftGeom* geom, const float* fl, float* data, int M, int nframes, int inverse,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(sg_fft_probe, dim3((unsigned)nframes), dim3(64), 2 * M * 8, s, geom, fl,
+                     reinterpret_cast<float2*>(data), inverse);
+  SG_LAUNCHED("sg_fft_probe");
+}
+void launch_ola(const DevicePlan& D, int64_t t0, int64_t n_tiles, hipStream_t s) {
   if (n_tiles <= 0) return;
   hipLaunchKernelGGL(sg_ola, dim3((unsigned)n_tiles), dim3(256), 0, s, D.olatiles + t0, D.olas, D.fs,
                      D.olatilemax + t0);
+  SG_LAUNCHED("sg_ola");
+}
+void launch_ola_max(const DevicePlan& D, int64_t o0, int64_t n_olas, hipStream_t s) {
+  if (n_olas <= 0) return;
   hipLaunchKernelGGL(sg_ola_max, dim3((unsigned)n_olas), dim3(64), 0, s, D.olas + o0, (int)n_olas, D.olatilemax,
                      D.olamax + o0);
+  SG_LAUNCHED("sg_ola_max");
 }
 void launch_mix(const DevicePlan& D, int64_t t0, int64_t n_tiles, float* out, hipStream_t s) {
   if (n_tiles <= 0) return;
   hipLaunchKernelGGL(sg_mix, dim3((unsigned)n_tiles), dim3(256), 0, s, D.mixtiles + t0, D.mixes, D.items, D.olamax,
                      D.cknots, D.fl, D.fs, out);
+  SG_LAUNCHED("sg_mix");
 }
 }  // namespace sg

@@ -295,25 +295,35 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize(
 // ---------------------------------------------------------------- launchers
 #include "sg_exec.h"
 namespace sg {
+#define SG_LAUNCHED(name)                                                                       \
+  do {                                                                                          \
+    const hipError_t _e = hipGetLastError();                                                    \
+    if (_e != hipSuccess) throw SgError(SG_E_DEVICE, std::string("launch " name ": ") + hipGetErrorString(_e)); \
+  } while (0)
+
 void launch_sine_bank(const DevicePlan& D, int64_t t0, int64_t n_tasks, hipStream_t s) {
   if (n_tasks <= 0) return;
   const int64_t blocks = (n_tasks + SG_TASKS_PER_BLOCK - 1) / SG_TASKS_PER_BLOCK;
   hipLaunchKernelGGL(sg_sine_bank, dim3((unsigned)blocks), dim3(256), 0, s, D.tasks + t0, n_tasks, D.amps, D.syls,
                      D.cknots, D.W, D.taskmax + t0);
+  SG_LAUNCHED("sg_sine_bank");
 }
 void launch_piece_max(const DevicePlan& D, int64_t p0, int64_t n_ptiles, hipStream_t s) {
   if (n_ptiles <= 0) return;
   hipLaunchKernelGGL(sg_piece_max, dim3((unsigned)n_ptiles), dim3(256), 0, s, D.ptiles + p0, D.pieces, D.syls,
                      D.cknots, D.W, D.ptilemax + p0);
+  SG_LAUNCHED("sg_piece_max");
 }
 void launch_syl_max(const DevicePlan& D, int64_t s0, int64_t n_syls, hipStream_t s) {
   if (n_syls <= 0) return;
   hipLaunchKernelGGL(sg_syl_max, dim3((unsigned)n_syls), dim3(256), 0, s, D.syls + s0, D.taskmax, D.ptilemax,
                      D.maxes);
+  SG_LAUNCHED("sg_syl_max");
 }
 void launch_harm_finalize(const DevicePlan& D, int64_t f0, int64_t n_stiles, float* out, hipStream_t s) {
   if (n_stiles <= 0) return;
   hipLaunchKernelGGL(sg_harm_finalize, dim3((unsigned)n_stiles), dim3(256), 0, s, D.syl_tiles + f0, D.pieces, D.syls,
                      D.cknots, D.W, D.maxes, out, D.fs);
+  SG_LAUNCHED("sg_harm_finalize");
 }
 }  // namespace sg

@@ -50,11 +50,16 @@ struct Batch {
   std::vector<Copy> copies;              // fl -> fs before the filter phase
   // derived (finalize_spec)
   std::vector<SgFrameGroup> fgroups;
-  int64_t fgroup_split = 0;              // groups [0, split) noise, [split, end) filter
-  int fgroup_lds[2] = {0, 0};            // max dynamic LDS per phase
+  // per phase (0 noise, 1 filter): groups [r1, r2) run sg_fft_frames ([r0, r1) empty: wavefront-kernel
+  // geometries run fused in sg_stft_ola, fgroup_lds[ph][0] = its dynamic LDS)
+  int64_t fgroup_range[2][3] = {{0, 0, 0}, {0, 0, 0}};
+  int fgroup_lds[2][2] = {{0, 0}, {0, 0}};  // max dynamic LDS per phase and kernel
   std::vector<SgOla> olas_dev;
   std::vector<SgOlaTile> olatiles;
   int64_t olatile_split = 0, ola_split = 0;
+  std::vector<SgSegment> olasegs;        // sg_stft_ola work units, SG_FFT_WAVES per workgroup
+  int32_t n_segslots = 0;                // real (non-padding) segments: max slots after the tile slots
+  int64_t seg_range[2][2] = {{0, 0}, {0, 0}};
   std::vector<SgMix> mixes_dev;
   std::vector<SgMixTile> mixtiles;
   int64_t mixtile_split = 0;

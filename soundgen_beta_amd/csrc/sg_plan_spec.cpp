@@ -58,6 +58,22 @@ int geometry(Batch& B, int wl) {
     tw[2 * g.M + 2 * t + 1] = std::sin(b);
   }
   g.tw = fl_push(B, tw.data(), (int64_t)tw.size());
+  {
+    vec ts(2 * (size_t)std::max(1, g.M - 1), 0.0);
+    int ns = 1;
+    for (int s = 0; s < g.nstages; ++s) {
+      const int r = g.radix[s];
+      for (int q = 1; q < r; ++q)
+        for (int jm = 0; jm < ns; ++jm) {
+          const size_t e = (size_t)(ns - 1 + (q - 1) * ns + jm);
+          const double a = -2.0 * M_PI * (double)q * (double)jm / ((double)ns * r);
+          ts[2 * e] = std::cos(a);
+          ts[2 * e + 1] = std::sin(a);
+        }
+      ns *= r;
+    }
+    g.tws = fl_push(B, ts.data(), (int64_t)ts.size());
+  }
   // seewave ftwindow: hamming.w (seewave.r:7431-7437), hanning.w (:7444-7450)
   vec win(2 * (size_t)wl);
   for (int i = 0; i < wl; ++i) {
@@ -67,9 +83,35 @@ int geometry(Batch& B, int wl) {
   g.win = fl_push(B, win.data(), (int64_t)win.size());
   // frames per workgroup: one in-place LDS buffer of fb * M complex points,
   // fb * M <= 8192 (64 KB: two workgroups per CU; sg_fft.hip SG_FFT_SLOTS)
-  g.fb = std::max(1, std::min(16, kFftSlots / g.M));
-  if (g.fb * g.M > kFftSlots) throw SgError(SG_E_UNSUPPORTED, "FFT: window too long for LDS (wl > 16384)");
-  g.lds_bytes = g.fb * g.M * 8;
+  // wavefront-per-frame kernel when every stage's butterflies fit the
+  // register state of one wavefront: ceil(M / R / 64) <= max(1, SG_WAVE_STATE / R)
+  g.kind = SG_FFT_WAVE;
+  for (int s = 0; s < g.nstages; ++s) {
+    const int r = g.radix[s], nb = (g.M / r + 63) / 64;
+    if (nb > std::max(1, SG_WAVE_STATE / r)) g.kind = SG_FFT_WG;
+  }
+  // sg_stft_ola: the next frame's inputs fit the prefetch registers, and the
+  // LDS tables (twiddles, W_N^k, hamming, hanning) + SG_FFT_WAVES frame
+  // slices, M pairs each, fit the 160 KB of a CU
+  if (g.M > 64 * SG_PF_SRC || g.M / 2 + 1 > 64 * SG_PF_PAIR) g.kind = SG_FFT_WG;
+  if ((int64_t)(SG_FFT_WAVES + 4) * g.M * 8 > 160 * 1024) g.kind = SG_FFT_WG;
+  if (g.kind == SG_FFT_WAVE) {
+    g.fb = SG_FFT_WAVES;
+    g.lds_bytes = (SG_FFT_WAVES + 4) * g.M * 8;
+  } else {
+    g.fb = std::max(1, std::min(16, kFftSlots / g.M));
+    if (g.fb * g.M > kFftSlots) throw SgError(SG_E_UNSUPPORTED, "FFT: window too long for LDS (wl > 16384)");
+    g.lds_bytes = (g.fb + 1) * g.M * 8;  // + the W_M twiddle table
+  }
+  auto magic = [](int d) -> uint32_t { return d <= 1 ? 0u : (uint32_t)(((1ull << 32) + (uint64_t)d - 1) / (uint64_t)d); };
+  int ns = 1;
+  for (int s = 0; s < g.nstages; ++s) {
+    g.mr_magic[s] = magic(g.M / g.radix[s]);
+    g.ns_magic[s] = magic(ns);
+    ns *= g.radix[s];
+  }
+  g.m_magic = magic(g.M);
+  g.hp_magic = magic(g.M / 2 + 1);
   B.geoms.push_back(g);
   return (int)B.geoms.size() - 1;
 }
@@ -93,9 +135,18 @@ static IstftGeom istft_geom(int wl, int64_t nc, double ovlp) {
   return g;
 }
 
+// sg_stft_ola handles the OLA when its geometry runs one wavefront per frame
+// and the overlap carried between frames fits the carry registers
+static bool fusable(const SgFftGeom& g, double hop) {
+  return g.kind == SG_FFT_WAVE && hop >= 1 && (double)g.wl - std::floor(hop) <= 128.0 * SG_CARRY_PAIRS;
+}
+
 static int push_ola(Batch& B, int phase, int64_t frames, int64_t nframes, int wl, const IstftGeom& ig, int64_t first,
-                    int64_t len, int64_t out) {
+                    int64_t len, int64_t out, bool fused) {
+  if (fused && ig.xlen >= (int64_t)1 << 31) throw SgError(SG_E_UNSUPPORTED, "istft: output longer than 2^31 samples");
   SgOla o{};
+  o.fidx = (int32_t)((int64_t)B.frames[phase].size() - nframes);
+  o.fused = fused ? 1 : 0;
   o.frames = frames;
   o.out = out;
   o.first = first;
@@ -105,6 +156,7 @@ static int push_ola(Batch& B, int phase, int64_t frames, int64_t nframes, int wl
   o.nframes = (int32_t)nframes;
   o.wl = wl;
   o.scale = ig.scale;
+  o.hi = (ig.h == std::floor(ig.h) && ig.h >= 1 && ig.h < 2147483647.0) ? (int32_t)ig.h : 0;
   B.olas[phase].push_back(o);
   return (int)B.olas[phase].size() - 1;
 }
@@ -121,12 +173,13 @@ int plan_filter(Batch& B, int64_t sound, int64_t L, int wl, double overlap, cons
   for (double x0 : step)
     if ((int64_t)x0 - 1 + wl > L) throw SgError(SG_E_DOMAIN, "stft: frame beyond the sound");
   const int64_t env_off = fl_push(B, env.data(), (int64_t)env.size());
-  const int64_t fr = fs_alloc(B, nc * wl);
+  const bool fused = fusable(B.geoms[gi], (double)wl * (100 - overlap) / 100);
+  const int64_t fr = fused ? 0 : fs_alloc(B, nc * wl);  // frame scratch only for the unfused path
   for (int64_t c = 0; c < nc; ++c) {
     SgFrame f{};
     f.src = sound + (int64_t)step[c] - 1;  // wave[x:(x + wl - 1)], x truncated
     f.env = env_off + (env_nc == 1 ? 0 : c * nr);
-    f.dst = fr + c * wl;
+    f.dst = fused ? -1 : fr + c * wl;
     B.frames[1].push_back(f);
     B.frame_geom[1].push_back(gi);
   }
@@ -135,7 +188,7 @@ int plan_filter(Batch& B, int64_t sound, int64_t L, int wl, double overlap, cons
   B.fft_frames += nc;
   *out_len = ig.xlen;
   *out_fs = out;
-  return push_ola(B, 1, fr, nc, wl, ig, 0, ig.xlen, out);
+  return push_ola(B, 1, fr, nc, wl, ig, 0, ig.xlen, out, fused);
 }
 
 bool plan_noise(Batch& B, Rng& R, int64_t len, const sg_anchors& noiseAnchors, double rolloffNoise,
@@ -168,12 +221,13 @@ bool plan_noise(Batch& B, Rng& R, int64_t len, const sg_anchors& noiseAnchors, d
   vec u((size_t)(nr * nc));
   for (auto& x : u) x = R.unif();
   const int64_t u_off = fl_push(B, u.data(), (int64_t)u.size());
-  const int64_t fr = fs_alloc(B, nc * wl);
+  const bool fused = fusable(B.geoms[gi], (double)wl * (100 - overlap) / 100);
+  const int64_t fr = fused ? 0 : fs_alloc(B, nc * wl);
   for (int64_t c = 0; c < nc; ++c) {
     SgFrame f{};
     f.src = u_off + c * nr;
     f.env = filt_off + ((int64_t)fri[c] - 1) * nr;
-    f.dst = fr + c * wl;
+    f.dst = fused ? -1 : fr + c * wl;
     B.frames[0].push_back(f);
     B.frame_geom[0].push_back(gi);
   }
@@ -187,7 +241,7 @@ bool plan_noise(Batch& B, Rng& R, int64_t len, const sg_anchors& noiseAnchors, d
     first = start - 1 - (ig.xlen < len ? len : 0);
   }
   const int64_t raw = fs_alloc(B, len);
-  const int ola = push_ola(B, 0, fr, nc, wl, ig, first, len, raw);
+  const int ola = push_ola(B, 0, fr, nc, wl, ig, first, len, raw, fused);
   B.fft_frames += nc;
   item->raw = raw;
   item->len = len;
@@ -418,48 +472,126 @@ vec spectral_envelope(Rng& R, int64_t nr, int64_t nc, const sg_formants* F, doub
 
 // ------------------------------------------------------------ finalize
 void finalize_spec(Batch& B) {
-  // frame groups: per phase, frames of one geometry in runs of g.fb
+  // frames: per phase, sorted by (kernel, geometry), stable so that the
+  // frames of one OLA stay consecutive; groups for the workgroup kernel only
   B.fgroups.clear();
+  std::vector<int64_t> pos[2];
   for (int ph = 0; ph < 2; ++ph) {
-    if (ph == 1) B.fgroup_split = (int64_t)B.fgroups.size();
-    // frames are emitted per call; sort them by geometry keeping order
+    auto key = [&](int64_t i) {
+      const int gi = B.frame_geom[ph][i];
+      return (int64_t)(B.geoms[gi].kind == SG_FFT_WAVE ? 0 : 1) * (1 << 20) + gi;
+    };
     std::vector<int64_t> idx(B.frames[ph].size());
     for (size_t i = 0; i < idx.size(); ++i) idx[i] = (int64_t)i;
-    std::stable_sort(idx.begin(), idx.end(),
-                     [&](int64_t a, int64_t b) { return B.frame_geom[ph][a] < B.frame_geom[ph][b]; });
+    std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return key(a) < key(b); });
     std::vector<SgFrame> fr(idx.size());
     std::vector<int32_t> fg(idx.size());
-    for (size_t i = 0; i < idx.size(); ++i) { fr[i] = B.frames[ph][idx[i]]; fg[i] = B.frame_geom[ph][idx[i]]; }
+    pos[ph].assign(idx.size(), 0);
+    for (size_t i = 0; i < idx.size(); ++i) {
+      fr[i] = B.frames[ph][idx[i]];
+      fg[i] = B.frame_geom[ph][idx[i]];
+      pos[ph][idx[i]] = (int64_t)i;
+    }
     B.frames[ph] = fr;
     B.frame_geom[ph] = fg;
     const int32_t base = ph == 0 ? 0 : (int32_t)B.frames[0].size();
-    int lds = 0;
+    B.fgroup_lds[ph][0] = B.fgroup_lds[ph][1] = 0;
+    B.fgroup_range[ph][0] = B.fgroup_range[ph][1] = (int64_t)B.fgroups.size();
     for (size_t i = 0; i < fr.size();) {
       const int gi = fg[i];
       const SgFftGeom& g = B.geoms[gi];
+      if (g.kind == SG_FFT_WAVE) {  // transformed inside sg_stft_ola
+        B.fgroup_lds[ph][0] = std::max(B.fgroup_lds[ph][0], g.lds_bytes);
+        ++i;
+        continue;
+      }
       size_t j = i;
       while (j < fr.size() && fg[j] == gi && (int)(j - i) < g.fb) ++j;
       B.fgroups.push_back(SgFrameGroup{gi, ph == 0 ? SG_FRAME_NOISE : SG_FRAME_FILTER, base + (int32_t)i,
                                        (int32_t)(j - i)});
-      lds = std::max(lds, g.lds_bytes);
+      B.fgroup_lds[ph][1] = std::max(B.fgroup_lds[ph][1], g.lds_bytes);
       i = j;
     }
-    B.fgroup_lds[ph] = lds;
+    B.fgroup_range[ph][2] = (int64_t)B.fgroups.size();
   }
-  // OLAs: device table [noise..., filter...]; tiles per phase
+  // OLAs: device table [noise..., filter...]; unfused ones get sg_ola tiles
+  // (slots [0, #tiles)), fused ones sg_stft_ola segments (slots after them)
   B.olas_dev.clear();
   B.olatiles.clear();
+  B.olasegs.clear();
   B.ola_split = (int64_t)B.olas[0].size();
   for (int ph = 0; ph < 2; ++ph) {
     if (ph == 1) B.olatile_split = (int64_t)B.olatiles.size();
+    const int32_t base = ph == 0 ? 0 : (int32_t)B.frames[0].size();
     for (const SgOla& o0 : B.olas[ph]) {
       SgOla o = o0;
-      o.tile0 = (int32_t)B.olatiles.size();
+      o.fidx = base + (int32_t)pos[ph][o0.fidx];
       const int32_t oi = (int32_t)B.olas_dev.size();
-      for (int64_t q0 = 0; q0 < o.len; q0 += SG_OLA_TILE) B.olatiles.push_back(SgOlaTile{oi, 0, q0});
+      if (!o.fused) {
+        o.tile0 = (int32_t)B.olatiles.size();
+        for (int64_t q0 = 0; q0 < o.len; q0 += SG_OLA_TILE) B.olatiles.push_back(SgOlaTile{oi, 0, q0});
+        o.nslot = (int32_t)B.olatiles.size() - o.tile0;
+      }
       B.olas_dev.push_back(o);
     }
   }
+  const int32_t nt = (int32_t)B.olatiles.size();
+  int32_t nslots = 0;  // real segments so far (slots nt + nslots)
+  for (int ph = 0; ph < 2; ++ph) {
+    B.seg_range[ph][0] = (int64_t)B.olasegs.size();
+    const size_t o_lo = ph == 0 ? 0 : (size_t)B.ola_split, o_hi = ph == 0 ? (size_t)B.ola_split : B.olas_dev.size();
+    const int32_t fbase = ph == 0 ? 0 : (int32_t)B.frames[0].size();
+    // fused OLAs of the phase ordered by geometry; a workgroup's SG_FFT_WAVES
+    // segments share one geometry (padding segments have nf = 0)
+    std::vector<size_t> order;
+    for (size_t oi = o_lo; oi < o_hi; ++oi)
+      if (B.olas_dev[oi].fused) order.push_back(oi);
+    auto geom_of = [&](size_t oi) { return B.frame_geom[ph][B.olas_dev[oi].fidx - fbase]; };
+    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return geom_of(a) < geom_of(b); });
+    int cur_geom = -1;
+    auto pad = [&]() {
+      while (B.olasegs.size() % SG_FFT_WAVES) {
+        SgSegment d{};
+        d.geom = cur_geom;
+        B.olasegs.push_back(d);
+      }
+    };
+    for (size_t oi : order) {
+      SgOla& o = B.olas_dev[oi];
+      const int gi = geom_of(oi);
+      if (gi != cur_geom) {
+        pad();
+        cur_geom = gi;
+      }
+      auto bstart = [&](int64_t f) -> int64_t {
+        return o.hi > 0 ? f * o.hi : (int64_t)std::floor((double)f * o.h);
+      };
+      const int64_t n = o.nframes;
+      const int64_t nseg = std::max<int64_t>(1, (n + SG_SEG_FRAMES - 1) / SG_SEG_FRAMES);
+      o.tile0 = nt + nslots;
+      o.nslot = (int32_t)nseg;
+      for (int64_t k = 0; k < nseg; ++k) {
+        const int64_t F0 = k * n / nseg, F1 = (k + 1) * n / nseg;
+        SgSegment sg{};
+        sg.ola = (int32_t)oi;
+        sg.geom = gi;
+        sg.mode = ph == 0 ? SG_FRAME_NOISE : SG_FRAME_FILTER;
+        sg.pa = k == 0 ? 0 : (int32_t)bstart(F0);
+        sg.pb = k == nseg - 1 ? (int32_t)o.xlen : (int32_t)bstart(F1);
+        int64_t f0 = F0;
+        while (f0 > 0 && bstart(f0 - 1) + o.wl > sg.pa) --f0;  // frames overlapping the first owned sample
+        sg.f0 = (int32_t)f0;
+        sg.nf = (int32_t)(F1 - f0);
+        sg.fdev = o.fidx + (int32_t)f0;
+        sg.slot = nt + nslots++;
+        sg.flags = (k == 0 ? SG_SEG_FIRST : 0) | (k == nseg - 1 ? SG_SEG_LAST : 0);
+        B.olasegs.push_back(sg);
+      }
+    }
+    pad();
+    B.seg_range[ph][1] = (int64_t)B.olasegs.size();
+  }
+  B.n_segslots = nslots;
   // items and mixes referring to filter-phase OLAs: device index = ola_split + i
   for (SgNoiseItem& it : B.items)
     if (it.flags & SG_ITEM_FILTER_OLA) {

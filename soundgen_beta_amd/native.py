@@ -11,7 +11,7 @@ import re
 from . import _abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libsoundgen_hip.so")
+LIB_PATH = os.environ.get("SG_HIP_LIB") or os.path.join(_HERE, "lib", "libsoundgen_hip.so")  # override: experiments
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "soundgen_hip.h")
 
 _lib = None
@@ -82,6 +82,8 @@ def lib():
                                        C.c_double, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double,
                                        C.c_double, C.POINTER(_abi.sg_random), dp]
     L.sg_get_rolloff.argtypes = [dp, C.c_int32, C.c_int32] + [C.c_double] * 8 + [dp, C.POINTER(C.c_int32)]
+    fp = C.POINTER(C.c_float)
+    L.sg_debug_wave_fft.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, fp, fp]
     L.sg_abi_version.restype = C.c_int
     _lib = L
     return L

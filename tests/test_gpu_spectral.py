@@ -14,6 +14,32 @@ def _rms(a, b):
     return float(np.sqrt(np.mean((np.asarray(a, np.float64) - b) ** 2)))
 
 
+@pytest.mark.parametrize("wl", [8, 64, 440, 800, 1000, 1764, 2048, 2204, 2400])
+def test_wave_fft_vs_numpy(wl):
+    """The wavefront FFT stages (radices 2, 4, odd primes) against numpy, both directions."""
+    import ctypes as C
+    from soundgen_beta_amd import native
+    M, nf = wl // 2, 3
+    rng = np.random.default_rng(wl)
+    x = (rng.normal(size=(nf, M)) + 1j * rng.normal(size=(nf, M))).astype(np.complex64)
+    ctx = native.Context(0)
+    try:
+        for inv in (0, 1):
+            src = np.ascontiguousarray(x).view(np.float32).ravel()
+            dst = np.zeros_like(src)
+            fp = C.POINTER(C.c_float)
+            rc = native.lib().sg_debug_wave_fft(ctx.ptr, wl, inv, nf, src.ctypes.data_as(fp), dst.ctypes.data_as(fp))
+            if rc == -4:  # SG_E_UNSUPPORTED: not a wavefront-path geometry
+                pytest.skip("wl %d runs the workgroup FFT" % wl)
+            native.check(rc, ctx.ptr)
+            got = dst.view(np.complex64).reshape(nf, M)
+            want = np.fft.ifft(x, axis=1) * M if inv else np.fft.fft(x, axis=1)
+            err = np.abs(got - want).max() / np.abs(want).max()
+            assert err < 2e-6 * np.log2(M) + 1e-6, (wl, inv, err)
+    finally:
+        ctx.close()
+
+
 @pytest.mark.parametrize("wl", [440, 800, 1764, 2204])
 def test_formant_filter_vs_oracle(oracle, wl):
     from soundgen_beta_amd import api

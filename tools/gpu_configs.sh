@@ -6,7 +6,7 @@ cd "$R"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r01}
-for cfg in c3 c4; do
+for cfg in ${CFGS:-c3 c4}; do
   timeout -k 10 500 python bench.py --config $cfg --steps 5 --warmup 2 --cpu-budget 10 > gpurun_out/bench_${cfg}_$TAG.json 2> gpurun_out/bench_${cfg}_$TAG.err || { tail -20 gpurun_out/bench_${cfg}_$TAG.err; exit 1; }
   cat gpurun_out/bench_${cfg}_$TAG.json
   cd /tmp
