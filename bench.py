@@ -127,6 +127,8 @@ def main():
     ap.add_argument("--calls", type=int, default=0, help="calls per GPU (default: the config's)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gather", action="store_true",
+                    help="after the timed steps, time the packed-output gather to rank 0 (RCCL point-to-point)")
     args = ap.parse_args()
 
     import torch
@@ -188,6 +190,28 @@ def main():
         samples_all = float(samples_rank)
     value = samples_all * args.steps / dt
 
+    gather_ms = None
+    if args.gather and dist:
+        # SURVEY §8e exchange step: every peer sends its packed output to rank 0
+        # concurrently (one xGMI link each); rank 0 receives into one buffer
+        n_loc = torch.tensor([plan.total], device=dev, dtype=torch.int64)
+        counts = [torch.zeros_like(n_loc) for _ in range(world)]
+        dist.all_gather(counts, n_loc)
+        counts = [int(c.item()) for c in counts]
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        tg = time.perf_counter()
+        if rank == 0:
+            bufs = [torch.empty(max(counts[r], 1), dtype=torch.float32, device=dev) for r in range(1, world)]
+            ops = [dist.P2POp(dist.irecv, bufs[r - 1][:counts[r]], r) for r in range(1, world) if counts[r]]
+        else:
+            ops = [dist.P2POp(dist.isend, out[:plan.total], 0)] if plan.total else []
+        for w in (dist.batch_isend_irecv(ops) if ops else []):
+            w.wait()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        gather_ms = (time.perf_counter() - tg) * 1e3
+
     if rank == 0:
         st = plan.stats()
         # algorithmic bytes of one sine-bank launch: fp32 epoch
@@ -222,6 +246,8 @@ def main():
                                   "peak_ops_s": VALU_PEAK_OPS,
                                   "frac": valu_ops / sine_s / VALU_PEAK_OPS if sine_s else 0}},
         }
+        if gather_ms is not None:
+            res["gather_ms"] = gather_ms
         if not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(calls, args.cpu_budget)
         print(json.dumps(res), flush=True)

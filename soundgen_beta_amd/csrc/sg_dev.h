@@ -97,6 +97,8 @@ struct SgContour {
   int64_t k_off;     // offset (doubles) of x[nk], y, b, c, d arrays (5*nk)
   double a, b;       // flat value / seq from,to ; spline x0,x1
   double lo, hi;     // clamp (use -inf/inf when absent)
+  double by;         // (b - a) / (L - 1) for the planned length L (device skips the division)
+  int64_t L;
   int32_t db;        // 1: apply 2^(v/10)
   int32_t pad;
 };
@@ -130,6 +132,10 @@ struct SgSylTile {
   int32_t syl;
   int32_t piece;     // piece containing k0
   int64_t k0;
+  // finalize tiles: per wavefront w (samples k0 + 256 w ...) the piece and the
+  // drift-knot interval containing its first sample (planner; no device search)
+  int32_t wpiece[4];
+  int32_t wdrift[4];
 };
 
 // ------------------------------------------------------------------------

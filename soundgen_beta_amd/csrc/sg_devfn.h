@@ -19,7 +19,7 @@ __device__ __forceinline__ double contour_at(const SgContour& c, const double* _
   else if (c.kind == 2) {
     if (k == 0 || c.a == c.b) v = c.a;
     else if (k == L - 1) v = c.b;
-    else v = c.a + (double)k * ((c.b - c.a) / (double)(L - 1));
+    else v = c.a + (double)k * (L == c.L ? c.by : (c.b - c.a) / (double)(L - 1));
   } else {
     const double* x = ck + c.k_off;
     const double* y = x + c.nk;
@@ -30,7 +30,7 @@ __device__ __forceinline__ double contour_at(const SgContour& c, const double* _
     if (k == 0) u = c.a;
     else if (k == L - 1) u = c.b;
     else {
-      const double by = (c.b - c.a) / (double)(L - 1);
+      const double by = L == c.L ? c.by : (c.b - c.a) / (double)(L - 1);
       u = (k < L / 2) ? c.a + (double)k * by : c.b - (double)(L - 1 - k) * by;
     }
     int i = 0, j = c.nk;
@@ -40,7 +40,7 @@ __device__ __forceinline__ double contour_at(const SgContour& c, const double* _
     v = v < c.lo ? c.lo : v;
     v = v > c.hi ? c.hi : v;
   }
-  return c.db ? exp2(v * 0.1) : v;
+  return c.db ? (double)exp2f((float)(v * 0.1)) : v;  // 2^(dB/10); fp32 exp2 (rel. err ~1e-7)
 }
 
 __device__ __forceinline__ double linear_at(const SgLinear& l, const double* __restrict__ ck, int64_t L, int64_t k) {
@@ -55,6 +55,33 @@ __device__ __forceinline__ double linear_at(const SgLinear& l, const double* __r
   }
   int i = 0, j = l.nk - 1;
   while (i < j - 1) { int ij = (i + j) >> 1; if (u < x[ij]) j = ij; else i = ij; }
+  if (u == x[j]) return y[j];
+  if (u == x[i]) return y[i];
+  return y[i] + (y[j] - y[i]) * ((u - x[i]) / (x[j] - x[i]));
+}
+
+// linear_at for monotonically increasing k with a caller-held interval
+// cursor i (start at -1): same interval as the bisection above (largest i in
+// [0, nk - 2] with x[i] <= u), found by bisection once, then by stepping.
+__device__ __forceinline__ double linear_at_cursor(const SgLinear& l, const double* __restrict__ ck, int64_t L,
+                                                   int64_t k, int& i) {
+  const double* x = ck + l.k_off;
+  const double* y = x + l.nk;
+  double u;
+  if (k == 0) u = l.x0;
+  else if (k == L - 1) u = l.x1;
+  else {
+    const double by = (l.x1 - l.x0) / (double)(L - 1);
+    u = (k < L / 2) ? l.x0 + (double)k * by : l.x1 - (double)(L - 1 - k) * by;
+  }
+  if (i < 0) {
+    int a = 0, b = l.nk - 1;
+    while (a < b - 1) { int ab = (a + b) >> 1; if (u < x[ab]) b = ab; else a = ab; }
+    i = a;
+  } else {
+    while (i + 1 <= l.nk - 2 && x[i + 1] <= u) ++i;
+  }
+  const int j = i + 1;
   if (u == x[j]) return y[j];
   if (u == x[i]) return y[i];
   return y[i] + (y[j] - y[i]) * ((u - x[i]) / (x[j] - x[i]));

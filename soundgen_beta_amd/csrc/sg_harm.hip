@@ -230,8 +230,9 @@ extern "C" __global__ __launch_bounds__(256) void sg_piece_max(
 }
 
 // out[k] = assembled[k] * env[k] / max * fade[k] * drift[k]   (R/source.R:436-467)
-// Each thread owns 4 consecutive samples; a tile lying inside one direct
-// piece with a 16-B aligned source and destination moves float4s.
+// A tile lying inside one direct piece with a 16-B aligned source and
+// destination moves float4s (4 consecutive samples per thread); otherwise
+// each thread takes samples k0 + 256 e + tid.
 __device__ __forceinline__ float fade_at(int lf, int64_t L, int64_t k) {
   float f = 1.f;
   const float by = 1.f / (float)(lf - 1);
@@ -277,18 +278,74 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize(
     }
     return;
   }
-  int p = tl.piece;
+  // general path: wave w owns samples [k0 + 256 w, +256), lane l takes
+  // c0 + 64 e + l (coalesced). The planner gives each wave the piece and the
+  // drift-knot interval of its first sample; up to 8 knots from there are
+  // held as wave-uniform values and each lane picks its interval by compares
+  // (no dependent loads); chunks spanning more knots or pieces step per lane.
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int64_t c0 = tl.k0 + 256 * wv;
+  if (c0 >= tile_end) return;
+  const int64_t c1 = c0 + 256 < tile_end ? c0 + 256 : tile_end;
+  const int pu = stiles[blockIdx.x].wpiece[wv];
+  const bool one_piece = pu + 1 >= pend || pieces[pu + 1].start >= c1;
+  const SgLinear dr = sy.drift;
+  const bool drift = dr.nk > 1;
+  const int d0 = stiles[blockIdx.x].wdrift[wv];
+  constexpr int KW = 8;
+  double xs[KW], ys[KW];
+  bool local_knots = false;
+  const double dby = drift ? (dr.x1 - dr.x0) / (double)(sy.L - 1) : 0.0;
+  auto u_at = [&](int64_t k) -> double {
+    if (k == 0) return dr.x0;
+    if (k == sy.L - 1) return dr.x1;
+    return (k < sy.L / 2) ? dr.x0 + (double)k * dby : dr.x1 - (double)(sy.L - 1 - k) * dby;
+  };
+  if (drift) {
+    const double* x = cknots + dr.k_off;
+#pragma unroll
+    for (int t = 0; t < KW; ++t) {
+      const int idx = d0 + t < dr.nk ? d0 + t : dr.nk - 1;
+      xs[t] = x[idx];
+      ys[t] = x[dr.nk + idx];
+    }
+    // every sample of the chunk lies in intervals d0 .. d0 + KW - 2
+    local_knots = d0 + KW - 1 >= dr.nk - 1 || u_at(c1 - 1) < xs[KW - 1];
+  }
+  int p = pu, di = d0;
+#pragma unroll
   for (int e = 0; e < 4; ++e) {
-    const int64_t k = kt + e;
-    if (k >= tile_end) break;
-    while (p + 1 < pend && pieces[p + 1].start <= k) ++p;
-    const SgPiece& pc = pieces[p];
-    float v = pc.nterms == 0 ? 0.f : piece_value(pc, W, k - pc.start);
-    if (sy.env.kind != 0) v = (float)((double)v * contour_at(sy.env, cknots, sy.L, k));
-    v *= inv_max;
-    if (sy.fade >= 2) v *= fade_at(sy.fade, sy.L, k);
-    if (sy.drift.nk > 0) v = (float)((double)v * linear_at(sy.drift, cknots, sy.L, k));
-    out[sy.out_off + k] = v;
+    const int64_t k = c0 + 64 * e + lane;
+    if (k >= c1) break;
+    float x;
+    if (one_piece) {
+      const SgPiece& pc = pieces[pu];
+      x = pc.nterms == 0 ? 0.f : piece_value(pc, W, k - pc.start);
+    } else {
+      while (p + 1 < pend && pieces[p + 1].start <= k) ++p;
+      const SgPiece& pc = pieces[p];
+      x = pc.nterms == 0 ? 0.f : piece_value(pc, W, k - pc.start);
+    }
+    if (sy.env.kind != 0) x = (float)((double)x * contour_at(sy.env, cknots, sy.L, k));
+    x *= inv_max;
+    if (sy.fade >= 2) x *= fade_at(sy.fade, sy.L, k);
+    if (drift) {
+      double dm;
+      if (local_knots) {  // linear_at's interval and arithmetic, knots from registers
+        const double u = u_at(k);
+        double xi = xs[0], xj = xs[1], yi = ys[0], yj = ys[1];
+#pragma unroll
+        for (int t = 1; t < KW - 1; ++t)
+          if (d0 + t <= dr.nk - 2 && xs[t] <= u) { xi = xs[t]; xj = xs[t + 1]; yi = ys[t]; yj = ys[t + 1]; }
+        dm = u == xj ? yj : (u == xi ? yi : yi + (yj - yi) * ((u - xi) / (xj - xi)));
+      } else {
+        dm = sgd::linear_at_cursor(dr, cknots, sy.L, k, di);
+      }
+      x = (float)((double)x * dm);
+    } else if (dr.nk == 1) {
+      x = (float)((double)x * cknots[dr.k_off + 1]);
+    }
+    out[sy.out_off + k] = x;
   }
 }
 

@@ -54,13 +54,18 @@ SgContour contour_desc(Batch& B, const sg_anchors& an, int64_t L, bool has_floor
                        bool has_ceil, double vceil, bool db) {
   SgContour c{};
   c.lo = -INFINITY; c.hi = INFINITY; c.db = db ? 1 : 0;
+  c.L = L;
   if (an.n <= 0 || L <= 0) { c.kind = 0; return c; }
   const int64_t n = an.n;
   vec t(an.time, an.time + n), v(an.value, an.value + n);
   if (has_floor) for (auto& x : v) if (x < vfloor) x = vfloor;
   if (has_ceil) for (auto& x : v) if (x > vceil) x = vceil;
   if (n == 1) { c.kind = 1; c.a = v[0]; return c; }
-  if (n == 2) { c.kind = 2; c.a = v[0]; c.b = v[1]; return c; }
+  if (n == 2) {
+    c.kind = 2; c.a = v[0]; c.b = v[1];
+    c.by = L > 1 ? (c.b - c.a) / (double)(L - 1) : 0.0;
+    return c;
+  }
   if (n <= 10) throw SgError(SG_E_UNSUPPORTED, "getSmoothContour: loess (3-10 anchors) not supported yet");
   const double tmin = r_min(t);
   for (auto& x : t) x -= tmin;
@@ -69,6 +74,7 @@ SgContour contour_desc(Batch& B, const sg_anchors& an, int64_t L, bool has_floor
   Spline s = fmm_spline(t, v);
   c.kind = 3; c.nk = (int32_t)n; c.k_off = (int64_t)B.cknots.size();
   c.a = t.front(); c.b = t.back();
+  c.by = L > 1 ? (c.b - c.a) / (double)(L - 1) : 0.0;
   if (has_floor) c.lo = vfloor;
   if (has_ceil) c.hi = vceil;
   for (const vec* a : {&s.x, &s.y, &s.b, &s.c, &s.d}) B.cknots.insert(B.cknots.end(), a->begin(), a->end());
@@ -825,6 +831,24 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
   return Lsyl;
 }
 
+// drift-knot interval of sample k: largest i in [0, nk - 2] with x[i] <= u(k),
+// u(k) exactly as sg_devfn.h linear_at computes it
+static int32_t drift_interval(const Batch& B, const SgSyllable& sy, int64_t k) {
+  const SgLinear& l = sy.drift;
+  const double* x = &B.cknots[l.k_off];
+  const int64_t L = sy.L;
+  double u;
+  if (k == 0) u = l.x0;
+  else if (k == L - 1) u = l.x1;
+  else {
+    const double by = (l.x1 - l.x0) / (double)(L - 1);
+    u = (k < L / 2) ? l.x0 + (double)k * by : l.x1 - (double)(L - 1 - k) * by;
+  }
+  int a = 0, b = l.nk - 1;
+  while (a < b - 1) { const int ab = (a + b) >> 1; if (u < x[ab]) b = ab; else a = ab; }
+  return a;
+}
+
 void tile_syllables(Batch& B, int first_syl) {
   constexpr int64_t STILE = 1024;
   for (int s = first_syl; s < (int)B.syls.size(); ++s) {
@@ -832,7 +856,18 @@ void tile_syllables(Batch& B, int first_syl) {
     int32_t p = sy.piece0;
     for (int64_t k0 = 0; k0 < sy.L; k0 += STILE) {
       while (p + 1 < sy.piece0 + sy.npiece && B.pieces[p + 1].start <= k0) ++p;
-      B.syl_tiles.push_back(SgSylTile{s, p, k0});
+      SgSylTile t{};
+      t.syl = s;
+      t.piece = p;
+      t.k0 = k0;
+      int32_t pw = p;
+      for (int w = 0; w < 4; ++w) {
+        const int64_t c0 = std::min<int64_t>(k0 + 256 * w, sy.L - 1);
+        while (pw + 1 < sy.piece0 + sy.npiece && B.pieces[pw + 1].start <= c0) ++pw;
+        t.wpiece[w] = pw;
+        t.wdrift[w] = sy.drift.nk > 1 ? drift_interval(B, sy, c0) : 0;
+      }
+      B.syl_tiles.push_back(t);
     }
   }
 }
