@@ -59,6 +59,9 @@ def lib():
         L.or_cross_fade.restype = i64
         L.or_vocal_fry_epochs.argtypes = [dp, i64, dp, i64, C.c_double, C.c_double, C.c_double, C.c_double,
                                           i64p, i64p, i64p, i64, dp, dp]
+        L.or_smooth_contour.argtypes = [dp, dp, i64, i64, C.c_int, C.c_int, C.c_int, C.c_double, C.c_int,
+                                        C.c_double, C.c_double, dp]
+        L.or_loess.argtypes = [dp, dp, C.c_int, C.c_double, dp, i64, dp]
         _lib = L
     return _lib
 
@@ -259,3 +262,25 @@ def vocal_fry(rolloff, pitch_per_gc, subFreq=100, subDep=100, throwaway=-120, sh
         mo += k
         ao += k * g
     return list(zip(st[:ne].tolist(), en[:ne].tolist())), res
+
+
+def smooth_contour(anchors, len, thisIsPitch=False, method="loess", valueFloor=None, valueCeiling=None,
+                   samplingRate=16000):
+    """getSmoothContour(anchors, len, ...) (R/smoothContours.R:53-227)."""
+    t = _f64(anchors["time"])
+    v = _f64(anchors["value"])
+    n_out = int(len)
+    out = np.zeros(n_out)
+    _check(lib().or_smooth_contour(_abi.dptr(t), _abi.dptr(v), t.size, n_out, int(bool(thisIsPitch)),
+                                   0 if method == "loess" else 1, int(valueFloor is not None),
+                                   float(valueFloor or 0.0), int(valueCeiling is not None),
+                                   float(valueCeiling or 0.0), float(samplingRate), _abi.dptr(out)))
+    return out
+
+
+def loess(x, y, span, z):
+    """loess(y ~ x, span = span) then predict at z (R 3.4 stats defaults, 1-D)."""
+    x, y, z = _f64(x), _f64(y), _f64(z)
+    out = np.zeros(len(z))
+    _check(lib().or_loess(_abi.dptr(x), _abi.dptr(y), len(x), float(span), _abi.dptr(z), len(z), _abi.dptr(out)))
+    return out

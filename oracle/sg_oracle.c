@@ -21,6 +21,7 @@
  * rgamma() uses Marsaglia-Tsang on the injected streams (NOT R's
  * Ahrens-Dieter; documented in DESIGN.md) — only reached at temperature > 0.
  */
+#include <float.h>
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -246,6 +247,199 @@ static int r_approx_n(const double* x, const double* y, int64_t nx, int64_t n, d
   return 0;
 }
 
+/* ------------------------------------------------------------ loess (1-D)
+ * loess(y ~ x, span = f) then predict(., newx) with R 3.4 stats defaults:
+ * degree 2, family "gaussian" (no robustness iterations), surface
+ * "interpolate", statistics "approximate", cell 0.2. Restated from the
+ * published netlib dloess algorithm that R's stats/src/loessf.f carries
+ * (lowesd, lowesb -> ehg131: ehg126 bounding box, ehg124 k-d tree, ehg139/ehg127
+ * vertex fits; lowese -> ehg133/ehg128 cubic Hermite interpolation) and
+ * loessc.c (nf, span * cell). PARITY UNPINNED: R is absent here; this follows
+ * the algorithm as published, not R output. x ascending, distinct. */
+typedef struct {
+  int n;              /* data points */
+  double vx[64];      /* vertices (creation order) */
+  double val[64], slope[64];
+  int nv;
+  /* cells (BFS order): point range [l, u] (1-based), vertex ids, split */
+  int cl[128], cu[128], cv0[128], cv1[128], split[128], lo_son[128], hi_son[128];
+  double xi[128];
+  int nc;
+} lo_tree;
+
+/* one-sided Jacobi SVD of B (m x 3, column-major in b[3][m]) -> sigma, V */
+static void svd3(double b[3][16], int m, double sigma[3], double V[3][3]) {
+  for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) V[i][j] = i == j;
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    double off = 0;
+    for (int p = 0; p < 2; ++p)
+      for (int q = p + 1; q < 3; ++q) {
+        double al = 0, be = 0, ga = 0;
+        for (int i = 0; i < m; ++i) { al += b[p][i] * b[p][i]; be += b[q][i] * b[q][i]; ga += b[p][i] * b[q][i]; }
+        if (ga == 0 || fabs(ga) <= 1e-300) continue;
+        off = fmax(off, fabs(ga) / sqrt(al * be));
+        const double zeta = (be - al) / (2 * ga);
+        const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1 + zeta * zeta));
+        const double c = 1 / sqrt(1 + t * t), sn = c * t;
+        for (int i = 0; i < m; ++i) {
+          const double bp = b[p][i], bq = b[q][i];
+          b[p][i] = c * bp - sn * bq;
+          b[q][i] = sn * bp + c * bq;
+        }
+        for (int i = 0; i < 3; ++i) {
+          const double vp = V[i][p], vq = V[i][q];
+          V[i][p] = c * vp - sn * vq;
+          V[i][q] = sn * vp + c * vq;
+        }
+      }
+    if (off < 1e-15) break;
+  }
+  for (int j = 0; j < 3; ++j) {
+    double s2 = 0;
+    for (int i = 0; i < m; ++i) s2 += b[j][i] * b[j][i];
+    sigma[j] = sqrt(s2);
+  }
+}
+
+/* local quadratic fit at vertex v (ehg127): value and slope */
+static int lo_vertex_fit(const double* x, const double* y, int n, int nf, double f, double v, double* val,
+                         double* slope) {
+  double d2[64]; int ord[64];
+  for (int i = 0; i < n; ++i) { d2[i] = (x[i] - v) * (x[i] - v); ord[i] = i; }
+  for (int i = 1; i < n; ++i)  /* stable insertion sort by distance */
+    for (int j = i; j > 0 && d2[ord[j]] < d2[ord[j - 1]]; --j) { int t = ord[j]; ord[j] = ord[j - 1]; ord[j - 1] = t; }
+  const double rho = d2[ord[nf - 1]] * (f > 1 ? f : 1.0);
+  if (!(rho > 0)) return fail(SG_E_UNSUPPORTED, "loess: neighbourhood radius 0 (span too small; R yields NaN)");
+  double b[3][16], eta[16];
+  const int m = nf < 3 ? 3 : nf;
+  for (int i = 0; i < m; ++i) { b[0][i] = b[1][i] = b[2][i] = 0; eta[i] = 0; }
+  for (int i = 0; i < nf; ++i) {
+    const int k = ord[i];
+    double w = sqrt(d2[k] / rho);
+    w = sqrt((1 - w * w * w) * (1 - w * w * w) * (1 - w * w * w));
+    const double dx = x[k] - v;
+    b[0][i] = w; b[1][i] = w * dx; b[2][i] = w * dx * dx;
+    eta[i] = w * y[k];
+  }
+  double colnor[3];
+  for (int j = 0; j < 3; ++j) {  /* equilibrate columns */
+    double sc = 0;
+    for (int i = 0; i < m; ++i) sc += b[j][i] * b[j][i];
+    sc = sqrt(sc);
+    if (sc > 0) { for (int i = 0; i < m; ++i) b[j][i] /= sc; colnor[j] = sc; } else colnor[j] = 1;
+  }
+  double bw[3][16];
+  memcpy(bw, b, sizeof b);
+  double sigma[3], V[3][3];
+  svd3(bw, m, sigma, V);
+  double smax = fmax(sigma[0], fmax(sigma[1], sigma[2]));
+  const double tol = smax * (100 * DBL_EPSILON);
+  double gam[3];
+  for (int j = 0; j < 3; ++j) {  /* gamma_j = u_j . eta / sigma_j, u_j = (B V)_j / sigma_j */
+    if (sigma[j] > tol) {
+      double ue = 0;
+      for (int i = 0; i < m; ++i) ue += bw[j][i] / sigma[j] * eta[i];
+      gam[j] = ue / sigma[j];
+    } else gam[j] = 0;
+  }
+  double s0 = 0, s1 = 0;
+  for (int j = 0; j < 3; ++j) { s0 += V[0][j] * gam[j]; s1 += V[1][j] * gam[j]; }
+  *val = s0 / colnor[0];
+  *slope = s1 / colnor[1];
+  return 0;
+}
+
+static int lo_build(const double* x, const double* y, int n, double f, lo_tree* T) {
+  if (n < 1 || n > 48) return fail(SG_E_UNSUPPORTED, "loess: 1..48 points");
+  if (floor(n * f + 1e-5) <= 0) return fail(SG_E_DOMAIN, "loess: span is too small");
+  const int nf = (int)fmin((double)n, floor(n * f));
+  if (nf <= 0) return fail(SG_E_DOMAIN, "loess: span is too small");
+  const int fc = (int)floor(n * (f * 0.2));
+  double alpha = x[0], beta = x[0];
+  for (int i = 1; i < n; ++i) { alpha = fmin(alpha, x[i]); beta = fmax(beta, x[i]); }
+  const double mu = 0.005 * fmax(beta - alpha, 1e-10 * fmax(fabs(alpha), fabs(beta)) + 1e-30);
+  T->n = n; T->nv = 2; T->vx[0] = alpha - mu; T->vx[1] = beta + mu;
+  T->nc = 1; T->cl[0] = 1; T->cu[0] = n; T->cv0[0] = 0; T->cv1[0] = 1;
+  for (int p = 0; p < T->nc; ++p) {
+    const int l = T->cl[p], u = T->cu[p];
+    int leaf = (u - l + 1) <= fc || (T->vx[T->cv1[p]] - T->vx[T->cv0[p]]) <= 0;
+    int m = (l + u) / 2;
+    if (!leaf) {
+      /* ties go to the high son: step m to a position where x changes */
+      int off = 0;
+      while (!(m + off >= u || m + off < l)) {
+        if (x[m + off - 1] == x[m + off]) { off = -off; if (off >= 0) off++; }
+        else { m += off; break; }
+      }
+      leaf = T->vx[T->cv0[p]] == x[m - 1] || T->vx[T->cv1[p]] == x[m - 1];
+    }
+    T->split[p] = !leaf;
+    if (leaf) continue;
+    if (T->nc + 2 > 128 || T->nv + 1 > 64) return fail(SG_E_UNSUPPORTED, "loess: k-d tree too large");
+    T->xi[p] = x[m - 1];
+    const int vn = T->nv++;
+    T->vx[vn] = x[m - 1];
+    const int a = T->nc++, b = T->nc++;
+    T->lo_son[p] = a; T->hi_son[p] = b;
+    T->cl[a] = l; T->cu[a] = m; T->cv0[a] = T->cv0[p]; T->cv1[a] = vn;
+    T->cl[b] = m + 1; T->cu[b] = u; T->cv0[b] = vn; T->cv1[b] = T->cv1[p];
+  }
+  for (int v = 0; v < T->nv; ++v) {
+    const int rc = lo_vertex_fit(x, y, n, nf, f, T->vx[v], &T->val[v], &T->slope[v]);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+static double lo_eval(const lo_tree* T, double z) {
+  int p = 0;
+  while (T->split[p]) p = z <= T->xi[p] ? T->lo_son[p] : T->hi_son[p];
+  const int a = T->cv0[p], b = T->cv1[p];
+  const double v0 = T->vx[a], v1 = T->vx[b];
+  const double h = (z - v0) / (v1 - v0);
+  const double phi0 = (1 - h) * (1 - h) * (1 + 2 * h), phi1 = h * h * (3 - 2 * h);
+  const double psi0 = h * (1 - h) * (1 - h), psi1 = -h * h * (1 - h);
+  return phi0 * T->val[a] + phi1 * T->val[b] + (psi0 * T->slope[a] + psi1 * T->slope[b]) * (v1 - v0);
+}
+
+/* the loess branch of getSmoothContour(), R/smoothContours.R:119-154:
+ * anchors (t in [0, 1], values) -> contour over 1..len */
+static int smooth_loess(const double* t, const double* val, int64_t n, int64_t len, double duration_ms,
+                        int has_floor, double vfloor, double* out) {
+  if (n > 48) return fail(SG_E_UNSUPPORTED, "loess: too many anchors");
+  /* anchors_long[anchor_time_points] = value: positions truncate, 0 drops, last wins */
+  double xv[48], yv[48]; int nx = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    double tp = t[i] / 1.0 * (double)len;  /* (t - min) / max * len with t already in [0, 1] */
+    if (tp == 0) tp = 1;
+    const int64_t idx = (int64_t)tp;
+    if (idx < 1 || idx > len) continue;
+    int k = 0;
+    while (k < nx && xv[k] != (double)idx) ++k;
+    if (k == nx) { xv[nx] = (double)idx; yv[nx] = val[i]; ++nx; } else yv[k] = val[i];
+  }
+  for (int i = 1; i < nx; ++i)  /* data frame rows in time order */
+    for (int j = i; j > 0 && xv[j] < xv[j - 1]; --j) {
+      double a = xv[j]; xv[j] = xv[j - 1]; xv[j - 1] = a;
+      a = yv[j]; yv[j] = yv[j - 1]; yv[j - 1] = a;
+    }
+  double span = (1 / (1 + exp(duration_ms / 500)) + 0.5) / pow(1.1, (double)(n - 3));
+  for (int iter = 0; iter < 200; ++iter) {
+    lo_tree T;
+    int rc = lo_build(xv, yv, nx, span, &T);
+    if (rc) return rc;
+    int below = 0;
+    for (int64_t k = 0; k < len; ++k) {
+      const double z = (double)(k + 1);
+      out[k] = (z < xv[0] || z > xv[nx - 1]) ? NAN : lo_eval(&T, z);
+      if (has_floor && out[k] < vfloor - 1e-6) below = 1;
+    }
+    if (!below) return 0;
+    span = span / 1.1;  /* less smoothing until no value falls below the floor */
+  }
+  return fail(SG_E_DOMAIN, "loess: contour stays below valueFloor");
+}
+
 /* ------------------------------------------------------- soundgen helpers */
 static double HzToSemitones(double h) { return log2(h / 16.3516) * 12; }
 static double semitonesToHz(double s) { return 16.3516 * pow(2.0, s / 12); }
@@ -255,7 +449,6 @@ static double semitonesToHz(double s) { return 16.3516 * pow(2.0, s / 12); }
 static int get_smooth_contour(sg_anchors an, int64_t len, int thisIsPitch,
                               int method, int has_floor, double vfloor,
                               int has_ceil, double vceil, double sr, dv* out) {
-  (void)sr;
   out->v = NULL; out->n = 0;
   if (an.n <= 0) return 0;                      /* NA anchors */
   int64_t n = an.n;
@@ -279,8 +472,13 @@ static int get_smooth_contour(sg_anchors an, int64_t len, int thisIsPitch,
   } else if (n == 2) {
     *out = r_seq_len(val.v[0], val.v[1], len);
   } else {
-    if (method != 1) { rc = fail(SG_E_UNSUPPORTED, "getSmoothContour: loess (3-10 anchors) not supported yet"); goto done; }
-    *out = r_spline(t.v, val.v, n, len);
+    if (method != 1) {
+      *out = dv_new(len);
+      rc = smooth_loess(t.v, val.v, n, len, (double)len / sr * 1000, has_floor, vfloor, out->v);
+      if (rc) { dv_free(out); out->n = 0; goto done; }
+    } else {
+      *out = r_spline(t.v, val.v, n, len);
+    }
     for (int64_t i = 0; i < len; ++i) {
       if (has_floor && out->v[i] < vfloor) out->v[i] = vfloor;
       if (has_ceil && out->v[i] > vceil) out->v[i] = vceil;
@@ -1248,6 +1446,29 @@ OR_API int or_get_rolloff(const double* pitch, int32_t nGC, int32_t nH, double r
 }
 
 /* helpers exported for unit tests */
+/* getSmoothContour() with len given (R/smoothContours.R:53-227); out has len values */
+OR_API int or_smooth_contour(const double* time, const double* value, int64_t n, int64_t len, int thisIsPitch,
+                             int method, int has_floor, double vfloor, int has_ceil, double vceil, double sr,
+                             double* out) {
+  sg_anchors an;
+  an.n = (int32_t)n;
+  an.time = time;
+  an.value = value;
+  dv c;
+  const int rc = get_smooth_contour(an, len, thisIsPitch, method, has_floor, vfloor, has_ceil, vceil, sr, &c);
+  if (rc) return rc;
+  for (int64_t i = 0; i < len; ++i) out[i] = i < c.n ? c.v[i] : NAN;
+  dv_free(&c);
+  return 0;
+}
+/* loess(y ~ x, span) + predict at z[m] (R stats defaults, 1-D) */
+OR_API int or_loess(const double* x, const double* y, int n, double span, const double* z, int64_t m, double* out) {
+  lo_tree T;
+  const int rc = lo_build(x, y, n, span, &T);
+  if (rc) return rc;
+  for (int64_t i = 0; i < m; ++i) out[i] = (z[i] < x[0] || z[i] > x[n - 1]) ? NAN : lo_eval(&T, z[i]);
+  return 0;
+}
 OR_API int64_t or_glottal_cycles(const double* pitch, int64_t len, double psr, double* out) {
   dv g = get_glottal_cycles(pitch, len, psr); memcpy(out, g.v, g.n * sizeof(double)); int64_t n = g.n; dv_free(&g); return n;
 }

@@ -83,13 +83,15 @@ int64_t plan_harmonics(Batch& B, const double* pitch, int64_t len, const sg_harm
                        int64_t* fs_off = nullptr);
 
 // getSmoothContour() for the lengths/values the planner needs on the host.
-// method: 0 loess (default; only 1, 2 or >10 anchors supported), 1 spline.
-// Returns false for R's NA.
+// method: 0 loess (default; 3-10 anchors -> sg_loess), 1 spline. sr is the
+// call site's samplingRate (loess span depends on len / sr). Returns false
+// for R's NA.
 bool smooth_contour(const sg_anchors& an, int64_t len, bool thisIsPitch, int method, bool has_floor,
-                    double vfloor, bool has_ceil, double vceil, vec& out);
-// Device contour descriptor for getSmoothContour(len = L) (no host expansion)
+                    double vfloor, bool has_ceil, double vceil, vec& out, double sr = 16000);
+// Device contour descriptor for getSmoothContour(len = L) (no host expansion;
+// a loess contour becomes piecewise cubic knots at the k-d tree vertices)
 SgContour contour_desc(Batch& B, const sg_anchors& an, int64_t L, bool has_floor, double vfloor,
-                       bool has_ceil, double vceil, bool db);
+                       bool has_ceil, double vceil, bool db, double sr);
 
 void tile_syllables(Batch& B, int first_syl);
 

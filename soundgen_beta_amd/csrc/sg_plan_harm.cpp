@@ -11,13 +11,14 @@
 #include <cmath>
 #include <cstring>
 
+#include "sg_loess.h"
 #include "sg_plan.h"
 
 namespace sg {
 
 // ------------------------------------------------------------- contours
 bool smooth_contour(const sg_anchors& an, int64_t len, bool thisIsPitch, int method, bool has_floor,
-                    double vfloor, bool has_ceil, double vceil, vec& out) {
+                    double vfloor, bool has_ceil, double vceil, vec& out, double sr) {
   out.clear();
   if (an.n <= 0) return false;
   const int64_t n = an.n;
@@ -38,8 +39,16 @@ bool smooth_contour(const sg_anchors& an, int64_t len, bool thisIsPitch, int met
   if (n == 1) out.assign(len, v[0]);
   else if (n == 2) out = r_seq_len(v[0], v[1], len);
   else {
-    if (method != 1) throw SgError(SG_E_UNSUPPORTED, "getSmoothContour: loess (3-10 anchors) not supported yet");
-    out = r_spline(t, v, len);
+    if (method != 1) {  // loess, R/smoothContours.R:119-154 (duration_ms = len / sr * 1000)
+      const LoessFit T = smooth_loess(t.data(), v.data(), n, len, (double)len / sr * 1000, has_floor, vfloor);
+      out.resize(len);
+      for (int64_t k = 0; k < len; ++k) {
+        const double z = (double)(k + 1);
+        out[k] = (z < T.xmin || z > T.xmax) ? NAN : T.eval(z);
+      }
+    } else {
+      out = r_spline(t, v, len);
+    }
     for (auto& x : out) {
       if (has_floor && x < vfloor) x = vfloor;
       if (has_ceil && x > vceil) x = vceil;
@@ -51,7 +60,7 @@ bool smooth_contour(const sg_anchors& an, int64_t len, bool thisIsPitch, int met
 }
 
 SgContour contour_desc(Batch& B, const sg_anchors& an, int64_t L, bool has_floor, double vfloor,
-                       bool has_ceil, double vceil, bool db) {
+                       bool has_ceil, double vceil, bool db, double sr) {
   SgContour c{};
   c.lo = -INFINITY; c.hi = INFINITY; c.db = db ? 1 : 0;
   c.L = L;
@@ -66,11 +75,37 @@ SgContour contour_desc(Batch& B, const sg_anchors& an, int64_t L, bool has_floor
     c.by = L > 1 ? (c.b - c.a) / (double)(L - 1) : 0.0;
     return c;
   }
-  if (n <= 10) throw SgError(SG_E_UNSUPPORTED, "getSmoothContour: loess (3-10 anchors) not supported yet");
   const double tmin = r_min(t);
   for (auto& x : t) x -= tmin;
   const double tmax = r_max(t);
   for (auto& x : t) x /= tmax;
+  if (n <= 10) {
+    // loess: evaluated at u = 1..L; the Hermite pieces between consecutive
+    // k-d tree vertices become power-basis cubics in dx = u - vertex
+    const LoessFit T = smooth_loess(t.data(), v.data(), n, L, (double)L / sr * 1000, has_floor, vfloor);
+    std::vector<int> ord(T.vx.size());
+    for (size_t i = 0; i < ord.size(); ++i) ord[i] = (int)i;
+    std::sort(ord.begin(), ord.end(), [&](int a, int b) { return T.vx[a] < T.vx[b]; });
+    const size_t nk = ord.size();
+    vec kx(nk), ky(nk), kb(nk), kc(nk, 0.0), kd(nk, 0.0);
+    for (size_t i = 0; i < nk; ++i) {
+      kx[i] = T.vx[ord[i]];
+      ky[i] = T.val[ord[i]];
+      kb[i] = T.slope[ord[i]];
+    }
+    for (size_t i = 0; i + 1 < nk; ++i) {
+      const double h = kx[i + 1] - kx[i], dy = ky[i + 1] - ky[i];
+      kc[i] = (3 * dy / h - 2 * kb[i] - kb[i + 1]) / h;
+      kd[i] = (-2 * dy / h + kb[i] + kb[i + 1]) / (h * h);
+    }
+    c.kind = 3; c.nk = (int32_t)nk; c.k_off = (int64_t)B.cknots.size();
+    c.a = 1; c.b = (double)L;
+    c.by = L > 1 ? (c.b - c.a) / (double)(L - 1) : 0.0;
+    if (has_floor) c.lo = vfloor;
+    if (has_ceil) c.hi = vceil;
+    for (const vec* a : {&kx, &ky, &kb, &kc, &kd}) B.cknots.insert(B.cknots.end(), a->begin(), a->end());
+    return c;
+  }
   Spline s = fmm_spline(t, v);
   c.kind = 3; c.nk = (int32_t)n; c.k_off = (int64_t)B.cknots.size();
   c.a = t.front(); c.b = t.back();
@@ -529,7 +564,7 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
   vec rolloffAmpl(nGC, 0.0);
   if (useAmpl) {
     vec ac;
-    smooth_contour(amplAnchors, nGC, false, 0, true, 0, true, -P.throwaway, ac);
+    smooth_contour(amplAnchors, nGC, false, 0, true, 0, true, -P.throwaway, ac, sr);
     for (int64_t g = 0; g < nGC; ++g) rolloffAmpl[g] = (ac[g] / std::fabs(P.throwaway) - 1) * P.rolloff_perAmpl;
   }
   vec rw(nGC, 1.0), vf_on(nGC, 1.0), jit_on(nGC, 1.0), drift;
@@ -668,7 +703,7 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
   sy.max_slot = syl_idx;
   const double lf = P.attackLen > 0 ? std::floor(P.attackLen * sr / 1000) : 0;
   sy.fade = (int32_t)(lf >= 2 ? std::min<double>(lf, (double)Lsyl) : 0);
-  sy.env = useAmpl ? contour_desc(B, amplAnchors, Lsyl, true, 0, false, 0, true) : SgContour{};
+  sy.env = useAmpl ? contour_desc(B, amplAnchors, Lsyl, true, 0, false, 0, true, sr) : SgContour{};
   if (!useAmpl) { sy.env.kind = 0; sy.env.lo = -INFINITY; sy.env.hi = INFINITY; }
   if (P.temperature > 0) {
     sy.drift.nk = (int32_t)nGC;

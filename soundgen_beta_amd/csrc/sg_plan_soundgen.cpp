@@ -382,7 +382,7 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
       vec pc;
       if (pA.n() > 0) {
         smooth_contour(pA.view(), (int64_t)r_round(dur * A.pitchSamplingRate / 1000), true, 0, true, A.pitchFloor,
-                       true, A.pitchCeiling, pc);
+                       true, A.pitchCeiling, pc, A.pitchSamplingRate);
         for (auto& v : pc) v *= pitchDeltas[s];
       }
       double minNoise = INFINITY;
@@ -452,7 +452,7 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
       if (amplG.n() > 0 && below) {
         Anc g2 = amplG;
         for (auto& v : g2.v) v = std::pow(2.0, v / 10);
-        pre.mult = contour_desc(B, g2.view(), Ls, true, 0, true, -A.throwaway, false);
+        pre.mult = contour_desc(B, g2.view(), Ls, true, 0, true, -A.throwaway, false, sr);
       }
     }
     B.mixes[0].push_back(pre);

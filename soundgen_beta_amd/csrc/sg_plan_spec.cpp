@@ -197,7 +197,7 @@ bool plan_noise(Batch& B, Rng& R, int64_t len, const sg_anchors& noiseAnchors, d
   // breathingStrength = getSmoothContour(noiseAnchors, len, valueFloor = -120, valueCeiling = 40)
   //   R/source.R:70-81 (NA when len == 0 or anchors NA)
   if (noiseAnchors.n <= 0 || len <= 0) return false;
-  SgContour strength = contour_desc(B, noiseAnchors, len, true, -120, true, 40, true);
+  SgContour strength = contour_desc(B, noiseAnchors, len, true, -120, true, 40, true, sr);
   // step = seq(1, len + wl, by = hop); nr = wl / 2; nc = length(step)   R/source.R:88-94
   const int gi = geometry(B, wl);
   const double hop = (double)wl - overlap * (double)wl / 100;

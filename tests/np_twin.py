@@ -289,3 +289,105 @@ def istft(z, ovlp, wl):
         end = min(len(x), i0 + wl)
         x[i0:end] += seg[: end - i0]
     return x * h / np.sum(win ** 2)
+
+
+# ---------------------------------------------------------------- loess
+# loess(y ~ x, span) + predict (R 3.4 stats defaults, 1-D; netlib dloess
+# algorithm as R's loessf.f carries it): widened bounding box, median k-d tree
+# down to floor(n span 0.2) points per cell, vertex fits (floor(n span) nearest,
+# tricube, equilibrated columns, SVD pseudo-inverse), cubic Hermite between
+# consecutive vertices. Written independently of oracle/sg_oracle.c.
+def _loess_vertices(x, span):
+    n = len(x)
+    fc = int(np.floor(n * (span * 0.2)))
+    lo, hi = x.min(), x.max()
+    mu = 0.005 * max(hi - lo, 1e-10 * max(abs(lo), abs(hi)) + 1e-30)
+    verts = [lo - mu, hi + mu]
+    queue = [(0, n - 1, lo - mu, hi + mu)]  # 0-based point ranges, breadth first
+    while queue:
+        l, u, v0, v1 = queue.pop(0)
+        if u - l + 1 <= fc or v1 - v0 <= 0:
+            continue
+        m = (l + u + 2) // 2 - 1  # R: floor((l + u) / 2) on 1-based positions
+        if x[m] == v0 or x[m] == v1:
+            continue
+        verts.append(x[m])
+        queue.append((l, m, v0, x[m]))
+        queue.append((m + 1, u, x[m], v1))
+    return np.array(sorted(verts))
+
+
+def _loess_vertex_fit(x, y, span, v):
+    n = len(x)
+    nf = int(min(n, np.floor(n * span)))
+    d2 = (x - v) ** 2
+    order = np.argsort(d2, kind="stable")[:nf]
+    rho = d2[order[-1]] * max(1.0, span)
+    r = np.sqrt(d2[order] / rho)
+    w = np.sqrt((1 - r ** 3) ** 3)
+    dx = x[order] - v
+    B = np.stack([w, w * dx, w * dx * dx], axis=1)
+    eta = w * y[order]
+    if B.shape[0] < 3:
+        B = np.vstack([B, np.zeros((3 - B.shape[0], 3))])
+        eta = np.concatenate([eta, np.zeros(3 - len(eta))])
+    cn = np.linalg.norm(B, axis=0)
+    cn[cn == 0] = 1
+    B = B / cn
+    U, s, Vt = np.linalg.svd(B, full_matrices=False)
+    tol = s.max() * 100 * np.finfo(float).eps
+    g = np.where(s > tol, (U.T @ eta) / np.where(s > 0, s, 1), 0.0)
+    coef = Vt.T @ g / cn
+    return coef[0], coef[1]
+
+
+def loess(x, y, span, z):
+    x = np.asarray(x, float)
+    y = np.asarray(y, float)
+    vx = _loess_vertices(x, span)
+    fits = np.array([_loess_vertex_fit(x, y, span, v) for v in vx])
+    z = np.asarray(z, float)
+    i = np.clip(np.searchsorted(vx, z, side="left") - 1, 0, len(vx) - 2)
+    v0, v1 = vx[i], vx[i + 1]
+    h = (z - v0) / (v1 - v0)
+    phi0, phi1 = (1 - h) ** 2 * (1 + 2 * h), h ** 2 * (3 - 2 * h)
+    psi0, psi1 = h * (1 - h) ** 2, -h ** 2 * (1 - h)
+    out = phi0 * fits[i, 0] + phi1 * fits[i + 1, 0] + (psi0 * fits[i, 1] + psi1 * fits[i + 1, 1]) * (v1 - v0)
+    out[(z < x.min()) | (z > x.max())] = np.nan
+    return out
+
+
+def smooth_contour_loess(time, value, len_, sr, floor=None, ceiling=None, pitch=False):
+    """getSmoothContour(anchors, len, method = 'loess') for 3-10 anchors."""
+    t = np.asarray(time, float)
+    v = np.asarray(value, float)
+    if floor is not None:
+        v = np.maximum(v, floor)
+    if ceiling is not None:
+        v = np.minimum(v, ceiling)
+    if pitch:
+        v = 12 * np.log2(v / 16.3516)
+        floor = 12 * np.log2(floor / 16.3516) if floor is not None else None
+        ceiling = 12 * np.log2(ceiling / 16.3516) if ceiling is not None else None
+    t = (t - t.min()) / (t - t.min()).max()
+    pos = {}
+    for tp, val in zip(t * len_, v):
+        tp = 1.0 if tp == 0 else tp
+        if int(tp) >= 1:
+            pos[int(tp)] = val
+    xs = np.array(sorted(pos))
+    ys = np.array([pos[k] for k in xs])
+    span = (1 / (1 + np.exp(len_ / sr * 1000 / 500)) + 0.5) / 1.1 ** (len(t) - 3)
+    z = np.arange(1, len_ + 1, dtype=float)
+    while True:
+        out = loess(xs, ys, span, z)
+        if floor is None or not np.any(out < floor - 1e-6):
+            break
+        span /= 1.1
+    if floor is not None:
+        out = np.maximum(out, floor)
+    if ceiling is not None:
+        out = np.minimum(out, ceiling)
+    if pitch:
+        out = 16.3516 * 2 ** (out / 12)
+    return out

@@ -154,3 +154,35 @@ def test_fft_any_length(oracle):
         x = rng.normal(size=n) + 1j * rng.normal(size=n)
         np.testing.assert_allclose(oracle.fft(x), np.fft.fft(x), rtol=1e-9, atol=1e-9)
         np.testing.assert_allclose(oracle.fft(x, inverse=True), np.fft.ifft(x) * n, rtol=1e-9, atol=1e-9)
+
+
+def test_loess_vs_twin(oracle):
+    """loess restatement (C oracle) vs the independent NumPy twin on random
+    3-10 point data and spans; parity vs R itself is unpinned."""
+    rng = np.random.default_rng(11)
+    checked = 0
+    for _ in range(150):
+        n = int(rng.integers(3, 11))
+        x = np.sort(rng.choice(np.arange(1, 800), n, replace=False)).astype(float)
+        y = rng.normal(size=n) * 10
+        span = float(rng.uniform(0.45, 1.6))
+        z = np.linspace(x[0], x[-1], 61)
+        try:
+            a = oracle.loess(x, y, span, z)
+        except Exception:  # degenerate neighbourhood (nf = 1 at a data point)
+            continue
+        np.testing.assert_allclose(a, T.loess(x, y, span, z), rtol=0, atol=1e-9 * max(1, np.abs(y).max()))
+        checked += 1
+    assert checked > 100
+
+
+@pytest.mark.parametrize("anchors,L,sr,kw", [
+    ({"time": [0, .1, .9, 1], "value": [100, 150, 135, 100]}, 1050, 3500, dict(pitch=True, floor=50, ceiling=3500)),
+    ({"time": [0, .3, .6, 1], "value": [0, 40, 10, 20]}, 5000, 16000, dict(floor=0)),
+    ({"time": [0, 200, 500, 900, 1000], "value": [-30, -10, -40, -20, -25]}, 16000, 16000, dict(floor=-120, ceiling=40)),
+])
+def test_smooth_contour_loess_vs_twin(oracle, anchors, L, sr, kw):
+    a = oracle.smooth_contour(anchors, L, thisIsPitch=kw.get("pitch", False), valueFloor=kw.get("floor"),
+                              valueCeiling=kw.get("ceiling"), samplingRate=sr)
+    b = T.smooth_contour_loess(anchors["time"], anchors["value"], L, sr, **kw)
+    np.testing.assert_allclose(a, b, rtol=1e-11, atol=1e-9)

@@ -55,6 +55,12 @@ SOUNDGEN_CASES = {
                        nonlinBalance=60, subDep=80, jitterDep=1, shimmerDep=5),
     "noise_only": dict(sylLen=300, samplingRate=16000, temperature=0, pitchAnchors=None,
                        noiseAnchors={"time": [0, 300], "value": [-20, -20]}),
+    # loess contours (3-10 anchors): the default 4-anchor pitch, amplitude and noise anchors
+    "default_pitch_loess": dict(sylLen=300, samplingRate=16000, temperature=0, addSilence=0),
+    "loess_ampl_noise": dict(sylLen=600, samplingRate=16000, temperature=0, addSilence=0,
+                             pitchAnchors={"time": [0, .2, .7, 1], "value": [140, 210, 180, 120]},
+                             amplAnchors={"time": [0, .4, 1], "value": [110, 90, 120]},
+                             noiseAnchors={"time": [0, 200, 400, 600], "value": [-40, -20, -25, -30]}),
 }
 
 
