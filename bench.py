@@ -85,10 +85,40 @@ def c4_calls(n_calls, rank=0):
     return calls
 
 
+def c5_calls(n_calls, rank=0):
+    """C5: calls drawn uniformly from the 33 presets (R/presets.R:158-399,
+    extracted to soundgen_beta_amd/presets.json); sylLen x U(0.5, 2) clamped to [20, 5000],
+    pitch anchor values x 2^U(-0.5, 0.5), samplingRate 44100, addSilence 0, the
+    preset's own temperature. Random draws come from one shared pre-drawn stream
+    (every call reads it from the start; synthetic data)."""
+    import copy
+    from soundgen_beta_amd import presets as P
+    rng = _rng(rank, 5)
+    names = P.names()
+    Z = rng.standard_normal(200000)
+    U = rng.uniform(size=4000000)
+    calls = []
+    for i in range(n_calls):
+        spk, nm = names[int(rng.integers(len(names)))]
+        a = copy.deepcopy(P.args(spk, nm))
+        a["sylLen"] = float(np.clip(a.get("sylLen", 300) * rng.uniform(0.5, 2), 20, 5000))
+        pa = a.get("pitchAnchors", "default")
+        f = 2 ** rng.uniform(-0.5, 0.5)
+        if pa == "default":
+            a["pitchAnchors"] = {"time": [0, .1, .9, 1], "value": [100 * f, 150 * f, 135 * f, 100 * f]}
+        elif pa is not None:
+            a["pitchAnchors"] = {"time": pa["time"], "value": list(np.asarray(pa["value"], float) * f)}
+        a["samplingRate"] = 44100
+        a["addSilence"] = 0
+        calls.append({"kind": "soundgen", "args": a, "normals": Z, "uniforms": U, "preset": spk + "$" + nm})
+    return calls
+
+
 CONFIGS = {
     "c2": (c2_calls, 1024, "C2: %d x 1 s static-f0 tones, generateHarmonics, 44.1 kHz, harmonics only"),
     "c3": (c3_calls, 1024, "C3: %d x 2 s vowels, soundgen() with formant filter + breathing noise, 44.1 kHz"),
     "c4": (c4_calls, 512, "C4: %d x 3 s soundgen() with subharmonics, jitter, shimmer, temperature 0.05, 44.1 kHz"),
+    "c5": (c5_calls, 8192, "C5: %d calls per GPU drawn from the 33 presets (65,536 over 8 GPUs), 44.1 kHz"),
 }
 
 

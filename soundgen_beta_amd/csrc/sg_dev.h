@@ -163,6 +163,7 @@ struct SgFftGeom {
 
 constexpr int SG_FFT_WG = 0;
 constexpr int SG_FFT_WAVE = 1;
+constexpr int SG_FFT_DFT = 2;   // M with a prime factor > 31: direct O(M^2) DFT in sg_fft_frames
 constexpr int SG_WAVE_STATE = 24;  // complex butterfly points a lane holds per stage in sg_stft_ola
 constexpr int SG_FFT_WAVES = 8;    // wavefronts (segments) per sg_stft_ola workgroup: one workgroup per CU
 constexpr int SG_PF_SRC = 20;      // sg_stft_ola register prefetch: sound pairs per lane (M <= 1280)

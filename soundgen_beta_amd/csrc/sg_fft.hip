@@ -365,6 +365,26 @@ __device__ __forceinline__ void fft_w(float2* X, const SgFftGeom& g, const float
   }
 }
 
+// Direct M-point DFT of one frame (geometries whose M has a prime factor
+// > 31): out[k] = sum_n x[n] W_M^{+-nk}, the exponent reduced mod M on the fly;
+// out-of-place into S, then copied back.
+template <bool INV>
+__device__ void dft_ip(float2* X, float2* S, const float2* twM, int M) {
+  for (int k = threadIdx.x; k < M; k += SG_FFT_THREADS) {
+    float2 acc = make_float2(0.f, 0.f);
+    int e = 0;
+    for (int n = 0; n < M; ++n) {
+      acc = cadd(acc, INV ? cmulc(X[n], twM[e]) : cmul(X[n], twM[e]));
+      e += k;
+      if (e >= M) e -= M;
+    }
+    S[k] = acc;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < M; k += SG_FFT_THREADS) X[k] = S[k];
+  __syncthreads();
+}
+
 }  // namespace
 
 extern "C" __global__ __launch_bounds__(SG_FFT_THREADS) void sg_fft_frames(
@@ -395,7 +415,8 @@ extern "C" __global__ __launch_bounds__(SG_FFT_THREADS) void sg_fft_frames(
       A[idx] = make_float2(s[2 * n] * ham[2 * n], s[2 * n + 1] * ham[2 * n + 1]);
     }
     __syncthreads();
-    fft_ip<false>(A, g, twM, fb);
+    if (g.kind == SG_FFT_DFT) dft_ip<false>(A, twM + M, twM, M);
+    else fft_ip<false>(A, g, twM, fb);
     // untangle the real transform: X[k] = E + W_N^k O, E = (Z_k + conj Z_{M-k})/2,
     // O = -i (Z_k - conj Z_{M-k}) / 2; Y = X / N * env; pack for the inverse
     float2 zk[NP], zm[NP], zh[NP];
@@ -476,7 +497,8 @@ extern "C" __global__ __launch_bounds__(SG_FFT_THREADS) void sg_fft_frames(
     }
     __syncthreads();
   }
-  fft_ip<true>(A, g, twM, fb);
+  if (g.kind == SG_FFT_DFT) dft_ip<true>(A, twM + M, twM, M);
+  else fft_ip<true>(A, g, twM, fb);
   // windowed frame: Re(ifft)/N x hann, y[2n] = Re z[n], y[2n+1] = Im z[n]
   for (int idx = threadIdx.x; idx < fb * M; idx += SG_FFT_THREADS) {
     const int f = udiv(idx, g.m_magic), n = idx - f * M;

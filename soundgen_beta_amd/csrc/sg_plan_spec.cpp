@@ -45,8 +45,15 @@ int geometry(Batch& B, int wl) {
       m /= r;
     }
   }
-  if (m != 1)
-    throw SgError(SG_E_UNSUPPORTED, "FFT: window length " + std::to_string(wl) + " has a prime factor > 31");
+  // a prime factor > 31 (windowLength_points shrinks to floor(L / 2) for short
+  // sounds, R/soundgen.R:743, so any length occurs): direct DFT, one frame per workgroup
+  const bool dft = m != 1;
+  if (dft) {
+    g.nstages = 0;
+    if ((int64_t)3 * g.M * 8 > 160 * 1024)
+      throw SgError(SG_E_UNSUPPORTED, "FFT: window length " + std::to_string(wl) + " has a prime factor > 31 and "
+                    "exceeds the direct-DFT LDS budget");
+  }
   // twiddles W_M^t (t < M), W_N^k (k < M), fp64 -> fp32
   vec tw(4 * (size_t)g.M);
   for (int t = 0; t < g.M; ++t) {
@@ -85,19 +92,22 @@ int geometry(Batch& B, int wl) {
   // fb * M <= 8192 (64 KB: two workgroups per CU; sg_fft.hip SG_FFT_SLOTS)
   // wavefront-per-frame kernel when every stage's butterflies fit the
   // register state of one wavefront: ceil(M / R / 64) <= max(1, SG_WAVE_STATE / R)
-  g.kind = SG_FFT_WAVE;
-  for (int s = 0; s < g.nstages; ++s) {
+  g.kind = dft ? SG_FFT_DFT : SG_FFT_WAVE;
+  for (int s = 0; s < g.nstages && !dft; ++s) {
     const int r = g.radix[s], nb = (g.M / r + 63) / 64;
     if (nb > std::max(1, SG_WAVE_STATE / r)) g.kind = SG_FFT_WG;
   }
   // sg_stft_ola: the next frame's inputs fit the prefetch registers, and the
   // LDS tables (twiddles, W_N^k, hamming, hanning) + SG_FFT_WAVES frame
   // slices, M pairs each, fit the 160 KB of a CU
-  if (g.M > 64 * SG_PF_SRC || g.M / 2 + 1 > 64 * SG_PF_PAIR) g.kind = SG_FFT_WG;
-  if ((int64_t)(SG_FFT_WAVES + 4) * g.M * 8 > 160 * 1024) g.kind = SG_FFT_WG;
+  if (!dft && (g.M > 64 * SG_PF_SRC || g.M / 2 + 1 > 64 * SG_PF_PAIR)) g.kind = SG_FFT_WG;
+  if (!dft && (int64_t)(SG_FFT_WAVES + 4) * g.M * 8 > 160 * 1024) g.kind = SG_FFT_WG;
   if (g.kind == SG_FFT_WAVE) {
     g.fb = SG_FFT_WAVES;
     g.lds_bytes = (SG_FFT_WAVES + 4) * g.M * 8;
+  } else if (g.kind == SG_FFT_DFT) {
+    g.fb = 1;
+    g.lds_bytes = 3 * g.M * 8;  // frame, W_M table, DFT output
   } else {
     g.fb = std::max(1, std::min(16, kFftSlots / g.M));
     if (g.fb * g.M > kFftSlots) throw SgError(SG_E_UNSUPPORTED, "FFT: window too long for LDS (wl > 16384)");

@@ -40,13 +40,13 @@ def test_wave_fft_vs_numpy(wl):
         ctx.close()
 
 
-@pytest.mark.parametrize("wl", [440, 800, 1764, 2204])
+@pytest.mark.parametrize("wl", [440, 800, 1764, 2204, 2038, 1998, 6000])
 def test_formant_filter_vs_oracle(oracle, wl):
     from soundgen_beta_amd import api
     rng = np.random.default_rng(wl)
     sound = np.sin(np.cumsum(rng.uniform(0.01, 0.2, 20 * wl))) + 0.1 * rng.normal(size=20 * wl)
     nr = wl // 2
-    step = np.arange(1, max(1, len(sound) - wl) + 1, wl // 4)
+    step = np.arange(1, max(1, len(sound) - wl) + 1e-9, wl * 0.25)  # seq(1, L - wl, by = hop)
     for env in (np.abs(rng.normal(1, 0.3, size=(nr, 1))), np.abs(rng.normal(1, 0.3, size=(nr, len(step))))):
         got = api.formantFilter(sound, env, wl, 75)
         want = oracle.formant_filter(sound, env, wl, 75)
@@ -54,7 +54,7 @@ def test_formant_filter_vs_oracle(oracle, wl):
         assert _rms(got, want) <= TOL
 
 
-@pytest.mark.parametrize("wl,sr", [(800, 16000), (2204, 44100), (440, 44100)])
+@pytest.mark.parametrize("wl,sr", [(800, 16000), (2204, 44100), (440, 44100), (1442, 44100)])
 def test_generate_noise_vs_oracle(oracle, wl, sr):
     from soundgen_beta_amd import api
     na = {"time": [0, 1000], "value": [-30, -10]}
