@@ -40,7 +40,7 @@ struct SgEpoch {
   int32_t pad;
 };
 
-constexpr int SG_ROW_CHUNK = 16;  // amplitude rows per scalar load (s_load_dwordx16)
+constexpr int SG_ROW_CHUNK = 8;   // amplitude rows per DPP group (R padded to a multiple)
 
 // One wave task of the sine bank: `len` (<= SG_TASK_MAX) consecutive samples
 // j0.. of one epoch that lie in ONE phase segment and whose approx() xout all
@@ -50,6 +50,8 @@ constexpr int SG_ROW_CHUNK = 16;  // amplitude rows per scalar load (s_load_dwor
 //   sample l = j - j0:  m = mbase + l,  integr/D = (c0 + m(c1 + m(c2 + m(c3 + m c4)))) * invD
 //                       t = (tc0 + l * xby) * rdx   (approx() weight inside the interval)
 constexpr int SG_TASK_CONST = 1;  // columns equal over the task: A chain only
+constexpr int SG_TASK_ENV = 4;    // the syllable has an amplitude envelope (max taken after it)
+constexpr int SG_TASK_LIN = 2;    // phase segment linear (c2 = c3 = c4 = 0): one fp64 FMA per sample
 constexpr int SG_TASK_MAX = 512;  // samples per task (8 slots of 64 lanes)
 struct SgWTask {
   int64_t w_off;       // W offset of epoch sample 0

@@ -35,7 +35,7 @@ __device__ __forceinline__ void sincospi_q(float x, float& s, float& c) {
 }
 
 // row_newbcast:K — every 16-lane row reads its lane K (gfx950 DPP): with
-// amplitude rows r0..r0+15 held in lanes 0..15 of every row, lane L gets row r0+K.
+// amplitude rows r0..r0+7 held in lanes 0..7 of every row, lane L gets row r0+K.
 #define SG_BC(v, K) \
   __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, (v)), 0x150 + (K), 0xf, 0xf, true))
 
@@ -53,31 +53,30 @@ __device__ __forceinline__ void sincospi_q(float x, float& s, float& c) {
       }                                                                 \
     }                                                                   \
   }
-#define SG_GROUP(g)                                                                                    \
-  if ((g) < ng) {                                                                                      \
-    SG_ROW(g, 15) SG_ROW(g, 14) SG_ROW(g, 13) SG_ROW(g, 12) SG_ROW(g, 11) SG_ROW(g, 10) SG_ROW(g, 9) \
-    SG_ROW(g, 8) SG_ROW(g, 7) SG_ROW(g, 6) SG_ROW(g, 5) SG_ROW(g, 4) SG_ROW(g, 3) SG_ROW(g, 2)       \
-    SG_ROW(g, 1) SG_ROW(g, 0)                                                                          \
+#define SG_GROUP(g)                                                                                   \
+  if ((g) < ng) {                                                                                     \
+    SG_ROW(g, 7) SG_ROW(g, 6) SG_ROW(g, 5) SG_ROW(g, 4) SG_ROW(g, 3) SG_ROW(g, 2) SG_ROW(g, 1) SG_ROW(g, 0) \
   }
 
 // Amplitude rows of one 64-row chunk, register resident: group g (rows
-// 16g..16g+15 of the chunk) is ONE coalesced 64-B vector load replicated into
-// the four 16-lane rows of va[g]; each row reaches every lane through a DPP
-// broadcast folded into the v_sub.
+// 8g..8g+7 of the chunk) is ONE coalesced 32-B vector load replicated into
+// lanes 0..7 of the four 16-lane rows of va[g]; each row reaches every lane
+// through a DPP broadcast folded into the v_sub. (8-row groups: the zero rows
+// a task pads its top group with average 3.5 instead of 7.5.)
 struct AmpChunk {
-  float va[4], vd[4];
+  float va[8], vd[8];
   int ng;
 };
 
 template <bool TWO>
 __device__ __forceinline__ void load_chunk(AmpChunk& c, const float* __restrict__ A, const float* __restrict__ D,
                                            int r0, int R, int lane) {
-  const int r = lane & 15;
-  c.ng = (R - r0) >= 64 ? 4 : (R - r0) >> 4;
+  const int r = lane & 7;
+  c.ng = (R - r0) >= 64 ? 8 : (R - r0) >> 3;
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    c.va[g] = (g < c.ng) ? A[r0 + 16 * g + r] : 0.f;
-    c.vd[g] = (TWO && g < c.ng) ? D[r0 + 16 * g + r] : 0.f;
+  for (int g = 0; g < 8; ++g) {
+    c.va[g] = (g < c.ng) ? A[r0 + 8 * g + r] : 0.f;
+    c.vd[g] = (TWO && g < c.ng) ? D[r0 + 8 * g + r] : 0.f;
   }
 }
 
@@ -86,9 +85,9 @@ template <int NS, bool TWO>
 __device__ __forceinline__ void clenshaw_chunk(const AmpChunk& c, const float (&al)[NS], float (&b1)[NS],
                                                float (&b2)[NS], float (&e1)[NS], float (&e2)[NS]) {
   const int ng = c.ng;
-  const float(&va)[4] = c.va;
-  const float(&vd)[4] = c.vd;
-  SG_GROUP(3) SG_GROUP(2) SG_GROUP(1) SG_GROUP(0)
+  const float(&va)[8] = c.va;
+  const float(&vd)[8] = c.vd;
+  SG_GROUP(7) SG_GROUP(6) SG_GROUP(5) SG_GROUP(4) SG_GROUP(3) SG_GROUP(2) SG_GROUP(1) SG_GROUP(0)
 }
 
 // Per-sample set-up for task sample l: approx() weight t, 2cos(theta), sin(theta).
@@ -96,7 +95,8 @@ template <bool TWO>
 __device__ __forceinline__ void sample_setup(const SgWTask& T, int l, float& t, float& al, float& sn) {
   t = TWO ? fmaf((float)l, T.xby, T.tc0) * T.rdx : 0.f;
   const double m = (double)(T.mbase + l);
-  const double P = fma(m, fma(m, fma(m, fma(m, T.c4, T.c3), T.c2), T.c1), T.c0);
+  const double P = (T.flags & SG_TASK_LIN) ? fma(m, T.c1, T.c0)  // constant pitch over the segment
+                                           : fma(m, fma(m, fma(m, fma(m, T.c4, T.c3), T.c2), T.c1), T.c0);
   const double v = P * T.invD;
   float x = (float)(v - rint(v));  // frac in [-1/2, 1/2] cycles
   float sigma = 1.f;
@@ -108,7 +108,7 @@ __device__ __forceinline__ void sample_setup(const SgWTask& T, int l, float& t, 
   al = sigma * fmaf(-4.f * sh, sh, 2.f);   // 2 cos(theta)
 }
 
-template <int NS, bool TWO>
+template <int NS, bool TWO, bool ENV>
 __device__ __forceinline__ void run_slots(const SgWTask& T, const AmpChunk& c0, const float* __restrict__ amps,
                                           const SgSyllable* __restrict__ syls, const double* __restrict__ cknots,
                                           float* __restrict__ W, int l0, int lane, float& tmax) {
@@ -134,20 +134,20 @@ __device__ __forceinline__ void run_slots(const SgWTask& T, const AmpChunk& c0, 
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const float y = (TWO ? fmaf(t[s], e1[s], b1[s]) : b1[s]) * sn[s];
-    if (valid[s]) {
-      const int j = T.j0 + l[s];
-      W[T.w_off + j] = y;
-      if (j >= T.dj0 && j < T.dj1) {
-        float cand = y;
-        const SgSyllable& sy = syls[T.syl];
-        if (sy.env.kind != 0) cand = (float)((double)y * contour_at(sy.env, cknots, sy.L, T.dk0 + j));
-        tmax = fmaxf(tmax, cand);
-      }
+    const int j = T.j0 + l[s];
+    if (valid[s]) W[T.w_off + j] = y;
+    // fused max over the samples that land 1:1 in the syllable (branch-free)
+    const bool in = valid[s] && j >= T.dj0 && j < T.dj1;
+    if (!ENV) {
+      tmax = in ? fmaxf(tmax, y) : tmax;
+    } else if (in) {  // amplAnchors envelope (rare): R's max is taken after it
+      const SgSyllable& sy = syls[T.syl];
+      tmax = fmaxf(tmax, (float)((double)y * contour_at(sy.env, cknots, sy.L, T.dk0 + j)));
     }
   }
 }
 
-template <bool TWO>
+template <bool TWO, bool ENV>
 __device__ __forceinline__ float run_task(const SgWTask& T, const float* __restrict__ amps,
                                           const SgSyllable* __restrict__ syls, const double* __restrict__ cknots,
                                           float* __restrict__ W, int lane) {
@@ -156,8 +156,8 @@ __device__ __forceinline__ float run_task(const SgWTask& T, const float* __restr
   float tmax = 0.f;
   int l0 = 0;
 #pragma unroll 1
-  for (; l0 + 64 < T.len; l0 += 128) run_slots<2, TWO>(T, c0, amps, syls, cknots, W, l0, lane, tmax);
-  if (l0 < T.len) run_slots<1, TWO>(T, c0, amps, syls, cknots, W, l0, lane, tmax);
+  for (; l0 + 64 < T.len; l0 += 128) run_slots<2, TWO, ENV>(T, c0, amps, syls, cknots, W, l0, lane, tmax);
+  if (l0 < T.len) run_slots<1, TWO, ENV>(T, c0, amps, syls, cknots, W, l0, lane, tmax);
   return tmax;
 }
 
@@ -173,8 +173,13 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank(
     const int64_t ti = tbase + q;
     if (ti >= ntasks) break;
     const SgWTask T = tasks[ti];
-    const float tmax = (T.flags & SG_TASK_CONST) ? run_task<false>(T, amps, syls, cknots, W, lane)
-                                                 : run_task<true>(T, amps, syls, cknots, W, lane);
+    float tmax;
+    if (T.flags & SG_TASK_ENV)  // amplAnchors envelope: rare, kept out of the hot variants
+      tmax = (T.flags & SG_TASK_CONST) ? run_task<false, true>(T, amps, syls, cknots, W, lane)
+                                       : run_task<true, true>(T, amps, syls, cknots, W, lane);
+    else
+      tmax = (T.flags & SG_TASK_CONST) ? run_task<false, false>(T, amps, syls, cknots, W, lane)
+                                       : run_task<true, false>(T, amps, syls, cknots, W, lane);
     const float wm = wave_max(tmax);
     if (lane == 0) taskmax[ti] = wm;
   }

@@ -854,7 +854,8 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
         T.j0 = (int32_t)j0; T.len = (int32_t)len;
         T.dj0 = ep.dj0; T.dj1 = ep.dj1;
         T.syl = ep.syl;
-        T.flags = cst[i] ? SG_TASK_CONST : 0;
+        T.flags = (cst[i] ? SG_TASK_CONST : 0) | (S.c2 == 0 && S.c3 == 0 && S.c4 == 0 ? SG_TASK_LIN : 0) |
+                  (B.syls[ep.syl].env.kind != 0 ? SG_TASK_ENV : 0);
         B.tasks.push_back(T);
         j0 += len;
       }
