@@ -33,6 +33,7 @@ C2_PARAMS = dict(samplingRate=44100, pitchSamplingRate=3500, temperature=0, nonl
                  pitchCeiling=3500, throwaway=-120)
 HBM_PEAK_GBS = 8000.0                 # MI355X_MICROARCH.md chip table (spec)
 VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9  # lane-ops/s: 256 CU x 4 SIMD-32 x 2.4 GHz (one op per lane per cycle)
+FP32_PEAK_TFLOPS = 157.3              # MI355X FP32 vector (packed FMA)
 
 
 def _rng(rank, salt):
@@ -148,6 +149,54 @@ def cpu_baseline(calls, budget_s):
                       % (n, n_samples)}
 
 
+def traffic_from_profiles(config, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of
+    this workload (profiles/rNN_<config>_traffic.json, tools/gpu_traffic.sh:
+    separate FETCH_SIZE / WRITE_SIZE passes, gfx950 FETCH_SIZE doubled)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_%s_traffic.json" % config)))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    hits = [v["hbm_bytes"] for k, v in d.get("kernels", {}).items() if k.split(" ")[0] == kernel and "hbm_bytes" in v]
+    if not hits:
+        return None, None
+    return max(hits), os.path.relpath(files[-1], ROOT)
+
+
+def roofline(st, prof, steps, config):
+    """Roofline of the step's dominant kernel (the one with the most event time):
+    achieved = algorithmic bytes per launch / average launch duration (HIP events on
+    the launch stream), SURVEY.md §8d per-unit bytes."""
+    tot = {k: v[0] * v[1] for k, v in prof.items()}
+    kern = max(tot, key=tot.get) if any(tot.values()) else "sg_sine_bank"
+    ms, n = prof[kern]
+    launches = max(1, n // steps)
+    sec = ms / 1e3
+    if kern == "sg_sine_bank":
+        # fp32 epoch waveform write + the amplitude blocks it reads (A and dA columns)
+        alg = (4 * st["harm_samples"] + st["harm_amp_bytes"]) / launches
+        valu_ops = 2.0 * st["harm_terms"] / launches  # Clenshaw: 2 lane-ops per (sample, row, chain)
+        extra = {"valu": {"ops_per_launch": valu_ops, "achieved_ops_s": valu_ops / sec if sec else 0,
+                          "peak_ops_s": VALU_PEAK_OPS, "frac": valu_ops / sec / VALU_PEAK_OPS if sec else 0}}
+    else:
+        # source / uniforms + envelope columns read, trimmed output written
+        alg = st["stft_bytes"] / launches
+        fl = st["stft_flops"] / launches
+        extra = {"flops": {"nominal_per_launch": fl, "achieved_tflops": fl / sec / 1e12 if sec else 0,
+                           "peak_tflops": FP32_PEAK_TFLOPS,
+                           "frac": fl / sec / 1e12 / FP32_PEAK_TFLOPS if sec else 0}}
+    achieved = alg / sec / 1e9 if sec > 0 else 0.0
+    traffic, src = traffic_from_profiles(config, kern)
+    r = {"bound": "hbm", "kernel": kern, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "alg_bytes_per_launch": alg,
+         "avg_launch_ms": ms, "launches_timed": n}
+    if src:
+        r["traffic_source"] = src
+    r.update(extra)
+    return r
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -205,8 +254,11 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     L.sg_set_profiling(ctx.ptr, 0)
-    sine_ms, nprof = C.c_double(), C.c_int64()
-    native.check(L.sg_profile_read(ctx.ptr, C.byref(sine_ms), C.byref(nprof)), ctx.ptr)
+    prof = {}
+    for kid, name in ((0, "sg_sine_bank"), (1, "sg_stft_ola")):
+        ms, n = C.c_double(), C.c_int64()
+        native.check(L.sg_profile_read_kernel(ctx.ptr, kid, C.byref(ms), C.byref(n)), ctx.ptr)
+        prof[name] = (ms.value, n.value)
 
     samples_rank = int(plan.lengths.sum())  # synthesized samples (slot padding excluded)
     if dist:
@@ -244,14 +296,7 @@ def main():
 
     if rank == 0:
         st = plan.stats()
-        # algorithmic bytes of one sine-bank launch: fp32 epoch
-        # waveform write + the amplitude blocks it reads (A and dA columns)
-        launches = max(1, nprof.value // args.steps)  # sine-bank launches per step (batch slices)
-        alg_bytes = (4 * st["harm_samples"] + st["harm_amp_bytes"]) / launches
-        sine_s = sine_ms.value / 1e3
-        achieved = alg_bytes / sine_s / 1e9 if sine_s > 0 else 0.0
-        # VALU: Clenshaw rows cost 2 lane-ops per (sample, row, chain)
-        valu_ops = 2.0 * st["harm_terms"] / launches
+        roof = roofline(st, prof, args.steps, args.config)
         from oracle import oracle as O
         rms = []
         host = None
@@ -268,13 +313,7 @@ def main():
                        "sampling_rate": 44100, "parallelism": "dp%d (independent shards)" % world,
                        "plan_s": t_plan, "failed_calls": failed},
             "rms_error_vs_oracle": max(rms) if rms else None,
-            "roofline": {"bound": "hbm", "kernel": "sg_sine_bank", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": sine_ms.value,
-                         "launches_timed": nprof.value,
-                         "valu": {"ops_per_launch": valu_ops, "achieved_ops_s": valu_ops / sine_s if sine_s else 0,
-                                  "peak_ops_s": VALU_PEAK_OPS,
-                                  "frac": valu_ops / sine_s / VALU_PEAK_OPS if sine_s else 0}},
+            "roofline": roof,
         }
         if gather_ms is not None:
             res["gather_ms"] = gather_ms

@@ -164,11 +164,19 @@ int sg_plan_upload(sg_ctx* ctx, sg_plan* plan);
  * No host synchronisation inside; graph-capturable. */
 int sg_execute(sg_ctx* ctx, sg_plan* plan, float* d_out, void* stream);
 /* Profiling: when enabled, sg_execute brackets every sine-bank launch (one
- * per batch slice) with HIP events on the launch stream; sg_profile_read
+ * per batch slice) and every sg_stft_ola launch with HIP events on the launch
+ * stream; sg_profile_read
  * returns the average launch duration (ms) and the number of launches
  * recorded, and clears them. */
 int sg_set_profiling(sg_ctx* ctx, int on);
 int sg_profile_read(sg_ctx* ctx, double* sine_ms_avg, int64_t* n);
+/* Same for one kernel: SG_PROF_SINE_BANK (sg_sine_bank, generateHarmonics'
+ * sine bank, R/source.R:389-419) or SG_PROF_STFT_OLA (sg_stft_ola, the fused
+ * seewave stft/istft + overlap-add of R/soundgen.R:743-807 and R/source.R:88-131;
+ * one event pair per phase launch). */
+#define SG_PROF_SINE_BANK 0
+#define SG_PROF_STFT_OLA 1
+int sg_profile_read_kernel(sg_ctx* ctx, int kernel, double* ms_avg, int64_t* n);
 int sg_synchronize(sg_ctx* ctx);
 /* Synchronous convenience: upload (if needed), execute and copy the packed
  * output to host doubles: call i's samples land at out_host + offset[i]
@@ -182,6 +190,11 @@ const char* sg_plan_call_message(const sg_plan* plan, int64_t i);
 int sg_plan_kernel_stats(const sg_plan* plan, int64_t* harm_samples,
                          int64_t* harm_terms, int64_t* harm_amp_bytes,
                          int64_t* fft_frames);
+/* sg_stft_ola work of the plan (fused seewave stft x envelope -> istft -> OLA,
+ * R/soundgen.R:743-807, and generateNoise's istft, R/source.R:88-131): trimmed
+ * output samples, algorithmic HBM bytes (source/uniforms + envelope columns +
+ * output) and nominal flops (5 wl log2 wl per transform). */
+int sg_plan_stft_stats(const sg_plan* plan, int64_t* samples, int64_t* alg_bytes, double* flops);
 
 /* ---- function-level entries mirroring the R API (synchronous) ---------- */
 int sg_generate_harmonics(sg_ctx* ctx, const double* pitch, int64_t len,

@@ -58,8 +58,10 @@ class Plan:
     def stats(self):
         v = [C.c_int64() for _ in range(4)]
         native.lib().sg_plan_kernel_stats(self.ptr, *[C.byref(x) for x in v])
+        w = [C.c_int64(), C.c_int64(), C.c_double()]
+        native.lib().sg_plan_stft_stats(self.ptr, *[C.byref(x) for x in w])
         return dict(harm_samples=v[0].value, harm_terms=v[1].value, harm_amp_bytes=v[2].value,
-                    fft_frames=v[3].value)
+                    fft_frames=v[3].value, stft_samples=w[0].value, stft_bytes=w[1].value, stft_flops=w[2].value)
 
     def device_bytes(self):
         return int(native.lib().sg_plan_device_bytes(self.ptr))

@@ -17,7 +17,7 @@ struct sg_ctx {
   hipStream_t aux = nullptr;  // finalize stream of the slice pipeline
   std::string err;
   bool profiling = false;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
+  std::vector<sg::SgProfEvent> prof_events;
 };
 
 struct sg_plan {
@@ -106,7 +106,7 @@ int sg_ctx_create(int device, sg_ctx** out) {
 void sg_ctx_destroy(sg_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
-  for (auto& ev : ctx->prof_events) { (void)hipEventDestroy(ev.first); (void)hipEventDestroy(ev.second); }
+  for (auto& ev : ctx->prof_events) { (void)hipEventDestroy(ev.e0); (void)hipEventDestroy(ev.e1); }
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
   delete ctx;
@@ -214,26 +214,38 @@ int sg_set_profiling(sg_ctx* ctx, int on) {
   return SG_OK;
 }
 
-// Average duration (ms) of the sine-bank kernel over the executes recorded
-// since profiling was enabled (events are on the launch stream).
-int sg_profile_read(sg_ctx* ctx, double* sine_ms_avg, int64_t* n) {
+// Average duration (ms) of one profiled kernel (SG_PROF_*) over the executes
+// recorded since profiling was enabled (events are on the launch stream). Reading
+// a kernel consumes its events; the others stay until read or destroyed.
+int sg_profile_read_kernel(sg_ctx* ctx, int kernel, double* ms_avg, int64_t* n) {
   return guarded(ctx, [&]() {
+    if (kernel != SG_PROF_SINE_BANK && kernel != SG_PROF_STFT_OLA)
+      throw sg::SgError(SG_E_ARG, "sg_profile_read_kernel: unknown kernel id");
     double tot = 0;
     int64_t cnt = 0;
+    std::vector<sg::SgProfEvent> keep;
     for (auto& ev : ctx->prof_events) {
-      HIPCHK(hipEventSynchronize(ev.second));
+      if (ev.kernel != kernel) {
+        keep.push_back(ev);
+        continue;
+      }
+      HIPCHK(hipEventSynchronize(ev.e1));
       float ms = 0;
-      HIPCHK(hipEventElapsedTime(&ms, ev.first, ev.second));
+      HIPCHK(hipEventElapsedTime(&ms, ev.e0, ev.e1));
       tot += ms;
       ++cnt;
-      (void)hipEventDestroy(ev.first);
-      (void)hipEventDestroy(ev.second);
+      (void)hipEventDestroy(ev.e0);
+      (void)hipEventDestroy(ev.e1);
     }
-    ctx->prof_events.clear();
-    *sine_ms_avg = cnt ? tot / cnt : 0;
+    ctx->prof_events.swap(keep);
+    *ms_avg = cnt ? tot / cnt : 0;
     *n = cnt;
     return SG_OK;
   });
+}
+
+int sg_profile_read(sg_ctx* ctx, double* sine_ms_avg, int64_t* n) {
+  return sg_profile_read_kernel(ctx, SG_PROF_SINE_BANK, sine_ms_avg, n);
 }
 
 int sg_plan_kernel_stats(const sg_plan* plan, int64_t* harm_samples, int64_t* harm_terms, int64_t* harm_amp_bytes,
@@ -243,6 +255,14 @@ int sg_plan_kernel_stats(const sg_plan* plan, int64_t* harm_samples, int64_t* ha
   *harm_terms = plan->B.harm_terms;
   *harm_amp_bytes = plan->B.harm_amp_bytes;
   *fft_frames = plan->B.fft_frames;
+  return SG_OK;
+}
+
+int sg_plan_stft_stats(const sg_plan* plan, int64_t* samples, int64_t* alg_bytes, double* flops) {
+  if (!plan) return SG_E_ARG;
+  *samples = plan->B.stft_samples;
+  *alg_bytes = plan->B.stft_bytes;
+  *flops = plan->B.stft_flops;
   return SG_OK;
 }
 

@@ -174,9 +174,9 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
 }
 
 void device_execute(const Batch& B, DevicePlan& D, float* d_out, hipStream_t s, hipStream_t s2,
-                    std::vector<std::pair<hipEvent_t, hipEvent_t>>* prof) {
+                    std::vector<SgProfEvent>* prof) {
   if (B.slices.empty()) {  // no harmonic syllables: spectral phases only
-    device_execute_spec(B, D, d_out, s);
+    device_execute_spec(B, D, d_out, s, prof);
     return;
   }
   const bool two = B.slices.size() > 1;
@@ -197,7 +197,7 @@ void device_execute(const Batch& B, DevicePlan& D, float* d_out, hipStream_t s, 
     launch_sine_bank(D, sl.t0, sl.t1 - sl.t0, s);
     if (prof) {
       HIPCHK(hipEventRecord(e1, s));
-      prof->emplace_back(e0, e1);
+      prof->push_back({SG_PROF_SINE_BANK, e0, e1});
     }
     launch_piece_max(D, sl.p0, sl.p1 - sl.p0, s);
     launch_syl_max(D, sl.s0, sl.s1 - sl.s0, s);
@@ -211,17 +211,29 @@ void device_execute(const Batch& B, DevicePlan& D, float* d_out, hipStream_t s, 
     HIPCHK(hipEventRecord(D.ev_join, s2));
     HIPCHK(hipStreamWaitEvent(s, D.ev_join, 0));
   }
-  device_execute_spec(B, D, d_out, s);
+  device_execute_spec(B, D, d_out, s, prof);
   HIPCHK(hipGetLastError());
 }
 
 // Spectral phases after the harmonic syllables: noise frames -> noise OLA,
 // pre-filter mixes (sounds), filter frames -> filter OLA, final mixes.
-void device_execute_spec(const Batch& B, const DevicePlan& D, float* d_out, hipStream_t s) {
+void device_execute_spec(const Batch& B, const DevicePlan& D, float* d_out, hipStream_t s,
+                         std::vector<SgProfEvent>* prof) {
   // phase: fused STFT/ISTFT/OLA segments, unfused frame groups + OLA tiles, per-OLA maxima
   auto phase = [&](int ph) {
     const int64_t* r = B.fgroup_range[ph];
-    launch_stft_ola(D, B.seg_range[ph][0], B.seg_range[ph][1] - B.seg_range[ph][0], B.fgroup_lds[ph][0], s);
+    const int64_t nseg = B.seg_range[ph][1] - B.seg_range[ph][0];
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (prof && nseg > 0) {
+      HIPCHK(hipEventCreate(&e0));
+      HIPCHK(hipEventCreate(&e1));
+      HIPCHK(hipEventRecord(e0, s));
+    }
+    launch_stft_ola(D, B.seg_range[ph][0], nseg, B.fgroup_lds[ph][0], s);
+    if (prof && nseg > 0) {
+      HIPCHK(hipEventRecord(e1, s));
+      prof->push_back({SG_PROF_STFT_OLA, e0, e1});
+    }
     launch_fft_frames(D, r[1], r[2] - r[1], B.fgroup_lds[ph][1], s);
     const int64_t t0 = ph == 0 ? 0 : B.olatile_split, t1 = ph == 0 ? B.olatile_split : (int64_t)B.olatiles.size();
     const int64_t o0 = ph == 0 ? 0 : B.ola_split, o1 = ph == 0 ? B.ola_split : (int64_t)B.olas_dev.size();

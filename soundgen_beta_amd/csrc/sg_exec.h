@@ -47,12 +47,18 @@ struct DevicePlan {
 int64_t device_bytes(const Batch& B);
 void device_upload(const Batch& B, DevicePlan& D, hipStream_t s);
 void device_free(DevicePlan& D);
+// HIP events bracketing one launch of a profiled kernel (SG_PROF_*), on its stream
+struct SgProfEvent {
+  int kernel;
+  hipEvent_t e0, e1;
+};
 // Slice pipeline: sine bank + maxes of slice c on s, finalize of slice c on
 // s2 (overlapping the sine bank of c+1); s waits for s2 at the end. prof
-// (optional) receives one event pair per sine-bank launch.
+// (optional) receives one event pair per sine-bank and sg_stft_ola launch.
 void device_execute(const Batch& B, DevicePlan& D, float* d_out, hipStream_t s, hipStream_t s2,
-                    std::vector<std::pair<hipEvent_t, hipEvent_t>>* prof);
-void device_execute_spec(const Batch& B, const DevicePlan& D, float* d_out, hipStream_t s);
+                    std::vector<SgProfEvent>* prof);
+void device_execute_spec(const Batch& B, const DevicePlan& D, float* d_out, hipStream_t s,
+                         std::vector<SgProfEvent>* prof = nullptr);
 
 // launchers (sg_harm.hip)
 void launch_sine_bank(const DevicePlan& D, int64_t t0, int64_t n_tasks, hipStream_t s);

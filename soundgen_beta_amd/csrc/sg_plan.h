@@ -72,6 +72,8 @@ struct Batch {
   int64_t total_out = 0;
   // ---- stats ----
   int64_t harm_samples = 0, harm_terms = 0, harm_amp_bytes = 0, fft_frames = 0;
+  int64_t stft_bytes = 0, stft_samples = 0;  // sg_stft_ola: algorithmic bytes, trimmed output samples
+  double stft_flops = 0;                     // sg_stft_ola: nominal 5 wl log2 wl per transform
 };
 
 // Plan one generateHarmonics() call; the finalized syllable is written at

@@ -547,6 +547,8 @@ void finalize_spec(Batch& B) {
   }
   const int32_t nt = (int32_t)B.olatiles.size();
   int32_t nslots = 0;  // real segments so far (slots nt + nslots)
+  B.stft_bytes = B.stft_samples = 0;
+  B.stft_flops = 0;
   for (int ph = 0; ph < 2; ++ph) {
     B.seg_range[ph][0] = (int64_t)B.olasegs.size();
     const size_t o_lo = ph == 0 ? 0 : (size_t)B.ola_split, o_hi = ph == 0 ? (size_t)B.ola_split : B.olas_dev.size();
@@ -578,6 +580,24 @@ void finalize_spec(Batch& B) {
       };
       const int64_t n = o.nframes;
       const int64_t nseg = std::max<int64_t>(1, (n + SG_SEG_FRAMES - 1) / SG_SEG_FRAMES);
+      {  // algorithmic bytes / flops of this OLA in sg_stft_ola (bench roofline)
+        const int64_t nr = o.wl / 2;
+        int64_t ncol = 0, prev = -1;
+        for (int64_t f = 0; f < n; ++f) {
+          const int64_t e = B.frames[ph][o.fidx - fbase + f].env;
+          if (e != prev) ++ncol;
+          prev = e;
+        }
+        const double fft = 5.0 * o.wl * std::log2((double)o.wl);
+        if (ph == 0) {  // noise: uniforms nr per frame + filter columns + trimmed output
+          B.stft_bytes += 4 * (nr * n + nr * ncol + o.len);
+          B.stft_flops += fft * n;
+        } else {  // filter: the sound under the frames + envelope columns + trimmed output
+          B.stft_bytes += 4 * (std::min<int64_t>(o.xlen, o.wl + (int64_t)std::ceil((n - 1) * o.h)) + nr * ncol + o.len);
+          B.stft_flops += 2 * fft * n;
+        }
+        B.stft_samples += o.len;
+      }
       o.tile0 = nt + nslots;
       o.nslot = (int32_t)nseg;
       for (int64_t k = 0; k < nseg; ++k) {

@@ -68,6 +68,8 @@ def lib():
     L.sg_execute.argtypes = [vp, vp, vp, vp]
     L.sg_set_profiling.argtypes = [vp, C.c_int]
     L.sg_profile_read.argtypes = [vp, dp, i64p]
+    L.sg_profile_read_kernel.argtypes = [vp, C.c_int, dp, i64p]
+    L.sg_plan_stft_stats.argtypes = [vp, i64p, i64p, dp]
     L.sg_plan_kernel_stats.argtypes = [vp, i64p, i64p, i64p, i64p]
     L.sg_synchronize.argtypes = [vp]
     L.sg_execute_to_host.argtypes = [vp, vp, dp]

@@ -1,0 +1,18 @@
+#!/bin/bash
+# HBM traffic per launch (MI355X guide, HBM/rocprofv3 section): FETCH_SIZE and
+# WRITE_SIZE in separate --pmc passes (they do not fit one TCC group), no tracing
+# domains; summarised by tools/pmc_summary.py.
+set -e
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd /tmp
+export TMPDIR=/tmp
+TAG=${1:-traffic}
+CFG=${CFG:-c2}
+i=0
+for grp in FETCH_SIZE WRITE_SIZE; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d "$R/gpurun_out/${TAG}_$i" -o run -- python "$R/bench.py" --config $CFG --steps 3 --warmup 1 --no-cpu-baseline > "$R/gpurun_out/${TAG}_$i.log" 2>&1 || { tail -20 "$R/gpurun_out/${TAG}_$i.log"; exit 1; }
+done
+cd "$R"
+python tools/pmc_summary.py $TAG $CFG > gpurun_out/${TAG}_summary.json
+cat gpurun_out/${TAG}_summary.json
