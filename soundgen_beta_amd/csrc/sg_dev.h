@@ -40,7 +40,7 @@ struct SgEpoch {
   int32_t pad;
 };
 
-constexpr int SG_ROW_CHUNK = 8;   // amplitude rows per DPP group (R padded to a multiple)
+constexpr int SG_ROW_CHUNK = 4;   // amplitude rows per ds_read_b128 (R padded to a multiple)
 
 // One wave task of the sine bank: `len` (<= SG_TASK_MAX) consecutive samples
 // j0.. of one epoch that lie in ONE phase segment and whose approx() xout all

@@ -1,10 +1,10 @@
 // sg_harm.hip — gfx950 kernels of the additive harmonic source
 // (generateHarmonics(), R/source.R:377-467).
 //
-// sg_sine_bank: one wave task = up to 64 consecutive samples of one epoch
+// sg_sine_bank: one wave task = up to 512 consecutive samples of one epoch
 // inside ONE amplitude interval (the approx() knots x_i, x_{i+1}, R/source.R:403-405),
 // so both amplitude columns A[i][.], dA[i][.] = A[i+1][.] - A[i][.] are wave-uniform
-// and stream through the scalar cache (s_load_dwordx16, prefetched one chunk ahead):
+// (staged in the wave's LDS slice, read back as broadcasts):
 //   integr(u)  closed-form quartic prefix sum of the FMM pitch spline (fp64, Horner)
 //   theta      = 2*pi*frac(integr / D)
 //   W(j)       = sum_r (A_r + t_j dA_r) sin(r theta)             (R/source.R:396-419)
@@ -24,94 +24,79 @@ using sgd::contour_at;
 using sgd::linear_at;
 using sgd::wave_max;
 
-// sin(pi*x), cos(pi*x) for |x| <= 1/4 (|pi*x| <= pi/4): Taylor to x^9 / x^10,
-// truncation < 2e-9, i.e. below fp32 rounding.
-__device__ __forceinline__ void sincospi_q(float x, float& s, float& c) {
-  const float a = 3.14159265358979f * x;
-  const float a2 = a * a;
-  s = a * fmaf(a2, fmaf(a2, fmaf(a2, fmaf(a2, 2.75573192e-6f, -1.98412698e-4f), 8.33333333e-3f), -1.66666667e-1f), 1.f);
-  c = fmaf(a2, fmaf(a2, fmaf(a2, fmaf(a2, fmaf(a2, -2.75573192e-7f, 2.48015873e-5f), -1.38888889e-3f),
-                          4.16666667e-2f), -0.5f), 1.f);
-}
-
-// row_newbcast:K — every 16-lane row reads its lane K (gfx950 DPP): with
-// amplitude rows r0..r0+7 held in lanes 0..7 of every row, lane L gets row r0+K.
-#define SG_BC(v, K) \
-  __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, (v)), 0x150 + (K), 0xf, 0xf, true))
-
-// Clenshaw rows g*16+K of group g: b = A_r + al*b1 - b2 (and the dA chain when TWO)
-#define SG_ROW(g, K)                                                    \
-  {                                                                     \
-    _Pragma("unroll") for (int s = 0; s < NS; ++s) {                    \
-      const float b = fmaf(al[s], b1[s], SG_BC(va[g], K) - b2[s]);      \
-      b2[s] = b1[s];                                                    \
-      b1[s] = b;                                                        \
-      if (TWO) {                                                        \
-        const float e = fmaf(al[s], e1[s], SG_BC(vd[g], K) - e2[s]);    \
-        e2[s] = e1[s];                                                  \
-        e1[s] = e;                                                      \
-      }                                                                 \
-    }                                                                   \
-  }
-#define SG_GROUP(g)                                                                                   \
-  if ((g) < ng) {                                                                                     \
-    SG_ROW(g, 7) SG_ROW(g, 6) SG_ROW(g, 5) SG_ROW(g, 4) SG_ROW(g, 3) SG_ROW(g, 2) SG_ROW(g, 1) SG_ROW(g, 0) \
-  }
-
-// Amplitude rows of one 64-row chunk, register resident: group g (rows
-// 8g..8g+7 of the chunk) is ONE coalesced 32-B vector load replicated into
-// lanes 0..7 of the four 16-lane rows of va[g]; each row reaches every lane
-// through a DPP broadcast folded into the v_sub. (8-row groups: the zero rows
-// a task pads its top group with average 3.5 instead of 7.5.)
-struct AmpChunk {
-  float va[8], vd[8];
-  int ng;
-};
+// Amplitude rows of the wave's task are staged in the wave's LDS slice (A
+// rows, then dA rows); every Clenshaw step reads 4 rows with one broadcast
+// ds_read_b128 (all lanes, same address) into VGPRs, so each row costs exactly
+// the two VALU ops of the recurrence. (A DPP row broadcast folded into the
+// v_sub measured 4.5 lane-instructions per (sample, row) on gfx950, VGPR/SGPR
+// operands 2.7 — tools/ubench/clenshaw_ubench.hip.)
+constexpr int SG_LDS_ROWS = 256;  // rows staged per wave; taller tasks stream 256-row chunks
 
 template <bool TWO>
-__device__ __forceinline__ void load_chunk(AmpChunk& c, const float* __restrict__ A, const float* __restrict__ D,
-                                           int r0, int R, int lane) {
-  const int r = lane & 7;
-  c.ng = (R - r0) >= 64 ? 8 : (R - r0) >> 3;
-#pragma unroll
-  for (int g = 0; g < 8; ++g) {
-    c.va[g] = (g < c.ng) ? A[r0 + 8 * g + r] : 0.f;
-    c.vd[g] = (TWO && g < c.ng) ? D[r0 + 8 * g + r] : 0.f;
+__device__ __forceinline__ void stage_rows(float* __restrict__ la, float* __restrict__ ld, const float* __restrict__ A,
+                                           const float* __restrict__ D, int r0, int n, int lane) {
+  for (int r = lane; r < n; r += 64) {
+    la[r] = A[r0 + r];
+    if (TWO) ld[r] = D[r0 + r];
   }
 }
 
-// Clenshaw over one chunk (top row first) continuing the recurrences b, e.
+// Clenshaw over staged rows n-1 .. 0 (n a multiple of 4), continuing b (and e)
+#define SG_ROW(a, d)                                                  \
+  {                                                                   \
+    _Pragma("unroll") for (int s = 0; s < NS; ++s) {                  \
+      const float b = fmaf(al[s], b1[s], (a) - b2[s]);                \
+      b2[s] = b1[s];                                                  \
+      b1[s] = b;                                                      \
+      if (TWO) {                                                      \
+        const float e = fmaf(al[s], e1[s], (d) - e2[s]);              \
+        e2[s] = e1[s];                                                \
+        e1[s] = e;                                                    \
+      }                                                               \
+    }                                                                 \
+  }
 template <int NS, bool TWO>
-__device__ __forceinline__ void clenshaw_chunk(const AmpChunk& c, const float (&al)[NS], float (&b1)[NS],
-                                               float (&b2)[NS], float (&e1)[NS], float (&e2)[NS]) {
-  const int ng = c.ng;
-  const float(&va)[8] = c.va;
-  const float(&vd)[8] = c.vd;
-  SG_GROUP(7) SG_GROUP(6) SG_GROUP(5) SG_GROUP(4) SG_GROUP(3) SG_GROUP(2) SG_GROUP(1) SG_GROUP(0)
+__device__ __forceinline__ void clenshaw_lds(const float* __restrict__ la, const float* __restrict__ ld, int n,
+                                             const float (&al)[NS], float (&b1)[NS], float (&b2)[NS],
+                                             float (&e1)[NS], float (&e2)[NS]) {
+  int q = (n >> 2) - 1;
+  if (q < 0) return;
+  float4 A4 = *reinterpret_cast<const float4*>(la + 4 * q);
+  float4 D4 = TWO ? *reinterpret_cast<const float4*>(ld + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 1
+  for (; q >= 0; --q) {
+    const int qn = q > 0 ? q - 1 : 0;  // next (lower) 4 rows, read ahead of their use
+    const float4 An = *reinterpret_cast<const float4*>(la + 4 * qn);
+    const float4 Dn = TWO ? *reinterpret_cast<const float4*>(ld + 4 * qn) : make_float4(0.f, 0.f, 0.f, 0.f);
+    SG_ROW(A4.w, D4.w)
+    SG_ROW(A4.z, D4.z)
+    SG_ROW(A4.y, D4.y)
+    SG_ROW(A4.x, D4.x)
+    A4 = An;
+    D4 = Dn;
+  }
 }
 
 // Per-sample set-up for task sample l: approx() weight t, 2cos(theta), sin(theta).
-template <bool TWO>
+// LIN: the phase segment is linear (wave-uniform, chosen per task), one fp64 FMA.
+// theta = 2 pi x with x the fractional cycle in [-1/2, 1/2]; v_sin_f32 / v_cos_f32
+// take revolutions (measured max abs error 1.24e-7 on gfx950, the fp32 rounding level).
+template <bool TWO, bool LIN>
 __device__ __forceinline__ void sample_setup(const SgWTask& T, int l, float& t, float& al, float& sn) {
   t = TWO ? fmaf((float)l, T.xby, T.tc0) * T.rdx : 0.f;
   const double m = (double)(T.mbase + l);
-  const double P = (T.flags & SG_TASK_LIN) ? fma(m, T.c1, T.c0)  // constant pitch over the segment
-                                           : fma(m, fma(m, fma(m, fma(m, T.c4, T.c3), T.c2), T.c1), T.c0);
+  const double P = LIN ? fma(m, T.c1, T.c0) : fma(m, fma(m, fma(m, fma(m, T.c4, T.c3), T.c2), T.c1), T.c0);
   const double v = P * T.invD;
-  float x = (float)(v - rint(v));  // frac in [-1/2, 1/2] cycles
-  float sigma = 1.f;
-  if (x > 0.25f) { x -= 0.5f; sigma = -1.f; }
-  else if (x < -0.25f) { x += 0.5f; sigma = -1.f; }
-  float sh, ch;
-  sincospi_q(x, sh, ch);
-  sn = sigma * (2.f * sh * ch);            // sin(theta)
-  al = sigma * fmaf(-4.f * sh, sh, 2.f);   // 2 cos(theta)
+  const float x = (float)(v - rint(v));
+  sn = __builtin_amdgcn_sinf(x);
+  al = 2.f * __builtin_amdgcn_cosf(x);
 }
 
-template <int NS, bool TWO, bool ENV>
-__device__ __forceinline__ void run_slots(const SgWTask& T, const AmpChunk& c0, const float* __restrict__ amps,
-                                          const SgSyllable* __restrict__ syls, const double* __restrict__ cknots,
-                                          float* __restrict__ W, int l0, int lane, float& tmax) {
+template <int NS, bool TWO, bool ENV, bool LIN>
+__device__ __forceinline__ void run_slots(const SgWTask& T, bool staged, float* __restrict__ la, float* __restrict__ ld,
+                                          const float* __restrict__ amps, const SgSyllable* __restrict__ syls,
+                                          const double* __restrict__ cknots, float* __restrict__ W, int l0, int lane,
+                                          float& tmax) {
   float t[NS], al[NS], sn[NS], b1[NS], b2[NS], e1[NS], e2[NS];
   int l[NS];
   bool valid[NS];
@@ -119,16 +104,16 @@ __device__ __forceinline__ void run_slots(const SgWTask& T, const AmpChunk& c0, 
   for (int s = 0; s < NS; ++s) {
     l[s] = l0 + 64 * s + lane;
     valid[s] = l[s] < T.len;
-    sample_setup<TWO>(T, valid[s] ? l[s] : 0, t[s], al[s], sn[s]);
+    sample_setup<TWO, LIN>(T, valid[s] ? l[s] : 0, t[s], al[s], sn[s]);
     b1[s] = b2[s] = e1[s] = e2[s] = 0.f;
   }
-  if (T.R <= 64) {
-    clenshaw_chunk<NS, TWO>(c0, al, b1, b2, e1, e2);
-  } else {  // rare (subharmonic epochs with many rows): stream 64-row chunks, top first
-    for (int r0 = (T.R - 1) / 64 * 64; r0 >= 0; r0 -= 64) {
-      AmpChunk c;
-      load_chunk<TWO>(c, amps + T.a_off, amps + T.d_off, r0, T.R, lane);
-      clenshaw_chunk<NS, TWO>(c, al, b1, b2, e1, e2);
+  if (staged) {
+    clenshaw_lds<NS, TWO>(la, ld, T.R, al, b1, b2, e1, e2);
+  } else {  // rare (subharmonic epochs with many rows): 256-row chunks, top first
+    for (int r0 = (T.R - 1) / SG_LDS_ROWS * SG_LDS_ROWS; r0 >= 0; r0 -= SG_LDS_ROWS) {
+      const int n = T.R - r0 < SG_LDS_ROWS ? T.R - r0 : SG_LDS_ROWS;
+      stage_rows<TWO>(la, ld, amps + T.a_off, amps + T.d_off, r0, n, lane);
+      clenshaw_lds<NS, TWO>(la, ld, n, al, b1, b2, e1, e2);
     }
   }
 #pragma unroll
@@ -147,17 +132,22 @@ __device__ __forceinline__ void run_slots(const SgWTask& T, const AmpChunk& c0, 
   }
 }
 
-template <bool TWO, bool ENV>
-__device__ __forceinline__ float run_task(const SgWTask& T, const float* __restrict__ amps,
-                                          const SgSyllable* __restrict__ syls, const double* __restrict__ cknots,
-                                          float* __restrict__ W, int lane) {
-  AmpChunk c0;  // rows [0, 64) stay in registers for every slot of the task
-  if (T.R <= 64) load_chunk<TWO>(c0, amps + T.a_off, amps + T.d_off, 0, T.R, lane);
+template <bool TWO, bool ENV, bool LIN>
+__device__ __forceinline__ float run_task(const SgWTask& T, float* __restrict__ la, float* __restrict__ ld,
+                                          const float* __restrict__ amps, const SgSyllable* __restrict__ syls,
+                                          const double* __restrict__ cknots, float* __restrict__ W, int lane) {
+  const bool staged = T.R <= SG_LDS_ROWS;  // rows stay in LDS for every pass of the task
+  if (staged) stage_rows<TWO>(la, ld, amps + T.a_off, amps + T.d_off, 0, T.R, lane);
   float tmax = 0.f;
   int l0 = 0;
+  // passes of 4 / 2 / 1 slots of 64 samples (a task has <= 8 slots)
 #pragma unroll 1
-  for (; l0 + 64 < T.len; l0 += 128) run_slots<2, TWO, ENV>(T, c0, amps, syls, cknots, W, l0, lane, tmax);
-  if (l0 < T.len) run_slots<1, TWO, ENV>(T, c0, amps, syls, cknots, W, l0, lane, tmax);
+  for (; T.len - l0 > 192; l0 += 256) run_slots<4, TWO, ENV, LIN>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax);
+  if (T.len - l0 > 64) {
+    run_slots<2, TWO, ENV, LIN>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax);
+    l0 += 128;
+  }
+  if (l0 < T.len) run_slots<1, TWO, ENV, LIN>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax);
   return tmax;
 }
 
@@ -165,8 +155,11 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank(
     const SgWTask* __restrict__ tasks, int64_t ntasks, const float* __restrict__ amps,
     const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, float* __restrict__ W,
     float* __restrict__ taskmax) {
+  __shared__ __attribute__((aligned(16))) float rows[4][2][SG_LDS_ROWS];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float* la = rows[wave][0];
+  float* ld = rows[wave][1];
   const int64_t tbase = (int64_t)blockIdx.x * SG_TASKS_PER_BLOCK;
 #pragma unroll 1
   for (int q = wave; q < SG_TASKS_PER_BLOCK; q += 4) {
@@ -175,11 +168,14 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank(
     const SgWTask T = tasks[ti];
     float tmax;
     if (T.flags & SG_TASK_ENV)  // amplAnchors envelope: rare, kept out of the hot variants
-      tmax = (T.flags & SG_TASK_CONST) ? run_task<false, true>(T, amps, syls, cknots, W, lane)
-                                       : run_task<true, true>(T, amps, syls, cknots, W, lane);
+      tmax = (T.flags & SG_TASK_CONST) ? run_task<false, true, false>(T, la, ld, amps, syls, cknots, W, lane)
+                                       : run_task<true, true, false>(T, la, ld, amps, syls, cknots, W, lane);
+    else if (T.flags & SG_TASK_LIN)  // constant pitch over the phase segment
+      tmax = (T.flags & SG_TASK_CONST) ? run_task<false, false, true>(T, la, ld, amps, syls, cknots, W, lane)
+                                       : run_task<true, false, true>(T, la, ld, amps, syls, cknots, W, lane);
     else
-      tmax = (T.flags & SG_TASK_CONST) ? run_task<false, false>(T, amps, syls, cknots, W, lane)
-                                       : run_task<true, false>(T, amps, syls, cknots, W, lane);
+      tmax = (T.flags & SG_TASK_CONST) ? run_task<false, false, false>(T, la, ld, amps, syls, cknots, W, lane)
+                                       : run_task<true, false, false>(T, la, ld, amps, syls, cknots, W, lane);
     const float wm = wave_max(tmax);
     if (lane == 0) taskmax[ti] = wm;
   }
