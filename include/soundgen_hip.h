@@ -79,6 +79,25 @@ typedef struct sg_random {
   void* user;
 } sg_random;
 
+/* R's default random number generation (R 3.4.0: Mersenne-Twister,
+ * Inversion normals), so that a seeded call draws what
+ * `set.seed(seed); soundgen(...)` draws in R without R present. Replaces the
+ * R runtime's unif_rand / norm_rand / exp_rand / rgamma (src/main/RNG.c,
+ * src/nmath/{snorm,qnorm,sexp,rgamma}.c) reached by the reference through
+ * runif/rnorm/rgamma calls, e.g. R/source.R:111, :278, :349,
+ * R/utilities_math.R:212, :295, R/sourceSpectrum.R:384. sg_random_bind_rrng
+ * points an sg_random's callbacks at one generator (one stream, so R's
+ * interleaving of the draw kinds is kept). */
+typedef struct sg_rrng sg_rrng;
+int sg_rrng_create(int32_t seed, sg_rrng** out);  /* = set.seed(seed) */
+void sg_rrng_destroy(sg_rrng* g);
+void sg_rrng_set_seed(sg_rrng* g, int32_t seed);
+double sg_rrng_unif(sg_rrng* g);                  /* runif(1) */
+double sg_rrng_norm(sg_rrng* g);                  /* rnorm(1) */
+double sg_rrng_exp(sg_rrng* g);                   /* rexp(1) */
+double sg_rrng_gamma(sg_rrng* g, double shape, double scale); /* rgamma(1, shape, scale = scale) */
+void sg_random_bind_rrng(sg_random* r, sg_rrng* g);
+
 /* Formals of generateHarmonics(), R/source.R:173-205 (pitch and amplAnchors
  * are separate arguments). */
 typedef struct sg_harm_params {

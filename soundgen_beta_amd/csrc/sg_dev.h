@@ -90,6 +90,29 @@ struct SgPiece {
   SgTerm t[SG_MAX_TERMS];
 };
 
+// Finalize tile of the fast path (sg_harm_copy): `n` (<= SG_COPY_TILE) samples
+// of a syllable without envelope / drift lying in ONE piece that is either a
+// direct copy of the epoch waveform or zeros (crossFade's leading 0, 0):
+//   out[dst + q] = W[src + q] / max * fade(k0 + q)    (zeros: 0)
+// SG_COPY_VEC: source and destination 16-B aligned and n % 4 == 0 (float4 path).
+constexpr int SG_COPY_TILE = 2048;
+constexpr int SG_COPY_FS = 1;     // destination is the spectral scratch fs
+constexpr int SG_COPY_VEC = 2;
+constexpr int SG_COPY_ZERO = 4;
+struct SgCopyTile {
+  int64_t src;       // W offset of the first sample
+  int64_t dst;       // destination offset (output buffer, or fs with SG_COPY_FS)
+  int64_t k0;        // syllable-local index of the first sample (fades)
+  int64_t L;         // syllable length
+  int32_t n;
+  int32_t max_slot;
+  int32_t fade;
+  int32_t flags;
+  int32_t syl;
+  int32_t pad[3];
+};
+static_assert(sizeof(SgCopyTile) == 64, "SgCopyTile layout");
+
 // Smooth contour over L samples (getSmoothContour(), R/smoothContours.R):
 // kind 0 none(=1 after conversion), 1 flat, 2 seq(from,to), 3 fmm spline on
 // xout = seq.int(x0, x1, L); then clamp, then optional 2^(v/10).

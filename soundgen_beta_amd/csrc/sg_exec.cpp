@@ -19,7 +19,7 @@ constexpr size_t ALIGN = 256;
 size_t up(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
 struct Layout {
-  size_t segs, epochs, knots, amps, tasks, pieces, syls, syl_tiles, ptiles, cknots, W, taskmax, ptilemax, maxes, total;
+  size_t segs, epochs, knots, amps, tasks, pieces, syls, syl_tiles, copy_tiles, ptiles, cknots, W, taskmax, ptilemax, maxes, total;
   size_t geoms, frames, fgroups, olas, olatiles, olasegs, olatilemax, olamax, items, mixes, mixtiles, fl, fs;
   explicit Layout(const Batch& B) {
     size_t o = 0;
@@ -31,7 +31,8 @@ struct Layout {
     tasks = take(B.tasks.size() * sizeof(SgWTask));
     pieces = take(B.pieces.size() * sizeof(SgPiece));
     syls = take(B.syls.size() * sizeof(SgSyllable));
-    syl_tiles = take(B.syl_tiles.size() * sizeof(SgSylTile));
+    syl_tiles = take(B.fin_tiles.size() * sizeof(SgSylTile));
+    copy_tiles = take(B.copy_tiles.size() * sizeof(SgCopyTile));
     ptiles = take(B.ptiles.size() * sizeof(SgSylTile));
     cknots = take(B.cknots.size() * sizeof(double));
     W = take((size_t)B.w_total * sizeof(float));
@@ -56,7 +57,55 @@ struct Layout {
 };
 }  // namespace
 
+// Split the 1024-sample finalize tiles of syllables without envelope or
+// drift: the parts of a tile lying in direct or zero pieces go to the fast
+// kernel (sg_harm_copy; aligned direct runs merged up to SG_COPY_TILE); tiles
+// touching a crossfade (multi-term) piece, and every tile of a syllable with an
+// envelope or drift, keep the general kernel.
+static void split_finalize_tiles(Batch& B) {
+  B.fin_tiles.clear();
+  B.copy_tiles.clear();
+  for (const SgSylTile& t : B.syl_tiles) {
+    const SgSyllable& sy = B.syls[t.syl];
+    const int64_t end = std::min<int64_t>(t.k0 + 1024, sy.L);
+    const int pend = sy.piece0 + sy.npiece;
+    bool ok = sy.env.kind == 0 && sy.drift.nk == 0;
+    for (int p = t.piece; ok && p < pend && B.pieces[p].start < end; ++p) ok = B.pieces[p].nterms <= 0;
+    if (!ok) {
+      B.fin_tiles.push_back(t);
+      continue;
+    }
+    for (int p = t.piece; p < pend && B.pieces[p].start < end; ++p) {
+      const SgPiece& pc = B.pieces[p];
+      const int64_t a = std::max<int64_t>(t.k0, pc.start), b = std::min<int64_t>(end, pc.start + pc.len);
+      if (b <= a) continue;
+      SgCopyTile c{};
+      const bool zero = pc.nterms == 0;
+      c.src = zero ? 0 : pc.t[0].src + (a - pc.start);
+      c.dst = sy.out_off + a;
+      c.k0 = a;
+      c.L = sy.L;
+      c.n = (int32_t)(b - a);
+      c.max_slot = sy.max_slot;
+      c.fade = sy.fade;
+      c.syl = t.syl;
+      c.flags = (sy.dst_fs ? SG_COPY_FS : 0) | (zero ? SG_COPY_ZERO : 0) |
+                (!zero && (c.src & 3) == 0 && (c.dst & 3) == 0 && (c.n & 3) == 0 ? SG_COPY_VEC : 0);
+      if (!B.copy_tiles.empty()) {  // extend the previous aligned run
+        SgCopyTile& q = B.copy_tiles.back();
+        if ((q.flags & SG_COPY_VEC) && (c.flags & SG_COPY_VEC) && q.syl == c.syl && q.flags == c.flags &&
+            q.k0 + q.n == c.k0 && q.src + q.n == c.src && q.n + c.n <= SG_COPY_TILE) {
+          q.n += c.n;
+          continue;
+        }
+      }
+      B.copy_tiles.push_back(c);
+    }
+  }
+}
+
 void finalize_plan(Batch& B) {
+  split_finalize_tiles(B);
   B.ptiles.clear();
   for (size_t s = 0; s < B.syls.size(); ++s) {
     SgSyllable& sy = B.syls[s];
@@ -73,7 +122,7 @@ void finalize_plan(Batch& B) {
   int64_t total = 0;
   for (const SgSyllable& sy : B.syls) total += sy.L;
   const int K = (int)std::min<int64_t>(SG_SLICES, nsyl);
-  int64_t acc = 0, ft = 0;
+  int64_t acc = 0, ft = 0, ct = 0;
   int32_t s0 = 0;
   for (int32_t s = 0; s < nsyl; ++s) {
     acc += B.syls[s].L;
@@ -86,8 +135,11 @@ void finalize_plan(Batch& B) {
     c.p0 = B.syls[s0].ptile0;
     c.p1 = B.syls[s].ptile0 + B.syls[s].nptile;
     c.f0 = ft;
-    while (ft < (int64_t)B.syl_tiles.size() && B.syl_tiles[ft].syl <= s) ++ft;
+    while (ft < (int64_t)B.fin_tiles.size() && B.fin_tiles[ft].syl <= s) ++ft;
     c.f1 = ft;
+    c.c0 = ct;
+    while (ct < (int64_t)B.copy_tiles.size() && B.copy_tiles[ct].syl <= s) ++ct;
+    c.c1 = ct;
     B.slices.push_back(c);
     s0 = s + 1;
   }
@@ -119,6 +171,7 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   D.pieces = (SgPiece*)(a + L.pieces);
   D.syls = (SgSyllable*)(a + L.syls);
   D.syl_tiles = (SgSylTile*)(a + L.syl_tiles);
+  D.copy_tiles = (SgCopyTile*)(a + L.copy_tiles);
   D.ptiles = (SgSylTile*)(a + L.ptiles);
   D.cknots = (double*)(a + L.cknots);
   D.W = (float*)(a + L.W);
@@ -148,7 +201,8 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   cp(D.tasks, B.tasks.data(), B.tasks.size() * sizeof(SgWTask));
   cp(D.pieces, B.pieces.data(), B.pieces.size() * sizeof(SgPiece));
   cp(D.syls, B.syls.data(), B.syls.size() * sizeof(SgSyllable));
-  cp(D.syl_tiles, B.syl_tiles.data(), B.syl_tiles.size() * sizeof(SgSylTile));
+  cp(D.syl_tiles, B.fin_tiles.data(), B.fin_tiles.size() * sizeof(SgSylTile));
+  cp(D.copy_tiles, B.copy_tiles.data(), B.copy_tiles.size() * sizeof(SgCopyTile));
   cp(D.ptiles, B.ptiles.data(), B.ptiles.size() * sizeof(SgSylTile));
   cp(D.cknots, B.cknots.data(), B.cknots.size() * sizeof(double));
   cp(D.geoms, B.geoms.data(), B.geoms.size() * sizeof(SgFftGeom));
@@ -205,6 +259,7 @@ void device_execute(const Batch& B, DevicePlan& D, float* d_out, hipStream_t s, 
       HIPCHK(hipEventRecord(D.ev_slice[c], s));
       HIPCHK(hipStreamWaitEvent(s2, D.ev_slice[c], 0));
     }
+    launch_harm_copy(D, sl.c0, sl.c1 - sl.c0, d_out, s2);
     launch_harm_finalize(D, sl.f0, sl.f1 - sl.f0, d_out, s2);
   }
   if (two) {  // join

@@ -20,7 +20,8 @@ struct DevicePlan {
   SgWTask* tasks = nullptr;
   SgPiece* pieces = nullptr;
   SgSyllable* syls = nullptr;
-  SgSylTile* syl_tiles = nullptr;
+  SgSylTile* syl_tiles = nullptr;    // general-path finalize tiles (Batch::fin_tiles)
+  SgCopyTile* copy_tiles = nullptr;
   SgSylTile* ptiles = nullptr;
   double* cknots = nullptr;
   float* W = nullptr;
@@ -65,6 +66,7 @@ void launch_sine_bank(const DevicePlan& D, int64_t t0, int64_t n_tasks, hipStrea
 void launch_syl_max(const DevicePlan& D, int64_t s0, int64_t n_syls, hipStream_t s);
 void launch_piece_max(const DevicePlan& D, int64_t p0, int64_t n_ptiles, hipStream_t s);
 void launch_harm_finalize(const DevicePlan& D, int64_t f0, int64_t n_stiles, float* out, hipStream_t s);
+void launch_harm_copy(const DevicePlan& D, int64_t c0, int64_t n_ctiles, float* out, hipStream_t s);
 // sg_fft.hip
 void launch_fft_frames(const DevicePlan& D, int64_t g0, int64_t n_groups, int lds_bytes, hipStream_t s);
 void launch_stft_ola(const DevicePlan& D, int64_t s0, int64_t n_segs, int lds_bytes, hipStream_t s);

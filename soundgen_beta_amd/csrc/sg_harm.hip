@@ -30,7 +30,10 @@ using sgd::wave_max;
 // the two VALU ops of the recurrence. (A DPP row broadcast folded into the
 // v_sub measured 4.5 lane-instructions per (sample, row) on gfx950, VGPR/SGPR
 // operands 2.7 — tools/ubench/clenshaw_ubench.hip.)
-constexpr int SG_LDS_ROWS = 256;  // rows staged per wave; taller tasks stream 256-row chunks
+constexpr int SG_LDS_ROWS = 256;
+#ifndef SG_SINE_PERSIST
+#define SG_SINE_PERSIST 0  // build knob: > 0 = persistent grid of that many blocks per CU
+#endif  // rows staged per wave; taller tasks stream 256-row chunks
 
 template <bool TWO>
 __device__ __forceinline__ void stage_rows(float* __restrict__ la, float* __restrict__ ld, const float* __restrict__ A,
@@ -55,25 +58,42 @@ __device__ __forceinline__ void stage_rows(float* __restrict__ la, float* __rest
       }                                                               \
     }                                                                 \
   }
+#ifndef SG_ROWS_IT
+#define SG_ROWS_IT 8  // rows per loop iteration (build knob: 4 or 8)
+#endif
 template <int NS, bool TWO>
 __device__ __forceinline__ void clenshaw_lds(const float* __restrict__ la, const float* __restrict__ ld, int n,
                                              const float (&al)[NS], float (&b1)[NS], float (&b2)[NS],
                                              float (&e1)[NS], float (&e2)[NS]) {
-  int q = (n >> 2) - 1;
-  if (q < 0) return;
-  float4 A4 = *reinterpret_cast<const float4*>(la + 4 * q);
-  float4 D4 = TWO ? *reinterpret_cast<const float4*>(ld + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll 1
-  for (; q >= 0; --q) {
-    const int qn = q > 0 ? q - 1 : 0;  // next (lower) 4 rows, read ahead of their use
-    const float4 An = *reinterpret_cast<const float4*>(la + 4 * qn);
-    const float4 Dn = TWO ? *reinterpret_cast<const float4*>(ld + 4 * qn) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (SG_ROWS_IT == 8 && (n & 4)) {  // odd group of 4 on top
+    const float4 A4 = *reinterpret_cast<const float4*>(la + n - 4);
+    const float4 D4 = TWO ? *reinterpret_cast<const float4*>(ld + n - 4) : z4;
     SG_ROW(A4.w, D4.w)
     SG_ROW(A4.z, D4.z)
     SG_ROW(A4.y, D4.y)
     SG_ROW(A4.x, D4.x)
-    A4 = An;
-    D4 = Dn;
+    n -= 4;
+  }
+#pragma unroll 1
+  for (int r = n - SG_ROWS_IT; r >= 0; r -= SG_ROWS_IT) {
+    const float4 A4 = *reinterpret_cast<const float4*>(la + r + SG_ROWS_IT - 4);
+    const float4 D4 = TWO ? *reinterpret_cast<const float4*>(ld + r + SG_ROWS_IT - 4) : z4;
+    float4 A0 = z4, D0 = z4;
+    if (SG_ROWS_IT == 8) {
+      A0 = *reinterpret_cast<const float4*>(la + r);
+      if (TWO) D0 = *reinterpret_cast<const float4*>(ld + r);
+    }
+    SG_ROW(A4.w, D4.w)
+    SG_ROW(A4.z, D4.z)
+    SG_ROW(A4.y, D4.y)
+    SG_ROW(A4.x, D4.x)
+    if (SG_ROWS_IT == 8) {
+      SG_ROW(A0.w, D0.w)
+      SG_ROW(A0.z, D0.z)
+      SG_ROW(A0.y, D0.y)
+      SG_ROW(A0.x, D0.x)
+    }
   }
 }
 
@@ -160,11 +180,18 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank(
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float* la = rows[wave][0];
   float* ld = rows[wave][1];
+#if SG_SINE_PERSIST
+  // persistent waves: wave w of the grid takes tasks w, w + 4 gridDim.x, ...
+  const int64_t stride = (int64_t)gridDim.x * 4;
+#pragma unroll 1
+  for (int64_t ti = (int64_t)blockIdx.x * 4 + wave; ti < ntasks; ti += stride) {
+#else
   const int64_t tbase = (int64_t)blockIdx.x * SG_TASKS_PER_BLOCK;
 #pragma unroll 1
   for (int q = wave; q < SG_TASKS_PER_BLOCK; q += 4) {
     const int64_t ti = tbase + q;
     if (ti >= ntasks) break;
+#endif
     const SgWTask T = tasks[ti];
     float tmax;
     if (T.flags & SG_TASK_ENV)  // amplAnchors envelope: rare, kept out of the hot variants
@@ -243,6 +270,51 @@ __device__ __forceinline__ float fade_at(int lf, int64_t L, int64_t k) {
   return f;
 }
 
+// Fast path of the finalize (tiles from the planner's split, SgCopyTile):
+// one wavefront per tile of <= 2048 samples; aligned tiles keep eight float4
+// loads per lane in flight before any store; one dependent descriptor level
+// (tile -> data + max).
+extern "C" __global__ __launch_bounds__(256) void sg_harm_copy(const SgCopyTile* __restrict__ tiles, int64_t ntiles,
+                                                               const float* __restrict__ W,
+                                                               const float* __restrict__ maxes,
+                                                               float* __restrict__ out_buf, float* __restrict__ fs) {
+  const int lane = threadIdx.x & 63;
+  const int64_t ti = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (ti >= ntiles) return;
+  const SgCopyTile T = tiles[ti];
+  const float* __restrict__ src = W + T.src;
+  float* __restrict__ dst = ((T.flags & SG_COPY_FS) ? fs : out_buf) + T.dst;
+  const float inv_max = 1.f / maxes[T.max_slot];
+  constexpr int E = SG_COPY_TILE / 256;
+  if (T.flags & SG_COPY_VEC) {
+    float4 v[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+      if (256 * e + 4 * lane < T.n) v[e] = *reinterpret_cast<const float4*>(src + 256 * e + 4 * lane);
+    const bool ramp = T.fade >= 2 && (T.k0 < T.fade || T.k0 + T.n > T.L - T.fade);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      if (256 * e + 4 * lane >= T.n) break;
+      v[e].x *= inv_max; v[e].y *= inv_max; v[e].z *= inv_max; v[e].w *= inv_max;
+      if (ramp) {
+        const int64_t k = T.k0 + 256 * e + 4 * lane;
+        v[e].x *= fade_at(T.fade, T.L, k); v[e].y *= fade_at(T.fade, T.L, k + 1);
+        v[e].z *= fade_at(T.fade, T.L, k + 2); v[e].w *= fade_at(T.fade, T.L, k + 3);
+      }
+      *reinterpret_cast<float4*>(dst + 256 * e + 4 * lane) = v[e];
+    }
+  } else {  // misaligned or short runs, zero pieces
+    const bool zero = T.flags & SG_COPY_ZERO;
+    for (int q = lane; q < T.n; q += 64) {
+      float v = zero ? 0.f : src[q] * inv_max;
+      if (T.fade >= 2) v *= fade_at(T.fade, T.L, T.k0 + q);
+      dst[q] = v;
+    }
+  }
+}
+
+// General path: the tiles the planner did not give to sg_harm_copy (crossfade
+// pieces, amplitude envelope, drift, misaligned slots).
 extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize(
     const SgSylTile* __restrict__ stiles, const SgPiece* __restrict__ pieces, const SgSyllable* __restrict__ syls,
     const double* __restrict__ cknots, const float* __restrict__ W, const float* __restrict__ maxes,
@@ -361,7 +433,13 @@ namespace sg {
 
 void launch_sine_bank(const DevicePlan& D, int64_t t0, int64_t n_tasks, hipStream_t s) {
   if (n_tasks <= 0) return;
+#if SG_SINE_PERSIST
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const int64_t blocks = std::min<int64_t>((n_tasks + 3) / 4, (int64_t)ncu * SG_SINE_PERSIST);
+#else
   const int64_t blocks = (n_tasks + SG_TASKS_PER_BLOCK - 1) / SG_TASKS_PER_BLOCK;
+#endif
   hipLaunchKernelGGL(sg_sine_bank, dim3((unsigned)blocks), dim3(256), 0, s, D.tasks + t0, n_tasks, D.amps, D.syls,
                      D.cknots, D.W, D.taskmax + t0);
   SG_LAUNCHED("sg_sine_bank");
@@ -377,6 +455,12 @@ void launch_syl_max(const DevicePlan& D, int64_t s0, int64_t n_syls, hipStream_t
   hipLaunchKernelGGL(sg_syl_max, dim3((unsigned)n_syls), dim3(256), 0, s, D.syls + s0, D.taskmax, D.ptilemax,
                      D.maxes);
   SG_LAUNCHED("sg_syl_max");
+}
+void launch_harm_copy(const DevicePlan& D, int64_t c0, int64_t n_ctiles, float* out, hipStream_t s) {
+  if (n_ctiles <= 0) return;
+  hipLaunchKernelGGL(sg_harm_copy, dim3((unsigned)((n_ctiles + 3) / 4)), dim3(256), 0, s, D.copy_tiles + c0, n_ctiles, D.W,
+                     D.maxes, out, D.fs);
+  SG_LAUNCHED("sg_harm_copy");
 }
 void launch_harm_finalize(const DevicePlan& D, int64_t f0, int64_t n_stiles, float* out, hipStream_t s) {
   if (n_stiles <= 0) return;

@@ -22,7 +22,8 @@ struct Slice {
   int64_t t0, t1;    // sine-bank tasks
   int32_t p0, p1;    // crossfade-piece max tiles
   int32_t s0, s1;    // syllables
-  int64_t f0, f1;    // finalize tiles
+  int64_t f0, f1;    // finalize tiles (general path, fin_tiles)
+  int64_t c0, c1;    // finalize tiles (fast path, copy_tiles)
 };
 
 struct Batch {
@@ -35,6 +36,8 @@ struct Batch {
   std::vector<SgPiece> pieces;
   std::vector<SgSyllable> syls;
   std::vector<SgSylTile> syl_tiles;
+  std::vector<SgSylTile> fin_tiles;    // derived (finalize_plan): syl_tiles the fast path does not take
+  std::vector<SgCopyTile> copy_tiles;  // derived (finalize_plan): fast-path finalize tiles
   std::vector<SgSylTile> ptiles;   // tiles over multi-term (crossfade) pieces
   std::vector<Slice> slices;
   // ---- spectral part (noise, formant filter, assembly) ----

@@ -70,6 +70,15 @@ def lib():
     L.sg_profile_read.argtypes = [vp, dp, i64p]
     L.sg_profile_read_kernel.argtypes = [vp, C.c_int, dp, i64p]
     L.sg_plan_stft_stats.argtypes = [vp, i64p, i64p, dp]
+    L.sg_rrng_create.argtypes = [C.c_int32, C.POINTER(vp)]
+    L.sg_rrng_destroy.argtypes = [vp]
+    L.sg_rrng_set_seed.argtypes = [vp, C.c_int32]
+    for f in ("unif", "norm", "exp"):
+        getattr(L, "sg_rrng_" + f).argtypes = [vp]
+        getattr(L, "sg_rrng_" + f).restype = C.c_double
+    L.sg_rrng_gamma.argtypes = [vp, C.c_double, C.c_double]
+    L.sg_rrng_gamma.restype = C.c_double
+    L.sg_random_bind_rrng.argtypes = [C.POINTER(_abi.sg_random), vp]
     L.sg_plan_kernel_stats.argtypes = [vp, i64p, i64p, i64p, i64p]
     L.sg_synchronize.argtypes = [vp]
     L.sg_execute_to_host.argtypes = [vp, vp, dp]

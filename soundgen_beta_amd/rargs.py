@@ -231,7 +231,10 @@ class Holder:
         if uniforms is not None:
             u = self.arr(uniforms)
             r.uniforms, r.n_uniforms = _abi.dptr(u), len(u)
-        if rng is not None:
+        if rng is not None and hasattr(rng, "bind"):  # RRng: native callbacks into the library
+            rng.bind(r)
+            self.keep.append(rng)
+        elif rng is not None:
             cbs = (_abi.NORM_CB(lambda _u: float(rng.standard_normal())),
                    _abi.UNIF_CB(lambda _u: float(rng.random())),
                    _abi.GAMMA_CB(lambda _u, shape, rate: float(rng.gamma(shape, 1.0 / rate))))
