@@ -52,7 +52,7 @@ constexpr int SG_ROW_CHUNK = 4;   // amplitude rows per ds_read_b128 (R padded t
 constexpr int SG_TASK_CONST = 1;  // columns equal over the task: A chain only
 constexpr int SG_TASK_ENV = 4;    // the syllable has an amplitude envelope (max taken after it)
 constexpr int SG_TASK_LIN = 2;    // phase segment linear (c2 = c3 = c4 = 0): one fp64 FMA per sample
-constexpr int SG_TASK_MAX = 512;  // samples per task (8 slots of 64 lanes)
+constexpr int SG_TASK_MAX = 1024;  // samples per task (16 slots of 64 lanes)
 struct SgWTask {
   int64_t w_off;       // W offset of epoch sample 0
   int64_t a_off;       // float offset of A[i][0..R)

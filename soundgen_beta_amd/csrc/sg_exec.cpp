@@ -2,6 +2,8 @@
 #include "sg_exec.h"
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <string>
 
@@ -106,6 +108,9 @@ static void split_finalize_tiles(Batch& B) {
 
 void finalize_plan(Batch& B) {
   split_finalize_tiles(B);
+  if (std::getenv("SG_DEBUG_PLAN"))
+    std::fprintf(stderr, "sg plan: %zu sine tasks, %zu syllables, %zu copy tiles, %zu general finalize tiles\n",
+                 B.tasks.size(), B.syls.size(), B.copy_tiles.size(), B.fin_tiles.size());
   B.ptiles.clear();
   for (size_t s = 0; s < B.syls.size(); ++s) {
     SgSyllable& sy = B.syls[s];
@@ -121,7 +126,9 @@ void finalize_plan(Batch& B) {
   if (nsyl == 0) return;
   int64_t total = 0;
   for (const SgSyllable& sy : B.syls) total += sy.L;
-  const int K = (int)std::min<int64_t>(SG_SLICES, nsyl);
+  int slices = SG_SLICES;
+  if (const char* e = std::getenv("SG_SLICES")) slices = std::max(1, std::atoi(e));  // experiment knob
+  const int K = (int)std::min<int64_t>(slices, nsyl);
   int64_t acc = 0, ft = 0, ct = 0;
   int32_t s0 = 0;
   for (int32_t s = 0; s < nsyl; ++s) {

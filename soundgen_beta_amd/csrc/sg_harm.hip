@@ -1,7 +1,7 @@
 // sg_harm.hip — gfx950 kernels of the additive harmonic source
 // (generateHarmonics(), R/source.R:377-467).
 //
-// sg_sine_bank: one wave task = up to 512 consecutive samples of one epoch
+// sg_sine_bank: one wave task = up to SG_TASK_MAX (1024) consecutive samples of one epoch
 // inside ONE amplitude interval (the approx() knots x_i, x_{i+1}, R/source.R:403-405),
 // so both amplitude columns A[i][.], dA[i][.] = A[i+1][.] - A[i][.] are wave-uniform
 // (staged in the wave's LDS slice, read back as broadcasts):
@@ -31,6 +31,9 @@ using sgd::wave_max;
 // v_sub measured 4.5 lane-instructions per (sample, row) on gfx950, VGPR/SGPR
 // operands 2.7 — tools/ubench/clenshaw_ubench.hip.)
 constexpr int SG_LDS_ROWS = 256;
+#ifndef SG_NS_MAX
+#define SG_NS_MAX 8  // build knob: largest slot pass (8 or 4)
+#endif
 #ifndef SG_SINE_PERSIST
 #define SG_SINE_PERSIST 0  // build knob: > 0 = persistent grid of that many blocks per CU
 #endif  // rows staged per wave; taller tasks stream 256-row chunks
@@ -160,7 +163,13 @@ __device__ __forceinline__ float run_task(const SgWTask& T, float* __restrict__ 
   if (staged) stage_rows<TWO>(la, ld, amps + T.a_off, amps + T.d_off, 0, T.R, lane);
   float tmax = 0.f;
   int l0 = 0;
-  // passes of 4 / 2 / 1 slots of 64 samples (a task has <= 8 slots)
+  // passes of 8 / 4 / 2 / 1 slots of 64 samples (8-slot passes on the A chain
+  // only: with the dA chain they exceed the VGPR budget)
+  if (!TWO && SG_NS_MAX >= 8) {
+#pragma unroll 1
+    for (; T.len - l0 > 448; l0 += 512)
+      run_slots<8, TWO, ENV, LIN>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax);
+  }
 #pragma unroll 1
   for (; T.len - l0 > 192; l0 += 256) run_slots<4, TWO, ENV, LIN>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax);
   if (T.len - l0 > 64) {

@@ -9,6 +9,7 @@
 // bank, the crossfades, normalisation, fades, envelopes — runs on the GPU.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "sg_loess.h"
@@ -540,6 +541,24 @@ static void cross_fade(Chain& A, const HostEpoch& W, int64_t e, double sr, doubl
 }
 
 // ----------------------------------------------------------- planner
+// samples per sine-bank task (SG_TASK_MAX; SG_TASK_MAX env override for experiments)
+static int64_t task_max() {
+  static const int64_t v = [] {
+    const char* e = std::getenv("SG_TASK_MAX");
+    const long x = e ? std::atol(e) : 0;
+    return (int64_t)(x >= 64 ? x : SG_TASK_MAX);
+  }();
+  return v;
+}
+
+// segment b continues segment a's line: both linear, same slope, and b's
+// offset equals a's line at b's start (to rounding)
+static bool lin_continues(const SgSeg& a, const SgSeg& b) {
+  if (a.c2 != 0 || a.c3 != 0 || a.c4 != 0 || b.c2 != 0 || b.c3 != 0 || b.c4 != 0 || a.c1 != b.c1) return false;
+  const double at = a.c0 + a.c1 * (b.t0 - a.t0);
+  return std::fabs(at - b.c0) <= 1e-12 * std::max(1.0, std::fabs(b.c0));
+}
+
 int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_harm_params& P,
                        const sg_anchors& amplAnchors, Rng& R, int64_t out_off, bool dry_run, bool to_fs,
                        int64_t* fs_off) {
@@ -833,9 +852,15 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
       for (int64_t j0 = ja; j0 < jend;) {
         const double u = (double)(he.u0 + j0);
         while (k + 1 < nseg && HS.segs[k + 1].t0 < u) ++k;
-        int64_t len = std::min<int64_t>(SG_TASK_MAX, jend - j0);
-        if (k + 1 < nseg) {  // stay inside segment k: u <= t0[k+1]
-          const int64_t jmax = (int64_t)HS.segs[k + 1].t0 - he.u0 + 1;
+        int64_t len = std::min<int64_t>(task_max(), jend - j0);
+        // a linear segment continues through the following segments that lie
+        // on the same line (constant pitch: one FMM piece per glottal cycle,
+        // all with equal slope), so a task may span them with segment k's
+        // coefficients; phase drift from the merge stays ~1e-12 cycles
+        int64_t kk = k;
+        while (kk + 1 < nseg && lin_continues(B.segs[seg_off + kk], B.segs[seg_off + kk + 1])) ++kk;
+        if (kk + 1 < nseg) {  // stay inside segments k..kk: u <= t0[kk+1]
+          const int64_t jmax = (int64_t)HS.segs[kk + 1].t0 - he.u0 + 1;
           if (j0 + len > jmax) len = jmax - j0;
         }
         const SgSeg& S = B.segs[seg_off + k];
