@@ -47,7 +47,7 @@ constexpr int SG_ROW_CHUNK = 4;   // amplitude rows per ds_read_b128 (R padded t
 // fall in one amplitude interval [knot i, knot i+1] (or in a run of intervals
 // whose columns are equal, flag CONST). Everything the wave needs is in this
 // record (wave-uniform scalar loads):
-//   sample l = j - j0:  m = mbase + l,  integr/D = (c0 + m(c1 + m(c2 + m(c3 + m c4)))) * invD
+//   sample l = j - j0:  m = mbase + l,  integr/D = c0 + m(c1 + m(c2 + m(c3 + m c4)))  (1/D folded in)
 //                       t = (tc0 + l * xby) * rdx   (approx() weight inside the interval)
 constexpr int SG_TASK_CONST = 1;  // columns equal over the task: A chain only
 constexpr int SG_TASK_ENV = 4;    // the syllable has an amplitude envelope (max taken after it)
@@ -58,7 +58,7 @@ struct SgWTask {
   int64_t a_off;       // float offset of A[i][0..R)
   int64_t d_off;       // float offset of dA[i][0..R) = A[i+1] - A[i]
   int64_t dk0;         // syllable sample (0-based) of epoch sample 0
-  double c0, c1, c2, c3, c4;  // phase segment, see SgSeg
+  double c0, c1, c2, c3, c4;  // phase segment (see SgSeg) times invD
   double invD;         // 1 / (nSubharm + 1)
   float rdx, tc0, xby;
   int32_t mbase;       // u(j0) - t0 of the segment
@@ -90,12 +90,13 @@ struct SgPiece {
   SgTerm t[SG_MAX_TERMS];
 };
 
-// Finalize tile of the fast path (sg_harm_copy): `n` (<= SG_COPY_TILE) samples
+// Finalize tile of the fast path (sg_harm_copy): `n` (<= SG_COPY_TILE_MAX) samples
 // of a syllable without envelope / drift lying in ONE piece that is either a
 // direct copy of the epoch waveform or zeros (crossFade's leading 0, 0):
 //   out[dst + q] = W[src + q] / max * fade(k0 + q)    (zeros: 0)
 // SG_COPY_VEC: source and destination 16-B aligned and n % 4 == 0 (float4 path).
-constexpr int SG_COPY_TILE = 2048;
+constexpr int SG_COPY_TILE = 2048;      // planner's merge target
+constexpr int SG_COPY_TILE_MAX = 4096;  // kernel limit (16 float4 per lane)
 constexpr int SG_COPY_FS = 1;     // destination is the spectral scratch fs
 constexpr int SG_COPY_VEC = 2;
 constexpr int SG_COPY_ZERO = 4;

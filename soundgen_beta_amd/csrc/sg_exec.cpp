@@ -65,6 +65,8 @@ struct Layout {
 // touching a crossfade (multi-term) piece, and every tile of a syllable with an
 // envelope or drift, keep the general kernel.
 static void split_finalize_tiles(Batch& B) {
+  int64_t copy_tile = SG_COPY_TILE;
+  if (const char* e = std::getenv("SG_COPY_TILE")) copy_tile = std::min<int64_t>(SG_COPY_TILE_MAX, std::max(1024, std::atoi(e)));
   B.fin_tiles.clear();
   B.copy_tiles.clear();
   for (const SgSylTile& t : B.syl_tiles) {
@@ -96,7 +98,7 @@ static void split_finalize_tiles(Batch& B) {
       if (!B.copy_tiles.empty()) {  // extend the previous aligned run
         SgCopyTile& q = B.copy_tiles.back();
         if ((q.flags & SG_COPY_VEC) && (c.flags & SG_COPY_VEC) && q.syl == c.syl && q.flags == c.flags &&
-            q.k0 + q.n == c.k0 && q.src + q.n == c.src && q.n + c.n <= SG_COPY_TILE) {
+            q.k0 + q.n == c.k0 && q.src + q.n == c.src && q.n + c.n <= copy_tile) {
           q.n += c.n;
           continue;
         }

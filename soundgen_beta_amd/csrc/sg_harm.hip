@@ -6,7 +6,7 @@
 // so both amplitude columns A[i][.], dA[i][.] = A[i+1][.] - A[i][.] are wave-uniform
 // (staged in the wave's LDS slice, read back as broadcasts):
 //   integr(u)  closed-form quartic prefix sum of the FMM pitch spline (fp64, Horner)
-//   theta      = 2*pi*frac(integr / D)
+//   theta      = 2*pi*frac(integr / D)   (1/D folded into the coefficients by the planner)
 //   W(j)       = sum_r (A_r + t_j dA_r) sin(r theta)             (R/source.R:396-419)
 //              = (b_1 + t_j e_1) sin(theta)  by Clenshaw's recurrence
 //                b_r = A_r + 2cos(theta) b_{r+1} - b_{r+2}  (2 VALU ops per row and chain)
@@ -109,7 +109,7 @@ __device__ __forceinline__ void sample_setup(const SgWTask& T, int l, float& t, 
   t = TWO ? fmaf((float)l, T.xby, T.tc0) * T.rdx : 0.f;
   const double m = (double)(T.mbase + l);
   const double P = LIN ? fma(m, T.c1, T.c0) : fma(m, fma(m, fma(m, fma(m, T.c4, T.c3), T.c2), T.c1), T.c0);
-  const double v = P * T.invD;
+  const double v = P;  // cycles of 1/D (planner folds 1/D into the coefficients)
   const float x = (float)(v - rint(v));
   sn = __builtin_amdgcn_sinf(x);
   al = 2.f * __builtin_amdgcn_cosf(x);
@@ -280,8 +280,8 @@ __device__ __forceinline__ float fade_at(int lf, int64_t L, int64_t k) {
 }
 
 // Fast path of the finalize (tiles from the planner's split, SgCopyTile):
-// one wavefront per tile of <= 2048 samples; aligned tiles keep eight float4
-// loads per lane in flight before any store; one dependent descriptor level
+// one wavefront per tile of <= SG_COPY_TILE_MAX samples; aligned tiles keep up to
+// sixteen float4 loads per lane in flight before any store; one dependent descriptor level
 // (tile -> data + max).
 extern "C" __global__ __launch_bounds__(256) void sg_harm_copy(const SgCopyTile* __restrict__ tiles, int64_t ntiles,
                                                                const float* __restrict__ W,
@@ -294,7 +294,7 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_copy(const SgCopyTile*
   const float* __restrict__ src = W + T.src;
   float* __restrict__ dst = ((T.flags & SG_COPY_FS) ? fs : out_buf) + T.dst;
   const float inv_max = 1.f / maxes[T.max_slot];
-  constexpr int E = SG_COPY_TILE / 256;
+  constexpr int E = SG_COPY_TILE_MAX / 256;
   if (T.flags & SG_COPY_VEC) {
     float4 v[E];
 #pragma unroll

@@ -869,7 +869,10 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
         T.a_off = ep.amp_off + i * ep.R;
         T.d_off = ep.da_off + i * ep.R;
         T.dk0 = ep.dk0;
-        T.c0 = S.c0; T.c1 = S.c1; T.c2 = S.c2; T.c3 = S.c3; T.c4 = S.c4;
+        // phase in cycles of the epoch's lowest multiplier: integr / D folded into the
+        // coefficients (the device evaluates the polynomial only)
+        T.c0 = S.c0 * ep.invD; T.c1 = S.c1 * ep.invD; T.c2 = S.c2 * ep.invD; T.c3 = S.c3 * ep.invD;
+        T.c4 = S.c4 * ep.invD;
         T.invD = ep.invD;
         T.rdx = (float)(1.0 / (he.knots[i + 1] - he.knots[i]));
         T.tc0 = (float)(r_seqint_at(he.knots.front(), he.knots.back(), he.n, j0) - he.knots[i]);
