@@ -70,7 +70,9 @@ struct SgWTask {
   int32_t pad;
 };
 static_assert(sizeof(SgWTask) == 128, "SgWTask layout");
-constexpr int SG_TASKS_PER_BLOCK = 8;  // 4 waves x 2 tasks
+#ifndef SG_TASKS_PER_BLOCK
+#define SG_TASKS_PER_BLOCK 4  // 4 waves x 1 task (build knob; measured better than 2 per wave)
+#endif
 // batch slices of the sine-bank / finalize pipeline; measured on MI355X (C2): 4 slices
 // on two streams ran 0.41 ms/step against 0.32 for one (both kernels slowed when
 // co-resident), so the default is a single slice
