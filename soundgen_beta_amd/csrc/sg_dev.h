@@ -277,7 +277,7 @@ struct SgMix {
   float am_dep, pad;
   SgContour mult;     // amplAnchorsGlobal envelope (kind 0: none)
 };
-constexpr int SG_MIX_TILE = 1024;
+constexpr int SG_MIX_TILE = 8192;  // samples per sg_mix workgroup (chunks of 1024: descriptors loaded once)
 struct SgMixTile {
   int32_t mix, pad;
   int64_t k0;

@@ -877,27 +877,59 @@ extern "C" __global__ __launch_bounds__(256) void sg_mix(const SgMixTile* __rest
   const SgMixTile T = tiles[blockIdx.x];
   const SgMix& X = mixes[T.mix];
   float* __restrict__ dst = X.to_fs ? fs : out;
-  for (int e = 0; e < SG_MIX_TILE / 256; ++e) {
-    const int64_t k = T.k0 + e * 256 + threadIdx.x;
-    if (k >= X.len) break;
-    float v = 0.f;
-    if (X.base_kind != SG_BASE_NONE && k < X.base_len) {
-      v = fs[X.base + k];
-      if (X.base_kind == SG_BASE_NORM) v = v / olamax[X.base_ola];
+  constexpr int E = 4;  // samples per thread and chunk
+  const int64_t kend = T.k0 + SG_MIX_TILE < X.len ? T.k0 + SG_MIX_TILE : X.len;
+  // per-tile constants, hoisted out of the sample loops (one scalar-load burst)
+  const float base_scale = X.base_kind == SG_BASE_NORM ? 1.f / olamax[X.base_ola] : 1.f;
+  const bool has_base = X.base_kind != SG_BASE_NONE;
+#pragma unroll 1
+  for (int64_t kc = T.k0; kc < kend; kc += E * 256) {
+    float v[E];
+    // loads are unconditional (clamped addresses), selects afterwards: a load
+    // under a branch is followed by its own vmcnt(0) wait, serialising the chunk
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int64_t k = kc + e * 256 + threadIdx.x;
+      const bool in = has_base && k < kend && k < X.base_len;
+      const float x = fs[X.base + (in ? k : 0)];
+      v[e] = in ? x * base_scale : 0.f;
     }
+    // noise items: descriptor once per chunk, then its samples (addVectors)
     for (int i = 0; i < X.nitems; ++i) {
       const SgNoiseItem& it = items[X.item0 + i];
-      const int64_t j = k - it.off;
-      if (j < 0 || j >= it.len) continue;
-      float nv = fs[it.raw + j];
-      if (it.ola >= 0) nv = nv / olamax[it.ola];
-      if (it.strength.kind != 0) nv = (float)((double)nv * contour_at(it.strength, cknots, it.len, j));
-      nv *= fade_in_out(it.fade, it.len, j);
-      v += nv;
+      const int64_t j0 = kc + threadIdx.x - it.off;
+      if (j0 + (E - 1) * 256 < 0 || j0 >= it.len) continue;  // no sample of this thread in the item
+      const float nscale = it.ola >= 0 ? 1.f / olamax[it.ola] : 1.f;
+      const bool flat = it.strength.kind == 1;
+      const float sflat = flat ? (float)contour_at(it.strength, cknots, it.len, 0) : 1.f;
+      float raw[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int64_t j = j0 + e * 256;
+        raw[e] = fs[it.raw + (j < 0 ? 0 : (j >= it.len ? it.len - 1 : j))];
+      }
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int64_t k = kc + e * 256 + threadIdx.x, j = j0 + e * 256;
+        if (k >= kend || j < 0 || j >= it.len) continue;
+        float nv = raw[e] * nscale;
+        if (flat) nv *= sflat;
+        else if (it.strength.kind != 0) nv = (float)((double)nv * contour_at(it.strength, cknots, it.len, j));
+        nv *= fade_in_out(it.fade, it.len, j);
+        v[e] += nv;
+      }
     }
-    if (X.mult.kind != 0) v = (float)((double)v * contour_at(X.mult, cknots, X.len, k));
-    if (X.am_lo > 0) v *= 1.f - sigmoid_at(fl + X.am_tab, X.am_lo, k) * X.am_dep / 100.f;
-    dst[X.dst + k] = v;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int64_t k = kc + e * 256 + threadIdx.x;
+      if (X.mult.kind != 0) v[e] = (float)((double)v[e] * contour_at(X.mult, cknots, X.len, k));
+      if (X.am_lo > 0) v[e] *= 1.f - sigmoid_at(fl + X.am_tab, X.am_lo, k) * X.am_dep / 100.f;
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int64_t k = kc + e * 256 + threadIdx.x;
+      if (k < kend) dst[X.dst + k] = v[e];
+    }
   }
 }
 

@@ -324,42 +324,15 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_copy(const SgCopyTile*
 
 // General path: the tiles the planner did not give to sg_harm_copy (crossfade
 // pieces, amplitude envelope, drift, misaligned slots).
-extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize(
-    const SgSylTile* __restrict__ stiles, const SgPiece* __restrict__ pieces, const SgSyllable* __restrict__ syls,
-    const double* __restrict__ cknots, const float* __restrict__ W, const float* __restrict__ maxes,
-    float* __restrict__ out_buf, float* __restrict__ fs) {
-  const SgSylTile tl = stiles[blockIdx.x];
+__device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece* __restrict__ pieces,
+                                              const SgSyllable* __restrict__ syls, const double* __restrict__ cknots,
+                                              const float* __restrict__ W, const float* __restrict__ maxes,
+                                              float* __restrict__ out_buf, float* __restrict__ fs) {
   const SgSyllable& sy = syls[tl.syl];
   float* __restrict__ out = sy.dst_fs ? fs : out_buf;
   const float inv_max = 1.f / maxes[sy.max_slot];
   const int pend = sy.piece0 + sy.npiece;
-  const int64_t kt = tl.k0 + 4 * (int64_t)threadIdx.x;
   const int64_t tile_end = tl.k0 + 1024 < sy.L ? tl.k0 + 1024 : sy.L;
-  const SgPiece& p0 = pieces[tl.piece];
-  const bool simple = sy.env.kind == 0 && sy.drift.nk == 0;
-  // fast path: whole tile inside one direct piece, aligned, no env/drift
-  if (simple && p0.nterms < 0 && p0.start <= tl.k0 && p0.start + p0.len >= tile_end &&
-      ((sy.out_off + tl.k0) & 3) == 0 && ((p0.t[0].src + (tl.k0 - p0.start)) & 3) == 0) {
-    if (kt >= tile_end) return;
-    const float* src = W + p0.t[0].src + (kt - p0.start);
-    float* dst = out + sy.out_off + kt;
-    if (kt + 4 <= tile_end) {
-      float4 v = *reinterpret_cast<const float4*>(src);
-      v.x *= inv_max; v.y *= inv_max; v.z *= inv_max; v.w *= inv_max;
-      if (sy.fade >= 2 && (kt < sy.fade || kt + 4 > sy.L - sy.fade)) {
-        v.x *= fade_at(sy.fade, sy.L, kt); v.y *= fade_at(sy.fade, sy.L, kt + 1);
-        v.z *= fade_at(sy.fade, sy.L, kt + 2); v.w *= fade_at(sy.fade, sy.L, kt + 3);
-      }
-      *reinterpret_cast<float4*>(dst) = v;
-    } else {
-      for (int64_t k = kt; k < tile_end; ++k) {
-        float v = src[k - kt] * inv_max;
-        if (sy.fade >= 2) v *= fade_at(sy.fade, sy.L, k);
-        dst[k - kt] = v;
-      }
-    }
-    return;
-  }
   // general path: wave w owns samples [k0 + 256 w, +256), lane l takes
   // c0 + 64 e + l (coalesced). The planner gives each wave the piece and the
   // drift-knot interval of its first sample; up to 8 knots from there are
@@ -369,11 +342,11 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize(
   const int64_t c0 = tl.k0 + 256 * wv;
   if (c0 >= tile_end) return;
   const int64_t c1 = c0 + 256 < tile_end ? c0 + 256 : tile_end;
-  const int pu = stiles[blockIdx.x].wpiece[wv];
+  const int pu = tl.wpiece[wv];
   const bool one_piece = pu + 1 >= pend || pieces[pu + 1].start >= c1;
   const SgLinear dr = sy.drift;
   const bool drift = dr.nk > 1;
-  const int d0 = stiles[blockIdx.x].wdrift[wv];
+  const int d0 = tl.wdrift[wv];
   constexpr int KW = 8;
   double xs[KW], ys[KW];
   bool local_knots = false;
@@ -395,9 +368,11 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize(
     local_knots = d0 + KW - 1 >= dr.nk - 1 || u_at(c1 - 1) < xs[KW - 1];
   }
   int p = pu, di = d0;
+  float res[4];  // every load of the chunk before its stores
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int64_t k = c0 + 64 * e + lane;
+    res[e] = 0.f;
     if (k >= c1) break;
     float x;
     if (one_piece) {
@@ -427,7 +402,27 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize(
     } else if (dr.nk == 1) {
       x = (float)((double)x * cknots[dr.k_off + 1]);
     }
-    out[sy.out_off + k] = x;
+    res[e] = x;
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int64_t k = c0 + 64 * e + lane;
+    if (k < c1) out[sy.out_off + k] = res[e];
+  }
+}
+
+// SG_FIN_TILES consecutive 1024-sample tiles per workgroup: the descriptor
+// chain (tile -> syllable -> piece, drift knots) of a syllable's next tile hits cache
+constexpr int SG_FIN_TILES = 4;
+extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize(
+    const SgSylTile* __restrict__ stiles, int64_t ntiles, const SgPiece* __restrict__ pieces,
+    const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, const float* __restrict__ W,
+    const float* __restrict__ maxes, float* __restrict__ out_buf, float* __restrict__ fs) {
+#pragma unroll 1
+  for (int i = 0; i < SG_FIN_TILES; ++i) {
+    const int64_t t = (int64_t)blockIdx.x * SG_FIN_TILES + i;
+    if (t >= ntiles) break;
+    finalize_tile(stiles[t], pieces, syls, cknots, W, maxes, out_buf, fs);
   }
 }
 
@@ -473,7 +468,8 @@ void launch_harm_copy(const DevicePlan& D, int64_t c0, int64_t n_ctiles, float* 
 }
 void launch_harm_finalize(const DevicePlan& D, int64_t f0, int64_t n_stiles, float* out, hipStream_t s) {
   if (n_stiles <= 0) return;
-  hipLaunchKernelGGL(sg_harm_finalize, dim3((unsigned)n_stiles), dim3(256), 0, s, D.syl_tiles + f0, D.pieces, D.syls,
+  hipLaunchKernelGGL(sg_harm_finalize, dim3((unsigned)((n_stiles + SG_FIN_TILES - 1) / SG_FIN_TILES)), dim3(256), 0, s,
+                     D.syl_tiles + f0, n_stiles, D.pieces, D.syls,
                      D.cknots, D.W, D.maxes, out, D.fs);
   SG_LAUNCHED("sg_harm_finalize");
 }
