@@ -241,6 +241,8 @@ struct SgSegment {
 constexpr int SG_SEG_FIRST = 1;
 constexpr int SG_SEG_LAST = 2;
 constexpr int SG_SEG_FRAMES = 48;   // target frames owned per segment (one wavefront each)
+constexpr int SG_SEG_MIN_FRAMES = 8;  // shortest segment the planner picks (3 recomputed frames each)
+constexpr int64_t SG_RESIDENT_WAVES = 256 * SG_FFT_WAVES;  // sg_stft_ola waves resident on a 256-CU MI355X
 constexpr int SG_CARRY_PAIRS = 16;  // sg_stft_ola carry registers: wl - floor(hop) <= 128 * 16 samples
 struct SgOlaTile {
   int32_t ola, pad;

@@ -336,6 +336,11 @@ vec spectral_envelope(Rng& R, int64_t nr, int64_t nc, const sg_formants* F, doub
   }
   vec env((size_t)(nr * nc), 0.0);
   vec mouth((size_t)nc, 0.5), mbin((size_t)nc, 1.0);
+  vec logk((size_t)nr), log2k((size_t)nr);
+  for (int64_t k = 0; k < nr; ++k) {
+    logk[k] = std::log((double)(k + 1));
+    log2k[k] = std::log2((double)(k + 1));
+  }
   if (nF > 0) {
     int64_t nPoints = 0;
     for (int f = 0; f < nF; ++f) nPoints = std::max<int64_t>(nPoints, np[f]);
@@ -452,6 +457,8 @@ vec spectral_envelope(Rng& R, int64_t nr, int64_t nc, const sg_formants* F, doub
       fu.push_back(z);
     }
     // dgamma(1:nr, shape = mu^2/sd^2, rate = mu/sd^2), normalised by its max   R/sourceSpectrum.R:507-522
+    // (log density from a shared log(k) table; exp only where the column is
+    // within e^-80 of its max, below which a term cannot move the dB sum)
     vec col((size_t)nr);
     for (const auto& tr : fu)
       for (int64_t c = 0; c < nc; ++c) {
@@ -462,20 +469,25 @@ vec spectral_envelope(Rng& R, int64_t nr, int64_t nc, const sg_formants* F, doub
         double lmax = -INFINITY;
         for (int64_t k = 0; k < nr; ++k) {
           const double x = (double)(k + 1);
-          const double l = (shape == 1) ? -rate * x : (shape - 1) * std::log(x) - rate * x;
+          const double l = (shape == 1) ? -rate * x : (shape - 1) * logk[k] - rate * x;
           col[k] = l;
           if (l > lmax) lmax = l;
         }
-        for (int64_t k = 0; k < nr; ++k) env[c * nr + k] += std::exp(col[k] - lmax) * tr.amp[c];
+        const double amp = tr.amp[c], lcut = lmax - 80;
+        double* e = &env[c * nr];
+        for (int64_t k = 0; k < nr; ++k)
+          if (col[k] > lcut) e[k] += std::exp(col[k] - lmax) * amp;
       }
     for (auto& v : env) v *= formantDep;
   }
   // lip radiation, open-mouth boost, dB -> linear (2^(x/10))   R/sourceSpectrum.R:524-541
-  for (int64_t c = 0; c < nc; ++c)
+  for (int64_t c = 0; c < nc; ++c) {
+    const double boost = std::pow(2.0, mouth[c] * openMouthBoost / 10);
     for (int64_t k = 0; k < nr; ++k) {
-      const double lip = rolloffLip * std::log2((double)(k + 1));
-      env[c * nr + k] = (env[c * nr + k] + lip * mbin[c]) * std::pow(2.0, mouth[c] * openMouthBoost / 10);
+      const double lip = rolloffLip * log2k[k];
+      env[c * nr + k] = (env[c * nr + k] + lip * mbin[c]) * boost;
     }
+  }
   for (auto& v : env) v = std::pow(2.0, v / 10);
   return env;
 }
@@ -560,6 +572,33 @@ void finalize_spec(Batch& B) {
       if (B.olas_dev[oi].fused) order.push_back(oi);
     auto geom_of = [&](size_t oi) { return B.frame_geom[ph][B.olas_dev[oi].fidx - fbase]; };
     std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return geom_of(a) < geom_of(b); });
+    // Segment length: SG_SEG_FRAMES frames would leave a partial last round of
+    // workgroups (one per CU), so pick the length that packs the segments into
+    // whole rounds of SG_RESIDENT_WAVES (the fewest rounds SG_SEG_FRAMES needs).
+    int64_t seg_frames = SG_SEG_FRAMES;
+    {
+      auto segs_at = [&](int64_t S) {
+        int64_t tot = 0, run = 0;
+        int prev = -2;
+        for (size_t oi : order) {
+          const int g = geom_of(oi);
+          if (g != prev) {
+            tot += (SG_FFT_WAVES - run % SG_FFT_WAVES) % SG_FFT_WAVES;  // padding of the previous geometry
+            run = 0;
+            prev = g;
+          }
+          const int64_t k = std::max<int64_t>(1, (B.olas_dev[oi].nframes + S - 1) / S);
+          tot += k;
+          run += k;
+        }
+        return tot + (SG_FFT_WAVES - run % SG_FFT_WAVES) % SG_FFT_WAVES;
+      };
+      const int64_t base = segs_at(SG_SEG_FRAMES);
+      const int64_t rounds = (base + SG_RESIDENT_WAVES - 1) / SG_RESIDENT_WAVES;
+      int64_t S = SG_SEG_MIN_FRAMES;
+      while (S < SG_SEG_FRAMES && segs_at(S) > rounds * SG_RESIDENT_WAVES) S = std::max(S + 1, S * 9 / 8);
+      seg_frames = std::min<int64_t>(S, SG_SEG_FRAMES);
+    }
     int cur_geom = -1;
     auto pad = [&]() {
       while (B.olasegs.size() % SG_FFT_WAVES) {
@@ -579,7 +618,7 @@ void finalize_spec(Batch& B) {
         return o.hi > 0 ? f * o.hi : (int64_t)std::floor((double)f * o.h);
       };
       const int64_t n = o.nframes;
-      const int64_t nseg = std::max<int64_t>(1, (n + SG_SEG_FRAMES - 1) / SG_SEG_FRAMES);
+      const int64_t nseg = std::max<int64_t>(1, (n + seg_frames - 1) / seg_frames);
       {  // algorithmic bytes / flops of this OLA in sg_stft_ola (bench roofline)
         const int64_t nr = o.wl / 2;
         int64_t ncol = 0, prev = -1;
