@@ -317,7 +317,7 @@ def main():
         }
         if gather_ms is not None:
             res["gather_ms"] = gather_ms
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the CPU leg runs at N=1 only
             res["cpu_baseline"] = cpu_baseline(calls, args.cpu_budget)
         print(json.dumps(res), flush=True)
     plan.close()
