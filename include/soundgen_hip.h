@@ -132,6 +132,12 @@ typedef struct sg_soundgen_args {
   double samplingRate, windowLength, overlap, addSilence;
   double pitchFloor, pitchCeiling, pitchSamplingRate, throwaway;
   int32_t invalidArgAction; /* 0 adjust, 1 abort, 2 ignore */
+  /* max(unlist(lapply(formantsNoise, length))) evaluated on the caller's own
+   * formantsNoise (R/soundgen.R:662-663): 1 for a vowel string, the number of
+   * fields (4) for a list of formant lists. Noise formants are "moving" (one
+   * envelope column per 10 ms) when it exceeds 1 or the mouth moves.
+   * 0 = not supplied: treated as a list of formant lists (moving). */
+  int32_t formantsNoise_rlen;
 } sg_soundgen_args;
 
 /* One call of a batch: either a whole soundgen() call or a bare

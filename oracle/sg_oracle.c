@@ -1793,7 +1793,11 @@ OR_API int or_soundgen(const sg_soundgen_args* A_in, const sg_random* rnd, doubl
         int64_t uvDur = (int64_t)r_round((r_max(ns.t, ns.n) - r_min(ns.t, ns.n)) * sr / 1000);
         double* envN = NULL; int64_t nInt = 0;
         if (nFN > 0) {
-          nInt = (int64_t)r_round((r_max(ns.t, ns.n) - r_min(ns.t, ns.n)) / 10);  /* noise formants always "moving" */
+          {  /* R/soundgen.R:662-666: max(lengths(formantsNoise)) > 1 | mouth moves */
+            int moving = A.formantsNoise_rlen == 0 || A.formantsNoise_rlen > 1;
+            for (int64_t q = 0; q < mouthA.n; ++q) if (mouthA.v[q] != .5) moving = 1;
+            nInt = moving ? (int64_t)r_round((r_max(ns.t, ns.n) - r_min(ns.t, ns.n)) / 10) : 1;
+          }
           envN = (double*)malloc((size_t)(wlp / 2) * (nInt > 0 ? nInt : 1) * sizeof(double));
           rc = spectral_envelope(&R, (int64_t)(wlp / 2), nInt, &A.formantsNoise, A.formantDep, A.rolloffLip, anc_view(&mouthA), 0, 0,
                                  A.vocalTract, T, A.tempEffects[1], A.tempEffects[2], A.formantDepStoch, 1, sr, 35400, envN);

@@ -37,6 +37,10 @@ generateHarmonics = function(pitch, attackLen = 50, nonlinBalance = 0, nonlinDep
 soundgen_hip = function(...) {
   a = list(...)
   if (is.character(a$formants)) a$formants = convertStringToFormants(a$formants)
+  # R/soundgen.R:662: noise formants "move" when max(lengths(formantsNoise)) > 1,
+  # evaluated on the caller's value (a string counts 1, a formant list its fields)
+  a$formantsNoise_rlen = if (length(a$formantsNoise) && !is.na(a$formantsNoise[1]))
+    as.integer(max(unlist(lapply(a$formantsNoise, length)))) else 0L
   if (is.character(a$formantsNoise)) a$formantsNoise = convertStringToFormants(a$formantsNoise)
   for (nm in c('pitchAnchors', 'pitchAnchorsGlobal', 'noiseAnchors', 'mouthAnchors', 'amplAnchors',
                'amplAnchorsGlobal')) {

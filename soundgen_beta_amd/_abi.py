@@ -85,7 +85,7 @@ class sg_soundgen_args(C.Structure):
         ("samplingRate", C.c_double), ("windowLength", C.c_double), ("overlap", C.c_double),
         ("addSilence", C.c_double), ("pitchFloor", C.c_double), ("pitchCeiling", C.c_double),
         ("pitchSamplingRate", C.c_double), ("throwaway", C.c_double),
-        ("invalidArgAction", C.c_int32),
+        ("invalidArgAction", C.c_int32), ("formantsNoise_rlen", C.c_int32),
     ]
 
 

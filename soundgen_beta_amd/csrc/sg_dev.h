@@ -193,7 +193,10 @@ constexpr int SG_FFT_WG = 0;
 constexpr int SG_FFT_WAVE = 1;
 constexpr int SG_FFT_DFT = 2;   // M with a prime factor > 31: direct O(M^2) DFT in sg_fft_frames
 constexpr int SG_WAVE_STATE = 24;  // complex butterfly points a lane holds per stage in sg_stft_ola
-constexpr int SG_FFT_WAVES = 8;    // wavefronts (segments) per sg_stft_ola workgroup: one workgroup per CU
+#ifndef SG_FFT_WAVES_N
+#define SG_FFT_WAVES_N 8  // build knob
+#endif
+constexpr int SG_FFT_WAVES = SG_FFT_WAVES_N;    // wavefronts (segments) per sg_stft_ola workgroup: one workgroup per CU
 constexpr int SG_PF_SRC = 20;      // sg_stft_ola register prefetch: sound pairs per lane (M <= 1280)
 constexpr int SG_PF_PAIR = 10;     // bin pairs per lane (M / 2 + 1 <= 640)
 

@@ -19,6 +19,9 @@
 #include <hip/hip_runtime.h>
 
 #include "sg_dev.h"
+#ifndef SG_FFT_WPE
+#define SG_FFT_WPE 2  // build knob: waves per SIMD for sg_stft_ola
+#endif
 #include "sg_devfn.h"
 #include "sg_roots.h"
 
@@ -663,7 +666,7 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
 // registers while this frame's inverse FFT runs. Frames never leave LDS;
 // summation is in frame order, so results are deterministic.
 // LDS: twS (M pairs), twN (M pairs), ham + han (M pairs each), SG_FFT_WAVES slices (M pairs each).
-extern "C" __global__ __launch_bounds__(SG_FFT_WAVES * 64) __attribute__((amdgpu_waves_per_eu(2))) void sg_stft_ola(
+extern "C" __global__ __launch_bounds__(SG_FFT_WAVES * 64) __attribute__((amdgpu_waves_per_eu(SG_FFT_WPE))) void sg_stft_ola(
     const SgSegment* __restrict__ segs, const SgOla* __restrict__ olas, const SgFrame* __restrict__ frames,
     const SgFftGeom* __restrict__ geoms, const float* __restrict__ fl, float* __restrict__ fs,
     float* __restrict__ slotmax) {

@@ -406,7 +406,9 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
         vec envN;
         int64_t nInt = 0;
         if (postNoise) {
-          bool moving = formants_moving(A.formantsNoise);
+          // R/soundgen.R:662-663: max(lengths(formantsNoise)) > 1 | mouth moves;
+          // a list of formant lists always has 4 fields, so it counts as moving
+          bool moving = A.formantsNoise_rlen == 0 || A.formantsNoise_rlen > 1;
           bool mouthMoves = false;
           for (double v : mouthA.v) if (v != .5) mouthMoves = true;
           if (mouthMoves) moving = true;

@@ -167,6 +167,18 @@ def as_anchors(x, time_to=1.0):
     return _seq_len(0.0, float(time_to), len(v)), np.ascontiguousarray(v)
 
 
+def r_max_lengths(x):
+    """max(unlist(lapply(x, length))) as R evaluates it on formantsNoise
+    (R/soundgen.R:662): 1 per string, the field count of each formant list; 0 for NA."""
+    if _is_na(x):
+        return 0
+    if isinstance(x, str):
+        return 1
+    if isinstance(x, dict):
+        return max((len(v) if isinstance(v, dict) else np.atleast_1d(v).size) for v in x.values())
+    return max((np.atleast_1d(v).size for v in x), default=0)
+
+
 def as_formants(x, speaker="M1"):
     """formants -> ordered list of (name, time, freq, amp, width) or None."""
     if _is_na(x):
@@ -264,7 +276,7 @@ def fill_soundgen_args(h, kw):
     for f, _ in _abi.sg_soundgen_args._fields_:
         if f in ("pitchAnchors", "pitchAnchorsGlobal", "noiseAnchors", "mouthAnchors",
                  "amplAnchors", "amplAnchorsGlobal", "formants", "formantsNoise",
-                 "tempEffects", "invalidArgAction"):
+                 "tempEffects", "invalidArgAction", "formantsNoise_rlen"):
             continue
         v = a[f]
         setattr(s, f, float("nan") if _is_na(v) else float(v))
@@ -277,6 +289,7 @@ def fill_soundgen_args(h, kw):
     s.noiseAnchors = h.anchors(as_anchors(a["noiseAnchors"], time_to=a["sylLen"]))
     s.formants = h.formants(as_formants(a["formants"]))
     s.formantsNoise = h.formants(as_formants(a["formantsNoise"]))
+    s.formantsNoise_rlen = r_max_lengths(a["formantsNoise"])
     s.invalidArgAction = {"adjust": 0, "abort": 1, "ignore": 2}[a["invalidArgAction"]]
     return s
 

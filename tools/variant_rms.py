@@ -1,0 +1,48 @@
+"""Diagnostic: GPU path vs oracle RMS for one preset under argument variants.
+python tools/variant_rms.py Speaker Name"""
+import copy, os, sys, json
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+import bench
+from soundgen_beta_amd import batch, native, presets as P
+from oracle import oracle as O
+
+spk, nm = sys.argv[1], sys.argv[2]
+rng = np.random.default_rng(5)
+Z = rng.standard_normal(200000)
+U = rng.uniform(size=4000000)
+base = P.args(spk, nm)
+base["samplingRate"] = 44100
+base["addSilence"] = 0
+variants = json.loads(sys.argv[3]) if len(sys.argv) > 3 else {}
+variants = {"as is": {}, **variants}
+calls, labels = [], []
+for lab, mod in variants.items():
+    a = copy.deepcopy(base)
+    for k, v in mod.items():
+        if v is None:
+            a.pop(k, None)
+        else:
+            a[k] = v
+    calls.append({"kind": "soundgen", "args": a, "normals": Z, "uniforms": U})
+    labels.append(lab)
+ctx = native.Context(0)
+plan = batch.Plan(calls, ctx)
+plan.upload()
+out = torch.empty(max(plan.total, 1), dtype=torch.float32, device="cuda")
+plan.execute(out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+torch.cuda.synchronize()
+for i, lab in enumerate(labels):
+    if plan.status[i]:
+        print("%-28s status %d %s" % (lab, plan.status[i], plan.message(i)))
+        continue
+    lo, L = int(plan.offsets[i]), int(plan.lengths[i])
+    y = out[lo:lo + L].double().cpu().numpy()
+    ref = bench.oracle_call(O, calls[i])
+    if len(ref) != L:
+        print("%-28s len %d vs oracle %d" % (lab, L, len(ref)))
+        continue
+    e = y - ref
+    k = int(np.abs(e).argmax())
+    print("%-28s rms %.3e maxabs %.2e at %d/%d (gpu %.4f oracle %.4f)" % (lab, np.sqrt(np.mean(e ** 2)), abs(e[k]), k, L, y[k], ref[k]))
