@@ -21,6 +21,7 @@ constexpr size_t ALIGN = 256;
 size_t up(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
 struct Layout {
+  size_t tall;
   size_t segs, epochs, knots, amps, tasks, pieces, syls, syl_tiles, copy_tiles, ptiles, cknots, W, taskmax, ptilemax, maxes, total;
   size_t geoms, frames, fgroups, olas, olatiles, olasegs, olatilemax, olamax, items, mixes, mixtiles, fl, fs;
   explicit Layout(const Batch& B) {
@@ -31,6 +32,7 @@ struct Layout {
     knots = take(B.knots.size() * sizeof(double));
     amps = take(B.amps.size() * sizeof(float) + 64 * sizeof(float));
     tasks = take(B.tasks.size() * sizeof(SgWTask));
+    tall = take(B.tasks.size() * sizeof(int32_t));
     pieces = take(B.pieces.size() * sizeof(SgPiece));
     syls = take(B.syls.size() * sizeof(SgSyllable));
     syl_tiles = take(B.fin_tiles.size() * sizeof(SgSylTile));
@@ -177,6 +179,7 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   D.knots = (double*)(a + L.knots);
   D.amps = (float*)(a + L.amps);
   D.tasks = (SgWTask*)(a + L.tasks);
+  D.tall = (int32_t*)(a + L.tall);
   D.pieces = (SgPiece*)(a + L.pieces);
   D.syls = (SgSyllable*)(a + L.syls);
   D.syl_tiles = (SgSylTile*)(a + L.syl_tiles);
@@ -208,6 +211,10 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   cp(D.knots, B.knots.data(), B.knots.size() * sizeof(double));
   cp(D.amps, B.amps.data(), B.amps.size() * sizeof(float));
   cp(D.tasks, B.tasks.data(), B.tasks.size() * sizeof(SgWTask));
+  D.tall_host.clear();
+  for (size_t i = 0; i < B.tasks.size(); ++i)
+    if (B.tasks[i].R > SG_ROWS_F32) D.tall_host.push_back((int32_t)i);
+  cp(D.tall, D.tall_host.data(), D.tall_host.size() * sizeof(int32_t));
   cp(D.pieces, B.pieces.data(), B.pieces.size() * sizeof(SgPiece));
   cp(D.syls, B.syls.data(), B.syls.size() * sizeof(SgSyllable));
   cp(D.syl_tiles, B.fin_tiles.data(), B.fin_tiles.size() * sizeof(SgSylTile));
@@ -258,6 +265,11 @@ void device_execute(const Batch& B, DevicePlan& D, float* d_out, hipStream_t s, 
       HIPCHK(hipEventRecord(e0, s));
     }
     launch_sine_bank(D, sl.t0, sl.t1 - sl.t0, s);
+    {  // tall tasks of the slice (ascending indices)
+      const auto lo = std::lower_bound(D.tall_host.begin(), D.tall_host.end(), (int32_t)sl.t0);
+      const auto hi = std::lower_bound(D.tall_host.begin(), D.tall_host.end(), (int32_t)sl.t1);
+      launch_sine_bank_tall(D, lo - D.tall_host.begin(), hi - lo, s);
+    }
     if (prof) {
       HIPCHK(hipEventRecord(e1, s));
       prof->push_back({SG_PROF_SINE_BANK, e0, e1});

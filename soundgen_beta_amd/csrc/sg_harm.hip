@@ -31,6 +31,7 @@ using sgd::wave_max;
 // v_sub measured 4.5 lane-instructions per (sample, row) on gfx950, VGPR/SGPR
 // operands 2.7 — tools/ubench/clenshaw_ubench.hip.)
 constexpr int SG_LDS_ROWS = 256;
+
 #ifndef SG_NS_MAX
 #define SG_NS_MAX 8  // build knob: largest slot pass (8 or 4)
 #endif
@@ -51,11 +52,11 @@ __device__ __forceinline__ void stage_rows(float* __restrict__ la, float* __rest
 #define SG_ROW(a, d)                                                  \
   {                                                                   \
     _Pragma("unroll") for (int s = 0; s < NS; ++s) {                  \
-      const float b = fmaf(al[s], b1[s], (a) - b2[s]);                \
+      const Acc b = fma(al[s], b1[s], (Acc)(a) - b2[s]);              \
       b2[s] = b1[s];                                                  \
       b1[s] = b;                                                      \
       if (TWO) {                                                      \
-        const float e = fmaf(al[s], e1[s], (d) - e2[s]);              \
+        const Acc e = fma(al[s], e1[s], (Acc)(d) - e2[s]);            \
         e2[s] = e1[s];                                                \
         e1[s] = e;                                                    \
       }                                                               \
@@ -64,10 +65,10 @@ __device__ __forceinline__ void stage_rows(float* __restrict__ la, float* __rest
 #ifndef SG_ROWS_IT
 #define SG_ROWS_IT 8  // rows per loop iteration (build knob: 4 or 8)
 #endif
-template <int NS, bool TWO>
+template <int NS, bool TWO, typename Acc>
 __device__ __forceinline__ void clenshaw_lds(const float* __restrict__ la, const float* __restrict__ ld, int n,
-                                             const float (&al)[NS], float (&b1)[NS], float (&b2)[NS],
-                                             float (&e1)[NS], float (&e2)[NS]) {
+                                             const Acc (&al)[NS], Acc (&b1)[NS], Acc (&b2)[NS],
+                                             Acc (&e1)[NS], Acc (&e2)[NS]) {
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   if (SG_ROWS_IT == 8 && (n & 4)) {  // odd group of 4 on top
     const float4 A4 = *reinterpret_cast<const float4*>(la + n - 4);
@@ -115,12 +116,26 @@ __device__ __forceinline__ void sample_setup(const SgWTask& T, int l, float& t, 
   al = 2.f * __builtin_amdgcn_cosf(x);
 }
 
-template <int NS, bool TWO, bool ENV, bool LIN>
+// fp64 variant for tall tasks (T.R > SG_ROWS_F32, subharmonic sidebands): the
+// fp32 recurrence loses ~R^2 eps near theta = 0 and fp32 cos(theta) misplaces
+// the angle by ~eps/theta, which row R multiplies by R.
+template <bool TWO, bool LIN>
+__device__ __forceinline__ void sample_setup(const SgWTask& T, int l, float& t, double& al, double& sn) {
+  t = TWO ? fmaf((float)l, T.xby, T.tc0) * T.rdx : 0.f;
+  const double m = (double)(T.mbase + l);
+  const double P = LIN ? fma(m, T.c1, T.c0) : fma(m, fma(m, fma(m, fma(m, T.c4, T.c3), T.c2), T.c1), T.c0);
+  double cs;
+  sincospi(2.0 * (P - rint(P)), &sn, &cs);
+  al = 2.0 * cs;
+}
+
+template <int NS, bool TWO, bool ENV, bool LIN, typename Acc>
 __device__ __forceinline__ void run_slots(const SgWTask& T, bool staged, float* __restrict__ la, float* __restrict__ ld,
                                           const float* __restrict__ amps, const SgSyllable* __restrict__ syls,
                                           const double* __restrict__ cknots, float* __restrict__ W, int l0, int lane,
                                           float& tmax) {
-  float t[NS], al[NS], sn[NS], b1[NS], b2[NS], e1[NS], e2[NS];
+  float t[NS];
+  Acc al[NS], sn[NS], b1[NS], b2[NS], e1[NS], e2[NS];
   int l[NS];
   bool valid[NS];
 #pragma unroll
@@ -128,20 +143,20 @@ __device__ __forceinline__ void run_slots(const SgWTask& T, bool staged, float* 
     l[s] = l0 + 64 * s + lane;
     valid[s] = l[s] < T.len;
     sample_setup<TWO, LIN>(T, valid[s] ? l[s] : 0, t[s], al[s], sn[s]);
-    b1[s] = b2[s] = e1[s] = e2[s] = 0.f;
+    b1[s] = b2[s] = e1[s] = e2[s] = (Acc)0;
   }
   if (staged) {
-    clenshaw_lds<NS, TWO>(la, ld, T.R, al, b1, b2, e1, e2);
+    clenshaw_lds<NS, TWO, Acc>(la, ld, T.R, al, b1, b2, e1, e2);
   } else {  // rare (subharmonic epochs with many rows): 256-row chunks, top first
     for (int r0 = (T.R - 1) / SG_LDS_ROWS * SG_LDS_ROWS; r0 >= 0; r0 -= SG_LDS_ROWS) {
       const int n = T.R - r0 < SG_LDS_ROWS ? T.R - r0 : SG_LDS_ROWS;
       stage_rows<TWO>(la, ld, amps + T.a_off, amps + T.d_off, r0, n, lane);
-      clenshaw_lds<NS, TWO>(la, ld, n, al, b1, b2, e1, e2);
+      clenshaw_lds<NS, TWO, Acc>(la, ld, n, al, b1, b2, e1, e2);
     }
   }
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    const float y = (TWO ? fmaf(t[s], e1[s], b1[s]) : b1[s]) * sn[s];
+    const float y = (float)((TWO ? fma((Acc)t[s], e1[s], b1[s]) : b1[s]) * sn[s]);
     const int j = T.j0 + l[s];
     if (valid[s]) W[T.w_off + j] = y;
     // fused max over the samples that land 1:1 in the syllable (branch-free)
@@ -155,7 +170,7 @@ __device__ __forceinline__ void run_slots(const SgWTask& T, bool staged, float* 
   }
 }
 
-template <bool TWO, bool ENV, bool LIN>
+template <bool TWO, bool ENV, bool LIN, typename Acc = float>
 __device__ __forceinline__ float run_task(const SgWTask& T, float* __restrict__ la, float* __restrict__ ld,
                                           const float* __restrict__ amps, const SgSyllable* __restrict__ syls,
                                           const double* __restrict__ cknots, float* __restrict__ W, int lane) {
@@ -165,18 +180,20 @@ __device__ __forceinline__ float run_task(const SgWTask& T, float* __restrict__ 
   int l0 = 0;
   // passes of 8 / 4 / 2 / 1 slots of 64 samples (8-slot passes on the A chain
   // only: with the dA chain they exceed the VGPR budget)
-  if (!TWO && SG_NS_MAX >= 8) {
+  constexpr bool F32 = sizeof(Acc) == 4;
+  if (F32 && !TWO && SG_NS_MAX >= 8) {
 #pragma unroll 1
     for (; T.len - l0 > 448; l0 += 512)
-      run_slots<8, TWO, ENV, LIN>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax);
+      run_slots<8, TWO, ENV, LIN, Acc>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax);
   }
 #pragma unroll 1
-  for (; T.len - l0 > 192; l0 += 256) run_slots<4, TWO, ENV, LIN>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax);
+  for (; T.len - l0 > 192; l0 += 256)
+    run_slots<4, TWO, ENV, LIN, Acc>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax);
   if (T.len - l0 > 64) {
-    run_slots<2, TWO, ENV, LIN>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax);
+    run_slots<2, TWO, ENV, LIN, Acc>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax);
     l0 += 128;
   }
-  if (l0 < T.len) run_slots<1, TWO, ENV, LIN>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax);
+  if (l0 < T.len) run_slots<1, TWO, ENV, LIN, Acc>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax);
   return tmax;
 }
 
@@ -202,6 +219,7 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank(
     if (ti >= ntasks) break;
 #endif
     const SgWTask T = tasks[ti];
+    if (T.R > SG_ROWS_F32) continue;  // sg_sine_bank_tall
     float tmax;
     if (T.flags & SG_TASK_ENV)  // amplAnchors envelope: rare, kept out of the hot variants
       tmax = (T.flags & SG_TASK_CONST) ? run_task<false, true, false>(T, la, ld, amps, syls, cknots, W, lane)
@@ -215,6 +233,32 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank(
     const float wm = wave_max(tmax);
     if (lane == 0) taskmax[ti] = wm;
   }
+}
+
+// The tasks with more than SG_ROWS_F32 rows (listed in idx): fp64 sincospi of the
+// reduced phase and fp64 Clenshaw chains, one task per wave.
+extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_tall(
+    const int32_t* __restrict__ idx, int64_t n, const SgWTask* __restrict__ tasks, const float* __restrict__ amps,
+    const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, float* __restrict__ W,
+    float* __restrict__ taskmax) {
+  __shared__ __attribute__((aligned(16))) float rows[4][2][SG_LDS_ROWS];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t k = (int64_t)blockIdx.x * 4 + wave;
+  if (k >= n) return;
+  const int64_t ti = idx[k];
+  const SgWTask T = tasks[ti];
+  float* la = rows[wave][0];
+  float* ld = rows[wave][1];
+  float tmax;
+  if (T.flags & SG_TASK_ENV)
+    tmax = (T.flags & SG_TASK_CONST) ? run_task<false, true, false, double>(T, la, ld, amps, syls, cknots, W, lane)
+                                     : run_task<true, true, false, double>(T, la, ld, amps, syls, cknots, W, lane);
+  else
+    tmax = (T.flags & SG_TASK_CONST) ? run_task<false, false, false, double>(T, la, ld, amps, syls, cknots, W, lane)
+                                     : run_task<true, false, false, double>(T, la, ld, amps, syls, cknots, W, lane);
+  const float wm = wave_max(tmax);
+  if (lane == 0) taskmax[ti] = wm;
 }
 
 // per-syllable max over its task slots and crossfade-piece slots
@@ -447,6 +491,12 @@ void launch_sine_bank(const DevicePlan& D, int64_t t0, int64_t n_tasks, hipStrea
   hipLaunchKernelGGL(sg_sine_bank, dim3((unsigned)blocks), dim3(256), 0, s, D.tasks + t0, n_tasks, D.amps, D.syls,
                      D.cknots, D.W, D.taskmax + t0);
   SG_LAUNCHED("sg_sine_bank");
+}
+void launch_sine_bank_tall(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(sg_sine_bank_tall, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, D.tall + k0, n, D.tasks,
+                     D.amps, D.syls, D.cknots, D.W, D.taskmax);
+  SG_LAUNCHED("sg_sine_bank_tall");
 }
 void launch_piece_max(const DevicePlan& D, int64_t p0, int64_t n_ptiles, hipStream_t s) {
   if (n_ptiles <= 0) return;

@@ -78,3 +78,29 @@ def test_soundgen_cases_one_batch(oracle):
         r = _rms(y, ref)
         print(n, "rms", r)
         assert r <= TOL, (n, r)
+
+
+def test_c5_presets_one_batch(oracle):
+    """C5: calls drawn from the 33 presets of R/presets.R with scaled
+    sylLen and pitch, 44.1 kHz, the presets' own temperatures and separately
+    filtered noise (formantsNoise), subharmonic sidebands up to ~400 rows
+    (sg_sine_bank_tall). Every planned call is compared with the oracle; calls the
+    planner refuses (loess radius 0, odd window lengths) must be refused by status."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from soundgen_beta_amd import batch
+    calls = bench.c5_calls(96)
+    plan = batch.Plan(calls, None)
+    ok = [i for i in range(len(calls)) if plan.status[i] == 0]
+    assert len(ok) >= 48
+    outs = batch.synthesize([calls[i] for i in ok])
+    worst = 0.0
+    for i, y in zip(ok, outs):
+        ref = bench.oracle_call(oracle, calls[i])
+        assert len(y) == len(ref), calls[i]["preset"]
+        r = _rms(y, ref)
+        worst = max(worst, r)
+        assert r <= TOL, (i, calls[i]["preset"], r)
+    print("C5 worst rms", worst, "over", len(ok), "calls")

@@ -71,3 +71,20 @@ def test_soundgen_plan_lengths_match_oracle(oracle, name):
     assert p.status[0] == 0, p.message(0)
     y = oracle.soundgen(normals=N, uniforms=U, **kw)
     assert p.lengths[0] == len(y)
+
+
+def test_c5_plan_lengths_match_oracle(oracle):
+    """C5 preset calls (bench.c5_calls): every planned length equals the oracle's,
+    including presets with separately filtered noise, nSyl > 1 and temperature > 0
+    (the draw order decides the lengths), and the failures are the documented ones."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    calls = bench.c5_calls(40)
+    plan = batch.Plan(calls, None)
+    for i, c in enumerate(calls):
+        if plan.status[i]:
+            assert ("loess" in plan.message(i)) or ("odd window" in plan.message(i)), plan.message(i)
+            continue
+        assert plan.lengths[i] == len(bench.oracle_call(oracle, c)), (i, c["preset"])
