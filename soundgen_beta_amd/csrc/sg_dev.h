@@ -53,7 +53,7 @@ constexpr int SG_TASK_CONST = 1;  // columns equal over the task: A chain only
 constexpr int SG_TASK_ENV = 4;    // the syllable has an amplitude envelope (max taken after it)
 // tasks with more rows than this (subharmonic sidebands) run in sg_sine_bank_tall:
 // fp64 angle and recurrence (parity on the C5 presets with subFreq << f0)
-constexpr int SG_ROWS_F32 = 64;
+constexpr int SG_ROWS_F32 = 96;
 constexpr int SG_TASK_LIN = 2;    // phase segment linear (c2 = c3 = c4 = 0): one fp64 FMA per sample
 constexpr int SG_TASK_MAX = 1024;  // samples per task (16 slots of 64 lanes)
 struct SgWTask {

@@ -48,15 +48,23 @@ __device__ __forceinline__ void stage_rows(float* __restrict__ la, float* __rest
   }
 }
 
+#ifndef SG_PK
+#define SG_PK 1  // build knob: slot pairs as packed fp32 (v_pk_fma_f32 / v_pk_add_f32)
+#endif
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float vfma(float a, float b, float c) { return fmaf(a, b, c); }
+__device__ __forceinline__ double vfma(double a, double b, double c) { return fma(a, b, c); }
+__device__ __forceinline__ f2 vfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
 // Clenshaw over staged rows n-1 .. 0 (n a multiple of 4), continuing b (and e)
 #define SG_ROW(a, d)                                                  \
   {                                                                   \
     _Pragma("unroll") for (int s = 0; s < NS; ++s) {                  \
-      const Acc b = fma(al[s], b1[s], (Acc)(a) - b2[s]);              \
+      const Acc b = vfma(al[s], b1[s], (Acc)(a) - b2[s]);             \
       b2[s] = b1[s];                                                  \
       b1[s] = b;                                                      \
       if (TWO) {                                                      \
-        const Acc e = fma(al[s], e1[s], (Acc)(d) - e2[s]);            \
+        const Acc e = vfma(al[s], e1[s], (Acc)(d) - e2[s]);           \
         e2[s] = e1[s];                                                \
         e1[s] = e;                                                    \
       }                                                               \
@@ -116,6 +124,40 @@ __device__ __forceinline__ void sample_setup(const SgWTask& T, int l, float& t, 
   al = 2.f * __builtin_amdgcn_cosf(x);
 }
 
+// fp32 slots in pairs: each row is one v_pk_add_f32 + one v_pk_fma_f32 per two samples
+template <int NS, bool TWO>
+__device__ __forceinline__ void clenshaw_pk(const float* __restrict__ la, const float* __restrict__ ld, int n,
+                                            const float (&al)[NS], float (&b1)[NS], float (&b2)[NS], float (&e1)[NS],
+                                            float (&e2)[NS]) {
+  constexpr int NP = NS / 2;
+  f2 al2[NP], p1[NP], p2[NP], q1[NP], q2[NP];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    al2[i] = f2{al[2 * i], al[2 * i + 1]};
+    p1[i] = f2{b1[2 * i], b1[2 * i + 1]};
+    p2[i] = f2{b2[2 * i], b2[2 * i + 1]};
+    q1[i] = f2{e1[2 * i], e1[2 * i + 1]};
+    q2[i] = f2{e2[2 * i], e2[2 * i + 1]};
+  }
+  clenshaw_lds<NP, TWO, f2>(la, ld, n, al2, p1, p2, q1, q2);
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    b1[2 * i] = p1[i].x; b1[2 * i + 1] = p1[i].y;
+    b2[2 * i] = p2[i].x; b2[2 * i + 1] = p2[i].y;
+    e1[2 * i] = q1[i].x; e1[2 * i + 1] = q1[i].y;
+    e2[2 * i] = q2[i].x; e2[2 * i + 1] = q2[i].y;
+  }
+}
+template <int NS, bool TWO, typename Acc>
+__device__ __forceinline__ void clenshaw_any(const float* __restrict__ la, const float* __restrict__ ld, int n,
+                                             const Acc (&al)[NS], Acc (&b1)[NS], Acc (&b2)[NS], Acc (&e1)[NS],
+                                             Acc (&e2)[NS]) {
+  if constexpr (SG_PK && sizeof(Acc) == 4 && NS % 2 == 0)
+    clenshaw_pk<NS, TWO>(la, ld, n, al, b1, b2, e1, e2);
+  else
+    clenshaw_lds<NS, TWO, Acc>(la, ld, n, al, b1, b2, e1, e2);
+}
+
 // fp64 variant for tall tasks (T.R > SG_ROWS_F32, subharmonic sidebands): the
 // fp32 recurrence loses ~R^2 eps near theta = 0 and fp32 cos(theta) misplaces
 // the angle by ~eps/theta, which row R multiplies by R.
@@ -129,11 +171,15 @@ __device__ __forceinline__ void sample_setup(const SgWTask& T, int l, float& t, 
   al = 2.0 * cs;
 }
 
+#ifndef SG_ROT
+#define SG_ROT 1  // build knob: linear-phase slots 1..7 by rotation of slot 0 (no per-slot fp64 / v_sin / v_cos)
+#endif
 template <int NS, bool TWO, bool ENV, bool LIN, typename Acc>
 __device__ __forceinline__ void run_slots(const SgWTask& T, bool staged, float* __restrict__ la, float* __restrict__ ld,
                                           const float* __restrict__ amps, const SgSyllable* __restrict__ syls,
                                           const double* __restrict__ cknots, float* __restrict__ W, int l0, int lane,
-                                          float& tmax) {
+                                          float& tmax, const float (&rc)[8], const float (&rs)[8]) {
+  constexpr bool ROT = SG_ROT && LIN && sizeof(Acc) == 4 && NS > 1;
   float t[NS];
   Acc al[NS], sn[NS], b1[NS], b2[NS], e1[NS], e2[NS];
   int l[NS];
@@ -142,16 +188,23 @@ __device__ __forceinline__ void run_slots(const SgWTask& T, bool staged, float* 
   for (int s = 0; s < NS; ++s) {
     l[s] = l0 + 64 * s + lane;
     valid[s] = l[s] < T.len;
-    sample_setup<TWO, LIN>(T, valid[s] ? l[s] : 0, t[s], al[s], sn[s]);
     b1[s] = b2[s] = e1[s] = e2[s] = (Acc)0;
+    if (ROT && s > 0) {  // slot s = slot 0 rotated by 64 s samples of a linear phase
+      t[s] = TWO ? fmaf((float)l[s], T.xby, T.tc0) * T.rdx : 0.f;
+      const float h = 0.5f * (float)al[0], s2 = 2.f * (float)sn[0];
+      al[s] = fmaf((float)al[0], rc[s], -s2 * rs[s]);
+      sn[s] = fmaf((float)sn[0], rc[s], h * rs[s]);
+    } else {
+      sample_setup<TWO, LIN>(T, valid[s] ? l[s] : 0, t[s], al[s], sn[s]);
+    }
   }
   if (staged) {
-    clenshaw_lds<NS, TWO, Acc>(la, ld, T.R, al, b1, b2, e1, e2);
+    clenshaw_any<NS, TWO, Acc>(la, ld, T.R, al, b1, b2, e1, e2);
   } else {  // rare (subharmonic epochs with many rows): 256-row chunks, top first
     for (int r0 = (T.R - 1) / SG_LDS_ROWS * SG_LDS_ROWS; r0 >= 0; r0 -= SG_LDS_ROWS) {
       const int n = T.R - r0 < SG_LDS_ROWS ? T.R - r0 : SG_LDS_ROWS;
       stage_rows<TWO>(la, ld, amps + T.a_off, amps + T.d_off, r0, n, lane);
-      clenshaw_lds<NS, TWO, Acc>(la, ld, n, al, b1, b2, e1, e2);
+      clenshaw_any<NS, TWO, Acc>(la, ld, n, al, b1, b2, e1, e2);
     }
   }
 #pragma unroll
@@ -181,19 +234,34 @@ __device__ __forceinline__ float run_task(const SgWTask& T, float* __restrict__ 
   // passes of 8 / 4 / 2 / 1 slots of 64 samples (8-slot passes on the A chain
   // only: with the dA chain they exceed the VGPR budget)
   constexpr bool F32 = sizeof(Acc) == 4;
+  // cos / sin of the linear phase advance over 64 k samples, k = 0..7 (wave-uniform)
+  float rc[8], rs[8];
+  if (SG_ROT && LIN && F32) {
+    const double x = (double)(64 * (lane & 7)) * T.c1;
+    const float f = (float)(x - rint(x));
+    const int c = __builtin_bit_cast(int, __builtin_amdgcn_cosf(f)), sv = __builtin_bit_cast(int, __builtin_amdgcn_sinf(f));
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      rc[k] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(c, k));
+      rs[k] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(sv, k));
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) rc[k] = rs[k] = 0.f;
+  }
   if (F32 && !TWO && SG_NS_MAX >= 8) {
 #pragma unroll 1
     for (; T.len - l0 > 448; l0 += 512)
-      run_slots<8, TWO, ENV, LIN, Acc>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax);
+      run_slots<8, TWO, ENV, LIN, Acc>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax, rc, rs);
   }
 #pragma unroll 1
   for (; T.len - l0 > 192; l0 += 256)
-    run_slots<4, TWO, ENV, LIN, Acc>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax);
+    run_slots<4, TWO, ENV, LIN, Acc>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax, rc, rs);
   if (T.len - l0 > 64) {
-    run_slots<2, TWO, ENV, LIN, Acc>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax);
+    run_slots<2, TWO, ENV, LIN, Acc>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax, rc, rs);
     l0 += 128;
   }
-  if (l0 < T.len) run_slots<1, TWO, ENV, LIN, Acc>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax);
+  if (l0 < T.len) run_slots<1, TWO, ENV, LIN, Acc>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax, rc, rs);
   return tmax;
 }
 
