@@ -32,7 +32,7 @@ C2_PARAMS = dict(samplingRate=44100, pitchSamplingRate=3500, temperature=0, nonl
                  rolloff=-12, rolloffOct=-12, rolloffKHz=-6, rolloffParab=0, rolloffParabHarm=3, pitchFloor=50,
                  pitchCeiling=3500, throwaway=-120)
 HBM_PEAK_GBS = 8000.0                 # MI355X_MICROARCH.md chip table (spec)
-VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9  # lane-ops/s: 256 CU x 4 SIMD-32 x 2.4 GHz (one op per lane per cycle)
+VALU_PEAK_OPS = 157.3e12  # f32 lane-ops/s at the packed rate (v_pk_fma_f32 / v_pk_add_f32), which the sine bank uses
 FP32_PEAK_TFLOPS = 157.3              # MI355X FP32 vector (packed FMA)
 
 

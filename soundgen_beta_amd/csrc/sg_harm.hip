@@ -391,6 +391,27 @@ __device__ __forceinline__ float fade_at(int lf, int64_t L, int64_t k) {
   return f;
 }
 
+#ifndef SG_COPY_NT
+#define SG_COPY_NT 0  // build knob: non-temporal W loads (last use) and output stores
+#endif
+__device__ __forceinline__ float4 ld_last(const float4* p) {
+#if SG_COPY_NT
+  typedef float v4 __attribute__((ext_vector_type(4)));
+  const v4 r = __builtin_nontemporal_load(reinterpret_cast<const v4*>(p));
+  return make_float4(r.x, r.y, r.z, r.w);
+#else
+  return *p;
+#endif
+}
+__device__ __forceinline__ void st_stream(float4* p, float4 v) {
+#if SG_COPY_NT
+  typedef float v4 __attribute__((ext_vector_type(4)));
+  __builtin_nontemporal_store(v4{v.x, v.y, v.z, v.w}, reinterpret_cast<v4*>(p));
+#else
+  *p = v;
+#endif
+}
+
 // Fast path of the finalize (tiles from the planner's split, SgCopyTile):
 // one wavefront per tile of <= SG_COPY_TILE_MAX samples; aligned tiles keep up to
 // sixteen float4 loads per lane in flight before any store; one dependent descriptor level
@@ -411,7 +432,7 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_copy(const SgCopyTile*
     float4 v[E];
 #pragma unroll
     for (int e = 0; e < E; ++e)
-      if (256 * e + 4 * lane < T.n) v[e] = *reinterpret_cast<const float4*>(src + 256 * e + 4 * lane);
+      if (256 * e + 4 * lane < T.n) v[e] = ld_last(reinterpret_cast<const float4*>(src + 256 * e + 4 * lane));
     const bool ramp = T.fade >= 2 && (T.k0 < T.fade || T.k0 + T.n > T.L - T.fade);
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -422,7 +443,7 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_copy(const SgCopyTile*
         v[e].x *= fade_at(T.fade, T.L, k); v[e].y *= fade_at(T.fade, T.L, k + 1);
         v[e].z *= fade_at(T.fade, T.L, k + 2); v[e].w *= fade_at(T.fade, T.L, k + 3);
       }
-      *reinterpret_cast<float4*>(dst + 256 * e + 4 * lane) = v[e];
+      st_stream(reinterpret_cast<float4*>(dst + 256 * e + 4 * lane), v[e]);
     }
   } else {  // misaligned or short runs, zero pieces
     const bool zero = T.flags & SG_COPY_ZERO;
