@@ -70,3 +70,37 @@ def test_edge_single_and_empty_batches(oracle):
     ref = oracle.generate_harmonics(c["pitch"], **c["params"])
     assert len(out[0]) == len(ref) and _rms(out[0], ref) <= TOL
     assert batch.synthesize([]) == []
+
+
+def test_c2_full_batch_properties():
+    """C2 at its full size (1024 x 1 s tones, bench.c2_calls), checked by
+    size-independent properties: every call's signed max is 1 after R's
+    wave / max(wave) (R/source.R:449; up to the fades at the ends), two
+    executions of one plan are bit-identical (deterministic max reduction, no
+    atomics), and every call's length is the planner's bit-exact length."""
+    import os
+    import sys
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from soundgen_beta_amd import batch, native
+    calls = bench.c2_calls(1024)
+    ctx = native.default_context(0)
+    plan = batch.Plan(calls, ctx)
+    assert (plan.status == 0).all()
+    plan.upload()
+    outs = []
+    for _ in range(2):
+        out = torch.full((plan.total,), float("nan"), dtype=torch.float32, device="cuda")
+        plan.execute(out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        outs.append(out.cpu().numpy())
+    assert np.array_equal(outs[0], outs[1], equal_nan=True)  # slot padding stays NaN
+    y = outs[0]
+    for i in range(plan.n):
+        lo, n = int(plan.offsets[i]), int(plan.lengths[i])
+        seg = y[lo:lo + n]
+        assert np.isfinite(seg).all(), i
+        # <= 1 exactly up to rounding; a fade can shave the largest peak, the next
+        # peak of a sampled sinusoid is within ~1e-5 of it
+        assert 1.0 - 1e-4 <= float(seg.max()) <= 1.0 + 1e-6, (i, float(seg.max()))
