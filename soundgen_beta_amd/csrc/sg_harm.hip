@@ -546,7 +546,10 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
 
 // SG_FIN_TILES consecutive 1024-sample tiles per workgroup: the descriptor
 // chain (tile -> syllable -> piece, drift knots) of a syllable's next tile hits cache
-constexpr int SG_FIN_TILES = 4;
+#ifndef SG_FIN_TILES_N
+#define SG_FIN_TILES_N 4  // build knob
+#endif
+constexpr int SG_FIN_TILES = SG_FIN_TILES_N;
 extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize(
     const SgSylTile* __restrict__ stiles, int64_t ntiles, const SgPiece* __restrict__ pieces,
     const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, const float* __restrict__ W,
