@@ -31,6 +31,9 @@ using sgd::wave_max;
 // v_sub measured 4.5 lane-instructions per (sample, row) on gfx950, VGPR/SGPR
 // operands 2.7 — tools/ubench/clenshaw_ubench.hip.)
 constexpr int SG_LDS_ROWS = 256;
+#ifndef SG_NS8_TWO
+#define SG_NS8_TWO 0  // build knob: 8-slot passes also with the dA chain
+#endif
 
 #ifndef SG_NS_MAX
 #define SG_NS_MAX 8  // build knob: largest slot pass (8 or 4)
@@ -249,7 +252,7 @@ __device__ __forceinline__ float run_task(const SgWTask& T, float* __restrict__ 
 #pragma unroll
     for (int k = 0; k < 8; ++k) rc[k] = rs[k] = 0.f;
   }
-  if (F32 && !TWO && SG_NS_MAX >= 8) {
+  if (F32 && (!TWO || SG_NS8_TWO) && SG_NS_MAX >= 8) {
 #pragma unroll 1
     for (; T.len - l0 > 448; l0 += 512)
       run_slots<8, TWO, ENV, LIN, Acc>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax, rc, rs);
