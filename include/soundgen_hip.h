@@ -184,7 +184,8 @@ int sg_plan_status(const sg_plan* plan, int32_t* out_status);
 int64_t sg_plan_device_bytes(const sg_plan* plan);
 /* Upload descriptors/inputs to HBM (outside any timed region). */
 int sg_plan_upload(sg_ctx* ctx, sg_plan* plan);
-/* Run every kernel of the plan on `stream` (hipStream_t, NULL = ctx stream)
+/* Run every kernel of the plan on `stream` (hipStream_t; NULL = the null
+ * stream, ordered after earlier null-stream work such as torch's default stream)
  * writing fp32 samples into device buffer d_out (packed, offsets as above).
  * No host synchronisation inside; graph-capturable. */
 int sg_execute(sg_ctx* ctx, sg_plan* plan, float* d_out, void* stream);

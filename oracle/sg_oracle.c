@@ -301,6 +301,9 @@ static void svd3(double b[3][16], int m, double sigma[3], double V[3][3]) {
   }
 }
 
+/* lo_build / lo_vertex_fit: the fit has a NaN vertex (not an error code) */
+#define LO_ZERO_WIDTH 1
+
 /* local quadratic fit at vertex v (ehg127): value and slope */
 static int lo_vertex_fit(const double* x, const double* y, int n, int nf, double f, double v, double* val,
                          double* slope) {
@@ -309,7 +312,11 @@ static int lo_vertex_fit(const double* x, const double* y, int n, int nf, double
   for (int i = 1; i < n; ++i)  /* stable insertion sort by distance */
     for (int j = i; j > 0 && d2[ord[j]] < d2[ord[j - 1]]; --j) { int t = ord[j]; ord[j] = ord[j - 1]; ord[j - 1] = t; }
   const double rho = d2[ord[nf - 1]] * (f > 1 ? f : 1.0);
-  if (!(rho > 0)) return fail(SG_E_UNSUPPORTED, "loess: neighbourhood radius 0 (span too small; R yields NaN)");
+  /* rho = 0 (a vertex on a data point with floor(n f) = 1): the tricube
+   * weights are 0/0, so the vertex value is NaN. loess() itself returns;
+   * predict()'s .C(C_loess_ifit, ..., vval) then stops on the NaN (NAOK is
+   * FALSE), which is the try-error smooth_loess retries with span + 0.1. */
+  if (!(rho > 0)) return LO_ZERO_WIDTH;
   double b[3][16], eta[16];
   const int m = nf < 3 ? 3 : nf;
   for (int i = 0; i < m; ++i) { b[0][i] = b[1][i] = b[2][i] = 0; eta[i] = 0; }
@@ -384,11 +391,13 @@ static int lo_build(const double* x, const double* y, int n, double f, lo_tree* 
     T->cl[a] = l; T->cu[a] = m; T->cv0[a] = T->cv0[p]; T->cv1[a] = vn;
     T->cl[b] = m + 1; T->cu[b] = u; T->cv0[b] = vn; T->cv1[b] = T->cv1[p];
   }
+  int nan_vertex = 0;
   for (int v = 0; v < T->nv; ++v) {
     const int rc = lo_vertex_fit(x, y, n, nf, f, T->vx[v], &T->val[v], &T->slope[v]);
-    if (rc) return rc;
+    if (rc == LO_ZERO_WIDTH) { T->val[v] = T->slope[v] = NAN; nan_vertex = 1; }
+    else if (rc) return rc;
   }
-  return 0;
+  return nan_vertex ? LO_ZERO_WIDTH : 0;
 }
 
 static double lo_eval(const lo_tree* T, double z) {
@@ -424,9 +433,23 @@ static int smooth_loess(const double* t, const double* val, int64_t n, int64_t l
       a = yv[j]; yv[j] = yv[j - 1]; yv[j - 1] = a;
     }
   double span = (1 / (1 + exp(duration_ms / 500)) + 0.5) / pow(1.1, (double)(n - 3));
+  /* smoothContour = try(predict(l, time)); while (try-error) span = span + 0.1
+   * (R/smoothContours.R:133-143). RESTATED, UNPINNED: that predict() fails
+   * exactly when a vertex value is NaN (LO_ZERO_WIDTH) follows from .C's NAOK
+   * rule, not from R output. */
+  for (int k = 0;; ++k) {
+    lo_tree T;
+    const int rc = lo_build(xv, yv, nx, span, &T);
+    if (rc != LO_ZERO_WIDTH) { if (rc) return rc; break; }
+    if (k == 200) return fail(SG_E_DOMAIN, "loess: no span gives a finite fit");
+    span = span + 0.1;
+  }
   for (int iter = 0; iter < 200; ++iter) {
     lo_tree T;
     int rc = lo_build(xv, yv, nx, span, &T);
+    /* a zero-width fit inside the valueFloor loop would leave R comparing a
+     * try-error string against valueFloor: not restated */
+    if (rc == LO_ZERO_WIDTH) return fail(SG_E_UNSUPPORTED, "loess: zero-width fit inside the valueFloor refits");
     if (rc) return rc;
     int below = 0;
     for (int64_t k = 0; k < len; ++k) {
@@ -1112,7 +1135,10 @@ OR_API void or_fft(const double* re, const double* im, int64_t n, int inverse, d
 }
 
 /* seewave::istft(stft, ovlp, wl, wn = "hanning"), seewave.r:3447-3486.
- * stft: nr x nc complex (col-major, re/im separate; im may be NULL). */
+ * stft: nr x nc complex (col-major, re/im separate; im may be NULL). The
+ * inverse has length(X) = 2 nr points (wl - 1 for an odd wl) and is divided
+ * by that length; xprim * win then recycles xprim against the wl-point
+ * window (:3477-3479): sample i of the frame is xprim[i mod 2 nr] * win[i]. */
 static dv istft(const double* zre, const double* zim, int64_t nr, int64_t nc, double ovlp, int64_t wl) {
   double h = (double)wl * (100 - ovlp) / 100;
   double xlen = (double)wl + (double)(nc - 1) * h;
@@ -1127,14 +1153,13 @@ static dv istft(const double* zre, const double* zim, int64_t nr, int64_t nc, do
     int64_t col = (int64_t)(1 + b / h) - 1;
     const double* cr = zre + col * nr; const double* ci = zim ? zim + col * nr : NULL;
     for (int64_t k = 0; k < nr; ++k) { Xr[k] = cr[k]; Xi[k] = ci ? ci[k] : 0; }
+    const int64_t n2 = 2 * nr;  /* length(X) */
     Xr[nr] = cr[nr - 1]; Xi[nr] = 0;
-    for (int64_t k = 1; k < nr; ++k) { Xr[wl - k] = cr[k]; Xi[wl - k] = ci ? -ci[k] : 0; }
-    fft_rec(Xr, Xi, wl, 1, yr, yi, 1);
-    int64_t st = (int64_t)(b + 1) - 1;  /* (b+1):(b+wl) truncated */
-    for (int64_t i = 0; i < wl; ++i) {
+    for (int64_t k = 1; k < nr; ++k) { Xr[n2 - k] = cr[k]; Xi[n2 - k] = ci ? -ci[k] : 0; }
+    fft_rec(Xr, Xi, n2, 1, yr, yi, 1);
+    for (int64_t i = 0; i < wl; ++i) {  /* (b+1):(b+wl) truncated */
       int64_t q = (int64_t)(b + 1 + (double)i) - 1;
-      (void)st;
-      if (q < x.n) x.v[q] = x.v[q] + (yr[i] / (double)wl) * win.v[i];
+      if (q < x.n) x.v[q] = x.v[q] + (yr[i % n2] / (double)n2) * win.v[i];
     }
   }
   long double W0 = 0; for (int64_t i = 0; i < wl; ++i) W0 += win.v[i] * win.v[i];
@@ -1186,12 +1211,14 @@ static int generate_noise(rng_t* R, int64_t len, sg_anchors noiseAnchors, double
     dv fri = dv_new(nc);
     if (!filterNoise) for (int64_t c = 0; c < nc; ++c) fri.v[c] = 1;
     else { dv s = r_seq_len(1, (double)ncolF, nc); for (int64_t c = 0; c < nc; ++c) fri.v[c] = r_round(s.v[c]); dv_free(&s); }
+    /* runif(nr * nc) with nr = wl / 2 (x.5 for an odd wl: floor(nr * nc) draws),
+     * matrix(nrow = nr) keeps as.integer(nr) rows of them */
     zf = dv_new(nr * nc);
-    for (int64_t c = 0; c < nc; ++c)
-      for (int64_t k = 0; k < nr; ++k) {
-        double u; rc = rng_unif(R, &u); if (rc) { dv_free(&fri); goto done; }
-        zf.v[c * nr + k] = u * filt.v[((int64_t)fri.v[c] - 1) * nr + k];
-      }
+    const int64_t ndraw = (int64_t)((double)wl / 2 * (double)nc);
+    for (int64_t q = 0; q < ndraw; ++q) {
+      double u; rc = rng_unif(R, &u); if (rc) { dv_free(&fri); goto done; }
+      if (q < nr * nc) { const int64_t c = q / nr, k = q % nr; zf.v[q] = u * filt.v[((int64_t)fri.v[c] - 1) * nr + k]; }
+    }
     dv_free(&fri);
     br = istft(zf.v, NULL, nr, nc, overlap, wl);
     br2 = match_lengths_central(br, len);
@@ -1227,11 +1254,14 @@ static double* col_upsample(const double* t, const double* y, int64_t np, int64_
   } else for (int64_t i = 0; i < nc; ++i) o[i] = y[0];
   return o;
 }
-static int spectral_envelope(rng_t* R, int64_t nr, int64_t nc, const sg_formants* F, double formantDep,
+/* nrd = windowLength_points / 2 as R passes it: an odd window gives x.5, whose
+ * matrices have as.integer(nrd) rows while bin_width keeps nrd (:419) */
+static int spectral_envelope(rng_t* R, double nrd, int64_t nc, const sg_formants* F, double formantDep,
                              double rolloffLip, sg_anchors mouthAnchors, double mouthOpenThres, double openMouthBoost,
                              double vocalTract, double temperature, double formDrift, double formDisp,
                              double formantDepStoch, double slf, double sr, double speedSound, double* env) {
   int rc = 0;
+  const int64_t nr = (int64_t)nrd;
   int nF = F ? F->n_formants : 0;
   int haveVT = !isnan(vocalTract) || (vocalTract != vocalTract && 0); /* NaN encodes NULL */
   double VT = vocalTract;
@@ -1320,7 +1350,7 @@ static int spectral_envelope(rng_t* R, int64_t nr, int64_t nc, const sg_formants
           dv_free(&rw);
         }
     }
-    double bw = sr / 2 / (double)nr;
+    double bw = sr / 2 / nrd;
     for (int f = 0; f < nfu; ++f)
       for (int64_t c = 0; c < nc; ++c) { fu[f].freq[c] = (fu[f].freq[c] - bw / 2) / bw + 1; fu[f].width[c] = fu[f].width[c] / bw; }
     mouth = dv_new(nc); mbin = dv_new(nc);
@@ -1465,6 +1495,7 @@ OR_API int or_smooth_contour(const double* time, const double* value, int64_t n,
 OR_API int or_loess(const double* x, const double* y, int n, double span, const double* z, int64_t m, double* out) {
   lo_tree T;
   const int rc = lo_build(x, y, n, span, &T);
+  if (rc == LO_ZERO_WIDTH) return fail(SG_E_DOMAIN, "loess: NaN vertex value (predict() stops: NA/NaN/Inf in foreign function call)");
   if (rc) return rc;
   for (int64_t i = 0; i < m; ++i) out[i] = (z[i] < x[0] || z[i] > x[n - 1]) ? NAN : lo_eval(&T, z[i]);
   return 0;
@@ -1799,7 +1830,7 @@ OR_API int or_soundgen(const sg_soundgen_args* A_in, const sg_random* rnd, doubl
             nInt = moving ? (int64_t)r_round((r_max(ns.t, ns.n) - r_min(ns.t, ns.n)) / 10) : 1;
           }
           envN = (double*)malloc((size_t)(wlp / 2) * (nInt > 0 ? nInt : 1) * sizeof(double));
-          rc = spectral_envelope(&R, (int64_t)(wlp / 2), nInt, &A.formantsNoise, A.formantDep, A.rolloffLip, anc_view(&mouthA), 0, 0,
+          rc = spectral_envelope(&R, wlp / 2, nInt, &A.formantsNoise, A.formantDep, A.rolloffLip, anc_view(&mouthA), 0, 0,
                                  A.vocalTract, T, A.tempEffects[1], A.tempEffects[2], A.formantDepStoch, 1, sr, 35400, envN);
           if (rc) { free(envN); anc_free(&ns); anc_free(&pA); anc_free(&aA); free(sst); free(sen); free(ssi); goto done; }
         }
@@ -1829,7 +1860,6 @@ OR_API int or_soundgen(const sg_soundgen_args* A_in, const sg_random* rnd, doubl
     else {
       double fl = floor((double)sound.n / 2); if (fl < wlp) wlp = fl;
       int64_t wl = (int64_t)wlp;
-      if (wl % 2) { rc = fail(SG_E_UNSUPPORTED, "formant filter: odd window length"); free(sst); free(sen); free(ssi); goto done; }
       dv step = r_seq_by(1, (double)(sound.n - wl > 1 ? sound.n - wl : 1), (double)wl - (A.overlap * (double)wl / 100));
       int64_t nc = step.n, nr = wl / 2; dv_free(&step);
       int moving = formants_moving(&Fm);
@@ -1837,7 +1867,7 @@ OR_API int or_soundgen(const sg_soundgen_args* A_in, const sg_random* rnd, doubl
       if (mouthA.n > 0 && mouthMoves) moving = 1;
       int64_t nInt = moving ? nc : 1;
       double* env = (double*)malloc(nr * nInt * sizeof(double));
-      rc = spectral_envelope(&R, nr, nInt, &Fm, A.formantDep, A.rolloffLip, anc_view(&mouthA), 0, 0, A.vocalTract, T,
+      rc = spectral_envelope(&R, (double)wl / 2, nInt, &Fm, A.formantDep, A.rolloffLip, anc_view(&mouthA), 0, 0, A.vocalTract, T,
                              A.tempEffects[1], A.tempEffects[2], A.formantDepStoch, 1, sr, 35400, env);
       if (!rc) rc = formant_filter(sound.v, sound.n, env, nInt, wl, A.overlap, &filtered);
       free(env);

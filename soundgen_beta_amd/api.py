@@ -16,47 +16,31 @@ def _ctx(device):
     return native.default_context(device)
 
 
-def generateHarmonics(pitch, amplAnchors=rargs.NA, normals=None, uniforms=None, device=0, **kw):
-    """generateHarmonics(pitch, ...) — R/source.R:173-471."""
-    h = rargs.Holder()
-    p = rargs.fill_harm_params(kw)
-    pitch = h.arr(pitch)
-    rnd = h.random(normals, uniforms)
-    sr = p.samplingRate
-    cap = int(np.ceil(len(pitch) / p.pitchSamplingRate * sr * 1.2)) + int(sr) + 4096
-    out = np.zeros(cap)
-    n = C.c_int64()
+def _run_one(call, device):
+    """Plan ONE call once (its draws are consumed once, in the reference order),
+    size the output from the plan, execute on the GPU and copy to the host."""
+    from . import batch
     ctx = _ctx(device)
-    L = native.lib()
-    rc = L.sg_generate_harmonics(ctx.ptr, _abi.dptr(pitch), len(pitch), C.byref(p),
-                                 h.anchors(rargs.as_anchors(amplAnchors)), C.byref(rnd), _abi.dptr(out), cap,
-                                 C.byref(n))
-    if rc == _abi.SG_E_CAPACITY:
-        out = np.zeros(n.value)
-        rc = L.sg_generate_harmonics(ctx.ptr, _abi.dptr(pitch), len(pitch), C.byref(p),
-                                     h.anchors(rargs.as_anchors(amplAnchors)), C.byref(rnd), _abi.dptr(out),
-                                     n.value, C.byref(n))
-    native.check(rc, ctx.ptr)
-    return out[:n.value].copy()
+    plan = batch.Plan([call], ctx)
+    try:
+        if plan.status[0] != 0:
+            raise native.SoundgenError(int(plan.status[0]), plan.message(0))
+        out = np.zeros(max(plan.total, 1))
+        native.check(native.lib().sg_execute_to_host(ctx.ptr, plan.ptr, _abi.dptr(out)), ctx.ptr)
+        return out[:int(plan.lengths[0])].copy()
+    finally:
+        plan.close()
+
+
+def generateHarmonics(pitch, amplAnchors=rargs.NA, normals=None, uniforms=None, rng=None, device=0, **kw):
+    """generateHarmonics(pitch, ...) — R/source.R:173-471."""
+    return _run_one({"kind": "harmonics", "pitch": np.asarray(pitch, dtype=np.float64), "params": kw,
+                     "amplAnchors": amplAnchors, "normals": normals, "uniforms": uniforms, "rng": rng}, device)
 
 
 def soundgen(normals=None, uniforms=None, rng=None, device=0, **kw):
     """soundgen(...) — R/soundgen.R:208-862. Returns the waveform (float64)."""
-    h = rargs.Holder()
-    a = rargs.fill_soundgen_args(h, kw)
-    rnd = h.random(normals, uniforms, rng)
-    ctx = _ctx(device)
-    L = native.lib()
-    n = C.c_int64()
-    cap = 1 << 16
-    while True:
-        out = np.zeros(cap)
-        rc = L.sg_soundgen(ctx.ptr, C.byref(a), C.byref(rnd), _abi.dptr(out), cap, C.byref(n))
-        if rc == _abi.SG_E_CAPACITY:
-            cap = n.value
-            continue
-        native.check(rc, ctx.ptr)
-        return out[:n.value].copy()
+    return _run_one({"kind": "soundgen", "args": kw, "normals": normals, "uniforms": uniforms, "rng": rng}, device)
 
 
 def generateNoise(len, noiseAnchors=None, rolloffNoise=-6, attackLen=10, windowLength_points=1024,

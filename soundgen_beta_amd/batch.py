@@ -98,8 +98,7 @@ def synthesize(calls, device=0):
     out = torch.empty(max(plan.total, 1), dtype=torch.float32, device="cuda:%d" % device)
     stream = torch.cuda.current_stream(device)
     plan.execute(out.data_ptr(), stream.cuda_stream)
-    # torch's default stream has handle 0, which sg_execute reads as "the
-    # context's own stream" (non-blocking): wait for the device, not the stream
+    # sg_execute launches on torch's current stream (handle 0 = the null stream)
     torch.cuda.synchronize(device)
     host = out.cpu().numpy()
     res = []

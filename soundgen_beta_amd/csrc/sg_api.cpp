@@ -10,6 +10,10 @@
 
 #include "sg_plan.h"
 #include "sg_exec.h"
+#include "sg_prof.h"
+
+#include <cstdio>
+#include <cstdlib>
 
 struct sg_ctx {
   int device = 0;
@@ -24,6 +28,11 @@ struct sg_plan {
   sg::Batch B;
   sg::DevicePlan D;
 };
+
+namespace sg {
+std::atomic<int64_t> g_prof_ns[PF_N];
+bool g_prof_on = std::getenv("SG_PLAN_PROF") != nullptr;
+}  // namespace sg
 
 namespace {
 
@@ -155,8 +164,19 @@ int sg_plan_batch(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, sg_pl
       }
     }
     B.total_out = off;
-    sg::finalize_plan(B);
-    sg::finalize_spec(B);
+    {
+      sg::ProfScope ps(sg::PF_FINALIZE);
+      sg::finalize_plan(B);
+    }
+    {
+      sg::ProfScope ps(sg::PF_SPEC);
+      sg::finalize_spec(B);
+    }
+    if (sg::g_prof_on) {
+      static const char* names[] = {"harmonics", "rolloff", "contour", "envelope", "noise", "filter", "finalize", "finalize_spec"};
+      for (int i = 0; i < sg::PF_N; ++i)
+        std::fprintf(stderr, "sg_plan_prof %-14s %.3f s\n", names[i], sg::g_prof_ns[i].exchange(0) * 1e-9);
+    }
     *out = P.release();
     return SG_OK;
   });
@@ -202,8 +222,11 @@ int sg_plan_upload(sg_ctx* ctx, sg_plan* plan) {
 
 int sg_execute(sg_ctx* ctx, sg_plan* plan, float* d_out, void* stream) {
   return guarded(ctx, [&]() {
+    HIPCHK(hipSetDevice(ctx->device));
     if (!plan->D.uploaded) throw sg::SgError(SG_E_ARG, "sg_execute: plan not uploaded");
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    // NULL is the null (default) stream, as for every HIP API: the kernels are
+    // ordered after earlier null-stream work (e.g. torch's default stream)
+    hipStream_t s = (hipStream_t)stream;
     sg::device_execute(plan->B, plan->D, d_out, s, ctx->aux, ctx->profiling ? &ctx->prof_events : nullptr);
     return SG_OK;
   });
@@ -268,7 +291,9 @@ int sg_plan_stft_stats(const sg_plan* plan, int64_t* samples, int64_t* alg_bytes
 
 int sg_synchronize(sg_ctx* ctx) {
   return guarded(ctx, [&]() {
+    HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipStreamSynchronize(nullptr));  // sg_execute(..., NULL) work
     return SG_OK;
   });
 }

@@ -53,7 +53,10 @@ constexpr int SG_TASK_CONST = 1;  // columns equal over the task: A chain only
 constexpr int SG_TASK_ENV = 4;    // the syllable has an amplitude envelope (max taken after it)
 // tasks with more rows than this (subharmonic sidebands) run in sg_sine_bank_tall:
 // fp64 angle and recurrence (parity on the C5 presets with subFreq << f0)
-constexpr int SG_ROWS_F32 = 96;
+#ifndef SG_ROWS_F32_N
+#define SG_ROWS_F32_N 96  // build knob
+#endif
+constexpr int SG_ROWS_F32 = SG_ROWS_F32_N;
 constexpr int SG_TASK_LIN = 2;    // phase segment linear (c2 = c3 = c4 = 0): one fp64 FMA per sample
 constexpr int SG_TASK_MAX = 1024;  // samples per task (16 slots of 64 lanes)
 struct SgWTask {
@@ -195,6 +198,12 @@ struct SgFftGeom {
 constexpr int SG_FFT_WG = 0;
 constexpr int SG_FFT_WAVE = 1;
 constexpr int SG_FFT_DFT = 2;   // M with a prime factor > 31: direct O(M^2) DFT in sg_fft_frames
+// odd wl (windowLength_points = floor(L / 2) for short sounds, R/soundgen.R:743):
+// seewave's stft keeps wl %/% 2 = M rows, istft inverts 2M = wl - 1 points and
+// recycles them against the wl-point window (seewave.r:3468-3479). Direct DFTs,
+// one frame per sg_fft_frames workgroup; tw = wl pairs W_wl^t, tws = 2M pairs
+// exp(+2 pi i t / 2M)
+constexpr int SG_FFT_ODD = 3;
 constexpr int SG_WAVE_STATE = 24;  // complex butterfly points a lane holds per stage in sg_stft_ola
 #ifndef SG_FFT_WAVES_N
 #define SG_FFT_WAVES_N 8  // build knob

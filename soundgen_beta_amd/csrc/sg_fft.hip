@@ -388,6 +388,70 @@ __device__ void dft_ip(float2* X, float2* S, const float2* twM, int M) {
   __syncthreads();
 }
 
+// One frame of an odd window length N (SG_FFT_ODD): seewave's stft keeps
+// M = N %/% 2 bins of the N-point DFT (/N); istft inverts the 2M = N - 1
+// point Hermitian extension X = (Y_0..Y_{M-1}, Re Y_{M-1}, conj Y_{M-1}..conj Y_1)
+// and recycles it against the N-point Hann window (seewave.r:3468-3479):
+//   frame[i] = han[i] / 2M * (Re Y_0 + (-1)^n Re Y_{M-1} + 2 sum_{k=1}^{M-1} Re(Y_k e^{+2 pi i n k / 2M})),
+//   n = i mod 2M.
+// Direct sums (O(N M) per frame; odd lengths only occur for sounds shorter
+// than two windows), tables and the frame staged in LDS.
+__device__ void odd_frame(const SgFrameGroup& G, const SgFrame* __restrict__ frames, const SgFftGeom& g,
+                          const float* __restrict__ fl, float* __restrict__ fs, float4* lds4) {
+  const int N = g.wl, M = g.M, N2 = 2 * M;
+  float2* tw = reinterpret_cast<float2*>(lds4);  // W_N^t, t < N
+  float2* ti = tw + N;                           // exp(+2 pi i t / 2M), t < 2M
+  float2* Y = ti + N2;                           // M bins
+  float* x = reinterpret_cast<float*>(Y + M);    // N windowed samples
+  const float2* twg = reinterpret_cast<const float2*>(fl + g.tw);
+  const float2* tig = reinterpret_cast<const float2*>(fl + g.tws);
+  for (int t = threadIdx.x; t < N; t += SG_FFT_THREADS) tw[t] = twg[t];
+  for (int t = threadIdx.x; t < N2; t += SG_FFT_THREADS) ti[t] = tig[t];
+  const SgFrame F = frames[G.f0];
+  const float* ham = fl + g.win;
+  const float* han = ham + N;
+  if (G.mode == SG_FRAME_FILTER) {
+    const float* s = fs + F.src;
+    for (int n = threadIdx.x; n < N; n += SG_FFT_THREADS) x[n] = s[n] * ham[n];
+    __syncthreads();
+    const float* env = fl + F.env;
+    const float invN = 1.f / (float)N;
+    for (int k = threadIdx.x; k < M; k += SG_FFT_THREADS) {
+      float2 acc = make_float2(0.f, 0.f);
+      int e = 0;
+      for (int n = 0; n < N; ++n) {
+        acc.x = fmaf(x[n], tw[e].x, acc.x);
+        acc.y = fmaf(x[n], tw[e].y, acc.y);
+        e += k;
+        if (e >= N) e -= N;
+      }
+      const float sc = invN * env[k];
+      Y[k] = make_float2(acc.x * sc, acc.y * sc);
+    }
+  } else {  // SG_FRAME_NOISE: real spectrum u * filter
+    const float* u = fl + F.src;
+    const float* flt = fl + F.env;
+    for (int k = threadIdx.x; k < M; k += SG_FFT_THREADS) Y[k] = make_float2(u[k] * flt[k], 0.f);
+  }
+  __syncthreads();
+  const float invN2 = 1.f / (float)N2;
+  float* d = fs + F.dst;
+  for (int i = threadIdx.x; i < N; i += SG_FFT_THREADS) {
+    const int n = i < N2 ? i : i - N2;
+    float acc = Y[0].x + ((n & 1) ? -Y[M - 1].x : Y[M - 1].x);
+    float part = 0.f;
+    int e = n;
+    for (int k = 1; k < M; ++k) {
+      part = fmaf(Y[k].x, ti[e].x, part);
+      part = fmaf(-Y[k].y, ti[e].y, part);
+      e += n;
+      if (e >= N2) e -= N2;
+    }
+    acc = fmaf(2.f, part, acc);
+    d[i] = acc * invN2 * han[i];
+  }
+}
+
 }  // namespace
 
 extern "C" __global__ __launch_bounds__(SG_FFT_THREADS) void sg_fft_frames(
@@ -398,6 +462,10 @@ extern "C" __global__ __launch_bounds__(SG_FFT_THREADS) void sg_fft_frames(
   __shared__ SgFrame fr[16];
   const SgFrameGroup G = groups[blockIdx.x];
   const SgFftGeom& g = geoms[G.geom];
+  if (g.kind == SG_FFT_ODD) {  // workgroup-uniform
+    odd_frame(G, frames, g, fl, fs, lds4);
+    return;
+  }
   const int M = g.M, N = g.wl, fb = G.nf;
   const float2* twg = reinterpret_cast<const float2*>(fl + g.tw);
   const float2* twN = twg + M;  // L1/L2 resident (one read per bin pair)
@@ -938,6 +1006,9 @@ extern "C" __global__ __launch_bounds__(256) void sg_mix(const SgMixTile* __rest
 
 // ---------------------------------------------------------------- launchers
 #include "sg_exec.h"
+
+#include <map>
+#include <mutex>
 namespace sg {
 // launch failures (bad configuration, LDS over the opted-in size) are loud
 #define SG_LAUNCHED(name)                                                                       \
@@ -946,15 +1017,24 @@ namespace sg {
     if (_e != hipSuccess) throw SgError(SG_E_DEVICE, std::string("launch " name ": ") + hipGetErrorString(_e)); \
   } while (0)
 
+// Dynamic LDS above 64 KB must be opted into (160 KB per CU on gfx950). The
+// attribute is per device: remember the opted-in size per (kernel, device).
+static void lds_opt_in(const void* fn, int lds_bytes, const char* name) {
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, int> done;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) throw SgError(SG_E_DEVICE, std::string(name) + ": hipGetDevice failed");
+  std::lock_guard<std::mutex> lk(mu);
+  int& have = done[{fn, dev}];
+  if (lds_bytes <= have) return;
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes) != hipSuccess)
+    throw SgError(SG_E_DEVICE, std::string(name) + ": dynamic LDS " + std::to_string(lds_bytes) + " B refused");
+  have = lds_bytes;
+}
+
 void launch_fft_frames(const DevicePlan& D, int64_t g0, int64_t n_groups, int lds_bytes, hipStream_t s) {
   if (n_groups <= 0) return;
-  static int lds_max = 0;
-  if (lds_bytes > lds_max) {  // dynamic LDS above 64 KB must be opted into (160 KB per CU on gfx950)
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&sg_fft_frames), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            lds_bytes) != hipSuccess)
-      throw SgError(SG_E_DEVICE, "sg_fft_frames: dynamic LDS " + std::to_string(lds_bytes) + " B refused");
-    lds_max = lds_bytes;
-  }
+  lds_opt_in(reinterpret_cast<const void*>(&sg_fft_frames), lds_bytes, "sg_fft_frames");
   hipLaunchKernelGGL(sg_fft_frames, dim3((unsigned)n_groups), dim3(SG_FFT_THREADS), lds_bytes, s, D.fgroups + g0,
                      D.frames,
                      D.geoms, D.fl, D.fs);
@@ -962,13 +1042,7 @@ void launch_fft_frames(const DevicePlan& D, int64_t g0, int64_t n_groups, int ld
 }
 void launch_stft_ola(const DevicePlan& D, int64_t s0, int64_t n_segs, int lds_bytes, hipStream_t s) {
   if (n_segs <= 0) return;
-  static int lds_max = 0;
-  if (lds_bytes > lds_max) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&sg_stft_ola), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            lds_bytes) != hipSuccess)
-      throw SgError(SG_E_DEVICE, "sg_stft_ola: dynamic LDS " + std::to_string(lds_bytes) + " B refused");
-    lds_max = lds_bytes;
-  }
+  lds_opt_in(reinterpret_cast<const void*>(&sg_stft_ola), lds_bytes, "sg_stft_ola");
   hipLaunchKernelGGL(sg_stft_ola, dim3((unsigned)(n_segs / SG_FFT_WAVES)), dim3(SG_FFT_WAVES * 64), lds_bytes, s,
                      D.olasegs + s0,
                      D.olas, D.frames, D.geoms, D.fl, D.fs, D.olatilemax);

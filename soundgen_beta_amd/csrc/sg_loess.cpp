@@ -48,16 +48,21 @@ void jacobi_svd3(std::vector<double> (&a)[3], double V[3][3]) {
   }
 }
 
-// local quadratic at vertex v over the nf nearest points: value and slope
-void vertex_fit(const double* x, const double* y, int n, int nf, double f, double v, double& val, double& slope) {
+// local quadratic at vertex v over the nf nearest points: value and slope.
+// Returns false for a zero-width neighbourhood (rho = 0: a vertex on a data
+// point with floor(n f) = 1), where R's tricube weights are 0/0 and the vertex
+// value is NaN.
+bool vertex_fit(const double* x, const double* y, int n, int nf, double f, double v, double& val, double& slope) {
   std::vector<double> d2(n);
   std::vector<int> ord(n);
   for (int i = 0; i < n; ++i) d2[i] = (x[i] - v) * (x[i] - v);
   std::iota(ord.begin(), ord.end(), 0);
   std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return d2[a] < d2[b]; });
   const double rho = d2[ord[nf - 1]] * std::max(1.0, f);
-  if (!(rho > 0))
-    throw SgError(SG_E_UNSUPPORTED, "loess: neighbourhood radius 0 (span too small for the anchors)");
+  if (!(rho > 0)) {
+    val = slope = std::nan("");
+    return false;
+  }
   const size_t m = (size_t)std::max(nf, 3);
   std::vector<double> cols[3];
   for (auto& c : cols) c.assign(m, 0.0);
@@ -111,6 +116,7 @@ void vertex_fit(const double* x, const double* y, int n, int nf, double f, doubl
   }
   val = s0 / colnor[0];
   slope = s1 / colnor[1];
+  return true;
 }
 
 }  // namespace
@@ -126,7 +132,7 @@ double LoessFit::eval(double z) const {
   return phi0 * val[a] + phi1 * val[b] + (psi0 * slope[a] + psi1 * slope[b]) * (v1 - v0);
 }
 
-void loess_fit(const double* x, const double* y, int n, double f, LoessFit& T) {
+bool loess_fit(const double* x, const double* y, int n, double f, LoessFit& T) {
   if (n < 1) throw SgError(SG_E_DOMAIN, "loess: no data");
   if (std::floor(n * f + 1e-5) <= 0) throw SgError(SG_E_DOMAIN, "loess: span is too small");
   const int nf = (int)std::min<double>(n, std::floor(n * f));
@@ -184,7 +190,9 @@ void loess_fit(const double* x, const double* y, int n, double f, LoessFit& T) {
   }
   T.val.resize(T.vx.size());
   T.slope.resize(T.vx.size());
-  for (size_t v = 0; v < T.vx.size(); ++v) vertex_fit(x, y, n, nf, f, T.vx[v], T.val[v], T.slope[v]);
+  bool finite = true;
+  for (size_t v = 0; v < T.vx.size(); ++v) finite &= vertex_fit(x, y, n, nf, f, T.vx[v], T.val[v], T.slope[v]);
+  return finite;
 }
 
 LoessFit smooth_loess(const double* t, const double* v, int64_t n, int64_t len, double duration_ms, bool has_floor,
@@ -214,9 +222,22 @@ LoessFit smooth_loess(const double* t, const double* v, int64_t n, int64_t len, 
     y[i] = ys[ord[i]];
   }
   double span = (1 / (1 + std::exp(duration_ms / 500)) + 0.5) / std::pow(1.1, (double)(n - 3));
+  // smoothContour = try(predict(l, time)); while (try-error) span = span + 0.1
+  // (R/smoothContours.R:133-143). predict()'s .C(C_loess_ifit, ..., vval) stops
+  // on a NaN vertex value (NAOK = FALSE), so a zero-width fit is that error.
+  // Restated, unpinned against R output.
+  for (int k = 0;; ++k) {
+    LoessFit T;
+    if (loess_fit(x.data(), y.data(), (int)x.size(), span, T)) break;
+    if (k == 200) throw SgError(SG_E_DOMAIN, "loess: no span gives a finite fit");
+    span = span + 0.1;
+  }
   for (int iter = 0; iter < 200; ++iter) {
     LoessFit T;
-    loess_fit(x.data(), y.data(), (int)x.size(), span, T);
+    // a zero-width fit inside the valueFloor loop leaves R comparing a
+    // try-error string with valueFloor: not restated
+    if (!loess_fit(x.data(), y.data(), (int)x.size(), span, T))
+      throw SgError(SG_E_UNSUPPORTED, "loess: zero-width fit inside the valueFloor refits");
     bool below = false;
     if (has_floor)
       for (int64_t k = 0; k < len && !below; ++k) below = T.eval((double)(k + 1)) < vfloor - 1e-6;

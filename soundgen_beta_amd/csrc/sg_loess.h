@@ -23,12 +23,14 @@ struct LoessFit {
   double eval(double z) const;         // Hermite interpolation in the leaf cell containing z
 };
 
-// fit; throws SgError for spans R rejects or fits R cannot produce
-void loess_fit(const double* x, const double* y, int n, double f, LoessFit& out);
+// fit; throws SgError for spans R rejects. Returns false when a vertex value
+// is NaN (zero-width neighbourhood), which makes R's predict() stop.
+bool loess_fit(const double* x, const double* y, int n, double f, LoessFit& out);
 
 // getSmoothContour's loess branch: anchor times t (already scaled to [0, 1])
-// and values -> the fit R evaluates on 1..len (refitting with span / 1.1
-// while a value falls below valueFloor - 1e-6). Returns the final fit.
+// and values -> the fit R evaluates on 1..len (span + 0.1 while predict()
+// fails on a NaN vertex, then span / 1.1 while a value falls below
+// valueFloor - 1e-6). Returns the final fit.
 LoessFit smooth_loess(const double* t, const double* v, int64_t n, int64_t len, double duration_ms, bool has_floor,
                       double vfloor);
 

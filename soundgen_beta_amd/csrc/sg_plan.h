@@ -125,7 +125,9 @@ bool plan_noise(Batch& B, Rng& R, int64_t len, const sg_anchors& noiseAnchors, d
                 double attackLen, int wl, double sr, double overlap, const double* filterNoise, int64_t fnc,
                 SgNoiseItem* item);
 // getSpectralEnvelope(), R/sourceSpectrum.R:261-566 (host, fp64), nr x nc column-major
-vec spectral_envelope(Rng& R, int64_t nr, int64_t nc, const sg_formants* F, double formantDep, double rolloffLip,
+// nrd = windowLength_points / 2 as R passes it (x.5 for an odd window: the
+// matrix has as.integer(nrd) rows, bin_width uses nrd)
+vec spectral_envelope(Rng& R, double nrd, int64_t nc, const sg_formants* F, double formantDep, double rolloffLip,
                       const sg_anchors& mouthAnchors, double mouthOpenThres, double openMouthBoost,
                       double vocalTract, double temperature, double formDrift, double formDisp,
                       double formantDepStoch, double smoothLinearFactor, double sr, double speedSound);

@@ -14,12 +14,14 @@
 
 #include "sg_loess.h"
 #include "sg_plan.h"
+#include "sg_prof.h"
 
 namespace sg {
 
 // ------------------------------------------------------------- contours
 bool smooth_contour(const sg_anchors& an, int64_t len, bool thisIsPitch, int method, bool has_floor,
                     double vfloor, bool has_ceil, double vceil, vec& out, double sr) {
+  ProfScope ps(PF_CONTOUR);
   out.clear();
   if (an.n <= 0) return false;
   const int64_t n = an.n;
@@ -233,6 +235,7 @@ void clumper(vec& s, const vec& minLen_in) {
 vec get_rolloff(const vec& pitch, int64_t nH, const vec& rolloff, const vec& rolloffOct, double rolloffParab,
                 double rolloffParabHarm, const vec& rolloffKHz, double baseline, double throwaway, double sr,
                 int64_t& H) {
+  ProfScope ps(PF_ROLLOFF);
   const int64_t nGC = (int64_t)pitch.size();
   if (nH < 1) throw SgError(SG_E_DOMAIN, "getRolloff: nHarmonics < 1");
   vec r(nH * nGC);
@@ -562,6 +565,7 @@ static bool lin_continues(const SgSeg& a, const SgSeg& b) {
 int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_harm_params& P,
                        const sg_anchors& amplAnchors, Rng& R, int64_t out_off, bool dry_run, bool to_fs,
                        int64_t* fs_off) {
+  ProfScope ps(PF_HARM);
   const double sr = P.samplingRate;
   if (len < 2) throw SgError(SG_E_DOMAIN, "generateHarmonics: pitch contour too short");
   vec pitch(pitch_in, pitch_in + len);

@@ -413,7 +413,7 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
           for (double v : mouthA.v) if (v != .5) mouthMoves = true;
           if (mouthMoves) moving = true;
           nInt = moving ? (int64_t)r_round((r_max(ns.t) - r_min(ns.t)) / 10) : 1;
-          envN = spectral_envelope(R, (int64_t)(wlp / 2), nInt, &A.formantsNoise, A.formantDep, A.rolloffLip,
+          envN = spectral_envelope(R, wlp / 2, nInt, &A.formantsNoise, A.formantDep, A.rolloffLip,
                                    mouthA.view(), 0, 0, A.vocalTract, T, A.tempEffects[1], A.tempEffects[2],
                                    A.formantDepStoch, 1, sr, 35400);
         }
@@ -468,15 +468,14 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
       const double fl2 = std::floor((double)Ls / 2);
       if (fl2 < wlp) wlp = fl2;  // persists into later bouts and their noise
       const int wl = (int)wlp;
-      if (wl % 2) throw SgError(SG_E_UNSUPPORTED, "formant filter: odd window length");
       const vec step = r_seq_by(1, (double)std::max<int64_t>(1, Ls - wl), (double)wl - A.overlap * wl / 100);
-      const int64_t nc = (int64_t)step.size(), nr = wl / 2;
+      const int64_t nc = (int64_t)step.size();
       bool moving = formants_moving(Fm);
       bool mouthMoves = false;
       for (double v : mouthA.v) if (v != .5) mouthMoves = true;
       if (mouthA.n() > 0 && mouthMoves) moving = true;
       const int64_t nInt = moving ? nc : 1;
-      const vec env = spectral_envelope(R, nr, nInt, &Fm, A.formantDep, A.rolloffLip, mouthA.view(), 0, 0,
+      const vec env = spectral_envelope(R, (double)wl / 2, nInt, &Fm, A.formantDep, A.rolloffLip, mouthA.view(), 0, 0,
                                         A.vocalTract, T, A.tempEffects[1], A.tempEffects[2], A.formantDepStoch, 1,
                                         sr, 35400);
       int64_t filt_fs = 0, Lf = 0;

@@ -9,6 +9,7 @@
 #include <cstring>
 
 #include "sg_plan.h"
+#include "sg_prof.h"
 
 namespace sg {
 
@@ -30,10 +31,50 @@ int64_t fl_push(Batch& B, const double* v, int64_t n) {
   return o;
 }
 
+// seewave ftwindow: hamming.w (seewave.r:7431-7437), hanning.w (:7444-7450)
+static int64_t push_windows(Batch& B, int wl) {
+  vec win(2 * (size_t)wl);
+  for (int i = 0; i < wl; ++i) {
+    win[i] = 0.54 - 0.46 * std::cos(2 * M_PI * (double)i / (double)(wl - 1));
+    win[wl + i] = 0.5 - 0.5 * std::cos(2 * M_PI * (double)i / (double)(wl - 1));
+  }
+  return fl_push(B, win.data(), (int64_t)win.size());
+}
+
+// odd window length (SG_FFT_ODD, sg_dev.h): forward wl-point and inverse
+// (wl - 1)-point direct DFT tables
+static int geometry_odd(Batch& B, int wl) {
+  SgFftGeom g{};
+  g.wl = wl;
+  g.M = wl / 2;
+  g.kind = SG_FFT_ODD;
+  g.fb = 1;
+  // tables W_wl (wl pairs) and the inverse (2M pairs), M bins, the wl-point frame
+  g.lds_bytes = (int32_t)(((int64_t)wl * 8 + (int64_t)2 * g.M * 8 + (int64_t)g.M * 8 + (int64_t)wl * 4 + 15) / 16 * 16);
+  if (g.lds_bytes > 160 * 1024) throw SgError(SG_E_UNSUPPORTED, "FFT: odd window length exceeds the LDS budget");
+  vec tw(2 * (size_t)wl), ti(2 * (size_t)(2 * g.M));
+  for (int t = 0; t < wl; ++t) {
+    const double a = -2.0 * M_PI * (double)t / (double)wl;
+    tw[2 * t] = std::cos(a);
+    tw[2 * t + 1] = std::sin(a);
+  }
+  for (int t = 0; t < 2 * g.M; ++t) {
+    const double a = 2.0 * M_PI * (double)t / (double)(2 * g.M);
+    ti[2 * t] = std::cos(a);
+    ti[2 * t + 1] = std::sin(a);
+  }
+  g.tw = fl_push(B, tw.data(), (int64_t)tw.size());
+  g.tws = fl_push(B, ti.data(), (int64_t)ti.size());
+  g.win = push_windows(B, wl);
+  B.geoms.push_back(g);
+  return (int)B.geoms.size() - 1;
+}
+
 int geometry(Batch& B, int wl) {
   for (size_t i = 0; i < B.geoms.size(); ++i)
     if (B.geoms[i].wl == wl) return (int)i;
-  if (wl < 4 || wl % 2) throw SgError(SG_E_UNSUPPORTED, "FFT: window length must be even and >= 4");
+  if (wl < 3) throw SgError(SG_E_UNSUPPORTED, "FFT: window length must be >= 3");
+  if (wl % 2) return geometry_odd(B, wl);
   SgFftGeom g{};
   g.wl = wl;
   g.M = wl / 2;
@@ -81,13 +122,7 @@ int geometry(Batch& B, int wl) {
     }
     g.tws = fl_push(B, ts.data(), (int64_t)ts.size());
   }
-  // seewave ftwindow: hamming.w (seewave.r:7431-7437), hanning.w (:7444-7450)
-  vec win(2 * (size_t)wl);
-  for (int i = 0; i < wl; ++i) {
-    win[i] = 0.54 - 0.46 * std::cos(2 * M_PI * (double)i / (double)(wl - 1));
-    win[wl + i] = 0.5 - 0.5 * std::cos(2 * M_PI * (double)i / (double)(wl - 1));
-  }
-  g.win = fl_push(B, win.data(), (int64_t)win.size());
+  g.win = push_windows(B, wl);
   // frames per workgroup: one in-place LDS buffer of fb * M complex points,
   // fb * M <= 8192 (64 KB: two workgroups per CU; sg_fft.hip SG_FFT_SLOTS)
   // wavefront-per-frame kernel when every stage's butterflies fit the
@@ -173,6 +208,7 @@ static int push_ola(Batch& B, int phase, int64_t frames, int64_t nframes, int wl
 
 int plan_filter(Batch& B, int64_t sound, int64_t L, int wl, double overlap, const vec& env, int64_t env_nc,
                 int64_t* out_len, int64_t* out_fs) {
+  ProfScope ps(PF_FILTER);
   const int gi = geometry(B, wl);
   const int64_t nr = wl / 2;
   // step = seq(1, max(1, L - wl), by = wl - overlap * wl / 100)   R/soundgen.R:744-748
@@ -204,6 +240,7 @@ int plan_filter(Batch& B, int64_t sound, int64_t L, int wl, double overlap, cons
 bool plan_noise(Batch& B, Rng& R, int64_t len, const sg_anchors& noiseAnchors, double rolloffNoise,
                 double attackLen, int wl, double sr, double overlap, const double* filterNoise, int64_t fnc,
                 SgNoiseItem* item) {
+  ProfScope ps(PF_NOISE);
   // breathingStrength = getSmoothContour(noiseAnchors, len, valueFloor = -120, valueCeiling = 40)
   //   R/source.R:70-81 (NA when len == 0 or anchors NA)
   if (noiseAnchors.n <= 0 || len <= 0) return false;
@@ -228,8 +265,14 @@ bool plan_noise(Batch& B, Rng& R, int64_t len, const sg_anchors& noiseAnchors, d
     for (int64_t c = 0; c < nc; ++c) fri[c] = r_round(s[c]);
   }
   // z1 = complex(real = runif(nr * nc)), column-major: bin fastest   R/source.R:111
+  // (nr = wl / 2 is x.5 for an odd wl: floor(nr * nc) draws, matrix(nrow = nr)
+  // keeps as.integer(nr) rows of them)
   vec u((size_t)(nr * nc));
-  for (auto& x : u) x = R.unif();
+  const int64_t ndraw = (int64_t)((double)wl / 2 * (double)nc);
+  for (int64_t q = 0; q < ndraw; ++q) {
+    const double x = R.unif();
+    if (q < nr * nc) u[q] = x;
+  }
   const int64_t u_off = fl_push(B, u.data(), (int64_t)u.size());
   const bool fused = fusable(B.geoms[gi], (double)wl * (100 - overlap) / 100);
   const int64_t fr = fused ? 0 : fs_alloc(B, nc * wl);
@@ -294,10 +337,12 @@ vec col_upsample(const double* t, const double* y, int64_t np, int64_t nPoints, 
 }
 }  // namespace
 
-vec spectral_envelope(Rng& R, int64_t nr, int64_t nc, const sg_formants* F, double formantDep, double rolloffLip,
+vec spectral_envelope(Rng& R, double nrd, int64_t nc, const sg_formants* F, double formantDep, double rolloffLip,
                       const sg_anchors& mouthAnchors, double mouthOpenThres, double openMouthBoost,
                       double vocalTract, double temperature, double formDrift, double formDisp,
                       double formantDepStoch, double slf, double sr, double speedSound) {
+  ProfScope ps(PF_ENVELOPE);
+  const int64_t nr = (int64_t)nrd;  // matrix(nrow = nr): as.integer; bin_width keeps nrd
   int nF = F ? F->n_formants : 0;
   bool vtNull = std::isnan(vocalTract);
   double VT = vocalTract;
@@ -398,7 +443,7 @@ vec spectral_envelope(Rng& R, int64_t nr, int64_t nc, const sg_formants* F, doub
         }
     }
     // Hz -> bins   R/sourceSpectrum.R:417-424
-    const double bw = sr / 2 / (double)nr;
+    const double bw = sr / 2 / nrd;
     for (auto& tr : fu)
       for (int64_t c = 0; c < nc; ++c) {
         tr.freq[c] = (tr.freq[c] - bw / 2) / bw + 1;

@@ -282,10 +282,10 @@ def istft(z, ovlp, wl):
     win = hanning(wl)
     for f in range(nc):
         X = np.concatenate([z[:, f], [np.real(z[nr - 1, f])], np.conj(z[1:, f][::-1])])
-        y = np.real(np.fft.ifft(X)) * wl / wl  # R: Re(fft(X, inverse = TRUE)) / wl
+        y = np.real(np.fft.ifft(X))  # R: Re(fft(X, inverse = TRUE) / length(X))
         b = f * h
         i0 = int(b)
-        seg = y * win
+        seg = np.resize(y, wl) * win  # xprim * win recycles xprim (length 2 nr = wl - 1 for an odd wl)
         end = min(len(x), i0 + wl)
         x[i0:end] += seg[: end - i0]
     return x * h / np.sum(win ** 2)
@@ -323,6 +323,8 @@ def _loess_vertex_fit(x, y, span, v):
     d2 = (x - v) ** 2
     order = np.argsort(d2, kind="stable")[:nf]
     rho = d2[order[-1]] * max(1.0, span)
+    if not rho > 0:  # zero-width neighbourhood: R's weights are 0/0
+        return np.nan, np.nan
     r = np.sqrt(d2[order] / rho)
     w = np.sqrt((1 - r ** 3) ** 3)
     dx = x[order] - v
@@ -346,6 +348,8 @@ def loess(x, y, span, z):
     y = np.asarray(y, float)
     vx = _loess_vertices(x, span)
     fits = np.array([_loess_vertex_fit(x, y, span, v) for v in vx])
+    if np.isnan(fits).any():  # predict(): .C refuses the NaN vertex values
+        raise FloatingPointError("NA/NaN/Inf in foreign function call")
     z = np.asarray(z, float)
     i = np.clip(np.searchsorted(vx, z, side="left") - 1, 0, len(vx) - 2)
     v0, v1 = vx[i], vx[i + 1]
@@ -379,6 +383,12 @@ def smooth_contour_loess(time, value, len_, sr, floor=None, ceiling=None, pitch=
     ys = np.array([pos[k] for k in xs])
     span = (1 / (1 + np.exp(len_ / sr * 1000 / 500)) + 0.5) / 1.1 ** (len(t) - 3)
     z = np.arange(1, len_ + 1, dtype=float)
+    while True:  # try(predict(...)); while (try-error) span = span + 0.1
+        try:
+            out = loess(xs, ys, span, z)
+            break
+        except FloatingPointError:
+            span = span + 0.1
     while True:
         out = loess(xs, ys, span, z)
         if floor is None or not np.any(out < floor - 1e-6):

@@ -104,3 +104,23 @@ def test_c2_full_batch_properties():
         # <= 1 exactly up to rounding; a fade can shave the largest peak, the next
         # peak of a sampled sinusoid is within ~1e-5 of it
         assert 1.0 - 1e-4 <= float(seg.max()) <= 1.0 + 1e-6, (i, float(seg.max()))
+
+
+def test_api_plans_once_with_r_rng(oracle):
+    """api.soundgen / api.generateHarmonics plan a call once: a
+    stochastic 2.5 s sound drawn from R's generator (RRng, set.seed) matches the
+    oracle fed by a fresh RRng with the same seed, sample for sample."""
+    from soundgen_beta_amd import api
+    from soundgen_beta_amd.rrng import RRng
+    args = dict(sylLen=2500, samplingRate=44100, temperature=0.1, pitchAnchors=[180, 240], jitterDep=1,
+                shimmerDep=5, nonlinBalance=50, subDep=60, addSilence=0)
+    y = api.soundgen(rng=RRng(42), **args)
+    ref = oracle.soundgen(rng=RRng(42), **args)
+    assert len(y) == len(ref) > 1.5 * 44100
+    assert _rms(y, ref) <= TOL
+    prm = dict(samplingRate=44100, temperature=0.1, jitterDep=1, shimmerDep=5, pitchFloor=50)
+    p = np.full(7000, 150.0)
+    y = api.generateHarmonics(p, rng=RRng(9), **prm)
+    ref = oracle.generate_harmonics(p, rng=RRng(9), **prm)
+    assert len(y) == len(ref)
+    assert _rms(y, ref) <= TOL

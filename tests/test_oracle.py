@@ -139,12 +139,14 @@ def test_generate_harmonics_simple_vs_twin(oracle, name, sr):
 
 def test_istft_stft_vs_numpy(oracle):
     rng = np.random.default_rng(3)
-    for wl in (64, 440, 800):
+    # odd wl (windowLength_points = floor(L / 2) of a short sound): wl %/% 2 bins,
+    # a (wl - 1)-point inverse recycled against the wl-point window, fractional hops
+    for wl in (64, 440, 800, 65, 441, 2203):
         nr, nc = wl // 2, 7
         z = rng.normal(size=(nr, nc)) + 1j * rng.normal(size=(nr, nc))
         np.testing.assert_allclose(oracle.istft(z, 75, wl), T.istft(z, 75, wl), rtol=1e-9, atol=1e-12)
         wave = rng.normal(size=wl * 4)
-        step = np.arange(1, len(wave) - wl, wl // 4, dtype=float)
+        step = np.arange(1, len(wave) - wl, wl * 0.25, dtype=float)
         np.testing.assert_allclose(oracle.stft(wave, wl, step), T.stft(wave, wl, step), rtol=1e-9, atol=1e-12)
 
 
@@ -170,6 +172,8 @@ def test_loess_vs_twin(oracle):
         try:
             a = oracle.loess(x, y, span, z)
         except Exception:  # degenerate neighbourhood (nf = 1 at a data point)
+            with pytest.raises(FloatingPointError):  # the twin's predict() stops too
+                T.loess(x, y, span, z)
             continue
         np.testing.assert_allclose(a, T.loess(x, y, span, z), rtol=0, atol=1e-9 * max(1, np.abs(y).max()))
         checked += 1
@@ -180,6 +184,12 @@ def test_loess_vs_twin(oracle):
     ({"time": [0, .1, .9, 1], "value": [100, 150, 135, 100]}, 1050, 3500, dict(pitch=True, floor=50, ceiling=3500)),
     ({"time": [0, .3, .6, 1], "value": [0, 40, 10, 20]}, 5000, 16000, dict(floor=0)),
     ({"time": [0, 200, 500, 900, 1000], "value": [-30, -10, -40, -20, -25]}, 16000, 16000, dict(floor=-120, ceiling=40)),
+    # zero-width neighbourhoods (floor(n span) = 1): R's span + 0.1 retry
+    # (R/smoothContours.R:135-143); the vignette's own example
+    # (vignettes/sound_generation.Rmd:129-132), 2 s: span 0.518 -> 0.718
+    ({"time": [0, .1, 1], "value": [350, 700, 350]}, 7000, 3500, dict(pitch=True, floor=50, ceiling=3500)),
+    ({"time": [0, .5, 1], "value": [150, 420, 300]}, 10500, 3500, dict(pitch=True, floor=50, ceiling=3500)),
+    ({"time": [0, .2, .7, 1], "value": [90, 250, 180, 120]}, 14000, 3500, dict(pitch=True, floor=50, ceiling=3500)),
 ])
 def test_smooth_contour_loess_vs_twin(oracle, anchors, L, sr, kw):
     a = oracle.smooth_contour(anchors, L, thisIsPitch=kw.get("pitch", False), valueFloor=kw.get("floor"),

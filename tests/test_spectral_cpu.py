@@ -84,7 +84,18 @@ def test_c5_plan_lengths_match_oracle(oracle):
     calls = bench.c5_calls(40)
     plan = batch.Plan(calls, None)
     for i, c in enumerate(calls):
-        if plan.status[i]:
-            assert ("loess" in plan.message(i)) or ("odd window" in plan.message(i)), plan.message(i)
-            continue
+        assert plan.status[i] == 0, (i, c["preset"], plan.message(i))
         assert plan.lengths[i] == len(bench.oracle_call(oracle, c)), (i, c["preset"])
+
+
+def test_c4_c5_plan_nothing_refused():
+    """Every C4 call and 1024 C5 calls plan (no SG_E_UNSUPPORTED): zero-width
+    loess neighbourhoods take R's span + 0.1 retry, odd windows are planned."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    for calls in (bench.c4_calls(512), bench.c5_calls(1024)):
+        plan = batch.Plan(calls, None)
+        bad = np.nonzero(plan.status)[0]
+        assert len(bad) == 0, [(int(i), plan.message(int(i))) for i in bad[:5]]
