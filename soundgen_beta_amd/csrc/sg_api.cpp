@@ -3,8 +3,13 @@
 // No C++ exception crosses this boundary.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstring>
+#include <exception>
 #include <memory>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -87,6 +92,186 @@ struct Checkpoint {
   }
 };
 
+// Plan calls [c0, c1) into B (empty), output slots from offset 0.
+void plan_range(sg::Batch& B, const sg_call_desc* calls, int64_t c0, int64_t c1) {
+  const int64_t n = c1 - c0;
+  B.call_len.assign(n, 0);
+  B.call_off.assign(n, 0);
+  B.call_status.assign(n, 0);
+  B.call_msg.assign(n, "");
+  int64_t off = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const sg_call_desc& d = calls[c0 + i];
+    Checkpoint cp(B);
+    const int first_syl = (int)B.syls.size();
+    try {
+      sg::Rng R;
+      R.s = &d.random;
+      int64_t L = 0;
+      if (d.kind == SG_CALL_HARMONICS) {
+        if (!d.pitch || !d.harm) throw sg::SgError(SG_E_ARG, "harmonics call without pitch/params");
+        L = sg::plan_harmonics(B, d.pitch, d.pitch_len, *d.harm, d.amplAnchors, R, off, false);
+        sg::tile_syllables(B, first_syl);
+      } else if (d.kind == SG_CALL_SOUNDGEN) {
+        if (!d.args) throw sg::SgError(SG_E_ARG, "soundgen call without args");
+        L = sg::plan_soundgen(B, *d.args, R, off, first_syl);
+        sg::tile_syllables(B, first_syl);
+      } else {
+        throw sg::SgError(SG_E_ARG, "unknown call kind");
+      }
+      B.call_off[i] = off;
+      B.call_len[i] = L;
+      off += (L + 63) / 64 * 64;  // 256-B aligned call slots
+    } catch (const sg::SgError& e) {
+      cp.restore(B);
+      sg::restore_soundgen_tail(B, first_syl);
+      B.call_status[i] = e.code;
+      B.call_msg[i] = e.what();
+      B.call_off[i] = off;
+      B.call_len[i] = 0;
+    }
+  }
+  B.total_out = off;
+}
+
+// Host threads for planning: SG_PLAN_THREADS, else the hardware threads capped
+// at 16 (a GPU box's CPU share); one thread for small batches.
+int plan_threads(int64_t n_calls) {
+  int t = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+  if (const char* e = std::getenv("SG_PLAN_THREADS")) t = std::max(1, std::atoi(e));
+  return (int)std::min<int64_t>(t, std::max<int64_t>(1, n_calls / 4));
+}
+
+// Where one part's arrays land in the merged batch.
+struct PartBase {
+  int64_t out, fs, fl, w, amp, knot, ck, task, seg, syl, piece, st, item, copy, call, epoch;
+  int64_t fr[2], ola[2], mix[2];
+};
+
+// Concatenate per-chunk batches in call order, rebasing every cross-reference
+// (scratch, arena and output offsets, table indices). Bases are prefix sums
+// of the parts' sizes; geometries are matched by window length (a new one
+// keeps its tables, which move with the part's fl). The parts are rebased and
+// copied in parallel, each freed once copied.
+void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
+  const size_t np = parts.size();
+  std::vector<PartBase> base(np);
+  std::vector<std::vector<int32_t>> gmap(np);
+  PartBase c{};
+  for (size_t k = 0; k < np; ++k) {
+    sg::Batch& S = parts[k];
+    base[k] = c;
+    gmap[k].resize(S.geoms.size());
+    for (size_t g = 0; g < S.geoms.size(); ++g) {
+      int32_t j = 0;
+      while (j < (int32_t)D.geoms.size() && D.geoms[j].wl != S.geoms[g].wl) ++j;
+      if (j == (int32_t)D.geoms.size()) {
+        SgFftGeom G = S.geoms[g];
+        G.tw += c.fl; G.tws += c.fl; G.win += c.fl;
+        D.geoms.push_back(G);
+      }
+      gmap[k][g] = j;
+    }
+    c.out += S.total_out; c.fs += S.fs_total; c.fl += (int64_t)S.fl.size();
+    c.w = (c.w + S.w_total + 3) / 4 * 4;  // keeps the parts' 16-B alignment of epoch waveforms
+    c.amp += (int64_t)S.amps.size(); c.knot += (int64_t)S.knots.size(); c.ck += (int64_t)S.cknots.size();
+    c.task += (int64_t)S.tasks.size(); c.seg += (int64_t)S.segs.size(); c.syl += (int64_t)S.syls.size();
+    c.piece += (int64_t)S.pieces.size(); c.st += (int64_t)S.syl_tiles.size(); c.item += (int64_t)S.items.size();
+    c.copy += (int64_t)S.copies.size(); c.call += (int64_t)S.call_len.size(); c.epoch += (int64_t)S.epochs.size();
+    for (int ph = 0; ph < 2; ++ph) {
+      c.fr[ph] += (int64_t)S.frames[ph].size(); c.ola[ph] += (int64_t)S.olas[ph].size();
+      c.mix[ph] += (int64_t)S.mixes[ph].size();
+    }
+    D.harm_samples += S.harm_samples; D.harm_terms += S.harm_terms; D.harm_amp_bytes += S.harm_amp_bytes;
+    D.fft_frames += S.fft_frames;
+  }
+  D.total_out = c.out; D.fs_total = c.fs; D.w_total = c.w;
+  D.call_len.resize(c.call); D.call_off.resize(c.call); D.call_status.resize(c.call); D.call_msg.resize(c.call);
+  D.segs.resize(c.seg); D.epochs.resize(c.epoch); D.knots.resize(c.knot); D.amps.resize(c.amp);
+  D.tasks.resize(c.task); D.pieces.resize(c.piece); D.syls.resize(c.syl); D.syl_tiles.resize(c.st);
+  D.cknots.resize(c.ck); D.fl.resize(c.fl); D.items.resize(c.item); D.copies.resize(c.copy);
+  for (int ph = 0; ph < 2; ++ph) {
+    D.frames[ph].resize(c.fr[ph]); D.frame_geom[ph].resize(c.fr[ph]);
+    D.olas[ph].resize(c.ola[ph]); D.mixes[ph].resize(c.mix[ph]);
+  }
+  auto put = [](auto& dst, auto& src, int64_t at) {
+    std::copy(src.begin(), src.end(), dst.begin() + at);
+    std::remove_reference_t<decltype(src)>().swap(src);
+  };
+  auto one = [&](size_t k) {
+    sg::Batch& S = parts[k];
+    const PartBase& b = base[k];
+    auto ck = [&](SgContour& x) { if (x.kind == 3) x.k_off += b.ck; };
+    for (size_t i = 0; i < S.call_len.size(); ++i) {
+      D.call_len[b.call + i] = S.call_len[i];
+      D.call_off[b.call + i] = S.call_off[i] + b.out;
+      D.call_status[b.call + i] = S.call_status[i];
+      D.call_msg[b.call + i] = std::move(S.call_msg[i]);
+    }
+    for (auto& e : S.epochs) {
+      e.w_off += b.w; e.amp_off += b.amp; e.da_off += b.amp; e.knot_off += b.knot;
+      e.seg_off += (int32_t)b.seg; e.syl += (int32_t)b.syl;
+    }
+    for (auto& t : S.tasks) { t.w_off += b.w; t.a_off += b.amp; t.d_off += b.amp; t.syl += (int32_t)b.syl; }
+    for (auto& p : S.pieces)
+      for (int q = 0; q < (p.nterms < 0 ? 1 : p.nterms); ++q) p.t[q].src += b.w;
+    for (auto& s : S.syls) {
+      s.out_off += s.dst_fs ? b.fs : b.out;
+      s.piece0 += (int32_t)b.piece; s.max_slot += (int32_t)b.syl; s.task0 += b.task;
+      ck(s.env);
+      if (s.drift.nk > 0) s.drift.k_off += b.ck;
+    }
+    for (auto& t : S.syl_tiles) {
+      t.syl += (int32_t)b.syl; t.piece += (int32_t)b.piece;
+      for (int w = 0; w < 4; ++w) t.wpiece[w] += (int32_t)b.piece;
+    }
+    for (int ph = 0; ph < 2; ++ph) {
+      for (auto& f : S.frames[ph]) {
+        f.src += ph == 0 ? b.fl : b.fs;  // noise: uniforms in fl; filter: the sound in fs
+        f.env += b.fl;
+        if (f.dst >= 0) f.dst += b.fs;
+      }
+      for (auto& g : S.frame_geom[ph]) g = gmap[k][g];
+      for (auto& o : S.olas[ph]) {
+        o.fidx += (int32_t)b.fr[ph];
+        if (!o.fused) o.frames += b.fs;
+        o.out += b.fs;
+      }
+      for (auto& m : S.mixes[ph]) {
+        m.dst += m.to_fs ? b.fs : b.out;
+        if (m.base_kind != SG_BASE_NONE) m.base += b.fs;
+        if (m.base_kind == SG_BASE_NORM) m.base_ola += (int32_t)b.ola[1];
+        m.item0 += (int32_t)b.item;
+        if (m.am_lo > 0) m.am_tab += b.fl;
+        ck(m.mult);
+      }
+    }
+    for (auto& it : S.items) {
+      it.raw += b.fs;
+      if (it.flags & SG_ITEM_FILTER_OLA) it.ola += (int32_t)b.ola[1];
+      else if (it.ola >= 0) it.ola += (int32_t)b.ola[0];
+      ck(it.strength);
+    }
+    for (auto& x : S.copies) { x.fl_off += b.fl; x.fs_off += b.fs; }
+    put(D.segs, S.segs, b.seg); put(D.epochs, S.epochs, b.epoch); put(D.knots, S.knots, b.knot);
+    put(D.amps, S.amps, b.amp); put(D.tasks, S.tasks, b.task); put(D.pieces, S.pieces, b.piece);
+    put(D.syls, S.syls, b.syl); put(D.syl_tiles, S.syl_tiles, b.st); put(D.cknots, S.cknots, b.ck);
+    put(D.fl, S.fl, b.fl); put(D.items, S.items, b.item); put(D.copies, S.copies, b.copy);
+    for (int ph = 0; ph < 2; ++ph) {
+      put(D.frames[ph], S.frames[ph], b.fr[ph]); put(D.frame_geom[ph], S.frame_geom[ph], b.fr[ph]);
+      put(D.olas[ph], S.olas[ph], b.ola[ph]); put(D.mixes[ph], S.mixes[ph], b.mix[ph]);
+    }
+    S = sg::Batch();
+  };
+  std::atomic<size_t> next{0};
+  auto work = [&]() {
+    for (size_t k; (k = next.fetch_add(1)) < np;) one(k);
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < threads; ++t) pool.emplace_back(work);
+  work();
+  for (auto& t : pool) t.join();
+}
 }  // namespace
 
 extern "C" {
@@ -127,43 +312,43 @@ int sg_plan_batch(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, sg_pl
   return guarded(ctx, [&]() {
     auto P = std::make_unique<sg_plan>();
     sg::Batch& B = P->B;
-    B.call_len.assign(n_calls, 0);
-    B.call_off.assign(n_calls, 0);
-    B.call_status.assign(n_calls, 0);
-    B.call_msg.assign(n_calls, "");
-    int64_t off = 0;
-    for (int64_t c = 0; c < n_calls; ++c) {
-      const sg_call_desc& d = calls[c];
-      Checkpoint cp(B);
-      const int first_syl = (int)B.syls.size();
-      try {
-        sg::Rng R;
-        R.s = &d.random;
-        int64_t L = 0;
-        if (d.kind == SG_CALL_HARMONICS) {
-          if (!d.pitch || !d.harm) throw sg::SgError(SG_E_ARG, "harmonics call without pitch/params");
-          L = sg::plan_harmonics(B, d.pitch, d.pitch_len, *d.harm, d.amplAnchors, R, off, false);
-          sg::tile_syllables(B, first_syl);
-        } else if (d.kind == SG_CALL_SOUNDGEN) {
-          if (!d.args) throw sg::SgError(SG_E_ARG, "soundgen call without args");
-          L = sg::plan_soundgen(B, *d.args, R, off, first_syl);
-          sg::tile_syllables(B, first_syl);
-        } else {
-          throw sg::SgError(SG_E_ARG, "unknown call kind");
+    // Calls are independent and each reads its own injected draws, so chunks of
+    // calls are planned on host threads into private batches and concatenated in
+    // call order (the result equals serial planning). Draw callbacks (R's RNG
+    // through the shim, or one generator shared by the batch) are a single
+    // sequential stream: such batches plan on the calling thread.
+    bool callbacks = false;
+    for (int64_t c = 0; c < n_calls && !callbacks; ++c)
+      callbacks = calls[c].random.norm_cb || calls[c].random.unif_cb || calls[c].random.gamma_cb;
+    const int threads = callbacks ? 1 : plan_threads(n_calls);
+    if (threads <= 1) {
+      plan_range(B, calls, 0, n_calls);
+    } else {
+      const int64_t nchunk = std::min<int64_t>(n_calls, (int64_t)threads * 8);
+      std::vector<sg::Batch> parts((size_t)nchunk);
+      std::vector<std::exception_ptr> errs((size_t)nchunk);
+      std::atomic<int64_t> next{0};
+      auto work = [&]() {
+        for (int64_t k; (k = next.fetch_add(1)) < nchunk;) {
+          try {
+            plan_range(parts[k], calls, k * n_calls / nchunk, (k + 1) * n_calls / nchunk);
+          } catch (...) {
+            errs[k] = std::current_exception();
+          }
         }
-        B.call_off[c] = off;
-        B.call_len[c] = L;
-        off += (L + 63) / 64 * 64;  // 256-B aligned call slots
-      } catch (const sg::SgError& e) {
-        cp.restore(B);
-        sg::restore_soundgen_tail(B, first_syl);
-        B.call_status[c] = e.code;
-        B.call_msg[c] = e.what();
-        B.call_off[c] = off;
-        B.call_len[c] = 0;
-      }
+      };
+      std::vector<std::thread> pool;
+      for (int t = 1; t < threads; ++t) pool.emplace_back(work);
+      work();
+      for (auto& t : pool) t.join();
+      for (auto& e : errs)
+        if (e) std::rethrow_exception(e);
+      const auto tm = std::chrono::steady_clock::now();
+      merge_parts(B, parts, threads);
+      if (sg::g_prof_on)
+        std::fprintf(stderr, "sg_plan_prof merge (%d threads) %.3f s\n", threads,
+                     std::chrono::duration<double>(std::chrono::steady_clock::now() - tm).count());
     }
-    B.total_out = off;
     {
       sg::ProfScope ps(sg::PF_FINALIZE);
       sg::finalize_plan(B);
@@ -176,6 +361,13 @@ int sg_plan_batch(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, sg_pl
       static const char* names[] = {"harmonics", "rolloff", "contour", "envelope", "noise", "filter", "finalize", "finalize_spec"};
       for (int i = 0; i < sg::PF_N; ++i)
         std::fprintf(stderr, "sg_plan_prof %-14s %.3f s\n", names[i], sg::g_prof_ns[i].exchange(0) * 1e-9);
+      std::fprintf(stderr, "sg_plan_prof host MB: fl %.1f amps %.1f knots %.1f cknots %.1f tasks %.1f segs %.1f "
+                   "frames %.1f pieces %.1f syl_tiles %.1f; scratch MB: fs %.1f w %.1f\n",
+                   B.fl.size() * 4e-6, B.amps.size() * 4e-6, B.knots.size() * 8e-6, B.cknots.size() * 8e-6,
+                   B.tasks.size() * sizeof(SgWTask) * 1e-6, B.segs.size() * sizeof(SgSeg) * 1e-6,
+                   (B.frames[0].size() + B.frames[1].size()) * sizeof(SgFrame) * 1e-6,
+                   B.pieces.size() * sizeof(SgPiece) * 1e-6, B.syl_tiles.size() * sizeof(SgSylTile) * 1e-6,
+                   B.fs_total * 4e-6, B.w_total * 4e-6);
     }
     *out = P.release();
     return SG_OK;

@@ -3,6 +3,8 @@
 // crossing trims, output lengths) is done here in fp64, bit-exact with R.
 #pragma once
 #include <cstdint>
+#include <memory>
+#include <utility>
 #include <vector>
 
 #include "sg_dev.h"
@@ -10,6 +12,24 @@
 #include "soundgen_hip.h"
 
 namespace sg {
+
+// Allocator whose resize() leaves new elements default-initialised (no zero
+// fill): the planner's bulk arrays are always written after they grow, and the
+// merged batch is filled by parallel copies (first touch on the copying thread).
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind { using other = NoInitAlloc<U>; };
+  NoInitAlloc() = default;
+  template <class U>
+  NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+  template <class U, class... A>
+  void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
+  template <class U>
+  void construct(U* p) noexcept { ::new ((void*)p) U; }
+};
+template <class T>
+using bulk = std::vector<T, NoInitAlloc<T>>;
 
 struct DeviceArrays;  // sg_api.cpp
 
@@ -28,20 +48,20 @@ struct Slice {
 
 struct Batch {
   // ---- harmonic source ----
-  std::vector<SgSeg> segs;
-  std::vector<SgEpoch> epochs;
-  std::vector<double> knots;
-  std::vector<float> amps;
-  std::vector<SgWTask> tasks;
-  std::vector<SgPiece> pieces;
+  bulk<SgSeg> segs;
+  bulk<SgEpoch> epochs;
+  bulk<double> knots;
+  bulk<float> amps;
+  bulk<SgWTask> tasks;
+  bulk<SgPiece> pieces;
   std::vector<SgSyllable> syls;
-  std::vector<SgSylTile> syl_tiles;
+  bulk<SgSylTile> syl_tiles;
   std::vector<SgSylTile> fin_tiles;    // derived (finalize_plan): syl_tiles the fast path does not take
   std::vector<SgCopyTile> copy_tiles;  // derived (finalize_plan): fast-path finalize tiles
   std::vector<SgSylTile> ptiles;   // tiles over multi-term (crossfade) pieces
   std::vector<Slice> slices;
   // ---- spectral part (noise, formant filter, assembly) ----
-  std::vector<float> fl;                 // host-initialised floats (windows, twiddles, uniforms, envelopes, ...)
+  bulk<float> fl;                 // host-initialised floats (windows, twiddles, uniforms, envelopes, ...)
   int64_t fs_total = 0;                  // scratch floats (frames, sounds, raw noise)
   std::vector<SgFftGeom> geoms;
   std::vector<SgFrame> frames[2];        // [0] noise frames, [1] filter frames
@@ -66,7 +86,7 @@ struct Batch {
   std::vector<SgMix> mixes_dev;
   std::vector<SgMixTile> mixtiles;
   int64_t mixtile_split = 0;
-  std::vector<double> cknots;   // contour / linear knot data
+  bulk<double> cknots;   // contour / linear knot data
   int64_t w_total = 0;          // epoch-waveform scratch (floats)
   // ---- per call ----
   std::vector<int64_t> call_len, call_off;

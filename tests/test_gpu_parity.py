@@ -124,3 +124,26 @@ def test_api_plans_once_with_r_rng(oracle):
     ref = oracle.generate_harmonics(p, rng=RRng(9), **prm)
     assert len(y) == len(ref)
     assert _rms(y, ref) <= TOL
+
+
+def test_parallel_plan_output_byte_equal(monkeypatch):
+    """A batch planned on 7 host threads (chunks concatenated by merge_parts)
+    synthesizes exactly the bytes of the same batch planned serially."""
+    import torch
+    from test_planner import _mixed_calls
+    from soundgen_beta_amd import batch, native
+    calls = _mixed_calls()
+    ctx = native.default_context(0)
+    outs = []
+    for t in ("1", "7"):
+        monkeypatch.setenv("SG_PLAN_THREADS", t)
+        plan = batch.Plan(calls, ctx)
+        plan.upload()
+        out = torch.zeros(plan.total, dtype=torch.float32, device="cuda")
+        plan.execute(out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        outs.append((plan.offsets.copy(), plan.lengths.copy(), out.cpu().numpy()))
+        plan.close()
+    (o1, l1, y1), (o7, l7, y7) = outs
+    assert (o1 == o7).all() and (l1 == l7).all()
+    assert np.array_equal(y1.view(np.uint32), y7.view(np.uint32))

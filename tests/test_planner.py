@@ -88,3 +88,27 @@ def test_rng_callbacks_follow_the_same_draw_order(oracle):
     plan = batch.Plan([{"kind": "harmonics", "pitch": p, "params": prm, "rng": np.random.default_rng(5)}], None)
     ref = oracle.generate_harmonics(p, rng=np.random.default_rng(5), **prm)
     assert plan.status[0] == 0 and plan.lengths[0] == len(ref)
+
+
+def _mixed_calls(n5=96):
+    import bench
+    calls = bench.c5_calls(n5) + bench.c4_calls(8) + bench.c2_calls(8)
+    bad = {"kind": "harmonics", "pitch": np.full(1, 150.0), "params": C2}  # refused slot in the middle
+    return calls[:40] + [bad] + calls[40:]
+
+
+def test_parallel_planning_equals_serial(monkeypatch):
+    """sg_plan_batch plans chunks of calls on host threads and concatenates them
+    (sg_api.cpp merge_parts); lengths, offsets, statuses and kernel work must be
+    exactly those of serial planning."""
+    calls = _mixed_calls()
+    monkeypatch.setenv("SG_PLAN_THREADS", "1")
+    p1 = batch.Plan(calls, None)
+    monkeypatch.setenv("SG_PLAN_THREADS", "7")
+    p7 = batch.Plan(calls, None)
+    assert (p1.status == p7.status).all() and p1.status[40] == -2
+    assert (p1.lengths == p7.lengths).all() and (p1.offsets == p7.offsets).all()
+    assert p1.total == p7.total
+    s1, s7 = p1.stats(), p7.stats()
+    for k in ("harm_samples", "harm_terms", "harm_amp_bytes", "fft_frames", "stft_samples", "stft_bytes"):
+        assert s1[k] == s7[k], k
