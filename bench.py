@@ -92,16 +92,16 @@ def c5_calls(n_calls, rank=0):
     pitch anchor values x 2^U(-0.5, 0.5), samplingRate 44100, addSilence 0, the
     preset's own temperature. Random draws come from one shared pre-drawn stream
     (every call reads it from the start; synthetic data)."""
-    import copy
     from soundgen_beta_amd import presets as P
     rng = _rng(rank, 5)
     names = P.names()
+    base = {k: P.args(*k) for k in names}  # one copy per preset: calls share its formant lists
     Z = rng.standard_normal(200000)
     U = rng.uniform(size=4000000)
     calls = []
     for i in range(n_calls):
         spk, nm = names[int(rng.integers(len(names)))]
-        a = copy.deepcopy(P.args(spk, nm))
+        a = dict(base[(spk, nm)])
         a["sylLen"] = float(np.clip(a.get("sylLen", 300) * rng.uniform(0.5, 2), 20, 5000))
         pa = a.get("pitchAnchors", "default")
         f = 2 ** rng.uniform(-0.5, 0.5)

@@ -77,12 +77,13 @@ def getSpectralEnvelope(nr, nc, formants=None, formantDep=1, rolloffLip=6, mouth
     rnd = h.random(normals, uniforms, rng)
     out = np.zeros(int(nr) * int(nc))
     vt = float("nan") if vocalTract is None else float(vocalTract)
-    # host-side computation in the library (no device context needed)
-    native.check(native.lib().sg_spectral_envelope(None, int(nr), int(nc), C.byref(F), formantDep, rolloffLip,
+    # tracks and draws on the host, the nr x nc matrix on the GPU (sg_spec_env, fp32)
+    ctx = _ctx(device)
+    native.check(native.lib().sg_spectral_envelope(ctx.ptr, int(nr), int(nc), C.byref(F), formantDep, rolloffLip,
                                                    h.anchors(rargs.as_anchors(mouthAnchors)), mouthOpenThres,
                                                    openMouthBoost, vt, temperature, formDrift, formDisp,
                                                    formantDepStoch, smoothLinearFactor, samplingRate, speedSound,
-                                                   C.byref(rnd), _abi.dptr(out)))
+                                                   C.byref(rnd), _abi.dptr(out)), ctx.ptr)
     return out.reshape(int(nc), int(nr)).T
 
 

@@ -69,14 +69,15 @@ int guarded(sg_ctx* ctx, F&& f) {
 // Rolls a Batch back to a checkpoint when planning one call fails.
 struct Checkpoint {
   size_t segs, epochs, knots, amps, tasks, pieces, syls, syl_tiles, cknots, fl, items;
-  size_t frames[2], olas[2], mixes[2], copies;
-  int64_t w_total, harm_samples, harm_terms, harm_amp_bytes, fft_frames, fs_total;
+  size_t frames[2], olas[2], mixes[2], copies, eterms, ecols, envjobs;
+  int64_t w_total, harm_samples, harm_terms, harm_amp_bytes, fft_frames, fs_total, fe_total;
   explicit Checkpoint(const sg::Batch& B)
       : segs(B.segs.size()), epochs(B.epochs.size()), knots(B.knots.size()), amps(B.amps.size()),
         tasks(B.tasks.size()), pieces(B.pieces.size()), syls(B.syls.size()), syl_tiles(B.syl_tiles.size()),
         cknots(B.cknots.size()), fl(B.fl.size()), items(B.items.size()), copies(B.copies.size()),
-        w_total(B.w_total), harm_samples(B.harm_samples), harm_terms(B.harm_terms),
-        harm_amp_bytes(B.harm_amp_bytes), fft_frames(B.fft_frames), fs_total(B.fs_total) {
+        eterms(B.eterms.size()), ecols(B.ecols.size()), envjobs(B.envjobs.size()), w_total(B.w_total),
+        harm_samples(B.harm_samples), harm_terms(B.harm_terms), harm_amp_bytes(B.harm_amp_bytes),
+        fft_frames(B.fft_frames), fs_total(B.fs_total), fe_total(B.fe_total) {
     for (int p = 0; p < 2; ++p) { frames[p] = B.frames[p].size(); olas[p] = B.olas[p].size(); mixes[p] = B.mixes[p].size(); }
   }
   void restore(sg::Batch& B) const {
@@ -89,6 +90,7 @@ struct Checkpoint {
     }
     B.w_total = w_total; B.harm_samples = harm_samples; B.harm_terms = harm_terms;
     B.harm_amp_bytes = harm_amp_bytes; B.fft_frames = fft_frames; B.fs_total = fs_total;
+    B.eterms.resize(eterms); B.ecols.resize(ecols); B.envjobs.resize(envjobs); B.fe_total = fe_total;
   }
 };
 
@@ -144,7 +146,7 @@ int plan_threads(int64_t n_calls) {
 
 // Where one part's arrays land in the merged batch.
 struct PartBase {
-  int64_t out, fs, fl, w, amp, knot, ck, task, seg, syl, piece, st, item, copy, call, epoch;
+  int64_t out, fs, fl, w, amp, knot, ck, task, seg, syl, piece, st, item, copy, call, epoch, fe, term, col, job;
   int64_t fr[2], ola[2], mix[2];
 };
 
@@ -178,6 +180,8 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
     c.task += (int64_t)S.tasks.size(); c.seg += (int64_t)S.segs.size(); c.syl += (int64_t)S.syls.size();
     c.piece += (int64_t)S.pieces.size(); c.st += (int64_t)S.syl_tiles.size(); c.item += (int64_t)S.items.size();
     c.copy += (int64_t)S.copies.size(); c.call += (int64_t)S.call_len.size(); c.epoch += (int64_t)S.epochs.size();
+    c.fe += S.fe_total; c.term += (int64_t)S.eterms.size(); c.col += (int64_t)S.ecols.size();
+    c.job += (int64_t)S.envjobs.size();
     for (int ph = 0; ph < 2; ++ph) {
       c.fr[ph] += (int64_t)S.frames[ph].size(); c.ola[ph] += (int64_t)S.olas[ph].size();
       c.mix[ph] += (int64_t)S.mixes[ph].size();
@@ -185,7 +189,8 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
     D.harm_samples += S.harm_samples; D.harm_terms += S.harm_terms; D.harm_amp_bytes += S.harm_amp_bytes;
     D.fft_frames += S.fft_frames;
   }
-  D.total_out = c.out; D.fs_total = c.fs; D.w_total = c.w;
+  D.total_out = c.out; D.fs_total = c.fs; D.w_total = c.w; D.fe_total = c.fe;
+  D.eterms.resize(c.term); D.ecols.resize(c.col); D.envjobs.resize(c.job);
   D.call_len.resize(c.call); D.call_off.resize(c.call); D.call_status.resize(c.call); D.call_msg.resize(c.call);
   D.segs.resize(c.seg); D.epochs.resize(c.epoch); D.knots.resize(c.knot); D.amps.resize(c.amp);
   D.tasks.resize(c.task); D.pieces.resize(c.piece); D.syls.resize(c.syl); D.syl_tiles.resize(c.st);
@@ -228,7 +233,7 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
     for (int ph = 0; ph < 2; ++ph) {
       for (auto& f : S.frames[ph]) {
         f.src += ph == 0 ? b.fl : b.fs;  // noise: uniforms in fl; filter: the sound in fs
-        f.env += b.fl;
+        f.env = f.env < 0 ? f.env - b.fe : f.env + b.fl;  // envelope area (encoded) or fl
         if (f.dst >= 0) f.dst += b.fs;
       }
       for (auto& g : S.frame_geom[ph]) g = gmap[k][g];
@@ -253,6 +258,8 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
       ck(it.strength);
     }
     for (auto& x : S.copies) { x.fl_off += b.fl; x.fs_off += b.fs; }
+    for (auto& j : S.envjobs) { j.out += b.fe; j.term0 += b.term; j.col0 += b.col; }
+    put(D.eterms, S.eterms, b.term); put(D.ecols, S.ecols, b.col); put(D.envjobs, S.envjobs, b.job);
     put(D.segs, S.segs, b.seg); put(D.epochs, S.epochs, b.epoch); put(D.knots, S.knots, b.knot);
     put(D.amps, S.amps, b.amp); put(D.tasks, S.tasks, b.task); put(D.pieces, S.pieces, b.piece);
     put(D.syls, S.syls, b.syl); put(D.syl_tiles, S.syl_tiles, b.st); put(D.cknots, S.cknots, b.ck);
@@ -592,7 +599,7 @@ int sg_formant_filter(sg_ctx* ctx, const double* sound, int64_t len, const doubl
     const int64_t src = sg::fl_push(B, sound, len);
     const int64_t snd = sg::fs_alloc(B, len);
     B.copies.push_back(sg::Batch::Copy{src, snd, len});
-    const sg::vec e(env, env + (int64_t)(wl / 2) * env_nc);
+    const int64_t e = sg::fl_push(B, env, (int64_t)(wl / 2) * env_nc);
     int64_t Lf = 0, filt = 0;
     const int ola = sg::plan_filter(B, snd, len, wl, overlap, e, env_nc, &Lf, &filt);
     *out_len = Lf;
@@ -641,10 +648,22 @@ int sg_spectral_envelope(sg_ctx* ctx, int32_t nr, int32_t nc, const sg_formants*
   return guarded(ctx, [&]() {
     sg::Rng R;
     R.s = rnd;
-    const sg::vec e = sg::spectral_envelope(R, nr, nc, formants, formantDep, rolloffLip, mouthAnchors, mouthOpenThres,
-                                            openMouthBoost, vocalTract, temperature, formDrift, formDisp,
-                                            formantDepStoch, smoothLinearFactor, samplingRate, speedSound);
-    std::memcpy(out, e.data(), e.size() * sizeof(double));
+    if (!ctx) throw sg::SgError(SG_E_ARG, "sg_spectral_envelope: needs a device context (the matrix is computed on the GPU)");
+    auto P = std::make_unique<sg_plan>();
+    sg::Batch& B = P->B;
+    sg::plan_envelope(B, R, nr, nc, formants, formantDep, rolloffLip, mouthAnchors, mouthOpenThres, openMouthBoost,
+                      vocalTract, temperature, formDrift, formDisp, formantDepStoch, smoothLinearFactor, samplingRate,
+                      speedSound);
+    sg::finalize_spec(B);
+    HIPCHK(hipSetDevice(ctx->device));
+    sg::device_upload(B, P->D, ctx->stream);
+    sg::launch_spec_env(P->D, B, ctx->stream);
+    const size_t n = (size_t)nr * (size_t)nc;
+    std::vector<float> h(n);
+    if (n) HIPCHK(hipMemcpyAsync(h.data(), P->D.fl + B.fe_base + B.envjobs[0].out, n * sizeof(float),
+                                 hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    for (size_t i = 0; i < n; ++i) out[i] = h[i];
     return SG_OK;
   });
 }

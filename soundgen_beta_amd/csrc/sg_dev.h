@@ -299,3 +299,38 @@ struct SgMixTile {
   int32_t mix, pad;
   int64_t k0;
 };
+
+// ------------------------------------------------------------------------
+// getSpectralEnvelope() on the device (R/sourceSpectrum.R:507-541). The
+// planner restates everything up to the formant tracks in bins (upsampling,
+// stochastic formants, mouth opening, nasalization: sg_plan_spec.cpp); per
+// column c and track t it emits the log2-density parameters of
+//   dgamma(k, shape, rate) / max_k dgamma = 2^(A log2 k - Rr k - Lm),  k = 1..nr
+// (A = shape - 1, Rr = rate / ln 2, Lm = the column max in the same units) and
+// a bin range [klo, khi] (1-based) that contains every k where the term is
+// within e^-80 of the column max. sg_spec_env sums the terms in that range:
+//   v(k, c) = (sum_t amp_t 2^(A log2 k - Rr k - Lm)) + lip_c log2 k) * boost_c + slope log2 k
+//   env(k, c) = 2^(v / 10)        (fp32, column-major nr x nc)
+// with amp_t = formant dB x formantDep, lip_c = rolloffLip x (mouth open),
+// boost_c = 2^(mouth x openMouthBoost / 10) and slope = rolloffNoise for a noise
+// filter (R/source.R:95-100), 0 for a formant filter.
+struct SgEnvTerm {
+  double A, Rr, Lm, amp;
+  int32_t klo, khi;
+  int32_t pad[2];
+};
+static_assert(sizeof(SgEnvTerm) == 48, "SgEnvTerm layout");
+struct SgEnvCol {
+  float lip, boost;
+};
+struct SgEnvJob {
+  int64_t out;     // offset of the nr x nc output in the envelope area (fl + fe_base on the device)
+  int64_t term0;   // SgEnvTerm of column c, track t: term0 + c * ntr + t
+  int64_t col0;    // SgEnvCol of column c: col0 + c
+  int32_t nr, nc, ntr;
+  float slope;
+};
+constexpr int SG_ENV_COLS = 8;  // columns per wave task
+struct SgEnvTask {
+  int32_t job, c0;
+};

@@ -24,6 +24,7 @@ struct Layout {
   size_t tall;
   size_t segs, epochs, knots, amps, tasks, pieces, syls, syl_tiles, copy_tiles, ptiles, cknots, W, taskmax, ptilemax, maxes, total;
   size_t geoms, frames, fgroups, olas, olatiles, olasegs, olatilemax, olamax, items, mixes, mixtiles, fl, fs;
+  size_t eterms, ecols, envjobs, envtasks;
   explicit Layout(const Batch& B) {
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o += up(bytes > 0 ? bytes : 1); return r; };
@@ -54,7 +55,12 @@ struct Layout {
     items = take(B.items.size() * sizeof(SgNoiseItem));
     mixes = take(B.mixes_dev.size() * sizeof(SgMix));
     mixtiles = take(B.mixtiles.size() * sizeof(SgMixTile));
-    fl = take(B.fl.size() * sizeof(float));
+    eterms = take(B.eterms.size() * sizeof(SgEnvTerm));
+    ecols = take(B.ecols.size() * sizeof(SgEnvCol));
+    envjobs = take(B.envjobs.size() * sizeof(SgEnvJob));
+    envtasks = take(B.envtasks.size() * sizeof(SgEnvTask));
+    // uploaded floats, then the device-computed envelopes from fe_base on
+    fl = take((size_t)std::max<int64_t>((int64_t)B.fl.size(), B.fe_base + B.fe_total) * sizeof(float));
     fs = take((size_t)B.fs_total * sizeof(float) + 256);
     total = o;
   }
@@ -203,6 +209,10 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   D.mixtiles = (SgMixTile*)(a + L.mixtiles);
   D.fl = (float*)(a + L.fl);
   D.fs = (float*)(a + L.fs);
+  D.eterms = (SgEnvTerm*)(a + L.eterms);
+  D.ecols = (SgEnvCol*)(a + L.ecols);
+  D.envjobs = (SgEnvJob*)(a + L.envjobs);
+  D.envtasks = (SgEnvTask*)(a + L.envtasks);
   auto cp = [&](void* dst, const void* src, size_t bytes) {
     if (bytes) HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
   };
@@ -232,6 +242,10 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   cp(D.mixes, B.mixes_dev.data(), B.mixes_dev.size() * sizeof(SgMix));
   cp(D.mixtiles, B.mixtiles.data(), B.mixtiles.size() * sizeof(SgMixTile));
   cp(D.fl, B.fl.data(), B.fl.size() * sizeof(float));
+  cp(D.eterms, B.eterms.data(), B.eterms.size() * sizeof(SgEnvTerm));
+  cp(D.ecols, B.ecols.data(), B.ecols.size() * sizeof(SgEnvCol));
+  cp(D.envjobs, B.envjobs.data(), B.envjobs.size() * sizeof(SgEnvJob));
+  cp(D.envtasks, B.envtasks.data(), B.envtasks.size() * sizeof(SgEnvTask));
   HIPCHK(hipStreamSynchronize(s));
   while (D.ev_slice.size() < B.slices.size()) {
     hipEvent_t e;
@@ -295,6 +309,7 @@ void device_execute(const Batch& B, DevicePlan& D, float* d_out, hipStream_t s, 
 // pre-filter mixes (sounds), filter frames -> filter OLA, final mixes.
 void device_execute_spec(const Batch& B, const DevicePlan& D, float* d_out, hipStream_t s,
                          std::vector<SgProfEvent>* prof) {
+  launch_spec_env(D, B, s);  // envelopes and noise filters read by both phases
   // phase: fused STFT/ISTFT/OLA segments, unfused frame groups + OLA tiles, per-OLA maxima
   auto phase = [&](int ph) {
     const int64_t* r = B.fgroup_range[ph];

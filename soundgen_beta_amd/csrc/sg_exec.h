@@ -43,6 +43,10 @@ struct DevicePlan {
   SgMixTile* mixtiles = nullptr;
   float* fl = nullptr;
   float* fs = nullptr;
+  SgEnvTerm* eterms = nullptr;
+  SgEnvCol* ecols = nullptr;
+  SgEnvJob* envjobs = nullptr;
+  SgEnvTask* envtasks = nullptr;
   std::vector<hipEvent_t> ev_slice;  // slice c's maxes are ready (s -> s2)
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
@@ -78,5 +82,7 @@ void launch_ola_max(const DevicePlan& D, int64_t o0, int64_t n_olas, hipStream_t
 void launch_fft_probe(const SgFftGeom* geom, const float* fl, float* data, int M, int nframes, int inverse,
                       hipStream_t s);
 void launch_mix(const DevicePlan& D, int64_t t0, int64_t n_tiles, float* out, hipStream_t s);
+// sg_env.hip: every spectral-envelope job of the plan (getSpectralEnvelope)
+void launch_spec_env(const DevicePlan& D, const Batch& B, hipStream_t s);
 
 }  // namespace sg

@@ -88,6 +88,15 @@ struct Batch {
   int64_t mixtile_split = 0;
   bulk<double> cknots;   // contour / linear knot data
   int64_t w_total = 0;          // epoch-waveform scratch (floats)
+  // device spectral envelopes (sg_spec_env): per-column/track terms, per-column
+  // factors, jobs; outputs in the envelope area (fe_total floats after fe_base,
+  // the end of the uploaded fl floats, fixed at finalize_spec). Until then a
+  // frame's env < 0 encodes envelope-area offset -(env + 1).
+  bulk<SgEnvTerm> eterms;
+  std::vector<SgEnvCol> ecols;
+  std::vector<SgEnvJob> envjobs;
+  int64_t fe_total = 0, fe_base = 0;
+  std::vector<SgEnvTask> envtasks;  // derived (finalize_spec)
   // ---- per call ----
   std::vector<int64_t> call_len, call_off;
   std::vector<int32_t> call_status;
@@ -135,22 +144,29 @@ int geometry(Batch& B, int wl);
 int64_t fs_alloc(Batch& B, int64_t n);
 int64_t fl_push(Batch& B, const double* v, int64_t n);
 // STFT(hamming) x env -> ISTFT(hann) of the fs sound [sound, sound + L)
-// (R/soundgen.R:743-806). env: nr x env_nc (column-major); returns the
+// (R/soundgen.R:743-806). env: nr x env_nc (column-major) at fl offset env
+// (>= 0) or envelope-area offset -(env + 1) (< 0); returns the
 // filter OLA index (phase 1); *out_len = istft length.
-int plan_filter(Batch& B, int64_t sound, int64_t L, int wl, double overlap, const vec& env, int64_t env_nc,
+int plan_filter(Batch& B, int64_t sound, int64_t L, int wl, double overlap, int64_t env, int64_t env_nc,
                 int64_t* out_len, int64_t* out_fs);
 // generateNoise(), R/source.R:57-138: returns a noise item (off = 0);
-// ok == false when the noise contour is NA (R returns zeros).
+// ok == false when the noise contour is NA (R returns zeros). filterNoise: host
+// nr x fnc matrix; or filt_env < 0: a device envelope job (envelope-area
+// offset -(filt_env + 1), fnc columns) that already includes the rolloffNoise slope.
 bool plan_noise(Batch& B, Rng& R, int64_t len, const sg_anchors& noiseAnchors, double rolloffNoise,
                 double attackLen, int wl, double sr, double overlap, const double* filterNoise, int64_t fnc,
-                SgNoiseItem* item);
-// getSpectralEnvelope(), R/sourceSpectrum.R:261-566 (host, fp64), nr x nc column-major
+                SgNoiseItem* item, int64_t filt_env = 0);
+// getSpectralEnvelope(), R/sourceSpectrum.R:261-566: the host part (tracks,
+// draws) plus one sg_spec_env job computing the nr x nc matrix on the device;
+// returns its envelope-area offset encoded as -(offset + 1). slope: dB per
+// log2(bin) added after the boost (the noise rolloff, R/source.R:95-100).
 // nrd = windowLength_points / 2 as R passes it (x.5 for an odd window: the
 // matrix has as.integer(nrd) rows, bin_width uses nrd)
-vec spectral_envelope(Rng& R, double nrd, int64_t nc, const sg_formants* F, double formantDep, double rolloffLip,
-                      const sg_anchors& mouthAnchors, double mouthOpenThres, double openMouthBoost,
+int64_t plan_envelope(Batch& B, Rng& R, double nrd, int64_t nc, const sg_formants* F, double formantDep,
+                      double rolloffLip, const sg_anchors& mouthAnchors, double mouthOpenThres, double openMouthBoost,
                       double vocalTract, double temperature, double formDrift, double formDisp,
-                      double formantDepStoch, double smoothLinearFactor, double sr, double speedSound);
+                      double formantDepStoch, double smoothLinearFactor, double sr, double speedSound,
+                      double slope = 0);
 vec sigmoid_half(double sr, double freq, double shape, double spikiness);
 
 // getRolloff() with per-gc vector parameters (R/sourceSpectrum.R:71-186)

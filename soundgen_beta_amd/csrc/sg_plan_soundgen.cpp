@@ -403,8 +403,7 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
         Anc ns = noiseA;
         for (auto& t : ns.t) if (t > 0) t = t * dur / A.sylLen;
         const int64_t uvDur = (int64_t)r_round((r_max(ns.t) - r_min(ns.t)) * sr / 1000);
-        vec envN;
-        int64_t nInt = 0;
+        int64_t envN = 0, nInt = 0;
         if (postNoise) {
           // R/soundgen.R:662-663: max(lengths(formantsNoise)) > 1 | mouth moves;
           // a list of formant lists always has 4 fields, so it counts as moving
@@ -413,13 +412,14 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
           for (double v : mouthA.v) if (v != .5) mouthMoves = true;
           if (mouthMoves) moving = true;
           nInt = moving ? (int64_t)r_round((r_max(ns.t) - r_min(ns.t)) / 10) : 1;
-          envN = spectral_envelope(R, wlp / 2, nInt, &A.formantsNoise, A.formantDep, A.rolloffLip,
-                                   mouthA.view(), 0, 0, A.vocalTract, T, A.tempEffects[1], A.tempEffects[2],
-                                   A.formantDepStoch, 1, sr, 35400);
+          // the noise filter's rolloffNoise slope (R/source.R:103-105) is applied by the same job
+          envN = plan_envelope(B, R, wlp / 2, nInt, &A.formantsNoise, A.formantDep, A.rolloffLip, mouthA.view(), 0,
+                               0, A.vocalTract, T, A.tempEffects[1], A.tempEffects[2], A.formantDepStoch, 1, sr,
+                               35400, A.rolloffNoise);
         }
         SgNoiseItem it{};
-        if (!plan_noise(B, R, uvDur, ns.view(), A.rolloffNoise, HPs.attackLen, (int)wlp, sr, A.overlap,
-                        postNoise ? envN.data() : nullptr, nInt, &it)) {
+        if (!plan_noise(B, R, uvDur, ns.view(), A.rolloffNoise, HPs.attackLen, (int)wlp, sr, A.overlap, nullptr,
+                        nInt, &it, nInt > 0 ? envN : 0)) {  // an empty filter is NA in R (filterNoise[1])
           it = raw_item(0, uvDur, 0);  // NA contour: generateNoise returns rep(0, len)
           it.flags = SG_ITEM_ZERO;
         }
@@ -475,9 +475,9 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
       for (double v : mouthA.v) if (v != .5) mouthMoves = true;
       if (mouthA.n() > 0 && mouthMoves) moving = true;
       const int64_t nInt = moving ? nc : 1;
-      const vec env = spectral_envelope(R, (double)wl / 2, nInt, &Fm, A.formantDep, A.rolloffLip, mouthA.view(), 0, 0,
-                                        A.vocalTract, T, A.tempEffects[1], A.tempEffects[2], A.formantDepStoch, 1,
-                                        sr, 35400);
+      const int64_t env = plan_envelope(B, R, (double)wl / 2, nInt, &Fm, A.formantDep, A.rolloffLip, mouthA.view(),
+                                        0, 0, A.vocalTract, T, A.tempEffects[1], A.tempEffects[2],
+                                        A.formantDepStoch, 1, sr, 35400);
       int64_t filt_fs = 0, Lf = 0;
       const int ola = plan_filter(B, sound_fs, Ls, wl, A.overlap, env, nInt, &Lf, &filt_fs);
       SgNoiseItem fi = raw_item(filt_fs, Lf, 0);  // soundFiltered / max(soundFiltered)

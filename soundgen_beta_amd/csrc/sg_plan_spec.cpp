@@ -206,7 +206,7 @@ static int push_ola(Batch& B, int phase, int64_t frames, int64_t nframes, int wl
   return (int)B.olas[phase].size() - 1;
 }
 
-int plan_filter(Batch& B, int64_t sound, int64_t L, int wl, double overlap, const vec& env, int64_t env_nc,
+int plan_filter(Batch& B, int64_t sound, int64_t L, int wl, double overlap, int64_t env, int64_t env_nc,
                 int64_t* out_len, int64_t* out_fs) {
   ProfScope ps(PF_FILTER);
   const int gi = geometry(B, wl);
@@ -218,13 +218,13 @@ int plan_filter(Batch& B, int64_t sound, int64_t L, int wl, double overlap, cons
   if (env_nc != 1 && env_nc != nc) throw SgError(SG_E_ARG, "formant filter: envelope columns != frames");
   for (double x0 : step)
     if ((int64_t)x0 - 1 + wl > L) throw SgError(SG_E_DOMAIN, "stft: frame beyond the sound");
-  const int64_t env_off = fl_push(B, env.data(), (int64_t)env.size());
   const bool fused = fusable(B.geoms[gi], (double)wl * (100 - overlap) / 100);
   const int64_t fr = fused ? 0 : fs_alloc(B, nc * wl);  // frame scratch only for the unfused path
   for (int64_t c = 0; c < nc; ++c) {
     SgFrame f{};
     f.src = sound + (int64_t)step[c] - 1;  // wave[x:(x + wl - 1)], x truncated
-    f.env = env_off + (env_nc == 1 ? 0 : c * nr);
+    const int64_t col = env_nc == 1 ? 0 : c * nr;
+    f.env = env < 0 ? env - col : env + col;  // envelope area (encoded) or fl
     f.dst = fused ? -1 : fr + c * wl;
     B.frames[1].push_back(f);
     B.frame_geom[1].push_back(gi);
@@ -239,7 +239,7 @@ int plan_filter(Batch& B, int64_t sound, int64_t L, int wl, double overlap, cons
 
 bool plan_noise(Batch& B, Rng& R, int64_t len, const sg_anchors& noiseAnchors, double rolloffNoise,
                 double attackLen, int wl, double sr, double overlap, const double* filterNoise, int64_t fnc,
-                SgNoiseItem* item) {
+                SgNoiseItem* item, int64_t filt_env) {
   ProfScope ps(PF_NOISE);
   // breathingStrength = getSmoothContour(noiseAnchors, len, valueFloor = -120, valueCeiling = 40)
   //   R/source.R:70-81 (NA when len == 0 or anchors NA)
@@ -252,15 +252,19 @@ bool plan_noise(Batch& B, Rng& R, int64_t len, const sg_anchors& noiseAnchors, d
   const int64_t nr = wl / 2;
   // filter = [filterNoise or 1] * 2^(rolloffNoise / 10 * log2(1:nr)); column index per frame
   //   round(seq(1, ncol(filter), length.out = nc))   R/source.R:95-114
-  const int64_t ncolF = filterNoise ? fnc : 1;
-  vec filt((size_t)(nr * ncolF));
-  for (int64_t c = 0; c < ncolF; ++c)
-    for (int64_t k = 0; k < nr; ++k)
-      filt[c * nr + k] = (filterNoise ? filterNoise[c * nr + k] : 1.0) *
-                         std::pow(2.0, rolloffNoise / 10 * std::log2((double)(k + 1)));
-  const int64_t filt_off = fl_push(B, filt.data(), (int64_t)filt.size());
+  const bool dev = filt_env < 0;  // device envelope job, rolloff included
+  const int64_t ncolF = filterNoise || dev ? fnc : 1;
+  int64_t filt_off = filt_env;
+  if (!dev) {
+    vec filt((size_t)(nr * ncolF));
+    for (int64_t c = 0; c < ncolF; ++c)
+      for (int64_t k = 0; k < nr; ++k)
+        filt[c * nr + k] = (filterNoise ? filterNoise[c * nr + k] : 1.0) *
+                           std::pow(2.0, rolloffNoise / 10 * std::log2((double)(k + 1)));
+    filt_off = fl_push(B, filt.data(), (int64_t)filt.size());
+  }
   vec fri((size_t)nc, 1.0);
-  if (filterNoise) {
+  if (filterNoise || dev) {
     const vec s = r_seq_len(1, (double)ncolF, nc);
     for (int64_t c = 0; c < nc; ++c) fri[c] = r_round(s[c]);
   }
@@ -279,7 +283,8 @@ bool plan_noise(Batch& B, Rng& R, int64_t len, const sg_anchors& noiseAnchors, d
   for (int64_t c = 0; c < nc; ++c) {
     SgFrame f{};
     f.src = u_off + c * nr;
-    f.env = filt_off + ((int64_t)fri[c] - 1) * nr;
+    const int64_t col = ((int64_t)fri[c] - 1) * nr;
+    f.env = dev ? filt_off - col : filt_off + col;
     f.dst = fused ? -1 : fr + c * wl;
     B.frames[0].push_back(f);
     B.frame_geom[0].push_back(gi);
@@ -337,10 +342,10 @@ vec col_upsample(const double* t, const double* y, int64_t np, int64_t nPoints, 
 }
 }  // namespace
 
-vec spectral_envelope(Rng& R, double nrd, int64_t nc, const sg_formants* F, double formantDep, double rolloffLip,
-                      const sg_anchors& mouthAnchors, double mouthOpenThres, double openMouthBoost,
+int64_t plan_envelope(Batch& B, Rng& R, double nrd, int64_t nc, const sg_formants* F, double formantDep,
+                      double rolloffLip, const sg_anchors& mouthAnchors, double mouthOpenThres, double openMouthBoost,
                       double vocalTract, double temperature, double formDrift, double formDisp,
-                      double formantDepStoch, double slf, double sr, double speedSound) {
+                      double formantDepStoch, double slf, double sr, double speedSound, double slope) {
   ProfScope ps(PF_ENVELOPE);
   const int64_t nr = (int64_t)nrd;  // matrix(nrow = nr): as.integer; bin_width keeps nrd
   int nF = F ? F->n_formants : 0;
@@ -379,13 +384,12 @@ vec spectral_envelope(Rng& R, double nrd, int64_t nc, const sg_formants* F, doub
     nF = 1;
     f1_index = 0;
   }
-  vec env((size_t)(nr * nc), 0.0);
   vec mouth((size_t)nc, 0.5), mbin((size_t)nc, 1.0);
-  vec logk((size_t)nr), log2k((size_t)nr);
-  for (int64_t k = 0; k < nr; ++k) {
-    logk[k] = std::log((double)(k + 1));
-    log2k[k] = std::log2((double)(k + 1));
-  }
+  SgEnvJob job{};
+  job.nr = (int32_t)nr;
+  job.nc = (int32_t)nc;
+  job.slope = (float)slope;
+  job.term0 = (int64_t)B.eterms.size();
   if (nF > 0) {
     int64_t nPoints = 0;
     for (int f = 0; f < nF; ++f) nPoints = std::max<int64_t>(nPoints, np[f]);
@@ -501,44 +505,72 @@ vec spectral_envelope(Rng& R, double nrd, int64_t nc, const sg_formants* F, doub
       fu.push_back(p);
       fu.push_back(z);
     }
-    // dgamma(1:nr, shape = mu^2/sd^2, rate = mu/sd^2), normalised by its max   R/sourceSpectrum.R:507-522
-    // (log density from a shared log(k) table; exp only where the column is
-    // within e^-80 of its max, below which a term cannot move the dB sum)
-    vec col((size_t)nr);
-    for (const auto& tr : fu)
-      for (int64_t c = 0; c < nc; ++c) {
+    // dgamma(1:nr, shape = mu^2/sd^2, rate = mu/sd^2), normalised by its column max,
+    // times amp, summed over formants, times formantDep   R/sourceSpectrum.R:507-526
+    // (terms emitted for sg_spec_env; the log-density max over the integer bins is
+    // at floor or ceil of the mode (shape - 1) / rate, or at bin 1 for shape <= 1)
+    const double L2E = 1.4426950408889634;  // 1 / ln 2
+    job.ntr = (int32_t)fu.size();
+    B.eterms.resize(B.eterms.size() + (size_t)(nc * job.ntr));
+    SgEnvTerm* tm = &B.eterms[job.term0];
+    for (int64_t c = 0; c < nc; ++c)
+      for (size_t t = 0; t < fu.size(); ++t) {
+        const Track& tr = fu[t];
         const double mg = tr.freq[c];
         double sdg = tr.width[c];
         if (sdg == 0) sdg = 1;
         const double shape = mg * mg / (sdg * sdg), rate = mg / (sdg * sdg);
-        double lmax = -INFINITY;
-        for (int64_t k = 0; k < nr; ++k) {
-          const double x = (double)(k + 1);
-          const double l = (shape == 1) ? -rate * x : (shape - 1) * logk[k] - rate * x;
-          col[k] = l;
-          if (l > lmax) lmax = l;
+        SgEnvTerm& e = tm[c * job.ntr + t];
+        e = SgEnvTerm{};
+        e.A = shape - 1;
+        e.Rr = rate * L2E;
+        auto l2 = [&](double x) { return e.A * std::log2(x) - e.Rr * x; };  // log2 density (+ const), as the device
+        double kmax = 1;
+        if (e.A > 0 && rate > 0) kmax = std::min((double)nr, std::max(1.0, e.A / rate));
+        const double k0 = std::floor(kmax), k1 = std::min((double)nr, std::ceil(kmax));
+        e.Lm = std::max(l2(k0), l2(k1));
+        e.amp = tr.amp[c] * formantDep;
+        // bins within e^-80 of the max: superset from ln u - u + 1 <= -(u-1)^2/(2 max(u, 1))
+        e.klo = 1;
+        e.khi = (int32_t)nr;
+        if (e.A > 0 && rate > 0) {
+          const double xs = e.A / rate;
+          const double lc = (e.A * std::log(xs) - rate * xs) - e.Lm / L2E;  // continuous max - integer max (>= 0)
+          const double q = (80 + std::max(0.0, lc)) / e.A * (1 + 1e-6) + 1e-9;
+          const double xlo = xs * (1 - std::sqrt(2 * q)), xhi = xs * (1 + q + std::sqrt(q * q + 2 * q));
+          if (std::isfinite(xlo) && xlo > 2) e.klo = (int32_t)std::min<double>((double)nr + 1, std::floor(xlo) - 1);
+          if (std::isfinite(xhi) && xhi < (double)nr - 1) e.khi = (int32_t)std::max(0.0, std::ceil(xhi) + 1);
+        } else if (rate > 0) {
+          const double xhi = 1 + 80 / rate * (1 + 1e-6);
+          if (std::isfinite(xhi) && xhi < (double)nr - 1) e.khi = (int32_t)std::ceil(xhi) + 1;
         }
-        const double amp = tr.amp[c], lcut = lmax - 80;
-        double* e = &env[c * nr];
-        for (int64_t k = 0; k < nr; ++k)
-          if (col[k] > lcut) e[k] += std::exp(col[k] - lmax) * amp;
+        if (!std::isfinite(e.A) || !std::isfinite(e.Rr) || !std::isfinite(e.Lm)) {  // NaN track: no term passes the cut
+          e.klo = 1;
+          e.khi = 0;
+        }
       }
-    for (auto& v : env) v *= formantDep;
   }
   // lip radiation, open-mouth boost, dB -> linear (2^(x/10))   R/sourceSpectrum.R:524-541
-  for (int64_t c = 0; c < nc; ++c) {
-    const double boost = std::pow(2.0, mouth[c] * openMouthBoost / 10);
-    for (int64_t k = 0; k < nr; ++k) {
-      const double lip = rolloffLip * log2k[k];
-      env[c * nr + k] = (env[c * nr + k] + lip * mbin[c]) * boost;
-    }
-  }
-  for (auto& v : env) v = std::pow(2.0, v / 10);
-  return env;
+  job.col0 = (int64_t)B.ecols.size();
+  for (int64_t c = 0; c < nc; ++c)
+    B.ecols.push_back(SgEnvCol{(float)(rolloffLip * mbin[c]), (float)std::pow(2.0, mouth[c] * openMouthBoost / 10)});
+  job.out = B.fe_total;
+  B.fe_total += (nr * nc + 63) / 64 * 64;
+  B.envjobs.push_back(job);
+  return -(job.out + 1);
 }
 
 // ------------------------------------------------------------ finalize
 void finalize_spec(Batch& B) {
+  // envelope area after the uploaded floats: decode frame envelope offsets;
+  // sg_spec_env wave tasks of SG_ENV_COLS columns
+  B.fe_base = ((int64_t)B.fl.size() + 63) / 64 * 64;
+  for (int ph = 0; ph < 2; ++ph)
+    for (SgFrame& f : B.frames[ph])
+      if (f.env < 0) f.env = B.fe_base + (-f.env - 1);
+  B.envtasks.clear();
+  for (size_t j = 0; j < B.envjobs.size(); ++j)
+    for (int32_t c0 = 0; c0 < B.envjobs[j].nc; c0 += SG_ENV_COLS) B.envtasks.push_back(SgEnvTask{(int32_t)j, c0});
   // frames: per phase, sorted by (kernel, geometry), stable so that the
   // frames of one OLA stay consecutive; groups for the workgroup kernel only
   B.fgroups.clear();

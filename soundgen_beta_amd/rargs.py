@@ -201,6 +201,16 @@ class Holder:
 
     def __init__(self):
         self.keep = []
+        self._fmemo = {}  # formants converted once per object (a batch shares preset formant lists)
+
+    def formants_of(self, x):
+        """sg_formants of an R formants argument (vowel string, formant lists or NA);
+        the same string or the same (live) object is converted once per Holder."""
+        key = ("s", x) if isinstance(x, str) else ("o", id(x))
+        hit = self._fmemo.get(key)
+        if hit is None:
+            hit = self._fmemo[key] = (self.formants(as_formants(x)), x)  # x kept alive: its id stays unique
+        return hit[0]
 
     def arr(self, a, dtype=np.float64):
         a = np.ascontiguousarray(np.asarray(a, dtype=dtype))
@@ -287,8 +297,8 @@ def fill_soundgen_args(h, kw):
     s.amplAnchorsGlobal = h.anchors(as_anchors(a["amplAnchorsGlobal"]))
     s.mouthAnchors = h.anchors(as_anchors(a["mouthAnchors"]))
     s.noiseAnchors = h.anchors(as_anchors(a["noiseAnchors"], time_to=a["sylLen"]))
-    s.formants = h.formants(as_formants(a["formants"]))
-    s.formantsNoise = h.formants(as_formants(a["formantsNoise"]))
+    s.formants = h.formants_of(a["formants"])
+    s.formantsNoise = h.formants_of(a["formantsNoise"])
     s.formantsNoise_rlen = r_max_lengths(a["formantsNoise"])
     s.invalidArgAction = {"adjust": 0, "abort": 1, "ignore": 2}[a["invalidArgAction"]]
     return s

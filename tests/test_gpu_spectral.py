@@ -163,3 +163,45 @@ def test_c5_presets_one_batch(oracle):
         worst = max(worst, r)
         assert r <= TOL, (i, calls[i]["preset"], r)
     print("C5 worst rms", worst, "over", len(ok), "calls")
+
+# getSpectralEnvelope's matrix comes from sg_spec_env (fp32 terms, fp32 2^(dB/10)):
+# per-bin relative error vs the fp64 oracle <= 1e-5 (the waveform bar is RMS <= 1e-5)
+ENV_RTOL = 1e-5
+
+
+def _api():
+    from soundgen_beta_amd import api
+    return api
+
+
+@pytest.mark.parametrize("fm,nc,extra", [
+    (FORMANTS_A, 1, {}),
+    (MOVING, 37, {}),
+    ("a", 1, dict(vocalTract=15.5)),
+    ("u", 25, dict(mouthAnchors={"time": [0, 1], "value": [0, 0.8]}, mouthOpenThres=0.2, openMouthBoost=5)),
+    (None, 1, dict(vocalTract=17)),  # schwa from vocalTract
+])
+def test_spectral_envelope_matches_oracle(oracle, fm, nc, extra):
+    kw = dict(formants=fm, samplingRate=44100, **extra)
+    got = _api().getSpectralEnvelope(1102, nc, **kw)
+    want = oracle.spectral_envelope(1102, nc, **kw)
+    np.testing.assert_allclose(got, want, rtol=ENV_RTOL, atol=0)
+
+
+def test_spectral_envelope_stochastic_same_draws(oracle):
+    kw = dict(formants=FORMANTS_A, samplingRate=16000, temperature=0.1, vocalTract=15)
+    got = _api().getSpectralEnvelope(400, 9, rng=np.random.default_rng(9), **kw)
+    want = oracle.spectral_envelope(400, 9, rng=np.random.default_rng(9), **kw)
+    np.testing.assert_allclose(got, want, rtol=ENV_RTOL)
+
+
+
+
+def test_spectral_envelope_stochastic_formants_44k(oracle):
+    """temperature > 0 at 44.1 kHz adds stochastic formants up to sr/2 - 1000
+    (R/sourceSpectrum.R:347-415): ~20 tracks per column, narrow and wide."""
+    for seed in range(4):
+        kw = dict(formants=MOVING, samplingRate=44100, temperature=0.2, vocalTract=16)
+        got = _api().getSpectralEnvelope(1102, 61, rng=np.random.default_rng(seed), **kw)
+        want = oracle.spectral_envelope(1102, 61, rng=np.random.default_rng(seed), **kw)
+        np.testing.assert_allclose(got, want, rtol=ENV_RTOL)

@@ -1,6 +1,7 @@
-"""CPU: host parts of the spectral path — getSpectralEnvelope (host, fp64)
-against the oracle, and soundgen() planning: every output length (syllables,
-pauses, noise trims, istft lengths, bouts, silence) bit-exact with the oracle."""
+"""CPU: host parts of the spectral path — soundgen() planning: every output
+length (syllables, pauses, noise trims, istft lengths, bouts, silence)
+bit-exact with the oracle. (getSpectralEnvelope's matrix is computed on the
+GPU: tests/test_gpu_spectral.py.)"""
 import numpy as np
 import pytest
 
@@ -14,27 +15,6 @@ FORMANTS_A = {"f1": {"time": 0, "freq": 860, "amp": 30, "width": 120},
               "f3": {"time": 0, "freq": 2900, "amp": 25, "width": 200}}
 MOVING = {"f1": {"time": [0, 1], "freq": [700, 300], "amp": [30, 30], "width": [100, 100]},
           "f2": {"time": [0, .5, 1], "freq": [1200, 1800, 2400], "amp": [40, 40, 40], "width": [120, 120, 150]}}
-
-
-@pytest.mark.parametrize("fm,nc,extra", [
-    (FORMANTS_A, 1, {}),
-    (MOVING, 37, {}),
-    ("a", 1, dict(vocalTract=15.5)),
-    ("u", 25, dict(mouthAnchors={"time": [0, 1], "value": [0, 0.8]}, mouthOpenThres=0.2, openMouthBoost=5)),
-    (None, 1, dict(vocalTract=17)),  # schwa from vocalTract
-])
-def test_spectral_envelope_matches_oracle(oracle, fm, nc, extra):
-    kw = dict(formants=fm, samplingRate=44100, **extra)
-    got = api.getSpectralEnvelope(1102, nc, **kw)
-    want = oracle.spectral_envelope(1102, nc, **kw)
-    np.testing.assert_allclose(got, want, rtol=1e-12, atol=0)
-
-
-def test_spectral_envelope_stochastic_same_draws(oracle):
-    kw = dict(formants=FORMANTS_A, samplingRate=16000, temperature=0.1, vocalTract=15)
-    got = api.getSpectralEnvelope(400, 9, rng=np.random.default_rng(9), **kw)
-    want = oracle.spectral_envelope(400, 9, rng=np.random.default_rng(9), **kw)
-    np.testing.assert_allclose(got, want, rtol=1e-12)
 
 
 SOUNDGEN_CASES = {
