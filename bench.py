@@ -1,23 +1,33 @@
 """bench.py — synthesized audio samples/s of the soundgen hot path on MI355X.
 
-Default workload (BASELINE.json configs[1], the config the metric is quoted
-on, fits one GPU): C2 = 1024 x generateHarmonics(pitch = rep(f0, 3500),
-samplingRate = 44100, temperature = 0, nonlinBalance = 0, rolloff = -12,
-rolloffOct = -12, rolloffKHz = -6, pitchFloor = 50), f0 log-uniform in
-[80, 400] Hz, numpy PCG64 seed 20261015.
---config c3 / c4 run the other single-GPU configs:
-  C3 1024 x 2 s vowels, formant filter + breathing noise (uniform draws injected)
-  C4 512 x 3 s, subharmonics + jitter/shimmer, temperature 0.05 (draws injected)
+Default workload: C5 (BASELINE.json configs[4], the config the
+metric "(whole node)" is quoted on): ONE batch of 65,536 soundgen() calls drawn
+from the 33 presets (R/presets.R:158-399, soundgen_beta_amd/presets.json),
+sylLen x U(0.5, 2) clamped to [20, 5000] ms, pitch anchors x 2^U(-0.5, 0.5),
+44.1 kHz, numpy PCG64 seed 20261015, random draws injected. It fits one
+MI355X (~150 GB of HBM), so N=1 runs all of it; with N ranks the SAME batch is
+split by LPT over an analytic per-call cost (soundgen_beta_amd/dist.py), no
+data-path collective: "scaling": "strong".
+--config c2|c3|c4 run the other single-GPU configs (C2 1024 x 1 s tones,
+C3 1024 x 2 s vowels with formant filter + breathing noise, C4 512 x 3 s
+subharmonics/jitter/shimmer at temperature 0.05).
 
-A "step" = one pass of the hot path over the whole batch (planning and upload
-happen before the timed region; inputs are resident in HBM). With N ranks each
-rank synthesizes its own shard (weak scaling, no data-path collective);
-time = max over ranks, value = samples of all ranks / time.
+A "step" = one pass of the hot path over the whole batch: every kernel from
+the envelopes and the sine bank to the final mix, inputs resident in HBM
+(planning and upload happen before the timed region; plan time is reported).
+value = samples of all ranks / max over ranks of the timed wall time.
+value_host_resident adds the device-to-host copy of every waveform into pinned
+host memory inside the timed region ("to waveforms resident in
+host memory").
+
+With --gpus N and no WORLD_SIZE in the environment, bench.py starts itself
+under torch.distributed.run with N ranks (one per GPU) before touching the GPU.
 """
 import argparse
 import ctypes as C
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -31,23 +41,26 @@ METRIC = "synthesized audio samples/sec (whole node) @44.1 kHz; RMS error vs R r
 C2_PARAMS = dict(samplingRate=44100, pitchSamplingRate=3500, temperature=0, nonlinBalance=0, attackLen=50,
                  rolloff=-12, rolloffOct=-12, rolloffKHz=-6, rolloffParab=0, rolloffParabHarm=3, pitchFloor=50,
                  pitchCeiling=3500, throwaway=-120)
-HBM_PEAK_GBS = 8000.0                 # MI355X_MICROARCH.md chip table (spec)
-VALU_PEAK_OPS = 157.3e12  # f32 lane-ops/s at the packed rate (v_pk_fma_f32 / v_pk_add_f32), which the sine bank uses
-FP32_PEAK_TFLOPS = 157.3              # MI355X FP32 vector (packed FMA)
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+# VALU issue peak in f32 lane-operations/s at the packed rate: 256 CU x 4 SIMD x
+# 16 lanes x 2.4 GHz = 39.3e12 lane-instructions/s, x 2 for v_pk_* (an FMA
+# counted as ONE op; the 157.3 TFLOP/s figure counts it as two flops)
+VALU_PEAK_OPS = 78.6e12
+FP32_PEAK_TFLOPS = 157.3  # MI355X FP32 vector (packed FMA, 2 flops each)
 
 
-def _rng(rank, salt):
-    return np.random.Generator(np.random.PCG64(SEED + 7919 * rank + salt))
+def _rng(salt):
+    return np.random.Generator(np.random.PCG64(SEED + salt))
 
 
-def c2_calls(n_calls, rank=0):
-    rng = _rng(rank, 0)
+def c2_calls(n_calls):
+    rng = _rng(0)
     f0 = np.exp(rng.uniform(np.log(80.0), np.log(400.0), n_calls))
     return [{"kind": "harmonics", "pitch": np.full(3500, f), "params": C2_PARAMS} for f in f0]
 
 
-def c3_calls(n_calls, rank=0):
-    rng = _rng(rank, 3)
+def c3_calls(n_calls):
+    rng = _rng(3)
     vowels = np.array(list("aoieu0"))
     v = rng.choice(vowels, n_calls)
     a = np.exp(rng.uniform(np.log(90), np.log(250), n_calls))
@@ -64,8 +77,8 @@ def c3_calls(n_calls, rank=0):
     return calls
 
 
-def c4_calls(n_calls, rank=0):
-    rng = _rng(rank, 4)
+def c4_calls(n_calls):
+    rng = _rng(4)
     s = rng.uniform(60, 200, n_calls)
     d = rng.uniform(40, 150, n_calls)
     j = rng.uniform(0.3, 2, n_calls)
@@ -86,14 +99,14 @@ def c4_calls(n_calls, rank=0):
     return calls
 
 
-def c5_calls(n_calls, rank=0):
+def c5_calls(n_calls):
     """C5: calls drawn uniformly from the 33 presets (R/presets.R:158-399,
     extracted to soundgen_beta_amd/presets.json); sylLen x U(0.5, 2) clamped to [20, 5000],
     pitch anchor values x 2^U(-0.5, 0.5), samplingRate 44100, addSilence 0, the
     preset's own temperature. Random draws come from one shared pre-drawn stream
     (every call reads it from the start; synthetic data)."""
     from soundgen_beta_amd import presets as P
-    rng = _rng(rank, 5)
+    rng = _rng(5)
     names = P.names()
     base = {k: P.args(*k) for k in names}  # one copy per preset: calls share its formant lists
     Z = rng.standard_normal(200000)
@@ -119,7 +132,8 @@ CONFIGS = {
     "c2": (c2_calls, 1024, "C2: %d x 1 s static-f0 tones, generateHarmonics, 44.1 kHz, harmonics only"),
     "c3": (c3_calls, 1024, "C3: %d x 2 s vowels, soundgen() with formant filter + breathing noise, 44.1 kHz"),
     "c4": (c4_calls, 512, "C4: %d x 3 s soundgen() with subharmonics, jitter, shimmer, temperature 0.05, 44.1 kHz"),
-    "c5": (c5_calls, 8192, "C5: %d calls per GPU drawn from the 33 presets (65,536 over 8 GPUs), 44.1 kHz"),
+    "c5": (c5_calls, 65536, "C5: %d soundgen() calls drawn from the 33 presets (mixed sylLen and pitch contours), "
+                            "44.1 kHz"),
 }
 
 
@@ -129,39 +143,87 @@ def oracle_call(O, c):
     return O.soundgen(normals=c.get("normals"), uniforms=c.get("uniforms"), **c["args"])
 
 
+def host_cores():
+    """Host threads this job may use (the box exports its CPU share as
+    OMP_NUM_THREADS; os.cpu_count() shows the whole machine there)."""
+    n = os.cpu_count() or 1
+    try:
+        n = min(n, int(os.environ.get("OMP_NUM_THREADS", n)))
+    except ValueError:
+        pass
+    return max(1, n)
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(calls, budget_s):
-    """Oracle (C restatement of the R algorithm), 1 thread, bounded sample."""
+    """The oracle (oracle/sg_oracle.c, a C restatement of the R algorithm) on a
+    bounded sample of the same calls: one thread, then all host cores (a thread
+    pool over calls; the oracle releases the GIL inside its C call)."""
+    from concurrent.futures import ThreadPoolExecutor
     from oracle import oracle as O
     O.lib()
-    t0 = time.perf_counter()
-    n_samples = n = 0
-    for c in calls:
+
+    def one(c):
         try:
-            n_samples += len(oracle_call(O, c))
-        except Exception:  # same unsupported calls as the GPU path
-            continue
-        n += 1
-        if time.perf_counter() - t0 > budget_s:
+            return len(oracle_call(O, c))
+        except Exception:  # a call the oracle refuses counts no samples
+            return 0
+
+    t0 = time.perf_counter()
+    n1 = s1 = 0
+    for c in calls:
+        s1 += one(c)
+        n1 += 1
+        if time.perf_counter() - t0 > budget_s / 2:
             break
-    dt = time.perf_counter() - t0
-    return {"value": n_samples / dt, "unit": "samples/s", "cores": 1, "kind": "port",
-            "sample": "%d of the workload's calls (%d samples) through oracle/sg_oracle.c, single thread"
-                      % (n, n_samples)}
+    dt1 = time.perf_counter() - t0
+    cores = host_cores()
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(cores) as ex:
+        futs = []
+        for c in calls:
+            # keep 4 calls per thread in flight; stop submitting at the time budget
+            while sum(not f.done() for f in futs[-8 * cores:]) >= 4 * cores:
+                time.sleep(0.0005)
+            if time.perf_counter() - t0 > budget_s / 2:
+                break
+            futs.append(ex.submit(one, c))
+        sm = sum(f.result() for f in futs)
+    dtm = time.perf_counter() - t0
+    return {"value": sm / dtm, "unit": "samples/s", "cores": cores, "kind": "port",
+            "sample": "the first %d calls of the workload (%d samples) through oracle/sg_oracle.c on a %d-thread pool"
+                      % (len(futs), sm, cores),
+            "single_thread": {"value": s1 / dt1, "sample": "the first %d calls (%d samples), 1 thread" % (n1, s1)},
+            "host": {"nproc": os.cpu_count(), "cores_used": cores, "model": cpu_model()},
+            "note": "R unavailable; CPU baseline = C restatement of the R algorithm"}
 
 
-def traffic_from_profiles(config, kernel):
+def traffic_from_profiles(config, kernel, launches_per_step):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of
-    this workload (profiles/rNN_<config>_traffic.json, tools/gpu_traffic.sh:
-    separate FETCH_SIZE / WRITE_SIZE passes, gfx950 FETCH_SIZE doubled)."""
+    this workload (profiles/rNN_<config>_traffic.json by tools/gpu_traffic.sh:
+    separate FETCH_SIZE / WRITE_SIZE passes, gfx950 FETCH_SIZE doubled): the sum
+    over the kernel's launches of one execute, per launch."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_%s_traffic.json" % config)))
     if not files:
         return None, None
     d = json.load(open(files[-1]))
-    hits = [v["hbm_bytes"] for k, v in d.get("kernels", {}).items() if k.split(" ")[0] == kernel and "hbm_bytes" in v]
-    if not hits:
+    ex = d.get("executes")
+    hits = [(v["hbm_bytes"], v.get("launches")) for k, v in d.get("kernels", {}).items()
+            if k.split(" ")[0] == kernel and "hbm_bytes" in v]
+    if not hits or not ex or any(n is None for _, n in hits):
         return None, None
-    return max(hits), os.path.relpath(files[-1], ROOT)
+    per_step = sum(b * n for b, n in hits) / ex
+    return per_step / max(1, launches_per_step), os.path.relpath(files[-1], ROOT)
 
 
 def roofline(st, prof, steps, config):
@@ -171,23 +233,23 @@ def roofline(st, prof, steps, config):
     tot = {k: v[0] * v[1] for k, v in prof.items()}
     kern = max(tot, key=tot.get) if any(tot.values()) else "sg_sine_bank"
     ms, n = prof[kern]
-    launches = max(1, n // steps)
+    lps = max(1, n // steps)  # launches per step
     sec = ms / 1e3
     if kern == "sg_sine_bank":
         # fp32 epoch waveform write + the amplitude blocks it reads (A and dA columns)
-        alg = (4 * st["harm_samples"] + st["harm_amp_bytes"]) / launches
-        valu_ops = 2.0 * st["harm_terms"] / launches  # Clenshaw: 2 lane-ops per (sample, row, chain)
+        alg = (4 * st["harm_samples"] + st["harm_amp_bytes"]) / lps
+        valu_ops = 2.0 * st["harm_terms"] / lps  # Clenshaw: 2 lane-ops per (sample, row, chain)
         extra = {"valu": {"ops_per_launch": valu_ops, "achieved_ops_s": valu_ops / sec if sec else 0,
                           "peak_ops_s": VALU_PEAK_OPS, "frac": valu_ops / sec / VALU_PEAK_OPS if sec else 0}}
     else:
         # source / uniforms + envelope columns read, trimmed output written
-        alg = st["stft_bytes"] / launches
-        fl = st["stft_flops"] / launches
+        alg = st["stft_bytes"] / lps
+        fl = st["stft_flops"] / lps
         extra = {"flops": {"nominal_per_launch": fl, "achieved_tflops": fl / sec / 1e12 if sec else 0,
                            "peak_tflops": FP32_PEAK_TFLOPS,
                            "frac": fl / sec / 1e12 / FP32_PEAK_TFLOPS if sec else 0}}
     achieved = alg / sec / 1e9 if sec > 0 else 0.0
-    traffic, src = traffic_from_profiles(config, kern)
+    traffic, src = traffic_from_profiles(config, kern, lps)
     r = {"bound": "hbm", "kernel": kern, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "alg_bytes_per_launch": alg,
          "avg_launch_ms": ms, "launches_timed": n}
@@ -197,49 +259,90 @@ def roofline(st, prof, steps, config):
     return r
 
 
+def relaunch(args):
+    """--gpus N without a launcher: start N ranks under torch.distributed.run as a
+    child process (no GPU call has happened in this process) and return its status."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--calls", type=int, default=0, help="calls per GPU (default: the config's)")
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c5", choices=sorted(CONFIGS))
+    ap.add_argument("--calls", type=int, default=0, help="calls in the whole batch (default: the config's)")
+    ap.add_argument("--plan-chunk", type=int, default=16384,
+                    help="calls per plan (each uploaded, then its host copy freed)")
+    ap.add_argument("--host-steps", type=int, default=2, help="steps timed with the D2H copy (0: skip)")
+    ap.add_argument("--cpu-budget", type=float, default=16.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", action="store_true",
                     help="after the timed steps, time the packed-output gather to rank 0 (RCCL point-to-point)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch(args))
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl")
-    torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
     from soundgen_beta_amd import batch, native
+    from soundgen_beta_amd import dist as sharding
     make, n_default, desc = CONFIGS[args.config]
     n_calls = args.calls or n_default
-    calls = make(n_calls, rank)
+    t_gen = time.perf_counter()
+    calls = make(n_calls)  # the same batch on every rank
+    t_gen = time.perf_counter() - t_gen
+    if world > 1:
+        idx, mine, _ = sharding.shard(calls, rank, world)
+    else:
+        idx, mine = np.arange(n_calls), calls
     ctx = native.Context(local)
+    plans = []  # (plan, output base, the calls' indices in the batch)
     t_plan = time.perf_counter()
-    plan = batch.Plan(calls, ctx)
+    base = 0
+    failed = 0
+    first_msg = None
+    for a in range(0, len(mine), args.plan_chunk):
+        p = batch.Plan(mine[a:a + args.plan_chunk], ctx)
+        bad = np.nonzero(p.status)[0]
+        failed += len(bad)
+        if len(bad) and first_msg is None:
+            first_msg = p.message(int(bad[0]))
+        p.upload()
+        p.release_host()
+        plans.append((p, base, idx[a:a + args.plan_chunk]))
+        base += (p.total + 63) // 64 * 64
+        if rank == 0:
+            print("bench: planned + uploaded %d/%d calls (%.1f s)" % (min(a + args.plan_chunk, len(mine)), len(mine),
+                                                                      time.perf_counter() - t_plan), file=sys.stderr)
     t_plan = time.perf_counter() - t_plan
-    failed = int((plan.status != 0).sum())
-    if failed:  # e.g. loess-smoothed contours (3-10 anchors) are SG_E_UNSUPPORTED; their slots stay empty
-        print("bench: %d of %d calls not synthesized: %s" % (failed, plan.n, plan.message(int(np.nonzero(plan.status)[0][0]))),
-              file=sys.stderr)
-    plan.upload()
-    out = torch.empty(max(plan.total, 1), dtype=torch.float32, device=dev)
+    if failed:
+        print("bench: %d of %d calls not synthesized: %s" % (failed, len(mine), first_msg), file=sys.stderr)
+    out = torch.empty(max(base, 1), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
 
+    def step():
+        for p, b, _ in plans:
+            p.execute(out.data_ptr() + 4 * b, sptr)
+
     for _ in range(args.warmup):
-        plan.execute(out.data_ptr(), sptr)
+        step()
     torch.cuda.synchronize(dev)
     L = native.lib()
     L.sg_set_profiling(ctx.ptr, 1)
@@ -248,7 +351,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        plan.execute(out.data_ptr(), sptr)
+        step()
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -260,23 +363,49 @@ def main():
         native.check(L.sg_profile_read_kernel(ctx.ptr, kid, C.byref(ms), C.byref(n)), ctx.ptr)
         prof[name] = (ms.value, n.value)
 
-    samples_rank = int(plan.lengths.sum())  # synthesized samples (slot padding excluded)
+    # the same steps with every waveform copied to pinned host memory (the timed
+    # region ends with the samples resident on the host)
+    dt_host = None
+    if args.host_steps > 0:
+        try:
+            host = torch.empty(max(base, 1), dtype=torch.float32, pin_memory=True)
+            pinned = True
+        except RuntimeError:
+            host = torch.empty(max(base, 1), dtype=torch.float32)
+            pinned = False
+        host.copy_(out)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for _ in range(args.host_steps):
+            step()
+            host.copy_(out, non_blocking=pinned)
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        dt_host = time.perf_counter() - t1
+        del host
+
+    samples_rank = int(sum(int(p.lengths.sum()) for p, _, _ in plans))  # synthesized samples (padding excluded)
+    vals = [dt, t_plan, float(dt_host or 0.0)]
     if dist:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        t = torch.tensor(vals, device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-        s = torch.tensor([samples_rank], device=dev, dtype=torch.float64)
+        vals = [float(x) for x in t.tolist()]
+        s = torch.tensor([samples_rank, failed], device=dev, dtype=torch.float64)
         dist.all_reduce(s, op=dist.ReduceOp.SUM)
-        samples_all = float(s.item())
+        samples_all, failed_all = float(s[0].item()), int(s[1].item())
     else:
-        samples_all = float(samples_rank)
+        samples_all, failed_all = float(samples_rank), failed
+    dt, t_plan_max, dt_host = vals[0], vals[1], (vals[2] if args.host_steps > 0 else None)
     value = samples_all * args.steps / dt
 
     gather_ms = None
     if args.gather and dist:
         # SURVEY §8e exchange step: every peer sends its packed output to rank 0
-        # concurrently (one xGMI link each); rank 0 receives into one buffer
-        n_loc = torch.tensor([plan.total], device=dev, dtype=torch.int64)
+        # concurrently (one xGMI link each); rank 0 receives into one buffer per peer
+        n_loc = torch.tensor([base], device=dev, dtype=torch.int64)
         counts = [torch.zeros_like(n_loc) for _ in range(world)]
         dist.all_gather(counts, n_loc)
         counts = [int(c.item()) for c in counts]
@@ -287,7 +416,7 @@ def main():
             bufs = [torch.empty(max(counts[r], 1), dtype=torch.float32, device=dev) for r in range(1, world)]
             ops = [dist.P2POp(dist.irecv, bufs[r - 1][:counts[r]], r) for r in range(1, world) if counts[r]]
         else:
-            ops = [dist.P2POp(dist.isend, out[:plan.total], 0)] if plan.total else []
+            ops = [dist.P2POp(dist.isend, out[:base], 0)] if base else []
         for w in (dist.batch_isend_irecv(ops) if ops else []):
             w.wait()
         torch.cuda.synchronize(dev)
@@ -295,23 +424,32 @@ def main():
         gather_ms = (time.perf_counter() - tg) * 1e3
 
     if rank == 0:
-        st = plan.stats()
+        st = {}
+        for p, _, _ in plans:
+            for k, v in p.stats().items():
+                st[k] = st.get(k, 0) + v
         roof = roofline(st, prof, args.steps, args.config)
         from oracle import oracle as O
         rms = []
-        host = None
-        for i in [k for k in range(plan.n) if plan.status[k] == 0][:3]:
-            lo, n = int(plan.offsets[i]), int(plan.lengths[i])
+        p0, b0, i0 = plans[0]
+        for i in [k for k in range(p0.n) if p0.status[k] == 0][:3]:
+            lo, n = b0 + int(p0.offsets[i]), int(p0.lengths[i])
             y = out[lo:lo + n].double().cpu().numpy()
-            ref = oracle_call(O, calls[i])
+            ref = oracle_call(O, calls[int(i0[i])])
             rms.append(float(np.sqrt(np.mean((y - ref) ** 2))) if len(ref) == len(y) else float("inf"))
         res = {
             "metric": METRIC, "value": value, "unit": "samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "fp32 (fp64 phase)", "data": "synthetic",
-            "config": {"workload": desc % n_calls, "calls_per_gpu": n_calls, "samples_per_gpu": samples_rank,
-                       "sampling_rate": 44100, "parallelism": "dp%d (independent shards)" % world,
-                       "plan_s": t_plan, "failed_calls": failed},
+            "scaling": "strong", "vs_baseline": None, "dtype": "fp32 (fp64 phase)",
+            "data": "synthetic (PCG64 seed %d; random draws injected)" % SEED,
+            "config": {"workload": desc % n_calls, "calls": n_calls, "calls_rank0": len(mine),
+                       "samples": int(samples_all), "sampling_rate": 44100,
+                       "parallelism": "dp%d (one batch split by calls, LPT)" % world,
+                       "plans_per_rank": len(plans), "failed_calls": failed_all},
+            "value_host_resident": (samples_all * args.host_steps / dt_host) if dt_host else None,
+            "ms_per_step_host_resident": (dt_host / args.host_steps * 1e3) if dt_host else None,
+            "plan_s": t_plan_max, "calls_gen_s": t_gen,
+            "value_incl_planning": samples_all / (t_plan_max + dt / args.steps),
             "rms_error_vs_oracle": max(rms) if rms else None,
             "roofline": roof,
         }
@@ -320,7 +458,8 @@ def main():
         if not args.no_cpu_baseline and world == 1:  # the CPU leg runs at N=1 only
             res["cpu_baseline"] = cpu_baseline(calls, args.cpu_budget)
         print(json.dumps(res), flush=True)
-    plan.close()
+    for p, _, _ in plans:
+        p.close()
     ctx.close()
     if dist:
         dist.destroy_process_group()

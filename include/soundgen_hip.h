@@ -184,6 +184,11 @@ int sg_plan_status(const sg_plan* plan, int32_t* out_status);
 int64_t sg_plan_device_bytes(const sg_plan* plan);
 /* Upload descriptors/inputs to HBM (outside any timed region). */
 int sg_plan_upload(sg_ctx* ctx, sg_plan* plan);
+/* After upload: free the plan's host copies of descriptors and inputs (a
+ * 65,536-call preset batch holds ~0.7 MB per call on the host). Execution,
+ * lengths, offsets, statuses and messages keep working; re-upload does not.
+ * No reference counterpart (R holds nothing between calls). */
+int sg_plan_release_host(sg_plan* plan);
 /* Run every kernel of the plan on `stream` (hipStream_t; NULL = the null
  * stream, ordered after earlier null-stream work such as torch's default stream)
  * writing fp32 samples into device buffer d_out (packed, offsets as above).

@@ -33,7 +33,7 @@
 #define OR_API __attribute__((visibility("default")))
 
 /* ------------------------------------------------------------------ errors */
-static char g_err[512];
+static __thread char g_err[512];  /* per thread: bench.py runs oracle calls on a thread pool */
 static int fail(int code, const char* msg) {
   snprintf(g_err, sizeof g_err, "%s", msg);
   return code;

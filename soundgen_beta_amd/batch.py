@@ -72,6 +72,10 @@ class Plan:
         self.ctx = ctx
         self.uploaded = True
 
+    def release_host(self):
+        """Free the plan's host copies after upload (execution keeps working)."""
+        native.check(native.lib().sg_plan_release_host(self.ptr), None)
+
     def execute(self, d_out_ptr, stream_ptr=None):
         """Run the kernels writing fp32 samples to device pointer d_out_ptr."""
         native.check(native.lib().sg_execute(self.ctx.ptr, self.ptr, C.c_void_p(d_out_ptr),

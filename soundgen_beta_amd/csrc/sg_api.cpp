@@ -32,6 +32,7 @@ struct sg_ctx {
 struct sg_plan {
   sg::Batch B;
   sg::DevicePlan D;
+  bool host_released = false;  // sg_plan_release_host: bulk host arrays freed, re-upload impossible
 };
 
 namespace sg {
@@ -409,10 +410,29 @@ const char* sg_plan_call_message(const sg_plan* plan, int64_t i) {
   return plan->B.call_msg[i].c_str();
 }
 
-int64_t sg_plan_device_bytes(const sg_plan* plan) { return plan ? sg::device_bytes(plan->B) : 0; }
+int64_t sg_plan_device_bytes(const sg_plan* plan) {
+  if (!plan) return 0;
+  return plan->host_released ? (int64_t)plan->D.arena_bytes : sg::device_bytes(plan->B);
+}
+
+int sg_plan_release_host(sg_plan* plan) {
+  if (!plan) return SG_E_ARG;
+  if (!plan->D.uploaded) return SG_E_ARG;
+  sg::Batch& B = plan->B;
+  auto drop = [](auto& v) { std::remove_reference_t<decltype(v)>().swap(v); };
+  // what sg_execute reads from the host plan stays: slices, ranges and splits,
+  // the table sizes it launches over, the copy list, the envelope area base
+  drop(B.segs); drop(B.epochs); drop(B.knots); drop(B.amps); drop(B.tasks); drop(B.pieces); drop(B.syls);
+  drop(B.syl_tiles); drop(B.fin_tiles); drop(B.copy_tiles); drop(B.ptiles); drop(B.cknots); drop(B.fl);
+  drop(B.fgroups); drop(B.olasegs); drop(B.items); drop(B.mixes_dev); drop(B.eterms); drop(B.ecols); drop(B.envjobs);
+  for (int ph = 0; ph < 2; ++ph) { drop(B.frames[ph]); drop(B.frame_geom[ph]); drop(B.olas[ph]); drop(B.mixes[ph]); }
+  plan->host_released = true;
+  return SG_OK;
+}
 
 int sg_plan_upload(sg_ctx* ctx, sg_plan* plan) {
   return guarded(ctx, [&]() {
+    if (plan->host_released) throw sg::SgError(SG_E_ARG, "sg_plan_upload: host arrays released");
     HIPCHK(hipSetDevice(ctx->device));
     sg::device_upload(plan->B, plan->D, ctx->stream);
     return SG_OK;

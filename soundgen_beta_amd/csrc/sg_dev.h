@@ -308,7 +308,7 @@ struct SgMixTile {
 //   dgamma(k, shape, rate) / max_k dgamma = 2^(A log2 k - Rr k - Lm),  k = 1..nr
 // (A = shape - 1, Rr = rate / ln 2, Lm = the column max in the same units) and
 // a bin range [klo, khi] (1-based) that contains every k where the term is
-// within e^-80 of the column max. sg_spec_env sums the terms in that range:
+// within 2^-SG_ENV_CUT of the column max. sg_spec_env sums the terms in that range:
 //   v(k, c) = (sum_t amp_t 2^(A log2 k - Rr k - Lm)) + lip_c log2 k) * boost_c + slope log2 k
 //   env(k, c) = 2^(v / 10)        (fp32, column-major nr x nc)
 // with amp_t = formant dB x formantDep, lip_c = rolloffLip x (mouth open),
@@ -331,6 +331,10 @@ struct SgEnvJob {
   float slope;
 };
 constexpr int SG_ENV_COLS = 8;  // columns per wave task
+// Terms below 2^-30 of their own column max are dropped: each changes the dB sum
+// by <= |amp| 2^-30 (~6e-8 dB at 60 dB), far below the fp32 resolution of the sum;
+// R adds them all (R/sourceSpectrum.R:507-522)
+constexpr double SG_ENV_CUT = 30.0;
 struct SgEnvTask {
   int32_t job, c0;
 };

@@ -4,26 +4,34 @@
 // formantDep; lip radiation, open-mouth boost, 2^(dB / 10)), and the same for
 // the noise filter of generateNoise() with its rolloff slope (R/source.R:103-105).
 //
-// One wave per task = SG_ENV_COLS columns of one job. Lanes own bins: for each
-// chunk of 64 bins the wave computes log2(k) once (fp64), then per column sums
-// the formant terms whose planner-computed bin range [klo, khi] meets the chunk
-// (wave-uniform skip: a formant's term is nonzero within a band of ~25 widths)
-// and writes 64 consecutive fp32 values (coalesced). The log-density difference
-// A log2 k - Rr k - Lm is formed in fp64 (its two products are ~1e6 for narrow
-// formants, so fp32 would lose the difference); the power of two and the sum
-// over formants run in fp32.
+// One wave per task = SG_ENV_COLS columns of one job. Per column, lane t holds
+// the term of track t (and t + 64) in registers. Lanes then own bins, 64 per
+// chunk: a ballot over the tracks' bin ranges gives the tracks that reach the
+// chunk (a formant is nonzero within a band of a few tens of bins), and only
+// those are summed, their parameters broadcast from the owning lane. The
+// log-density difference A log2 k - Rr k - Lm is formed in fp64 from a log2(k)
+// table (its two products reach ~1e6 for narrow formants, so fp32 would lose
+// the difference); the power of two and the sum over formants run in fp32.
+// Each chunk ends with 64 consecutive fp32 stores (coalesced).
 //
-// Bound: neither HBM (4 B written per bin and column, ~48 B read per formant and
-// column) nor transcendental rate dominates; per active term 2 fp64 FMA +
-// cvt + v_exp_f32 + FMA.
+// Work per active (chunk, track): 2 fp64 FMA + cvt + v_exp_f32 + FMA + select,
+// plus 7 lane broadcasts. Output 4 B per bin and column, ~48 B per track and
+// column read once: VALU/issue-bound, not HBM-bound.
 #include <hip/hip_runtime.h>
 
 #include "sg_dev.h"
+
+__device__ __forceinline__ double bcast(double v, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+  return __hiloint2double(hi, lo);
+}
 
 extern "C" __global__ __launch_bounds__(256) void sg_spec_env(const SgEnvTask* __restrict__ tasks, int64_t ntask,
                                                               const SgEnvJob* __restrict__ jobs,
                                                               const SgEnvTerm* __restrict__ terms,
                                                               const SgEnvCol* __restrict__ cols,
+                                                              const double* __restrict__ lg2,
                                                               float* __restrict__ fe) {
   const int64_t w = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (w >= ntask) return;
@@ -31,27 +39,46 @@ extern "C" __global__ __launch_bounds__(256) void sg_spec_env(const SgEnvTask* _
   const SgEnvTask T = tasks[w];
   const SgEnvJob J = jobs[T.job];
   const int c1 = T.c0 + SG_ENV_COLS < J.nc ? T.c0 + SG_ENV_COLS : J.nc;
-  const double thr = -80.0 * 1.4426950408889634;  // e^-80 of the column max, in log2 units
+  const double thr = -SG_ENV_CUT;  // log2 units
 #pragma unroll 1
-  for (int k0 = 0; k0 < J.nr; k0 += 64) {
-    const int k = k0 + lane;
-    const double x = (double)(k + 1);
-    const double lx = log2(x);
-    const float lxf = (float)lx;
+  for (int c = T.c0; c < c1; ++c) {
+    const SgEnvTerm* __restrict__ tm = terms + J.term0 + (int64_t)c * J.ntr;
+    // lane t: term t (group 0) and term 64 + t (group 1); absent terms get an empty range
+    double A[2], Rr[2], Lm[2];
+    float amp[2];
+    int klo[2], khi[2];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const int t = g * 64 + lane;
+      const bool in = t < J.ntr;
+      const SgEnvTerm& e = tm[in ? t : 0];
+      A[g] = e.A; Rr[g] = e.Rr; Lm[g] = e.Lm; amp[g] = (float)e.amp;
+      klo[g] = in ? e.klo : 1 << 30;
+      khi[g] = in ? e.khi : -1;
+    }
+    const SgEnvCol C = cols[J.col0 + c];
+    float* __restrict__ dst = fe + J.out + (int64_t)c * J.nr;
 #pragma unroll 1
-    for (int c = T.c0; c < c1; ++c) {
-      const SgEnvTerm* __restrict__ tm = terms + J.term0 + (int64_t)c * J.ntr;
+    for (int k0 = 0; k0 < J.nr; k0 += 64) {
+      const int k = k0 + lane;
+      const double x = (double)(k + 1);
+      const double lx = lg2[k];
       float acc = 0.f;
-#pragma unroll 1
-      for (int t = 0; t < J.ntr; ++t) {
-        const SgEnvTerm& e = tm[t];
-        if (e.khi < k0 + 1 || e.klo > k0 + 64) continue;  // band misses the chunk
-        const double d = fma(e.A, lx, fma(-e.Rr, x, -e.Lm));
-        if (d > thr) acc = fmaf((float)e.amp, exp2f((float)d), acc);
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        uint64_t m = __ballot(klo[g] <= k0 + 64 && khi[g] >= k0 + 1);
+        while (m) {
+          const int t = __builtin_ctzll(m);
+          m &= m - 1;
+          const double a = bcast(A[g], t), r = bcast(Rr[g], t), l = bcast(Lm[g], t);
+          const float am = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amp[g]), t));
+          const double d = fma(a, lx, fma(-r, x, -l));
+          if (d > thr) acc = fmaf(am, exp2f((float)d), acc);
+        }
       }
-      const SgEnvCol C = cols[J.col0 + c];
+      const float lxf = (float)lx;
       const float v = fmaf(fmaf(C.lip, lxf, acc), C.boost, J.slope * lxf);
-      if (k < J.nr) fe[J.out + (int64_t)c * J.nr + k] = exp2f(v * 0.1f);
+      if (k < J.nr) dst[k] = exp2f(v * 0.1f);
     }
   }
 }
@@ -63,7 +90,7 @@ void launch_spec_env(const DevicePlan& D, const Batch& B, hipStream_t s) {
   const int64_t n = (int64_t)B.envtasks.size();
   if (n <= 0) return;
   hipLaunchKernelGGL(sg_spec_env, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, D.envtasks, n, D.envjobs, D.eterms,
-                     D.ecols, D.fl + B.fe_base);
+                     D.ecols, D.elog2, D.fl + B.fe_base);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw SgError(SG_E_DEVICE, std::string("launch sg_spec_env: ") + hipGetErrorString(e));
 }

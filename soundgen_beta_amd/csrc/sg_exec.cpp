@@ -24,7 +24,7 @@ struct Layout {
   size_t tall;
   size_t segs, epochs, knots, amps, tasks, pieces, syls, syl_tiles, copy_tiles, ptiles, cknots, W, taskmax, ptilemax, maxes, total;
   size_t geoms, frames, fgroups, olas, olatiles, olasegs, olatilemax, olamax, items, mixes, mixtiles, fl, fs;
-  size_t eterms, ecols, envjobs, envtasks;
+  size_t eterms, ecols, envjobs, envtasks, elog2;
   explicit Layout(const Batch& B) {
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o += up(bytes > 0 ? bytes : 1); return r; };
@@ -59,6 +59,7 @@ struct Layout {
     ecols = take(B.ecols.size() * sizeof(SgEnvCol));
     envjobs = take(B.envjobs.size() * sizeof(SgEnvJob));
     envtasks = take(B.envtasks.size() * sizeof(SgEnvTask));
+    elog2 = take(B.elog2.size() * sizeof(double));
     // uploaded floats, then the device-computed envelopes from fe_base on
     fl = take((size_t)std::max<int64_t>((int64_t)B.fl.size(), B.fe_base + B.fe_total) * sizeof(float));
     fs = take((size_t)B.fs_total * sizeof(float) + 256);
@@ -213,6 +214,7 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   D.ecols = (SgEnvCol*)(a + L.ecols);
   D.envjobs = (SgEnvJob*)(a + L.envjobs);
   D.envtasks = (SgEnvTask*)(a + L.envtasks);
+  D.elog2 = (double*)(a + L.elog2);
   auto cp = [&](void* dst, const void* src, size_t bytes) {
     if (bytes) HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
   };
@@ -246,6 +248,7 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   cp(D.ecols, B.ecols.data(), B.ecols.size() * sizeof(SgEnvCol));
   cp(D.envjobs, B.envjobs.data(), B.envjobs.size() * sizeof(SgEnvJob));
   cp(D.envtasks, B.envtasks.data(), B.envtasks.size() * sizeof(SgEnvTask));
+  cp(D.elog2, B.elog2.data(), B.elog2.size() * sizeof(double));
   HIPCHK(hipStreamSynchronize(s));
   while (D.ev_slice.size() < B.slices.size()) {
     hipEvent_t e;

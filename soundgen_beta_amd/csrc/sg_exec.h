@@ -47,6 +47,7 @@ struct DevicePlan {
   SgEnvCol* ecols = nullptr;
   SgEnvJob* envjobs = nullptr;
   SgEnvTask* envtasks = nullptr;
+  double* elog2 = nullptr;
   std::vector<hipEvent_t> ev_slice;  // slice c's maxes are ready (s -> s2)
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };

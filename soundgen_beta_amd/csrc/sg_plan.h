@@ -97,6 +97,7 @@ struct Batch {
   std::vector<SgEnvJob> envjobs;
   int64_t fe_total = 0, fe_base = 0;
   std::vector<SgEnvTask> envtasks;  // derived (finalize_spec)
+  std::vector<double> elog2;        // derived: log2(k), k = 1..max nr
   // ---- per call ----
   std::vector<int64_t> call_len, call_off;
   std::vector<int32_t> call_status;

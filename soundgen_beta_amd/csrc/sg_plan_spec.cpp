@@ -530,18 +530,19 @@ int64_t plan_envelope(Batch& B, Rng& R, double nrd, int64_t nc, const sg_formant
         const double k0 = std::floor(kmax), k1 = std::min((double)nr, std::ceil(kmax));
         e.Lm = std::max(l2(k0), l2(k1));
         e.amp = tr.amp[c] * formantDep;
-        // bins within e^-80 of the max: superset from ln u - u + 1 <= -(u-1)^2/(2 max(u, 1))
+        // bins where the term is within 2^-SG_ENV_CUT of its column max (sg_dev.h): superset
+        // from ln u - u + 1 <= -(u-1)^2/(2 max(u, 1))
         e.klo = 1;
         e.khi = (int32_t)nr;
         if (e.A > 0 && rate > 0) {
           const double xs = e.A / rate;
           const double lc = (e.A * std::log(xs) - rate * xs) - e.Lm / L2E;  // continuous max - integer max (>= 0)
-          const double q = (80 + std::max(0.0, lc)) / e.A * (1 + 1e-6) + 1e-9;
+          const double q = (SG_ENV_CUT / L2E + std::max(0.0, lc)) / e.A * (1 + 1e-6) + 1e-9;
           const double xlo = xs * (1 - std::sqrt(2 * q)), xhi = xs * (1 + q + std::sqrt(q * q + 2 * q));
           if (std::isfinite(xlo) && xlo > 2) e.klo = (int32_t)std::min<double>((double)nr + 1, std::floor(xlo) - 1);
           if (std::isfinite(xhi) && xhi < (double)nr - 1) e.khi = (int32_t)std::max(0.0, std::ceil(xhi) + 1);
         } else if (rate > 0) {
-          const double xhi = 1 + 80 / rate * (1 + 1e-6);
+          const double xhi = 1 + SG_ENV_CUT / L2E / rate * (1 + 1e-6);
           if (std::isfinite(xhi) && xhi < (double)nr - 1) e.khi = (int32_t)std::ceil(xhi) + 1;
         }
         if (!std::isfinite(e.A) || !std::isfinite(e.Rr) || !std::isfinite(e.Lm)) {  // NaN track: no term passes the cut
@@ -568,6 +569,13 @@ void finalize_spec(Batch& B) {
   for (int ph = 0; ph < 2; ++ph)
     for (SgFrame& f : B.frames[ph])
       if (f.env < 0) f.env = B.fe_base + (-f.env - 1);
+  int32_t maxnr = 0;
+  for (const SgEnvJob& j : B.envjobs) {
+    maxnr = std::max(maxnr, j.nr);
+    if (j.ntr > 2 * 64) throw SgError(SG_E_UNSUPPORTED, "spectral envelope: more than 128 formant tracks");
+  }
+  B.elog2.resize((size_t)maxnr + 64);  // log2(k) for k = 1.. (padded to whole 64-bin chunks)
+  for (size_t k = 0; k < B.elog2.size(); ++k) B.elog2[k] = std::log2((double)(k + 1));
   B.envtasks.clear();
   for (size_t j = 0; j < B.envjobs.size(); ++j)
     for (int32_t c0 = 0; c0 < B.envjobs[j].nc; c0 += SG_ENV_COLS) B.envtasks.push_back(SgEnvTask{(int32_t)j, c0});

@@ -65,6 +65,7 @@ def lib():
     L.sg_plan_device_bytes.argtypes = [vp]
     L.sg_plan_device_bytes.restype = i64
     L.sg_plan_upload.argtypes = [vp, vp]
+    L.sg_plan_release_host.argtypes = [vp]
     L.sg_execute.argtypes = [vp, vp, vp, vp]
     L.sg_set_profiling.argtypes = [vp, C.c_int]
     L.sg_profile_read.argtypes = [vp, dp, i64p]

@@ -147,3 +147,37 @@ def test_parallel_plan_output_byte_equal(monkeypatch):
     (o1, l1, y1), (o7, l7, y7) = outs
     assert (o1 == o7).all() and (l1 == l7).all()
     assert np.array_equal(y1.view(np.uint32), y7.view(np.uint32))
+
+
+def test_sharded_batch_byte_equal():
+    """bench.py's strong scaling splits ONE batch over ranks (dist.shard, LPT).
+    Every call synthesizes the same bytes whether planned in the whole batch or in
+    either rank's shard (per-call normalisation, deterministic reductions), so the
+    N=2 outputs equal the N=1 outputs call for call."""
+    import os
+    import sys
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from soundgen_beta_amd import batch, dist, native
+    calls = bench.c5_calls(192) + bench.c4_calls(8)
+    ctx = native.default_context(0)
+
+    def run(cs):
+        plan = batch.Plan(cs, ctx)
+        assert (plan.status == 0).all()
+        plan.upload()
+        out = torch.zeros(max(plan.total, 1), dtype=torch.float32, device="cuda")
+        plan.execute(out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        y = out.cpu().numpy()
+        res = [y[o:o + n].copy() for o, n in zip(plan.offsets, plan.lengths)]
+        plan.close()
+        return res
+
+    whole = run(calls)
+    for r in range(2):
+        idx, mine, owner = dist.shard(calls, r, 2)
+        assert 0 < len(idx) < len(calls)
+        for i, y in zip(idx, run(mine)):
+            assert np.array_equal(y.view(np.uint32), whole[i].view(np.uint32)), (r, int(i))

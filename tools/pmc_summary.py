@@ -12,7 +12,9 @@ import sys
 
 tag = sys.argv[1]
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
+passes = 0
 for path in sorted(glob.glob("gpurun_out/%s_*/run_counter_collection.csv" % tag)):
+    passes += 1
     for r in csv.DictReader(open(path)):
         key = "%s grid=%s" % (r["Kernel_Name"][:40], r["Grid_Size"])
         acc[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
@@ -21,10 +23,13 @@ for k, d in acc.items():
     if not k.startswith("sg_"):
         continue
     e = {c: sum(v) / len(v) for c, v in sorted(d.items())}
+    # launches of this (kernel, grid) in one pass (each counter is collected in one pass)
+    e["launches"] = len(d["FETCH_SIZE"] if "FETCH_SIZE" in d else next(iter(d.values())))
     if "FETCH_SIZE" in e and "WRITE_SIZE" in e:
         e["hbm_bytes"] = 2.0 * e["FETCH_SIZE"] * 1024 + e["WRITE_SIZE"] * 1024
     out[k] = e
 res = {"tag": tag, "config": sys.argv[2] if len(sys.argv) > 2 else None,
+       "executes": int(sys.argv[3]) if len(sys.argv) > 3 else None,  # sg_execute calls per pass (warmup + steps)
        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (tools/gpu_traffic.sh); "
                  "hbm_bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per launch (gfx950 FETCH_SIZE halving)",
        "kernels": out}
