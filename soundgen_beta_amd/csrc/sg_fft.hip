@@ -27,15 +27,61 @@
 
 namespace {
 
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-  return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
+// Complex values as packed fp32 pairs: gfx950 issues v_pk_fma_f32 / v_pk_mul_f32 /
+// v_pk_add_f32 on (re, im) in one instruction, halving the VALU work of the
+// butterflies (the odd-prime sums multiply both halves by one real root).
+typedef float v2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ v2 V(float2 a) { return v2{a.x, a.y}; }
+__device__ __forceinline__ float2 F(v2 a) { return make_float2(a.x, a.y); }
+__device__ __forceinline__ v2 pfma(v2 a, v2 b, v2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ v2 splat(float c) { return v2{c, c}; }
+// The swizzles and sign flips of a complex product fold into the VOP3P
+// op_sel / neg modifiers (the compiler emits separate moves and xors for them)
+__device__ __forceinline__ v2 vmul(v2 a, v2 w) {  // a * w = a.x w + a.y (-w.y, w.x)
+  v2 t, r;
+  __asm__("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(w));
+  __asm__("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+          : "=v"(r) : "v"(a), "v"(w), "v"(t));
+  return r;
 }
-__device__ __forceinline__ float2 cmulc(float2 a, float2 b) {  // a * conj(b)
-  return make_float2(fmaf(a.x, b.x, a.y * b.y), fmaf(a.y, b.x, -a.x * b.y));
+__device__ __forceinline__ v2 vmulc(v2 a, v2 w) {  // a * conj(w) = a.x (w.x, -w.y) + a.y (w.y, w.x)
+  v2 t, r;
+  __asm__("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1] neg_hi:[0,1]" : "=v"(t) : "v"(a), "v"(w));
+  __asm__("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1]" : "=v"(r) : "v"(a), "v"(w), "v"(t));
+  return r;
 }
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ v2 add_miq(v2 p, v2 q) {  // p - i q = (p.x + q.y, p.y - q.x)
+  v2 r;
+  __asm__("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(p), "v"(q));
+  return r;
+}
+__device__ __forceinline__ v2 add_piq(v2 p, v2 q) {  // p + i q = (p.x - q.y, p.y + q.x)
+  v2 r;
+  __asm__("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(p), "v"(q));
+  return r;
+}
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) { return F(vmul(V(a), V(b))); }
+__device__ __forceinline__ float2 cmulc(float2 a, float2 b) { return F(vmulc(V(a), V(b))); }
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return F(V(a) + V(b)); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return F(V(a) - V(b)); }
 __device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
+
+// Outputs k and R - k of an odd-prime butterfly from its symmetric sums
+// (st = [x0, a_1..a_H, b_1..b_H]): P = x0 + sum_m a_m cos(2 pi mk/R),
+// Q = sum_m b_m sin(2 pi mk/R); forward y_k = P - iQ, y_{R-k} = P + iQ.
+template <int R, bool INV>
+__device__ __forceinline__ void odd_out(const v2 (&st)[R], int k, v2& yk, v2& ymk) {
+  constexpr int H = (R - 1) / 2;
+  v2 P = st[0], Q = v2{0.f, 0.f};
+#pragma unroll
+  for (int m = 1; m <= H; ++m) {
+    const int id = (m * k) % R;
+    P = pfma(st[m], splat(SgRoots<R>::c(id)), P);
+    Q = pfma(st[H + m], splat(SgRoots<R>::s(id)), Q);
+  }
+  yk = INV ? add_piq(P, Q) : add_miq(P, Q);
+  ymk = INV ? add_miq(P, Q) : add_piq(P, Q);
+}
 
 // R-point DFT in registers. INV: exp(+2 pi i rk / R), else exp(-2 pi i rk / R).
 template <int R, bool INV>
@@ -43,37 +89,23 @@ struct Dft {
   // odd prime R: y_k = x0 + sum_m a_m cos - i sum_m b_m sin, a_m = x_m + x_{R-m}, b_m = x_m - x_{R-m}
   __device__ __forceinline__ static void run(float2 (&v)[R]) {
     constexpr int H = (R - 1) / 2;
-    float2 a[H], b[H];
+    v2 st[R];
+    st[0] = V(v[0]);
+    v2 y0 = st[0];
 #pragma unroll
     for (int m = 1; m <= H; ++m) {
-      a[m - 1] = cadd(v[m], v[R - m]);
-      b[m - 1] = csub(v[m], v[R - m]);
+      st[m] = V(v[m]) + V(v[R - m]);
+      st[H + m] = V(v[m]) - V(v[R - m]);
+      y0 += st[m];
     }
-    const float2 x0 = v[0];
-    float2 y0 = x0;
-#pragma unroll
-    for (int m = 0; m < H; ++m) y0 = cadd(y0, a[m]);
 #pragma unroll
     for (int k = 1; k <= H; ++k) {
-      float2 P = x0, Q = make_float2(0.f, 0.f);
-#pragma unroll
-      for (int m = 1; m <= H; ++m) {
-        const int idx = (m * k) % R;
-        const float c = SgRoots<R>::c(idx), s = SgRoots<R>::s(idx);
-        P.x = fmaf(a[m - 1].x, c, P.x);
-        P.y = fmaf(a[m - 1].y, c, P.y);
-        Q.x = fmaf(b[m - 1].x, s, Q.x);
-        Q.y = fmaf(b[m - 1].y, s, Q.y);
-      }
-      if (!INV) {  // -i Q = (Q.y, -Q.x)
-        v[k] = make_float2(P.x + Q.y, P.y - Q.x);
-        v[R - k] = make_float2(P.x - Q.y, P.y + Q.x);
-      } else {
-        v[k] = make_float2(P.x - Q.y, P.y + Q.x);
-        v[R - k] = make_float2(P.x + Q.y, P.y - Q.x);
-      }
+      v2 a, b;
+      odd_out<R, INV>(st, k, a, b);
+      v[k] = F(a);
+      v[R - k] = F(b);
     }
-    v[0] = y0;
+    v[0] = F(y0);
   }
 };
 template <bool INV>
@@ -147,7 +179,7 @@ __device__ __forceinline__ void stage_ip(float2* X, int M, int Ns, const float2*
   constexpr int H = ODD ? (R - 1) / 2 : 1;
   const int MR = M / R;
   const int total = fb * MR;
-  float2 st[NB][ODD ? (2 * H + 1) : R];  // odd: [x0, a_1..a_H, b_1..b_H]; even radix: outputs
+  v2 st[NB][R];  // odd: [x0, a_1..a_H, b_1..b_H]; even radix: outputs
   int base_o[NB];
   bool live[NB];
 #pragma unroll
@@ -172,16 +204,16 @@ __device__ __forceinline__ void stage_ip(float2* X, int M, int Ns, const float2*
     }
     base_o[q] = f * M + (j - jm) * R + jm;
     if constexpr (ODD) {
-      st[q][0] = v[0];
+      st[q][0] = V(v[0]);
 #pragma unroll
       for (int m = 1; m <= H; ++m) {
-        st[q][m] = cadd(v[m], v[R - m]);
-        st[q][H + m] = csub(v[m], v[R - m]);
+        st[q][m] = V(v[m]) + V(v[R - m]);
+        st[q][H + m] = V(v[m]) - V(v[R - m]);
       }
     } else {
       Dft<R, INV>::run(v);
 #pragma unroll
-      for (int r = 0; r < R; ++r) st[q][r] = v[r];
+      for (int r = 0; r < R; ++r) st[q][r] = V(v[r]);
     }
   }
   __syncthreads();
@@ -190,34 +222,20 @@ __device__ __forceinline__ void stage_ip(float2* X, int M, int Ns, const float2*
     if (!live[q]) continue;
     float2* y = X + base_o[q];
     if constexpr (ODD) {
-      const float2 x0 = st[q][0];
-      float2 y0 = x0;
+      v2 y0 = st[q][0];
 #pragma unroll
-      for (int m = 1; m <= H; ++m) y0 = cadd(y0, st[q][m]);
-      y[0] = y0;
+      for (int m = 1; m <= H; ++m) y0 += st[q][m];
+      y[0] = F(y0);
 #pragma unroll
       for (int k = 1; k <= H; ++k) {
-        float2 P = x0, Q = make_float2(0.f, 0.f);
-#pragma unroll
-        for (int m = 1; m <= H; ++m) {
-          const int id = (m * k) % R;
-          const float c = SgRoots<R>::c(id), s = SgRoots<R>::s(id);
-          P.x = fmaf(st[q][m].x, c, P.x);
-          P.y = fmaf(st[q][m].y, c, P.y);
-          Q.x = fmaf(st[q][H + m].x, s, Q.x);
-          Q.y = fmaf(st[q][H + m].y, s, Q.y);
-        }
-        if (!INV) {
-          y[k * Ns] = make_float2(P.x + Q.y, P.y - Q.x);
-          y[(R - k) * Ns] = make_float2(P.x - Q.y, P.y + Q.x);
-        } else {
-          y[k * Ns] = make_float2(P.x - Q.y, P.y + Q.x);
-          y[(R - k) * Ns] = make_float2(P.x + Q.y, P.y - Q.x);
-        }
+        v2 a, b;
+        odd_out<R, INV>(st[q], k, a, b);
+        y[k * Ns] = F(a);
+        y[(R - k) * Ns] = F(b);
       }
     } else {
 #pragma unroll
-      for (int r = 0; r < R; ++r) y[r * Ns] = st[q][r];
+      for (int r = 0; r < R; ++r) y[r * Ns] = F(st[q][r]);
     }
   }
   __syncthreads();
@@ -263,7 +281,7 @@ __device__ __forceinline__ void stage_w(float2* X, int M, int Ns, const float2* 
   constexpr bool ODD = (R % 2) == 1;
   constexpr int H = ODD ? (R - 1) / 2 : 1;
   const int MR = M / R;
-  float2 st[NB][ODD ? (2 * H + 1) : R];
+  v2 st[NB][R];
   int base_o[NB];
 #pragma unroll
   for (int q = 0; q < NB; ++q) {
@@ -276,18 +294,18 @@ __device__ __forceinline__ void stage_w(float2* X, int M, int Ns, const float2* 
     if constexpr (ODD) {
       // pairs (m, R - m) one at a time: inputs, twiddles and the symmetric
       // sums of one pair live at once (register budget of the fused kernel)
-      st[q][0] = X[j];
+      st[q][0] = V(X[j]);
       const float2* tw = twS + (Ns - 1) + jm;
 #pragma unroll
       for (int m = 1; m <= H; ++m) {
-        float2 a = X[j + m * MR], b = X[j + (R - m) * MR];
+        v2 a = V(X[j + m * MR]), b = V(X[j + (R - m) * MR]);
         if (Ns > 1) {
-          const float2 wa = tw[(m - 1) * Ns], wb = tw[(R - m - 1) * Ns];
-          a = INV ? cmulc(a, wa) : cmul(a, wa);
-          b = INV ? cmulc(b, wb) : cmul(b, wb);
+          const v2 wa = V(tw[(m - 1) * Ns]), wb = V(tw[(R - m - 1) * Ns]);
+          a = INV ? vmulc(a, wa) : vmul(a, wa);
+          b = INV ? vmulc(b, wb) : vmul(b, wb);
         }
-        st[q][m] = cadd(a, b);
-        st[q][H + m] = csub(a, b);
+        st[q][m] = a + b;
+        st[q][H + m] = a - b;
       }
       continue;
     }
@@ -305,7 +323,7 @@ __device__ __forceinline__ void stage_w(float2* X, int M, int Ns, const float2* 
     {
       Dft<R, INV>::run(v);
 #pragma unroll
-      for (int r = 0; r < R; ++r) st[q][r] = v[r];
+      for (int r = 0; r < R; ++r) st[q][r] = V(v[r]);
     }
   }
   sg_wave_fence();
@@ -315,34 +333,20 @@ __device__ __forceinline__ void stage_w(float2* X, int M, int Ns, const float2* 
     if (lane + q * 64 >= MR) continue;
     float2* y = X + base_o[q];
     if constexpr (ODD) {
-      const float2 x0 = st[q][0];
-      float2 y0 = x0;
+      v2 y0 = st[q][0];
 #pragma unroll
-      for (int m = 1; m <= H; ++m) y0 = cadd(y0, st[q][m]);
-      y[0] = y0;
+      for (int m = 1; m <= H; ++m) y0 += st[q][m];
+      y[0] = F(y0);
 #pragma unroll
       for (int k = 1; k <= H; ++k) {
-        float2 P = x0, Q = make_float2(0.f, 0.f);
-#pragma unroll
-        for (int m = 1; m <= H; ++m) {
-          const int id = (m * k) % R;
-          const float c = SgRoots<R>::c(id), s = SgRoots<R>::s(id);
-          P.x = fmaf(st[q][m].x, c, P.x);
-          P.y = fmaf(st[q][m].y, c, P.y);
-          Q.x = fmaf(st[q][H + m].x, s, Q.x);
-          Q.y = fmaf(st[q][H + m].y, s, Q.y);
-        }
-        if (!INV) {
-          y[k * Ns] = make_float2(P.x + Q.y, P.y - Q.x);
-          y[(R - k) * Ns] = make_float2(P.x - Q.y, P.y + Q.x);
-        } else {
-          y[k * Ns] = make_float2(P.x - Q.y, P.y + Q.x);
-          y[(R - k) * Ns] = make_float2(P.x + Q.y, P.y - Q.x);
-        }
+        v2 a, b;
+        odd_out<R, INV>(st[q], k, a, b);
+        y[k * Ns] = F(a);
+        y[(R - k) * Ns] = F(b);
       }
     } else {
 #pragma unroll
-      for (int r = 0; r < R; ++r) y[r * Ns] = st[q][r];
+      for (int r = 0; r < R; ++r) y[r * Ns] = F(st[q][r]);
     }
   }
   sg_wave_fence();
