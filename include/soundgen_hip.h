@@ -269,6 +269,15 @@ int sg_get_rolloff(const double* pitch_per_gc, int32_t n_gc,
                    double rolloffKHz, double baseline, double throwaway,
                    double samplingRate, double* out, int32_t* out_rows);
 
+/* Reference data tables the planner restates (pinned by tests/test_rda_fixtures.py
+ * against the decoded .rda files):
+ *   permittedValues rows 1..33 (data/permittedValues.rda, R/presets.R:22-56):
+ *     name, default, low, high of soundgen()'s range-checked arguments;
+ *   noiseThresholdsDict$q1/$q2[nonlinBalance + 1] (R/sysdata.rda,
+ *     data-raw/noiseThresholdsDict.R), which = 1 or 2. */
+int sg_permitted_value(int32_t i, const char** name, double* def_low_high);
+double sg_noise_threshold(int32_t which, double nonlinBalance);
+
 /* Test hook, no reference counterpart: the wavefront FFT stages used inside
  * the fused STFT/ISTFT kernel, on nframes frames of wl/2 complex points
  * (interleaved re, im, in place semantics: out = DFT(in), unscaled; inverse

@@ -621,6 +621,8 @@ static double noise_q(int which, double nonlinBalance) {
   return 100 / (1 + exp(0.1 * ((double)k - mid)));
 }
 
+OR_API double or_noise_threshold(int which, double nonlinBalance) { return noise_q(which, nonlinBalance); }
+
 /* getIntegerRandomWalk(), R/utilities_math.R:352-387 */
 static void get_integer_random_walk(const double* rw, int64_t len, double nonlinBalance,
                                     const double* minLength, double* out) {
@@ -1546,6 +1548,12 @@ static const double PV[33][3] = {{1,1,20},{1,1,10},{300,20,5000},{200,20,1000},{
   {0,0,100},{50,0,100},{3,0,24},{1,1,100},{5,3,10},{0,0,3},{0,0,100},{50,0,200},{-12,-60,0},{-12,-30,10},
   {0,-50,50},{3,1,20},{-6,-20,0},{6,0,20},{1,0,5},{30,0,60},{15.5,2,100},{100,10,1000},{100,0,500},{300,50,500},
   {0,0,100},{30,10,100},{0,-1,1},{16000,8000,44100},{40,5,100},{-14,-20,20}};
+OR_API int or_permitted_value(int i, const char** name, double* v3) {
+  if (i < 0 || i >= 33) return SG_E_ARG;
+  *name = PV_NAMES[i];
+  v3[0] = PV[i][0]; v3[1] = PV[i][1]; v3[2] = PV[i][2];
+  return 0;
+}
 #define PV_SYLLEN_LOW 20.0
 #define PV_SYLLEN_HIGH 5000.0
 #define PV_PAUSE_LOW 20.0

@@ -177,5 +177,6 @@ vec get_rolloff(const vec& pitch, int64_t nH, const vec& rolloff, const vec& rol
 vec get_random_walk(Rng& R, int64_t len, double rw_range, double rw_smoothing, int method, const vec& trend,
                     bool trend_lazy_rnorm);
 void clumper(vec& s, const vec& minLen);
+double noise_threshold(int which, double nonlinBalance);
 
 }  // namespace sg

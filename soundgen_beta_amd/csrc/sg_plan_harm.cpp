@@ -599,8 +599,7 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
     vec rwbin(nGC, 0.0);
     if (P.nonlinBalance == 100) rwbin.assign(nGC, 2.0);
     else if (P.nonlinBalance != 0) {
-      const double k = (double)(int64_t)(P.nonlinBalance + 1) - 1;  // R truncates the index
-      const double q1 = 100 / (1 + std::exp(0.1 * (k - 33))), q2 = 100 / (1 + std::exp(0.1 * (k - 66)));
+      const double q1 = noise_threshold(1, P.nonlinBalance), q2 = noise_threshold(2, P.nonlinBalance);
       for (int64_t g = 0; g < nGC; ++g) { if (r0100[g] > q1) rwbin[g] = 1; if (r0100[g] > q2) rwbin[g] = 2; }
       vec ml(nGC);
       for (int64_t g = 0; g < nGC; ++g) ml[g] = std::ceil(P.shortestEpoch / 1000 * ppg[g]);
@@ -915,6 +914,15 @@ static int32_t drift_interval(const Batch& B, const SgSyllable& sy, int64_t k) {
   int a = 0, b = l.nk - 1;
   while (a < b - 1) { const int ab = (a + b) >> 1; if (u < x[ab]) b = ab; else a = ab; }
   return a;
+}
+
+// noiseThresholdsDict$q1 / $q2 [nonlinBalance + 1] (R/sysdata.rda, built by
+// data-raw/noiseThresholdsDict.R:1-19: 100 / (1 + exp(-slope (amount - midpoint))),
+// slope -0.1, midpoints 33 and 66); R truncates the index. Pinned value for
+// value against the decoded sysdata.rda (tests/test_rda_fixtures.py).
+double noise_threshold(int which, double nonlinBalance) {
+  const double k = (double)(int64_t)(nonlinBalance + 1) - 1;
+  return 100 / (1 + std::exp(0.1 * (k - (which == 1 ? 33 : 66))));
 }
 
 void tile_syllables(Batch& B, int first_syl) {

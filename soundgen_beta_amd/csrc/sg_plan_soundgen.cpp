@@ -542,6 +542,17 @@ void restore_soundgen_tail(Batch&, int) {}
 
 }  // namespace sg
 
+extern "C" int sg_permitted_value(int32_t i, const char** name, double* def_low_high) {
+  if (i < 0 || i >= sg::kNPV) return SG_E_ARG;
+  *name = sg::kPVNames[i];
+  for (int j = 0; j < 3; ++j) def_low_high[j] = sg::kPV[i][j];
+  return SG_OK;
+}
+
+extern "C" double sg_noise_threshold(int32_t which, double nonlinBalance) {
+  return sg::noise_threshold(which, nonlinBalance);
+}
+
 extern "C" void sg_default_soundgen_args(sg_soundgen_args* a) {
   // formals of soundgen(), R/soundgen.R:208-277 (anchors and formants NA:
   // the caller supplies them, as the R wrapper does)
