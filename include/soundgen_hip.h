@@ -262,12 +262,26 @@ int sg_formant_filter(sg_ctx* ctx, const double* sound, int64_t len,
                       const double* env, int32_t env_nc,
                       int32_t windowLength_points, double overlap,
                       double* out, int64_t cap, int64_t* out_len);
-/* getRolloff() (host helper; R returns H x nGC). out cap = nHarmonics*nGC */
+/* getRolloff() (host helper; R returns H x nGC). out cap = nHarmonics*nGC.
+ * rolloffParabCeiling NaN = NULL (R/sourceSpectrum.R:77, :105-107). */
 int sg_get_rolloff(const double* pitch_per_gc, int32_t n_gc,
                    int32_t nHarmonics, double rolloff, double rolloffOct,
                    double rolloffParab, double rolloffParabHarm,
-                   double rolloffKHz, double baseline, double throwaway,
+                   double rolloffParabCeiling, double rolloffKHz,
+                   double baseline, double throwaway,
                    double samplingRate, double* out, int32_t* out_rows);
+
+/* ---- output writer: seewave::savewav (R/soundgen.R:856, R/morph.R:205) --- */
+/* 16-bit PCM of every call of an executed plan, as savewav(wave, f) converts a
+ * waveform (tuneR::normalize(unit = "16", level = min(max(wave), 1)): center,
+ * scale by level / max|x| unless that is ~0, round(x * 32767) half to even).
+ * d_in: the plan's packed fp32 output; d_out: int16 at the same offsets. */
+int sg_pcm16(sg_ctx* ctx, sg_plan* plan, const float* d_in, int16_t* d_out, void* stream);
+/* The same conversion for one host waveform in R's fp64 arithmetic (on the
+ * GPU); rescale NULL, or {lower, upper} for savewav(rescale = ...). */
+int sg_savewav_pcm(sg_ctx* ctx, const double* wave, int64_t n, const double* rescale, int16_t* pcm_out);
+/* The file tuneR::writeWave(extensible = TRUE) writes for a mono 16-bit Wave. */
+int sg_wav_write(const char* path, const int16_t* pcm, int64_t n, int32_t samplingRate);
 
 /* Reference data tables the planner restates (pinned by tests/test_rda_fixtures.py
  * against the decoded .rda files):

@@ -47,7 +47,7 @@ def lib():
         L.or_istft.argtypes = [dp, dp, i64, i64, C.c_double, i64, dpp, i64p]
         L.or_stft.argtypes = [dp, i64, i64, dp, i64, dp, dp]
         L.or_fft.argtypes = [dp, dp, i64, C.c_int, dp, dp]
-        L.or_get_rolloff.argtypes = [dp, C.c_int32, C.c_int32] + [C.c_double] * 8 + [dp, C.POINTER(C.c_int32)]
+        L.or_get_rolloff.argtypes = [dp, C.c_int32, C.c_int32] + [C.c_double] * 9 + [dp, C.POINTER(C.c_int32)]
         L.or_glottal_cycles.argtypes = [dp, i64, C.c_double, dp]
         L.or_glottal_cycles.restype = i64
         L.or_spline.argtypes = [dp, dp, i64, i64, dp]
@@ -188,12 +188,14 @@ def fft(x, inverse=False):
 
 
 def get_rolloff(pitch_per_gc, nHarmonics=100, rolloff=-12, rolloffOct=-2, rolloffParab=0,
-                rolloffParabHarm=2, rolloffKHz=-6, baseline=200, throwaway=-120, samplingRate=16000):
+                rolloffParabHarm=2, rolloffKHz=-6, baseline=200, throwaway=-120, samplingRate=16000,
+                rolloffParabCeiling=None):
     p = _f64(np.atleast_1d(pitch_per_gc))
     out = np.zeros(nHarmonics * len(p))
     rows = C.c_int32()
+    ceil = float("nan") if rolloffParabCeiling is None else float(rolloffParabCeiling)
     _check(lib().or_get_rolloff(_abi.dptr(p), len(p), nHarmonics, rolloff, rolloffOct, rolloffParab,
-                                rolloffParabHarm, rolloffKHz, baseline, throwaway, samplingRate,
+                                rolloffParabHarm, ceil, rolloffKHz, baseline, throwaway, samplingRate,
                                 _abi.dptr(out), C.byref(rows)))
     H = rows.value
     return out[:H * len(p)].reshape(len(p), H).T
@@ -284,3 +286,23 @@ def loess(x, y, span, z):
     out = np.zeros(len(z))
     _check(lib().or_loess(_abi.dptr(x), _abi.dptr(y), len(x), float(span), _abi.dptr(z), len(z), _abi.dptr(out)))
     return out
+
+
+def savewav_pcm(wave, rescale=None):
+    """The 16-bit samples seewave::savewav writes (seewave.r:5192-5229 ->
+    tuneR::normalize(unit = "16", level), tuneR/R/normalize.R; or seewave::rescale
+    + writeWave's as.integer), restated in numpy float64. mean() is R's
+    long-double mean; here the exact sum (math.fsum) divided by n."""
+    import math
+    x = np.asarray(wave, dtype=np.float64)
+    if rescale is not None:
+        nrange = rescale[1] - rescale[0]
+        y = (x - x.min()) * nrange / (x.max() - x.min()) - nrange / 2
+        return np.trunc(y).astype(np.int16)
+    mx = float(x.max())
+    level = mx if mx <= 1 else 1.0
+    xc = x - math.fsum(x) / len(x)
+    m = max(abs(float(xc.min())), abs(float(xc.max())))
+    if m > 1.5e-8:
+        xc = level * xc / m
+    return np.rint(xc * 32767).astype(np.int16)

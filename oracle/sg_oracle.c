@@ -637,7 +637,7 @@ static void get_integer_random_walk(const double* rw, int64_t len, double nonlin
  * out: nH x nGC col-major buffer; returns kept rows in *H (compacted). */
 static int get_rolloff(const double* pitch, int64_t nGC, int64_t nH,
                        const double* rolloff, const double* rolloffOct,
-                       double rolloffParab, double rolloffParabHarm,
+                       double rolloffParab, double rolloffParabHarm, double rolloffParabCeiling,
                        const double* rolloffKHz, double baseline, double throwaway,
                        double sr, dv* out, int64_t* H) {
   if (nH < 1) return fail(SG_E_DOMAIN, "getRolloff: nHarmonics < 1");
@@ -653,11 +653,12 @@ static int get_rolloff(const double* pitch, int64_t nGC, int64_t nH,
       R_(h, g) = v;
     }
   if (rolloffParab != 0) {
-    double rph = r_round(rolloffParabHarm);
-    if (rph == 2) rph = 3;
-    double a = -4 * rolloffParab / ((rph - 1) * (rph - 1));
-    double b = -a * (1 + rph), c = a * rph;
     for (int64_t g = 0; g < nGC; ++g) {
+      /* R/sourceSpectrum.R:104-110: a ceiling sets the count per gc */
+      double rph = isnan(rolloffParabCeiling) ? r_round(rolloffParabHarm) : r_round(rolloffParabCeiling / pitch[g]);
+      if (rph == 2) rph = 3;
+      double a = -4 * rolloffParab / ((rph - 1) * (rph - 1));
+      double b = -a * (1 + rph), c = a * rph;
       if (rph < 3) { if (rph < 2) R_(0, g) = R_(0, g) + rolloffParab; }
       else {
         if (rph > nH) { dv_free(&r); return fail(SG_E_DOMAIN, "getRolloff: subscript out of bounds (rolloffParabHarm > nHarmonics)"); }
@@ -1000,7 +1001,7 @@ static int gen_harm(const double* pitch_in, int64_t len, const sg_harm_params* P
       rk.v[g] = P->rolloffKHz * w;
     }
     int64_t H;
-    rc = get_rolloff(ppg.v, nGC, nH, ro.v, roo.v, P->rolloffParab, P->rolloffParabHarm, rk.v, 200, P->throwaway, sr, &roll, &H);
+    rc = get_rolloff(ppg.v, nGC, nH, ro.v, roo.v, P->rolloffParab, P->rolloffParabHarm, NAN, rk.v, 200, P->throwaway, sr, &roll, &H);
     dv_free(&ro); dv_free(&roo); dv_free(&rk);
     if (rc) goto done;
     /* shimmer */
@@ -1467,11 +1468,12 @@ OR_API int or_formant_filter(const double* sound, int64_t L, const double* env, 
 }
 
 OR_API int or_get_rolloff(const double* pitch, int32_t nGC, int32_t nH, double rolloff, double rolloffOct,
-                          double rolloffParab, double rolloffParabHarm, double rolloffKHz, double baseline,
-                          double throwaway, double sr, double* out, int32_t* out_rows) {
+                          double rolloffParab, double rolloffParabHarm, double rolloffParabCeiling, double rolloffKHz,
+                          double baseline, double throwaway, double sr, double* out, int32_t* out_rows) {
   dv ro = dv_new(nGC), roo = dv_new(nGC), rk = dv_new(nGC), r; int64_t H;
   for (int g = 0; g < nGC; ++g) { ro.v[g] = rolloff; roo.v[g] = rolloffOct; rk.v[g] = rolloffKHz; }
-  int rc = get_rolloff(pitch, nGC, nH, ro.v, roo.v, rolloffParab, rolloffParabHarm, rk.v, baseline, throwaway, sr, &r, &H);
+  int rc = get_rolloff(pitch, nGC, nH, ro.v, roo.v, rolloffParab, rolloffParabHarm, rolloffParabCeiling, rk.v, baseline,
+                       throwaway, sr, &r, &H);
   if (!rc) { memcpy(out, r.v, H * nGC * sizeof(double)); *out_rows = (int32_t)H; dv_free(&r); }
   dv_free(&ro); dv_free(&roo); dv_free(&rk);
   return rc;

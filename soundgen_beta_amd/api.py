@@ -6,6 +6,7 @@ runs on the GPU through libsoundgen_hip.so. Random draws are injected
 (`normals`, `uniforms`: R's rnorm()/runif() draws in the reference order).
 """
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -106,17 +107,43 @@ def formantFilter(sound, env, windowLength_points, overlap=75, device=0):
     return out[:n.value].copy()
 
 
+def savewav(wave, f=None, filename=None, rescale=None, device=0):
+    """seewave::savewav(wave, f, filename, rescale) as soundgen(savePath = ...)
+    and morph(savePath = ...) call it (R/soundgen.R:856, R/morph.R:205): the
+    16-bit conversion (tuneR::normalize(unit = "16", level = min(max(wave), 1)),
+    or seewave::rescale) runs on the GPU in R's fp64 arithmetic, the file is
+    tuneR::writeWave's WAVE_FORMAT_EXTENSIBLE layout. Returns the int16 samples."""
+    if f is None:
+        raise TypeError("savewav(): the sampling rate f is required for a numeric vector")
+    if filename is None:
+        raise TypeError("savewav(): filename is required (R would deparse the argument name)")
+    x = np.ascontiguousarray(np.asarray(wave, dtype=np.float64).ravel())
+    pcm = np.zeros(len(x), dtype=np.int16)
+    rs = None if rescale is None else np.ascontiguousarray(np.asarray(rescale, dtype=np.float64)[:2])
+    ctx = _ctx(device)
+    native.check(native.lib().sg_savewav_pcm(ctx.ptr, _abi.dptr(x), len(x), _abi.dptr(rs) if rs is not None else None,
+                                             pcm.ctypes.data_as(C.POINTER(C.c_int16))), ctx.ptr)
+    write_wav(filename, pcm, f)
+    return pcm
+
+
+def write_wav(filename, pcm, f):
+    """The file of tuneR::writeWave(Wave(pcm, samp.rate = f, bit = 16)) (extensible header)."""
+    pcm = np.ascontiguousarray(np.asarray(pcm, dtype=np.int16))
+    native.check(native.lib().sg_wav_write(os.fsencode(filename), pcm.ctypes.data_as(C.POINTER(C.c_int16)), len(pcm),
+                                           int(f)))
+
+
 def getRolloff(pitch_per_gc=(440,), nHarmonics=100, rolloff=-12, rolloffOct=-2, rolloffParab=0,
                rolloffParabHarm=2, rolloffParabCeiling=None, rolloffKHz=-6, baseline=200, throwaway=-120,
                samplingRate=16000, plot=False):
     """getRolloff() — R/sourceSpectrum.R:71-186 (host helper; H x nGC matrix)."""
-    if rolloffParabCeiling is not None:
-        raise NotImplementedError("rolloffParabCeiling")
     p = np.ascontiguousarray(np.atleast_1d(np.asarray(pitch_per_gc, dtype=np.float64)))
     out = np.zeros(nHarmonics * len(p))
     rows = C.c_int32()
+    ceil = float("nan") if rolloffParabCeiling is None else float(rolloffParabCeiling)
     rc = native.lib().sg_get_rolloff(_abi.dptr(p), len(p), nHarmonics, rolloff, rolloffOct, rolloffParab,
-                                     rolloffParabHarm, rolloffKHz, baseline, throwaway, samplingRate,
+                                     rolloffParabHarm, ceil, rolloffKHz, baseline, throwaway, samplingRate,
                                      _abi.dptr(out), C.byref(rows))
     native.check(rc)
     H = rows.value

@@ -81,6 +81,12 @@ class Plan:
         native.check(native.lib().sg_execute(self.ctx.ptr, self.ptr, C.c_void_p(d_out_ptr),
                                              C.c_void_p(stream_ptr) if stream_ptr else None), self.ctx.ptr)
 
+    def pcm16(self, d_in_ptr, d_out_ptr, stream_ptr=None):
+        """16-bit PCM of every call (seewave::savewav's conversion) from the packed fp32
+        output at d_in_ptr into int16 at the same offsets of d_out_ptr (device)."""
+        native.check(native.lib().sg_pcm16(self.ctx.ptr, self.ptr, C.c_void_p(d_in_ptr), C.c_void_p(d_out_ptr),
+                                           C.c_void_p(stream_ptr) if stream_ptr else None), self.ctx.ptr)
+
     def close(self):
         if self.ptr:
             native.lib().sg_plan_destroy(self.ptr)
@@ -91,6 +97,35 @@ class Plan:
             self.close()
         except Exception:
             pass
+
+
+def synthesize_to_wav(calls, paths, sampling_rates, device=0):
+    """soundgen(..., savePath = path) for a batch: synthesize on the GPU, convert
+    every call to 16-bit PCM on the GPU (half the bytes cross PCIe), write one
+    WAV file per call (R/soundgen.R:854-856). Returns the int16 arrays."""
+    import torch
+    from . import api
+    ctx = native.default_context(device)
+    plan = Plan(calls, ctx)
+    plan.upload()
+    dev = "cuda:%d" % device
+    out = torch.empty(max(plan.total, 1), dtype=torch.float32, device=dev)
+    pcm = torch.zeros(max(plan.total, 1), dtype=torch.int16, device=dev)
+    sptr = torch.cuda.current_stream(device).cuda_stream
+    plan.execute(out.data_ptr(), sptr)
+    plan.pcm16(out.data_ptr(), pcm.data_ptr(), sptr)
+    torch.cuda.synchronize(device)
+    host = pcm.cpu().numpy()
+    res = []
+    for i in range(plan.n):
+        if plan.status[i] != 0:
+            res.append(native.SoundgenError(int(plan.status[i]), plan.message(i)))
+            continue
+        y = host[plan.offsets[i]:plan.offsets[i] + plan.lengths[i]].copy()
+        api.write_wav(paths[i], y, sampling_rates[i] if hasattr(sampling_rates, "__len__") else sampling_rates)
+        res.append(y)
+    plan.close()
+    return res
 
 
 def synthesize(calls, device=0):

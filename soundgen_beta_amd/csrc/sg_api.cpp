@@ -688,14 +688,91 @@ int sg_spectral_envelope(sg_ctx* ctx, int32_t nr, int32_t nc, const sg_formants*
   });
 }
 
+// ---- output writer: seewave::savewav (R/soundgen.R:856, R/morph.R:205) -------
+int sg_pcm16(sg_ctx* ctx, sg_plan* plan, const float* d_in, int16_t* d_out, void* stream) {
+  return guarded(ctx, [&]() {
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    const sg::Batch& B = plan->B;
+    const int64_t n = (int64_t)B.call_len.size();
+    if (plan->D.pcm.n != n || !plan->D.pcm.buf) plan->D.pcm.prepare(B.call_off.data(), B.call_len.data(), n, s);
+    plan->D.pcm.run(d_in, false, SG_PCM_NORMALIZE, 0.0, d_out, s);
+    return SG_OK;
+  });
+}
+
+int sg_savewav_pcm(sg_ctx* ctx, const double* wave, int64_t n, const double* rescale, int16_t* pcm_out) {
+  return guarded(ctx, [&]() {
+    if (rescale) {  // seewave.r:5200-5204
+      if (rescale[0] >= 0) throw sg::SgError(SG_E_ARG, "The first value of 'rescale' should not be >=0");
+      if (rescale[1] <= 0) throw sg::SgError(SG_E_ARG, "The first value of 'rescale' should not be <=0");
+    }
+    if (n <= 0) return SG_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    double* din = nullptr;
+    int16_t* dout = nullptr;
+    HIPCHK(hipMalloc(&din, (size_t)n * sizeof(double)));
+    std::unique_ptr<void, hipError_t (*)(void*)> h1(din, hipFree);
+    HIPCHK(hipMalloc(&dout, (size_t)n * sizeof(int16_t)));
+    std::unique_ptr<void, hipError_t (*)(void*)> h2(dout, hipFree);
+    HIPCHK(hipMemcpyAsync(din, wave, (size_t)n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    sg::PcmJob job;
+    const int64_t off = 0;
+    job.prepare(&off, &n, 1, ctx->stream);
+    job.run(din, true, rescale ? SG_PCM_RESCALE : SG_PCM_NORMALIZE, rescale ? rescale[1] - rescale[0] : 0.0, dout,
+            ctx->stream);
+    HIPCHK(hipMemcpyAsync(pcm_out, dout, (size_t)n * sizeof(int16_t), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    job.free();
+    return SG_OK;
+  });
+}
+
+// tuneR::writeWave(object, filename, extensible = TRUE) of a mono 16-bit PCM
+// Wave (tuneR_1.3.2.tar.gz::tuneR/R/writeWave.R): RIFF/WAVE, a 40-byte
+// WAVE_FORMAT_EXTENSIBLE fmt chunk (channel mask 1 = front left, PCM subformat
+// GUID), a fact chunk with the sample count, then the little-endian samples.
+int sg_wav_write(const char* path, const int16_t* pcm, int64_t n, int32_t samplingRate) {
+  if (!path || (n > 0 && !pcm) || n < 0 || n > (int64_t)0x7fffffff / 2 - 72) return SG_E_ARG;
+  FILE* f = std::fopen(path, "wb");
+  if (!f) return SG_E_ARG;
+  auto u32 = [&](uint32_t v) { unsigned char b[4] = {(unsigned char)v, (unsigned char)(v >> 8), (unsigned char)(v >> 16), (unsigned char)(v >> 24)}; std::fwrite(b, 1, 4, f); };
+  auto u16 = [&](uint16_t v) { unsigned char b[2] = {(unsigned char)v, (unsigned char)(v >> 8)}; std::fwrite(b, 1, 2, f); };
+  const uint32_t bytes = (uint32_t)(n * 2);
+  std::fwrite("RIFF", 1, 4, f);
+  u32(bytes + 72);
+  std::fwrite("WAVEfmt ", 1, 8, f);
+  u32(40);
+  u16(65534);                              // WAVE_FORMAT_EXTENSIBLE
+  u16(1);                                  // channels
+  u32((uint32_t)samplingRate);
+  u32((uint32_t)samplingRate * 2);         // bytes per second
+  u16(2);                                  // block align
+  u16(16);                                 // bits per sample
+  u16(22);                                 // cbSize
+  u16(16);                                 // valid bits
+  u32(1);                                  // channel mask: FL
+  static const unsigned char guid[16] = {1, 0, 0, 0, 0, 0, 16, 0, 128, 0, 0, 170, 0, 56, 155, 113};  // PCM
+  std::fwrite(guid, 1, 16, f);
+  std::fwrite("fact", 1, 4, f);
+  u32(4);
+  u32((uint32_t)n);
+  std::fwrite("data", 1, 4, f);
+  u32(bytes);
+  for (int64_t i = 0; i < n; ++i) u16((uint16_t)pcm[i]);
+  const bool ok = std::ferror(f) == 0;
+  return std::fclose(f) == 0 && ok ? SG_OK : SG_E_ARG;
+}
+
 int sg_get_rolloff(const double* pitch_per_gc, int32_t n_gc, int32_t nHarmonics, double rolloff, double rolloffOct,
-                   double rolloffParab, double rolloffParabHarm, double rolloffKHz, double baseline,
-                   double throwaway, double samplingRate, double* out, int32_t* out_rows) {
+                   double rolloffParab, double rolloffParabHarm, double rolloffParabCeiling, double rolloffKHz,
+                   double baseline, double throwaway, double samplingRate, double* out, int32_t* out_rows) {
   return guarded(nullptr, [&]() {
     sg::vec p(pitch_per_gc, pitch_per_gc + n_gc);
     int64_t H = 0;
     sg::vec r = sg::get_rolloff(p, nHarmonics, sg::vec(n_gc, rolloff), sg::vec(n_gc, rolloffOct), rolloffParab,
-                                rolloffParabHarm, sg::vec(n_gc, rolloffKHz), baseline, throwaway, samplingRate, H);
+                                rolloffParabHarm, sg::vec(n_gc, rolloffKHz), baseline, throwaway, samplingRate, H,
+                                rolloffParabCeiling);
     std::memcpy(out, r.data(), r.size() * sizeof(double));
     *out_rows = (int32_t)H;
     return SG_OK;

@@ -338,3 +338,20 @@ constexpr double SG_ENV_CUT = 30.0;
 struct SgEnvTask {
   int32_t job, c0;
 };
+
+// ------------------------------------------------------------------------
+// 16-bit PCM output (seewave::savewav -> tuneR::normalize -> writeWave), sg_wav.hip
+constexpr int SG_PCM_NORMALIZE = 0;  // savewav(wave, f): center, level / max|x|, round(x * 32767)
+constexpr int SG_PCM_RESCALE = 1;    // savewav(wave, f, rescale = c(lower, upper))
+constexpr int SG_PCM_TILE = 4096;
+struct SgPcmCall {
+  int64_t off, len;  // the call's samples in the packed buffer (input and output)
+};
+struct SgPcmTile {
+  int32_t call, pad;
+  int64_t k0;
+};
+struct SgPcmStat {
+  double mean, level, m, min, max;
+  int32_t scale, pad;
+};

@@ -167,6 +167,7 @@ int64_t device_bytes(const Batch& B) { return (int64_t)Layout(B).total; }
 
 void device_free(DevicePlan& D) {
   if (D.arena) (void)hipFree(D.arena);
+  D.pcm.free();
   for (hipEvent_t e : D.ev_slice) (void)hipEventDestroy(e);
   if (D.ev_fork) (void)hipEventDestroy(D.ev_fork);
   if (D.ev_join) (void)hipEventDestroy(D.ev_join);

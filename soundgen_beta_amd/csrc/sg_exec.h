@@ -9,6 +9,18 @@
 
 namespace sg {
 
+// per-call 16-bit PCM conversion of a plan's output (sg_wav.hip); built on first use
+struct PcmJob {
+  char* buf = nullptr;
+  SgPcmCall* calls = nullptr;
+  SgPcmTile* tiles = nullptr;
+  SgPcmStat* stats = nullptr;
+  int64_t n = 0, ntiles = 0;
+  void prepare(const int64_t* off, const int64_t* len, int64_t n_calls, hipStream_t s);
+  void run(const void* in, bool f64, int mode, double nrange, int16_t* out, hipStream_t s) const;
+  void free();
+};
+
 struct DevicePlan {
   bool uploaded = false;
   char* arena = nullptr;
@@ -48,6 +60,7 @@ struct DevicePlan {
   SgEnvJob* envjobs = nullptr;
   SgEnvTask* envtasks = nullptr;
   double* elog2 = nullptr;
+  PcmJob pcm;
   std::vector<hipEvent_t> ev_slice;  // slice c's maxes are ready (s -> s2)
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };

@@ -173,7 +173,7 @@ vec sigmoid_half(double sr, double freq, double shape, double spikiness);
 // getRolloff() with per-gc vector parameters (R/sourceSpectrum.R:71-186)
 vec get_rolloff(const vec& pitch, int64_t nH, const vec& rolloff, const vec& rolloffOct, double rolloffParab,
                 double rolloffParabHarm, const vec& rolloffKHz, double baseline, double throwaway, double sr,
-                int64_t& H);
+                int64_t& H, double rolloffParabCeiling = NAN);  // NaN: NULL
 vec get_random_walk(Rng& R, int64_t len, double rw_range, double rw_smoothing, int method, const vec& trend,
                     bool trend_lazy_rnorm);
 void clumper(vec& s, const vec& minLen);

@@ -234,7 +234,7 @@ void clumper(vec& s, const vec& minLen_in) {
 // Returns H x nGC column-major (kept rows compacted, renumbered 1..H).
 vec get_rolloff(const vec& pitch, int64_t nH, const vec& rolloff, const vec& rolloffOct, double rolloffParab,
                 double rolloffParabHarm, const vec& rolloffKHz, double baseline, double throwaway, double sr,
-                int64_t& H) {
+                int64_t& H, double rolloffParabCeiling) {
   ProfScope ps(PF_ROLLOFF);
   const int64_t nGC = (int64_t)pitch.size();
   if (nH < 1) throw SgError(SG_E_DOMAIN, "getRolloff: nHarmonics < 1");
@@ -251,11 +251,13 @@ vec get_rolloff(const vec& pitch, int64_t nH, const vec& rolloff, const vec& rol
       at(h, g) = v;
     }
   if (rolloffParab != 0) {
-    double rph = r_round(rolloffParabHarm);
-    if (rph == 2) rph = 3;
-    const double a = -4 * rolloffParab / ((rph - 1) * (rph - 1));
-    const double b = -a * (1 + rph), c = a * rph;
     for (int64_t g = 0; g < nGC; ++g) {
+      // harmonics affected: round(rolloffParabCeiling / pitch_per_gc) per column when
+      // a ceiling is given, else round(rolloffParabHarm); 2 becomes 3 (boosts H1)
+      double rph = std::isnan(rolloffParabCeiling) ? r_round(rolloffParabHarm) : r_round(rolloffParabCeiling / pitch[g]);
+      if (rph == 2) rph = 3;
+      const double a = -4 * rolloffParab / ((rph - 1) * (rph - 1));
+      const double b = -a * (1 + rph), c = a * rph;
       if (rph < 3) { if (rph < 2) at(0, g) = at(0, g) + rolloffParab; }
       else {
         if (rph > nH) throw SgError(SG_E_DOMAIN, "getRolloff: subscript out of bounds (rolloffParabHarm > nHarmonics)");

@@ -93,9 +93,16 @@ def lib():
                                        C.c_double, _abi.sg_anchors, C.c_double, C.c_double, C.c_double,
                                        C.c_double, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double,
                                        C.c_double, C.POINTER(_abi.sg_random), dp]
-    L.sg_get_rolloff.argtypes = [dp, C.c_int32, C.c_int32] + [C.c_double] * 8 + [dp, C.POINTER(C.c_int32)]
+    L.sg_get_rolloff.argtypes = [dp, C.c_int32, C.c_int32] + [C.c_double] * 9 + [dp, C.POINTER(C.c_int32)]
     fp = C.POINTER(C.c_float)
     L.sg_debug_wave_fft.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, fp, fp]
+    i16p = C.POINTER(C.c_int16)
+    L.sg_pcm16.argtypes = [vp, vp, vp, vp, vp]
+    L.sg_savewav_pcm.argtypes = [vp, dp, i64, dp, i16p]
+    L.sg_wav_write.argtypes = [C.c_char_p, i16p, i64, C.c_int32]
+    L.sg_permitted_value.argtypes = [C.c_int32, C.POINTER(C.c_char_p), dp]
+    L.sg_noise_threshold.argtypes = [C.c_int32, C.c_double]
+    L.sg_noise_threshold.restype = C.c_double
     L.sg_abi_version.restype = C.c_int
     _lib = L
     return L

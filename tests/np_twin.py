@@ -139,7 +139,7 @@ def upsample(ppg, sr):
 
 
 def get_rolloff(pitch, nH, rolloff=-12, rolloffOct=-2, rolloffKHz=-6, baseline=200, throwaway=-120, sr=16000,
-                rolloffParab=0, rolloffParabHarm=2):
+                rolloffParab=0, rolloffParabHarm=2, rolloffParabCeiling=None):
     pitch = np.atleast_1d(np.asarray(pitch, float))
     h = np.arange(1, nH + 1)[:, None]
     r = (rolloff + rolloffKHz * (pitch[None, :] - baseline) / 1000) * np.log2(h)
@@ -147,19 +147,22 @@ def get_rolloff(pitch, nH, rolloff=-12, rolloffOct=-2, rolloffKHz=-6, baseline=2
         r = r + np.where(h >= 2, rolloffOct * (pitch[None, :] * h - baseline) / 1000, 0.0)
     r = np.where(h * pitch[None, :] >= sr / 2, -np.inf, r)
     if rolloffParab != 0:
-        rph = r_round(rolloffParabHarm)
-        if rph == 2:
-            rph = 3
-        with np.errstate(divide="ignore"):
-            a = -4 * rolloffParab / (rph - 1) ** 2
-        b = -a * (1 + rph)
-        c = a * rph
-        if rph < 3:
-            if rph < 2:
-                r[0] = r[0] + rolloffParab
-        else:
-            k = np.arange(1, int(rph) + 1)[:, None]
-            r[:int(rph)] = r[:int(rph)] + a * k ** 2 + b * k + c
+        # R/sourceSpectrum.R:103-132: per-column harmonic counts (a ceiling in Hz, or rolloffParabHarm)
+        rphs = [r_round(rolloffParabCeiling / p) if rolloffParabCeiling is not None else r_round(rolloffParabHarm)
+                for p in pitch]
+        for g, rph in enumerate(rphs):
+            if rph == 2:
+                rph = 3
+            with np.errstate(divide="ignore"):
+                a = -4 * rolloffParab / (rph - 1) ** 2
+            b = -a * (1 + rph)
+            c = a * rph
+            if rph < 3:
+                if rph < 2:
+                    r[0, g] = r[0, g] + rolloffParab
+            else:
+                k = np.arange(1, int(rph) + 1)
+                r[:int(rph), g] = r[:int(rph), g] + a * k ** 2 + b * k + c
     r = np.where(r < throwaway, -np.inf, r)
     r = r - r.max(axis=0, keepdims=True)
     r = 2.0 ** (r / 10)

@@ -51,16 +51,23 @@ ROLLOFF_EXAMPLES = [
     dict(pitch_per_gc=[400], rolloff=-12, rolloffOct=0, rolloffKHz=0, rolloffParab=10, rolloffParabHarm=2),
     dict(pitch_per_gc=[400], rolloff=-12, rolloffOct=0, rolloffKHz=0, rolloffParab=20, rolloffParabHarm=4),
     dict(pitch_per_gc=[400], rolloff=-12, rolloffOct=0, rolloffKHz=0, rolloffParab=-20, rolloffParabHarm=7),
+    # "only harmonics below 2000 Hz are affected" (R/sourceSpectrum.R:67-69)
+    dict(pitch_per_gc=[150, 600], rolloff=-12, rolloffOct=-2, rolloffKHz=-6, rolloffParab=-20, rolloffParabCeiling=2000),
+    dict(pitch_per_gc=[150, 333, 700, 1500], rolloff=-12, rolloffOct=-2, rolloffKHz=-6, rolloffParab=15,
+         rolloffParabCeiling=1000),
 ]
 
 
 @pytest.mark.parametrize("ex", ROLLOFF_EXAMPLES)
 def test_get_rolloff_examples(oracle, ex):
     kw = dict(rolloff=ex["rolloff"], rolloffOct=ex["rolloffOct"], rolloffKHz=ex["rolloffKHz"],
-              rolloffParab=ex.get("rolloffParab", 0), rolloffParabHarm=ex.get("rolloffParabHarm", 2))
+              rolloffParab=ex.get("rolloffParab", 0), rolloffParabHarm=ex.get("rolloffParabHarm", 2),
+              rolloffParabCeiling=ex.get("rolloffParabCeiling"))
     got = oracle.get_rolloff(ex["pitch_per_gc"], nHarmonics=100, samplingRate=16000, **kw)
     want = T.get_rolloff(ex["pitch_per_gc"], 100, kw["rolloff"], kw["rolloffOct"], kw["rolloffKHz"], 200, -120,
-                         16000, kw["rolloffParab"], kw["rolloffParabHarm"])
+                         16000, kw["rolloffParab"], kw["rolloffParabHarm"], kw["rolloffParabCeiling"])
+    from soundgen_beta_amd import api  # the product planner's getRolloff (host helper)
+    np.testing.assert_array_equal(api.getRolloff(ex["pitch_per_gc"], nHarmonics=100, samplingRate=16000, **kw), got)
     assert got.shape == want.shape
     np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-300)
     # every column is normalised to a maximum of exactly 1 (0 dB)
