@@ -32,10 +32,44 @@ generateHarmonics = function(pitch, attackLen = 50, nonlinBalance = 0, nonlinDep
        width = as.double(unlist(lapply(fs, function(f) f$width))))
 }
 
-# R/soundgen.R:208: same formals; the body keeps the reference's argument
-# coercions (R/soundgen.R:305-315, :384-389) and hands the call to the device.
-soundgen_hip = function(...) {
-  a = list(...)
+# R/soundgen.R:208-277: the reference's formals and defaults verbatim; the body
+# keeps the reference's argument coercions (R/soundgen.R:305-315, :384-389) and
+# hands the call to the device. Every formal is passed (as.list(environment())),
+# so the default pitch contour, the vowel-'a' formants and the noise/mouth
+# anchors reach the planner as R would use them.
+soundgen_hip = function(repeatBout = 1, nSyl = 1, sylLen = 300, pauseLen = 200,
+                        pitchAnchors = data.frame(time = c(0, .1, .9, 1), value = c(100, 150, 135, 100)),
+                        pitchAnchorsGlobal = NA, temperature = 0.025,
+                        tempEffects = list(sylLenDep = .02, formDrift = .3, formDisp = .2, pitchDriftDep = .5,
+                                           pitchDriftFreq = .125, pitchAnchorsDep = .05, noiseAnchorsDep = .1,
+                                           amplAnchorsDep = .1),
+                        maleFemale = 0, creakyBreathy = 0, nonlinBalance = 0, nonlinDep = 50, jitterLen = 1,
+                        jitterDep = 3, vibratoFreq = 5, vibratoDep = 0, shimmerDep = 0, attackLen = 50,
+                        rolloff = -12, rolloffOct = -12, rolloffKHz = -6, rolloffParab = 0, rolloffParabHarm = 3,
+                        rolloffLip = 6,
+                        formants = list(f1 = list(time = 0, freq = 860, amp = 30, width = 120),
+                                        f2 = list(time = 0, freq = 1280, amp = 40, width = 120),
+                                        f3 = list(time = 0, freq = 2900, amp = 25, width = 200)),
+                        formantDep = 1, formantDepStoch = 30, vocalTract = 15.5, subFreq = 100, subDep = 100,
+                        shortestEpoch = 300, amDep = 0, amFreq = 30, amShape = 0,
+                        noiseAnchors = data.frame(time = c(0, 300), value = c(-120, -120)),
+                        formantsNoise = NA, rolloffNoise = -14,
+                        mouthAnchors = data.frame(time = c(0, 1), value = c(.5, .5)),
+                        amplAnchors = NA, amplAnchorsGlobal = NA, samplingRate = 16000, windowLength = 50,
+                        overlap = 75, addSilence = 100, pitchFloor = 50, pitchCeiling = 3500,
+                        pitchSamplingRate = 3500, throwaway = -120,
+                        invalidArgAction = c('adjust', 'abort', 'ignore')[1],
+                        plot = FALSE, play = FALSE, savePath = NA, ...) {
+  a = as.list(environment())
+  a$plot = a$play = a$savePath = NULL
+  # a tempEffects list naming only some effects keeps the others' defaults
+  # (R/soundgen.R:458-470 reads them by name); flattened in the ABI's order
+  te = list(sylLenDep = .02, formDrift = .3, formDisp = .2, pitchDriftDep = .5, pitchDriftFreq = .125,
+            pitchAnchorsDep = .05, noiseAnchorsDep = .1, amplAnchorsDep = .1)
+  te[names(tempEffects)] = tempEffects
+  a$tempEffects = as.double(unlist(te[c('sylLenDep', 'formDrift', 'formDisp', 'pitchDriftDep', 'pitchDriftFreq',
+                                        'pitchAnchorsDep', 'noiseAnchorsDep', 'amplAnchorsDep')]))
+  a$invalidArgAction = match(invalidArgAction, c('adjust', 'abort', 'ignore')) - 1L
   if (is.character(a$formants)) a$formants = convertStringToFormants(a$formants)
   # R/soundgen.R:662: noise formants "move" when max(lengths(formantsNoise)) > 1,
   # evaluated on the caller's value (a string counts 1, a formant list its fields)
@@ -46,9 +80,12 @@ soundgen_hip = function(...) {
                'amplAnchorsGlobal')) {
     v = a[[nm]]
     if (is.numeric(v)) a[[nm]] = data.frame(time = seq(0, 1, length.out = length(v)), value = v)
+    if (is.list(v) && !is.data.frame(v)) a[[nm]] = as.data.frame(v)
   }
   a$formants_flat = .sg_flatten_formants(a$formants)
   a$formantsNoise_flat = .sg_flatten_formants(a$formantsNoise)
   a$formants = a$formantsNoise = NULL
-  .Call(C_sg_soundgen, a)
+  bout = .Call(C_sg_soundgen, a)
+  if (!is.na(savePath)) seewave::savewav(bout, filename = savePath, f = samplingRate)  # R/soundgen.R:854-856
+  bout
 }

@@ -147,6 +147,7 @@ SEXP C_sg_soundgen(SEXP args) {
     else if (!strcmp(k, "amplAnchors")) a.amplAnchors = anchors(v);
     else if (!strcmp(k, "amplAnchorsGlobal")) a.amplAnchorsGlobal = anchors(v);
     else if (!strcmp(k, "formantsNoise_rlen")) a.formantsNoise_rlen = Rf_asInteger(v);
+    else if (!strcmp(k, "invalidArgAction")) a.invalidArgAction = Rf_asInteger(v);
     else if (!strcmp(k, "tempEffects") && TYPEOF(v) == REALSXP && Rf_xlength(v) == 8)
       memcpy(a.tempEffects, REAL(v), sizeof a.tempEffects);
   }
