@@ -114,10 +114,15 @@ void plan_range(sg::Batch& B, const sg_call_desc* calls, int64_t c0, int64_t c1)
       if (d.kind == SG_CALL_HARMONICS) {
         if (!d.pitch || !d.harm) throw sg::SgError(SG_E_ARG, "harmonics call without pitch/params");
         L = sg::plan_harmonics(B, d.pitch, d.pitch_len, *d.harm, d.amplAnchors, R, off, false);
+        sg::ProfScope pt(sg::PF_TILES);
         sg::tile_syllables(B, first_syl);
       } else if (d.kind == SG_CALL_SOUNDGEN) {
         if (!d.args) throw sg::SgError(SG_E_ARG, "soundgen call without args");
-        L = sg::plan_soundgen(B, *d.args, R, off, first_syl);
+        {
+          sg::ProfScope pg(sg::PF_SOUNDGEN);
+          L = sg::plan_soundgen(B, *d.args, R, off, first_syl);
+        }
+        sg::ProfScope pt(sg::PF_TILES);
         sg::tile_syllables(B, first_syl);
       } else {
         throw sg::SgError(SG_E_ARG, "unknown call kind");
@@ -366,7 +371,8 @@ int sg_plan_batch(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, sg_pl
       sg::finalize_spec(B);
     }
     if (sg::g_prof_on) {
-      static const char* names[] = {"harmonics", "rolloff", "contour", "envelope", "noise", "filter", "finalize", "finalize_spec"};
+      static const char* names[] = {"harmonics", "rolloff", "contour", "envelope", "noise", "filter", "finalize",
+                                    "finalize_spec", "fry", "crossfade", "emit", "tasks", "tiles", "soundgen"};
       for (int i = 0; i < sg::PF_N; ++i)
         std::fprintf(stderr, "sg_plan_prof %-14s %.3f s\n", names[i], sg::g_prof_ns[i].exchange(0) * 1e-9);
       std::fprintf(stderr, "sg_plan_prof host MB: fl %.1f amps %.1f knots %.1f cknots %.1f tasks %.1f segs %.1f "

@@ -242,14 +242,20 @@ vec get_rolloff(const vec& pitch, int64_t nH, const vec& rolloff, const vec& rol
   auto at = [&](int64_t h, int64_t g) -> double& { return r[g * nH + h]; };
   bool anyOct = false;
   for (double v : rolloffOct) if (v != 0) anyOct = true;
-  for (int64_t h = 0; h < nH; ++h)
-    for (int64_t g = 0; g < nGC; ++g) {
+  vec slope(nGC);
+  for (int64_t g = 0; g < nGC; ++g) slope[g] = rolloff[g] + rolloffKHz[g] * (pitch[g] - baseline) / 1000;
+  for (int64_t g = 0; g < nGC; ++g) {
+    double* col = &r[g * nH];
+    for (int64_t h = 0; h < nH; ++h) {
       const double hh = (double)(h + 1);
+      if (hh * pitch[g] >= sr / 2) {  // above Nyquist: -Inf for this and every higher row
+        for (int64_t k = h; k < nH; ++k) col[k] = -INFINITY;
+        break;
+      }
       const double delta = (anyOct && h >= 1) ? rolloffOct[g] * (pitch[g] * hh - baseline) / 1000 : 0.0;
-      double v = ((rolloff[g] + rolloffKHz[g] * (pitch[g] - baseline) / 1000) * std::log2(hh)) + delta;
-      if (hh * pitch[g] >= sr / 2) v = -INFINITY;
-      at(h, g) = v;
+      col[h] = (slope[g] * std::log2(hh)) + delta;
     }
+  }
   if (rolloffParab != 0) {
     for (int64_t g = 0; g < nGC; ++g) {
       // harmonics affected: round(rolloffParabCeiling / pitch_per_gc) per column when
@@ -271,7 +277,7 @@ vec get_rolloff(const vec& pitch, int64_t nH, const vec& rolloff, const vec& rol
     for (int64_t h = 0; h < nH; ++h) if (at(h, g) > mx) mx = at(h, g);
     for (int64_t h = 0; h < nH; ++h) at(h, g) = at(h, g) - mx;
   }
-  for (auto& v : r) v = std::pow(2.0, v / 10);
+  for (auto& v : r) v = v == -INFINITY ? 0.0 : std::pow(2.0, v / 10);
   std::vector<int64_t> keep;
   for (int64_t h = 0; h < nH; ++h) {
     long double s = 0;
@@ -319,11 +325,22 @@ static EpochMat fry_per_epoch(const double* roll, int64_t H, int64_t g0, int64_t
   for (int64_t g = 0; g < ncol; ++g) { RN(0, g) = 0; RN(nr - 1, g) = 0; }
   char a[64], b[64];
   for (int64_t h = 0; h < H; ++h) {  // match(rownames(rolloff), rownames(rolloff_new))
+    // rownames are 15-significant-digit strings: harmonic h + 1 can only match
+    // gseq[(h + 1) (nSub + 1)] (within an ulp of h + 1; every other entry is at
+    // least 1 / (nSub + 1) away). Confirm that one string, else search all.
+    int64_t hit = -1;
+    const int64_t i0 = (h + 1) * (nSub + 1);
     snprintf(a, sizeof a, "%.15g", (double)(h + 1));
-    for (int64_t i = 0; i < nr; ++i) {
-      snprintf(b, sizeof b, "%.15g", gseq[i]);
-      if (!strcmp(a, b)) { for (int64_t g = 0; g < ncol; ++g) RN(i, g) = roll[(g0 + g) * H + h]; break; }
+    if (i0 < nr) {
+      snprintf(b, sizeof b, "%.15g", gseq[i0]);
+      if (!strcmp(a, b)) hit = i0;
     }
+    for (int64_t i = 0; hit < 0 && i < nr; ++i) {
+      snprintf(b, sizeof b, "%.15g", gseq[i]);
+      if (!strcmp(a, b)) hit = i;
+    }
+    if (hit >= 0)
+      for (int64_t g = 0; g < ncol; ++g) RN(hit, g) = roll[(g0 + g) * H + h];
   }
   vec ml(nSub * ncol);
   for (int64_t s = 1; s <= nSub; ++s)
@@ -659,6 +676,7 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
       for (int64_t h = 0; h < H; ++h) roll[g * H + h] *= sh;
     }
   std::vector<EpochMat> mats;
+  ProfScope pfry(PF_FRY);
   if (P.subDep > 0 && P.nonlinBalance > 0) {
     vec sf(nGC), sd(nGC);
     for (int64_t g = 0; g < nGC; ++g) { const double w4 = std::pow(rw[g], 4); sf[g] = P.subFreq * w4; sd[g] = P.subDep * w4 * vf_on[g]; }
@@ -707,6 +725,7 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
     he.knots.assign(gc_up.begin() + mats[e].g0, gc_up.begin() + mats[e].g1 + 1);
   }
   // crossFade chain → pieces (host fp64 decisions)
+  ProfScope pxf(PF_XFADE);
   Chain A;
   A.E = &HE;
   A.P.push_back(HPiece{0, 1, {}});  // waveform = 0
@@ -719,6 +738,7 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
   }
 
   // ------------------------------------------------ emit device arrays
+  ProfScope pem(PF_EMIT);
   const int32_t syl_idx = (int32_t)B.syls.size();
   SgSyllable sy{};
   sy.L = Lsyl;
@@ -823,6 +843,7 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
   // sine-bank wave tasks: <= SG_TASK_MAX samples inside one amplitude
   // interval, or inside a run of intervals with equal columns
   B.syls.back().task0 = (int64_t)B.tasks.size();
+  ProfScope ptk(PF_TASKS);
   const int64_t nseg = (int64_t)HS.segs.size();
   for (size_t e = 0; e < mats.size(); ++e) {
     const HostEpoch& he = HE[e];

@@ -6,6 +6,8 @@
 // R's operation order; per-sample work runs in sg_fft.hip.
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "sg_plan.h"
@@ -26,8 +28,10 @@ int64_t fs_alloc(Batch& B, int64_t n) {
 
 int64_t fl_push(Batch& B, const double* v, int64_t n) {
   const int64_t o = (int64_t)B.fl.size();
-  for (int64_t i = 0; i < n; ++i) B.fl.push_back((float)v[i]);
-  while (B.fl.size() % 4) B.fl.push_back(0.f);  // 16-B aligned blocks
+  B.fl.resize((size_t)(o + (n + 3) / 4 * 4));  // 16-B aligned blocks
+  float* d = B.fl.data() + o;
+  for (int64_t i = 0; i < n; ++i) d[i] = (float)v[i];
+  for (int64_t i = n; i < (n + 3) / 4 * 4; ++i) d[i] = 0.f;
   return o;
 }
 
@@ -271,13 +275,11 @@ bool plan_noise(Batch& B, Rng& R, int64_t len, const sg_anchors& noiseAnchors, d
   // z1 = complex(real = runif(nr * nc)), column-major: bin fastest   R/source.R:111
   // (nr = wl / 2 is x.5 for an odd wl: floor(nr * nc) draws, matrix(nrow = nr)
   // keeps as.integer(nr) rows of them)
-  vec u((size_t)(nr * nc));
   const int64_t ndraw = (int64_t)((double)wl / 2 * (double)nc);
-  for (int64_t q = 0; q < ndraw; ++q) {
-    const double x = R.unif();
-    if (q < nr * nc) u[q] = x;
-  }
-  const int64_t u_off = fl_push(B, u.data(), (int64_t)u.size());
+  const int64_t u_off = (int64_t)B.fl.size();
+  B.fl.resize((size_t)(u_off + (nr * nc + 3) / 4 * 4), 0.f);
+  R.unif_f32(std::min<int64_t>(ndraw, nr * nc), B.fl.data() + u_off);
+  if (ndraw > nr * nc) R.unif_f32(ndraw - nr * nc, nullptr);
   const bool fused = fusable(B.geoms[gi], (double)wl * (100 - overlap) / 100);
   const int64_t fr = fused ? 0 : fs_alloc(B, nc * wl);
   for (int64_t c = 0; c < nc; ++c) {
@@ -746,6 +748,25 @@ void finalize_spec(Batch& B) {
     B.seg_range[ph][1] = (int64_t)B.olasegs.size();
   }
   B.n_segslots = nslots;
+  if (std::getenv("SG_DEBUG_PLAN")) {
+    int64_t owned = 0, run = 0, real = 0;
+    for (const SgSegment& sg : B.olasegs) {
+      if (sg.nf <= 0) continue;
+      ++real;
+      run += sg.nf;
+    }
+    for (const SgOla& o : B.olas_dev) if (o.fused) owned += o.nframes;
+    for (int ph = 0; ph < 2; ++ph) {
+      int64_t fr = 0, sgs = 0;
+      for (int64_t i = B.seg_range[ph][0]; i < B.seg_range[ph][1]; ++i)
+        if (B.olasegs[i].nf > 0) { fr += B.olasegs[i].nf; ++sgs; }
+      std::fprintf(stderr, "sg plan: phase %d: %lld frames computed in %lld segments (%zu frames, %zu unfused groups)\n", ph,
+                   (long long)fr, (long long)sgs, B.frames[ph].size(), (size_t)(B.fgroup_range[ph][2] - B.fgroup_range[ph][1]));
+    }
+    std::fprintf(stderr, "sg plan: %lld fused segments (%lld slots incl. padding), %lld frames owned, %lld computed (%.1f%% recomputed)\n",
+                 (long long)real, (long long)B.olasegs.size(), (long long)owned, (long long)run,
+                 owned ? 100.0 * (double)(run - owned) / (double)owned : 0.0);
+  }
   // items and mixes referring to filter-phase OLAs: device index = ola_split + i
   for (SgNoiseItem& it : B.items)
     if (it.flags & SG_ITEM_FILTER_OLA) {

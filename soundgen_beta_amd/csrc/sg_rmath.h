@@ -198,6 +198,21 @@ struct Rng {
     if (s && s->unif_cb) return s->unif_cb(s->user);
     throw SgError(SG_E_RANDOM, "uniform stream exhausted");
   }
+  // n consecutive runif() draws as floats (out may be null: draws consumed, discarded)
+  void unif_f32(int64_t n, float* out) {
+    int64_t k = 0;
+    if (s) {
+      const int64_t avail = std::max<int64_t>(0, std::min<int64_t>(n, s->n_uniforms - iu));
+      if (out)
+        for (int64_t q = 0; q < avail; ++q) out[q] = (float)s->uniforms[iu + q];
+      iu += avail;
+      k = avail;
+    }
+    for (; k < n; ++k) {
+      const double x = unif();
+      if (out) out[k] = (float)x;
+    }
+  }
   // rnorm(1, mu, sd): no draw when sd == 0 (nmath/rnorm.c)
   double rnorm(double mu, double sd) {
     if (sd == 0.0 || !std::isfinite(mu)) return mu;
