@@ -446,6 +446,47 @@ struct HostEpoch {
     }
     return acc;
   }
+  // W(j) by Clenshaw's recurrence over rows r -> multiplier (r + 1) / D (one
+  // sin/cos per sample instead of one sin per row). *err bounds |Wfast - W|:
+  // the recurrence (~R^2 eps), and R's 15-digit multipliers (rowname
+  // round trip) against (r + 1) / D, times the row amplitudes.
+  double Wfast(int64_t j, double* err) const {
+    const double v = r_seqint_at(knots.front(), knots.back(), n, j);
+    int64_t i = 0, jj = G - 1;
+    while (i < jj - 1) { int64_t ij = (i + jj) / 2; if (v < knots[ij]) jj = ij; else i = ij; }
+    const double t = (v - knots[i]) / (knots[jj] - knots[i]);
+    const double integ = S->integr(u0 + j);
+    double x = integ / (double)M->D;
+    x -= std::rint(x);
+    const double th = 2 * M_PI * x, c2 = 2 * std::cos(th);
+    double b1 = 0, b2 = 0, sabs = 0;
+    for (int64_t r = M->R - 1; r >= 0; --r) {
+      const double y0 = M->A[i * M->R + r], y1 = M->A[jj * M->R + r];
+      double am = (M->mult[r] == 0) ? 0.0 : (v == knots[jj] ? y1 : (v == knots[i] ? y0 : y0 + (y1 - y0) * t));
+      const double b = am + c2 * b1 - b2;
+      b2 = b1;
+      b1 = b;
+      sabs += std::fabs(am);
+    }
+    const double Rr = (double)M->R;
+    *err = sabs * (Rr * Rr * 1e-15 + 1e-14 * std::fabs(integ) * Rr / (double)M->D) + 1e-300;
+    return b1 * std::sin(th);
+  }
+  // sign-exact W for the zero-crossing search: the fast value where its error
+  // bound cannot change the sign, else R's row-by-row sum
+  double Wsign(int64_t j) const {
+    if (!fast_ok) return W(j);
+    double err;
+    const double f = Wfast(j, &err);
+    return std::fabs(f) > 1e3 * err ? f : W(j);
+  }
+  bool fast_ok = false;  // every present row's multiplier is (r + 1) / D
+  void init_fast() {
+    static const bool exact_only = std::getenv("SG_XFADE_EXACT") != nullptr;  // test knob: R's row sums only
+    fast_ok = M->D >= 1 && !exact_only;
+    for (int64_t r = 0; r < M->R && fast_ok; ++r)
+      if (M->mult[r] != 0 && std::fabs(M->mult[r] * (double)M->D - (double)(r + 1)) > 1e-9) fast_ok = false;
+  }
 };
 
 // --------------------------------------------------- crossFade chain
@@ -464,6 +505,24 @@ struct Chain {
     double v = 0;
     for (const HTerm& t : p.t) v += (t.w0 + q * (t.w1 + q * t.w2)) * (*E)[t.e].W(t.j0 + (k - p.start));
     return v;
+  }
+  // the same value where only its sign matters (zero-crossing search): fast
+  // Clenshaw terms with an error bound, R's exact sum when the bound is close
+  double sign_at(int64_t k) const {
+    int64_t lo = 0, hi = (int64_t)P.size() - 1;
+    while (lo < hi) { int64_t m = (lo + hi + 1) / 2; if (P[m].start <= k) lo = m; else hi = m - 1; }
+    const HPiece& p = P[lo];
+    const double q = (double)(k - p.start);
+    double v = 0, err = 0;
+    for (const HTerm& t : p.t) {
+      const HostEpoch& ep = (*E)[t.e];
+      if (!ep.fast_ok) return at(k);
+      double e;
+      const double w = t.w0 + q * (t.w1 + q * t.w2);
+      v += w * ep.Wfast(t.j0 + (k - p.start), &e);
+      err += std::fabs(w) * e;
+    }
+    return std::fabs(v) > 1e3 * (err + 1e-300) ? v : at(k);
   }
   void truncate(int64_t newL) {
     while (!P.empty() && P.back().start >= newL) P.pop_back();
@@ -515,12 +574,12 @@ static HTerm rebase(const HTerm& t, double s) {  // weight polynomial shifted by
 // crossFade(A, W_e), R/utilities_soundgen.R:328-375
 static void cross_fade(Chain& A, const HostEpoch& W, int64_t e, double sr, double crossLen) {
   const int64_t LA = A.L();
-  const int64_t zc1 = find_zero_crossing([&](int64_t k) { return A.at(k); }, LA, LA);
+  const int64_t zc1 = find_zero_crossing([&](int64_t k) { return A.sign_at(k); }, LA, LA);
   if (zc1) {
     A.truncate(zc1);
     A.P.push_back(HPiece{zc1, 1, {}});
   }
-  const int64_t zc2 = find_zero_crossing([&](int64_t j) { return W.W(j); }, W.n, 1);
+  const int64_t zc2 = find_zero_crossing([&](int64_t j) { return W.Wsign(j); }, W.n, 1);
   const int64_t w0 = zc2;  // W' = W[zc2 ..] (0-based)
   const int64_t lenW = W.n - w0;
   const int64_t L1 = A.L();
@@ -723,6 +782,7 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
     he.G = mats[e].g1 - mats[e].g0 + 1;
     if (he.G < 2) throw SgError(SG_E_DOMAIN, "approx: need at least two non-NA values to interpolate");
     he.knots.assign(gc_up.begin() + mats[e].g0, gc_up.begin() + mats[e].g1 + 1);
+    he.init_fast();
   }
   // crossFade chain → pieces (host fp64 decisions)
   ProfScope pxf(PF_XFADE);
