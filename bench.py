@@ -18,7 +18,7 @@ the envelopes and the sine bank to the final mix, inputs resident in HBM
 value = samples of all ranks / max over ranks of the timed wall time.
 value_host_resident adds the device-to-host copy of every waveform into pinned
 host memory inside the timed region ("to waveforms resident in
-host memory").
+host memory"); each plan chunk's copy overlaps the kernels of the chunks after it.
 
 With --gpus N and no WORLD_SIZE in the environment, bench.py starts itself
 under torch.distributed.run with N ranks (one per GPU) before touching the GPU.
@@ -364,7 +364,9 @@ def main():
         prof[name] = (ms.value, n.value)
 
     # the same steps with every waveform copied to pinned host memory (the timed
-    # region ends with the samples resident on the host)
+    # region ends with the samples resident on the host). The copy of plan c's
+    # outputs runs on a second stream while the following plans compute; plan c
+    # of the next step waits only for that copy.
     dt_host = None
     if args.host_steps > 0:
         try:
@@ -374,13 +376,25 @@ def main():
             host = torch.empty(max(base, 1), dtype=torch.float32)
             pinned = False
         host.copy_(out)
+        cstream = torch.cuda.Stream(dev)
+        ends = [b + (p.total + 63) // 64 * 64 for p, b, _ in plans]
         if dist:
             dist.barrier()
         torch.cuda.synchronize(dev)
         t1 = time.perf_counter()
+        copied = [None] * len(plans)
         for _ in range(args.host_steps):
-            step()
-            host.copy_(out, non_blocking=pinned)
+            for i, ((p, b, _), e) in enumerate(zip(plans, ends)):
+                if copied[i] is not None:
+                    stream.wait_event(copied[i])  # plan i's region is free again
+                p.execute(out.data_ptr() + 4 * b, sptr)
+                done = torch.cuda.Event()
+                done.record(stream)
+                cstream.wait_event(done)
+                with torch.cuda.stream(cstream):
+                    host[b:e].copy_(out[b:e], non_blocking=pinned)
+                copied[i] = torch.cuda.Event()
+                copied[i].record(cstream)
         torch.cuda.synchronize(dev)
         if dist:
             dist.barrier()

@@ -43,6 +43,39 @@ __device__ __forceinline__ double contour_at(const SgContour& c, const double* _
   return c.db ? (double)exp2f((float)(v * 0.1)) : v;  // 2^(dB/10); fp32 exp2 (rel. err ~1e-7)
 }
 
+// contour_at for a caller-held interval cursor i (start at -1) and k increasing
+// between calls: the first call bisects (as contour_at), later calls step forward,
+// finding the same interval (the largest i with x[i] <= u) in ~1 load instead of
+// log2(nk) dependent loads.
+__device__ __forceinline__ double contour_at_cursor(const SgContour& c, const double* __restrict__ ck, int64_t L,
+                                                    int64_t k, int& i) {
+  if (c.kind != 3) return contour_at(c, ck, L, k);
+  const double* x = ck + c.k_off;
+  const double* y = x + c.nk;
+  const double* b = y + c.nk;
+  const double* cc = b + c.nk;
+  const double* d = cc + c.nk;
+  double u;
+  if (k == 0) u = c.a;
+  else if (k == L - 1) u = c.b;
+  else {
+    const double by = L == c.L ? c.by : (c.b - c.a) / (double)(L - 1);
+    u = (k < L / 2) ? c.a + (double)k * by : c.b - (double)(L - 1 - k) * by;
+  }
+  if (i < 0) {
+    int a = 0, j = c.nk;
+    do { int m = (a + j) >> 1; if (u < x[m]) j = m; else a = m; } while (j > a + 1);
+    i = a;
+  } else {
+    while (i + 1 <= c.nk - 1 && x[i + 1] <= u) ++i;
+  }
+  const double dx = u - x[i];
+  double v = y[i] + dx * (b[i] + dx * (cc[i] + dx * d[i]));
+  v = v < c.lo ? c.lo : v;
+  v = v > c.hi ? c.hi : v;
+  return c.db ? (double)exp2f((float)(v * 0.1)) : v;
+}
+
 __device__ __forceinline__ double linear_at(const SgLinear& l, const double* __restrict__ ck, int64_t L, int64_t k) {
   const double* x = ck + l.k_off;
   const double* y = x + l.nk;

@@ -957,6 +957,12 @@ extern "C" __global__ __launch_bounds__(256) void sg_mix(const SgMixTile* __rest
   // per-tile constants, hoisted out of the sample loops (one scalar-load burst)
   const float base_scale = X.base_kind == SG_BASE_NORM ? 1.f / olamax[X.base_ola] : 1.f;
   const bool has_base = X.base_kind != SG_BASE_NONE;
+  // contour interval cursors (sgd::contour_at_cursor): a thread's samples of an
+  // item only move forward, so after one bisection each lookup is a step
+  constexpr int NC = 8;  // items with an LDS-held cursor per thread
+  __shared__ int curs[NC][256];
+  for (int i = 0; i < NC && i < X.nitems; ++i) curs[i][threadIdx.x] = -1;
+  int mcur = -1;
 #pragma unroll 1
   for (int64_t kc = T.k0; kc < kend; kc += E * 256) {
     float v[E];
@@ -983,21 +989,25 @@ extern "C" __global__ __launch_bounds__(256) void sg_mix(const SgMixTile* __rest
         const int64_t j = j0 + e * 256;
         raw[e] = fs[it.raw + (j < 0 ? 0 : (j >= it.len ? it.len - 1 : j))];
       }
+      int cur = i < NC ? curs[i][threadIdx.x] : -1;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const int64_t k = kc + e * 256 + threadIdx.x, j = j0 + e * 256;
         if (k >= kend || j < 0 || j >= it.len) continue;
         float nv = raw[e] * nscale;
         if (flat) nv *= sflat;
-        else if (it.strength.kind != 0) nv = (float)((double)nv * contour_at(it.strength, cknots, it.len, j));
+        else if (it.strength.kind != 0)
+          nv = (float)((double)nv * sgd::contour_at_cursor(it.strength, cknots, it.len, j, cur));
         nv *= fade_in_out(it.fade, it.len, j);
         v[e] += nv;
       }
+      if (i < NC) curs[i][threadIdx.x] = cur;
     }
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int64_t k = kc + e * 256 + threadIdx.x;
-      if (X.mult.kind != 0) v[e] = (float)((double)v[e] * contour_at(X.mult, cknots, X.len, k));
+      if (X.mult.kind != 0 && k < kend)
+        v[e] = (float)((double)v[e] * sgd::contour_at_cursor(X.mult, cknots, X.len, k, mcur));
       if (X.am_lo > 0) v[e] *= 1.f - sigmoid_at(fl + X.am_tab, X.am_lo, k) * X.am_dep / 100.f;
     }
 #pragma unroll
