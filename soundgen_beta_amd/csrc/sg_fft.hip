@@ -352,8 +352,31 @@ __device__ __forceinline__ void stage_w(float2* X, int M, int Ns, const float2* 
   sg_wave_fence();
 }
 
+// Diagnostic build only (-DSG_STFT_STAMPS): cycles per section of the
+// sg_stft_ola frame loop, accumulated per wave with s_memtime and summed into a
+// buffer that nothing else reads (sg_debug_stft_stamps).
+#ifdef SG_STFT_STAMPS
+__device__ unsigned long long sg_stft_st[16];
+#define SG_ST(i)                                          \
+  do {                                                    \
+    if (st_acc) {                                         \
+      const uint64_t _t = __builtin_amdgcn_s_memtime();   \
+      st_acc[i] += _t - *st_last;                         \
+      *st_last = _t;                                      \
+    }                                                     \
+  } while (0)
+#define SG_ST_PARAMS , uint64_t *st_acc = nullptr, uint64_t *st_last = nullptr
+#define SG_ST_ARGS , st_acc, st_last
+#else
+#define SG_ST(i) \
+  do {           \
+  } while (0)
+#define SG_ST_PARAMS
+#define SG_ST_ARGS
+#endif
+
 template <bool INV>
-__device__ __forceinline__ void fft_w(float2* X, const SgFftGeom& g, const float2* twS, int lane) {
+__device__ __forceinline__ void fft_w(float2* X, const SgFftGeom& g, const float2* twS, int lane SG_ST_PARAMS) {
   int Ns = 1;
   for (int s = 0; s < g.nstages; ++s) {
     const int R = g.radix[s];
@@ -369,6 +392,7 @@ __device__ __forceinline__ void fft_w(float2* X, const SgFftGeom& g, const float
       default: break;
     }
     Ns *= R;
+    SG_ST((INV ? 5 : 1) + (s < 2 ? s : 2));
   }
 }
 
@@ -634,7 +658,7 @@ __device__ __forceinline__ void frame_prefetch(FramePf& P, const SgFrame& F, int
 // hamming -> forward FFT -> untangle, /wl x envelope, seewave's Hermitian
 // mirror; NOISE: uniforms x filter). Tables in LDS: ham (wl floats), twN (M pairs).
 __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mode, const SgFftGeom& g,
-                                            const float2* twS, const float2* twN, const float* ham, int lane) {
+                                            const float2* twS, const float2* twN, const float* ham, int lane SG_ST_PARAMS) {
   int M = g.M, N = g.wl;
   __asm__ __volatile__("" : "+s"(M), "+s"(N));  // opaque: no hoisting across the caller's frame loop
   const float invN = 1.f / (float)N;
@@ -646,7 +670,8 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
       if (n < M) A[n] = make_float2(P.s[i].x * ham[2 * n], P.s[i].y * ham[2 * n + 1]);
     }
     sg_wave_fence();
-    fft_w<false>(A, g, twS, lane);
+    SG_ST(0);
+    fft_w<false>(A, g, twS, lane SG_ST_ARGS);
     // untangle X[k] = E + W_N^k O (E, O from Z_k, conj Z_{M-k}), Y = X / wl x env,
     // pack for the inverse; pair k owns slots k and M - k, the k = 0 lane also
     // reads slots 1, M - 1 and half; every read of an iteration precedes its writes
@@ -779,6 +804,12 @@ extern "C" __global__ __launch_bounds__(SG_FFT_WAVES * 64) __attribute__((amdgpu
 #pragma unroll
   for (int r = 0; r < SG_CARRY_PAIRS; ++r) C[r] = make_float2(0.f, 0.f);
   FramePf P;
+#ifdef SG_STFT_STAMPS
+  uint64_t st_accv[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t st_lastv = __builtin_amdgcn_s_memtime();
+  uint64_t* st_acc = st_accv;
+  uint64_t* st_last = &st_lastv;
+#endif
   int bf = bstart(S.f0);
   for (int k = 0; k < S.nf; ++k) {
     {
@@ -786,8 +817,9 @@ extern "C" __global__ __launch_bounds__(SG_FFT_WAVES * 64) __attribute__((amdgpu
       __asm__ __volatile__("" : "+s"(Mk));
       frame_prefetch(P, frames[S.fdev + k], S.mode, Mk, fl, fs, lane);
     }
-    frame_front(A, P, S.mode, g, twS, twN, ham, lane);
-    fft_w<true>(A, g, twS, lane);
+    frame_front(A, P, S.mode, g, twS, twN, ham, lane SG_ST_ARGS);
+    SG_ST(4);
+    fft_w<true>(A, g, twS, lane SG_ST_ARGS);
     int Mk = M, Nk = N;
     __asm__ __volatile__("" : "+s"(Mk), "+s"(Nk));
     // window (/wl x hanning) and add the carry (pairs n = 64 r + lane)
@@ -804,6 +836,7 @@ extern "C" __global__ __launch_bounds__(SG_FFT_WAVES * 64) __attribute__((amdgpu
       A[n] = make_float2(v.x * invN * han[2 * n], v.y * invN * han[2 * n + 1]);
     }
     sg_wave_fence();
+    SG_ST(8);
     const bool lastf = k == S.nf - 1;
     const int bn = lastf ? S.pb : bstart(S.f0 + k + 1);
     const int D = bn - bf;  // samples [bf, bn) are final
@@ -825,7 +858,15 @@ extern "C" __global__ __launch_bounds__(SG_FFT_WAVES * 64) __attribute__((amdgpu
     }
     sg_wave_fence();  // the next frame overwrites the slice
     bf = bn;
+    SG_ST(9);
   }
+#ifdef SG_STFT_STAMPS
+  if (lane == 0) {
+    for (int i = 0; i < 10; ++i) atomicAdd(&sg_stft_st[i], (unsigned long long)st_acc[i]);
+    atomicAdd(&sg_stft_st[10], (unsigned long long)S.nf);
+    atomicAdd(&sg_stft_st[11], 1ull);
+  }
+#endif
   // matchLengths padding (zeros) outside the istft output
   if (S.flags & SG_SEG_FIRST)
     for (int q = lane; q < min(len, -first); q += 64) {
@@ -1087,3 +1128,11 @@ void launch_mix(const DevicePlan& D, int64_t t0, int64_t n_tiles, float* out, hi
   SG_LAUNCHED("sg_mix");
 }
 }  // namespace sg
+
+#ifdef SG_STFT_STAMPS
+extern "C" int sg_debug_stft_stamps(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(sg_stft_st), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+  unsigned long long z[16] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(sg_stft_st), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif

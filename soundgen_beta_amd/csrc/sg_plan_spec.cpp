@@ -9,6 +9,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <string>
 
 #include "sg_plan.h"
 #include "sg_prof.h"
@@ -762,6 +764,19 @@ void finalize_spec(Batch& B) {
         if (B.olasegs[i].nf > 0) { fr += B.olasegs[i].nf; ++sgs; }
       std::fprintf(stderr, "sg plan: phase %d: %lld frames computed in %lld segments (%zu frames, %zu unfused groups)\n", ph,
                    (long long)fr, (long long)sgs, B.frames[ph].size(), (size_t)(B.fgroup_range[ph][2] - B.fgroup_range[ph][1]));
+    }
+    std::map<int32_t, int64_t> gfr;  // fused frames per geometry
+    for (const SgSegment& sg : B.olasegs)
+      if (sg.nf > 0) gfr[sg.geom] += sg.nf;
+    std::vector<std::pair<int64_t, int32_t>> gs;
+    for (const auto& kv : gfr) gs.push_back({kv.second, kv.first});
+    std::sort(gs.rbegin(), gs.rend());
+    for (size_t i = 0; i < gs.size() && i < 16; ++i) {
+      const SgFftGeom& g = B.geoms[gs[i].second];
+      std::string rs;
+      for (int s = 0; s < g.nstages; ++s) rs += (s ? "x" : "") + std::to_string(g.radix[s]);
+      std::fprintf(stderr, "sg plan: geom wl=%d M=%d radices %s: %lld frames\n", g.wl, g.M, rs.c_str(),
+                   (long long)gs[i].first);
     }
     std::fprintf(stderr, "sg plan: %lld fused segments (%lld slots incl. padding), %lld frames owned, %lld computed (%.1f%% recomputed)\n",
                  (long long)real, (long long)B.olasegs.size(), (long long)owned, (long long)run,
