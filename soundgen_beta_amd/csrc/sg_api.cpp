@@ -176,6 +176,11 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
       if (j == (int32_t)D.geoms.size()) {
         SgFftGeom G = S.geoms[g];
         G.tw += c.fl; G.tws += c.fl; G.win += c.fl;
+        for (SgCdft& cd : G.cd) {  // sub-geometries precede their users in the part
+          if (cd.n == 0) continue;
+          cd.geom = gmap[k][cd.geom];
+          cd.chirp += c.fl; cd.bf += c.fl;
+        }
         D.geoms.push_back(G);
       }
       gmap[k][g] = j;

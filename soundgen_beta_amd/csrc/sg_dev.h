@@ -178,9 +178,22 @@ struct SgSylTile {
 // `fl`; intermediate buffers (frame scratch, sound, raw noise) in `fs`.
 
 constexpr int SG_FFT_MAX_STAGES = 12;
+// One complex n-point DFT of sg_fft_frames (SG_FFT_DFT, SG_FFT_ODD geometries):
+// a workgroup Stockham FFT when every prime factor of n is <= 31, else
+// Bluestein's chirp-z form X_k = c_k sum_j (x_j c_j) conj(c_{k-j}), c_m = exp(-pi i m^2 / n),
+// whose convolution runs as two L-point FFTs (L >= 2n - 1, 5-smooth).
+struct SgCdft {
+  int32_t n;      // points
+  int32_t geom;   // geometry index of the FFT of size n (L == 0) or L (its M)
+  int32_t L;      // Bluestein length, 0 = plain FFT
+  int32_t pad;
+  int64_t chirp;  // fl offset: n pairs c_m
+  int64_t bf;     // fl offset: L pairs FFT_L(b) / L, b = conj(c) wrapped circularly
+};
 // FFT geometry of one window length wl = N (even), computed as a complex
 // FFT of M = N/2 points (real-input / Hermitian-output packing).
 struct SgFftGeom {
+  SgCdft cd[2];                    // SG_FFT_DFT: cd[0] = the M-point transform; SG_FFT_ODD: cd[0] = wl points, cd[1] = wl - 1
   int32_t wl, M, nstages, fb;      // fb: frames per workgroup
   int32_t radix[SG_FFT_MAX_STAGES];
   int64_t tw;                      // fl offset: M pairs W_M^t, then M pairs W_N^k (interleaved re, im)
@@ -197,12 +210,11 @@ struct SgFftGeom {
 
 constexpr int SG_FFT_WG = 0;
 constexpr int SG_FFT_WAVE = 1;
-constexpr int SG_FFT_DFT = 2;   // M with a prime factor > 31: direct O(M^2) DFT in sg_fft_frames
+constexpr int SG_FFT_DFT = 2;   // M with a prime factor > 31: Bluestein (SgCdft) in sg_fft_frames
 // odd wl (windowLength_points = floor(L / 2) for short sounds, R/soundgen.R:743):
 // seewave's stft keeps wl %/% 2 = M rows, istft inverts 2M = wl - 1 points and
-// recycles them against the wl-point window (seewave.r:3468-3479). Direct DFTs,
-// one frame per sg_fft_frames workgroup; tw = wl pairs W_wl^t, tws = 2M pairs
-// exp(+2 pi i t / 2M)
+// recycles them against the wl-point window (seewave.r:3468-3479). Complex
+// wl-point and 2M-point DFTs (cd[0], cd[1]), one frame per sg_fft_frames workgroup
 constexpr int SG_FFT_ODD = 3;
 constexpr int SG_WAVE_STATE = 24;  // complex butterfly points a lane holds per stage in sg_stft_ola
 #ifndef SG_FFT_WAVES_N

@@ -2,6 +2,7 @@
 #include "sg_exec.h"
 
 #include <algorithm>
+#include <map>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -119,9 +120,27 @@ static void split_finalize_tiles(Batch& B) {
 
 void finalize_plan(Batch& B) {
   split_finalize_tiles(B);
-  if (std::getenv("SG_DEBUG_PLAN"))
+  if (std::getenv("SG_DEBUG_PLAN")) {
     std::fprintf(stderr, "sg plan: %zu sine tasks, %zu syllables, %zu copy tiles, %zu general finalize tiles\n",
                  B.tasks.size(), B.syls.size(), B.copy_tiles.size(), B.fin_tiles.size());
+    // sine-bank work: (sample, row) terms of the fp32 and the tall tasks, rows histogram of the tall ones
+    double terms[2] = {0, 0};
+    int64_t ntask[2] = {0, 0}, rmax = 0, samples[2] = {0, 0};
+    std::map<int, int64_t> rh;
+    for (const SgWTask& t : B.tasks) {
+      const int k = t.R > SG_ROWS_F32 ? 1 : 0;
+      terms[k] += (double)t.R * t.len * ((t.flags & SG_TASK_CONST) ? 1 : 2);
+      ++ntask[k];
+      samples[k] += t.len;
+      if (k) {
+        rmax = std::max<int64_t>(rmax, t.R);
+        rh[t.R < 256 ? 0 : t.R < 512 ? 1 : t.R < 1024 ? 2 : t.R < 2048 ? 3 : 4]++;
+      }
+    }
+    std::fprintf(stderr, "sg plan: sine tasks fp32 %lld (%lld samples, %.3g chain terms), tall %lld (%lld samples, %.3g chain terms, max R %lld; R<256 %lld, <512 %lld, <1024 %lld, <2048 %lld, more %lld)\n",
+                 (long long)ntask[0], (long long)samples[0], terms[0], (long long)ntask[1], (long long)samples[1], terms[1],
+                 (long long)rmax, (long long)rh[0], (long long)rh[1], (long long)rh[2], (long long)rh[3], (long long)rh[4]);
+  }
   B.ptiles.clear();
   for (size_t s = 0; s < B.syls.size(); ++s) {
     SgSyllable& sy = B.syls[s];

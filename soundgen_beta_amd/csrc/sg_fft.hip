@@ -22,6 +22,9 @@
 #ifndef SG_FFT_WPE
 #define SG_FFT_WPE 2  // build knob: waves per SIMD for sg_stft_ola
 #endif
+#ifndef SG_PF_AHEAD
+#define SG_PF_AHEAD 0  // build knob: issue the next frame's input loads before this frame's inverse FFT
+#endif
 #include "sg_devfn.h"
 #include "sg_roots.h"
 
@@ -248,7 +251,8 @@ __device__ void fft_ip(float2* X, const SgFftGeom& g, const float2* twM, int fb)
     const int R = g.radix[s];
     const uint32_t mm = g.mr_magic[s], nm = g.ns_magic[s];
     int Ms = g.M;
-    __asm__ __volatile__("" : "+s"(Ms));  // keep M / R and its multiples inside the stage (no hoisted SGPRs)
+    Ms = __builtin_amdgcn_readfirstlane(Ms);  // wave-uniform also when called out of line
+
     const int ts = udiv(Ms / R, nm);      // M / (Ns R)
     switch (R) {
 #define SG_STAGE(RR) \
@@ -275,11 +279,14 @@ struct NbW {
   static constexpr int value = SG_WAVE_STATE / R > 0 ? SG_WAVE_STATE / R : 1;
 };
 
-template <int R, bool INV>
-__device__ __forceinline__ void stage_w(float2* X, int M, int Ns, const float2* twS, uint32_t ns_magic, int lane) {
+// CM, CNS > 0: the frame size and the stage's stride are compile-time constants
+// (the dominant geometry's specialisation: index math folds away)
+template <int R, bool INV, int CM = 0, int CNS = 0>
+__device__ __forceinline__ void stage_w(float2* X, int M_, int Ns_, const float2* twS, uint32_t ns_magic, int lane) {
   constexpr int NB = NbW<R>::value;
   constexpr bool ODD = (R % 2) == 1;
   constexpr int H = ODD ? (R - 1) / 2 : 1;
+  const int M = CM ? CM : M_, Ns = CNS ? CNS : Ns_;
   const int MR = M / R;
   v2 st[NB][R];
   int base_o[NB];
@@ -289,7 +296,7 @@ __device__ __forceinline__ void stage_w(float2* X, int M, int Ns, const float2* 
     const int j = lane + q * 64;
     base_o[q] = 0;
     if (j >= MR) continue;
-    const int jm = j - udiv(j, ns_magic) * Ns;
+    const int jm = CNS ? j % CNS : j - udiv(j, ns_magic) * Ns;
     base_o[q] = (j - jm) * R + jm;
     if constexpr (ODD) {
       // pairs (m, R - m) one at a time: inputs, twiddles and the symmetric
@@ -396,23 +403,51 @@ __device__ __forceinline__ void fft_w(float2* X, const SgFftGeom& g, const float
   }
 }
 
-// Direct M-point DFT of one frame (geometries whose M has a prime factor
-// > 31): out[k] = sum_n x[n] W_M^{+-nk}, the exponent reduced mod M on the fly;
-// out-of-place into S, then copied back.
+// The dominant geometry (C5: 94 % of frames are wl = 2204, M = 1102 = 2 x 19 x 29)
+// with every size and stride a compile-time constant
+template <bool INV, int CM, int R0, int R1, int R2>
+__device__ __forceinline__ void fft_wc(float2* X, const float2* twS, int lane SG_ST_PARAMS) {
+  stage_w<R0, INV, CM, 1>(X, CM, 1, twS, 0u, lane);
+  SG_ST(INV ? 5 : 1);
+  stage_w<R1, INV, CM, R0>(X, CM, R0, twS, 0u, lane);
+  SG_ST(INV ? 6 : 2);
+  stage_w<R2, INV, CM, R0 * R1>(X, CM, R0 * R1, twS, 0u, lane);
+  SG_ST(INV ? 7 : 3);
+}
+#ifndef SG_STFT_SPEC
+#define SG_STFT_SPEC 1  // build knob: compile-time specialisation of sg_stft_ola for M = 1102 = 2 x 19 x 29
+#endif
+
+// Complex n-point DFT of X (LDS, n points, in place) by the workgroup (sg_fft_frames):
+// the Stockham FFT of size n, or Bluestein's chirp-z form through two L-point
+// FFTs in Z (L points) -- SgCdft, planned by make_cdft (sg_plan_spec.cpp).
+// INV: exp(+2 pi i jk / n), computed as conj(DFT(conj x)). tw: >= max(n, L) pairs.
 template <bool INV>
-__device__ void dft_ip(float2* X, float2* S, const float2* twM, int M) {
-  for (int k = threadIdx.x; k < M; k += SG_FFT_THREADS) {
-    float2 acc = make_float2(0.f, 0.f);
-    int e = 0;
-    for (int n = 0; n < M; ++n) {
-      acc = cadd(acc, INV ? cmulc(X[n], twM[e]) : cmul(X[n], twM[e]));
-      e += k;
-      if (e >= M) e -= M;
-    }
-    S[k] = acc;
+__device__ void cdft(float2* X, const SgCdft& c, const SgFftGeom* __restrict__ geoms, const float* __restrict__ fl,
+                     float2* Z, float2* tw) {
+  const SgFftGeom& gs = geoms[c.geom];
+  const int T = c.L ? c.L : c.n;
+  const float2* twg = reinterpret_cast<const float2*>(fl + gs.tw);  // W_T^t, t < T
+  for (int t = threadIdx.x; t < T; t += SG_FFT_THREADS) tw[t] = twg[t];
+  if (!c.L) {
+    __syncthreads();
+    fft_ip<INV>(X, gs, tw, 1);
+    return;
   }
+  const int n = c.n, L = c.L;
+  const float2* ch = reinterpret_cast<const float2*>(fl + c.chirp);
+  const float2* bf = reinterpret_cast<const float2*>(fl + c.bf);
+  for (int j = threadIdx.x; j < L; j += SG_FFT_THREADS)
+    Z[j] = j < n ? cmul(INV ? cconj(X[j]) : X[j], ch[j]) : make_float2(0.f, 0.f);
   __syncthreads();
-  for (int k = threadIdx.x; k < M; k += SG_FFT_THREADS) X[k] = S[k];
+  fft_ip<false>(Z, gs, tw, 1);
+  for (int k = threadIdx.x; k < L; k += SG_FFT_THREADS) Z[k] = cmul(Z[k], bf[k]);
+  __syncthreads();
+  fft_ip<true>(Z, gs, tw, 1);
+  for (int k = threadIdx.x; k < n; k += SG_FFT_THREADS) {
+    const float2 v = cmul(Z[k], ch[k]);
+    X[k] = INV ? cconj(v) : v;
+  }
   __syncthreads();
 }
 
@@ -420,64 +455,50 @@ __device__ void dft_ip(float2* X, float2* S, const float2* twM, int M) {
 // M = N %/% 2 bins of the N-point DFT (/N); istft inverts the 2M = N - 1
 // point Hermitian extension X = (Y_0..Y_{M-1}, Re Y_{M-1}, conj Y_{M-1}..conj Y_1)
 // and recycles it against the N-point Hann window (seewave.r:3468-3479):
-//   frame[i] = han[i] / 2M * (Re Y_0 + (-1)^n Re Y_{M-1} + 2 sum_{k=1}^{M-1} Re(Y_k e^{+2 pi i n k / 2M})),
-//   n = i mod 2M.
-// Direct sums (O(N M) per frame; odd lengths only occur for sounds shorter
-// than two windows), tables and the frame staged in LDS.
+//   frame[i] = han[i] / 2M * Re(sum_t X_t e^{+2 pi i n t / 2M}),  n = i mod 2M.
+// Both transforms are complex DFTs of the frame buffer B (N points) in place.
 __device__ void odd_frame(const SgFrameGroup& G, const SgFrame* __restrict__ frames, const SgFftGeom& g,
-                          const float* __restrict__ fl, float* __restrict__ fs, float4* lds4) {
+                          const SgFftGeom* __restrict__ geoms, const float* __restrict__ fl, float* __restrict__ fs,
+                          float4* lds4) {
   const int N = g.wl, M = g.M, N2 = 2 * M;
-  float2* tw = reinterpret_cast<float2*>(lds4);  // W_N^t, t < N
-  float2* ti = tw + N;                           // exp(+2 pi i t / 2M), t < 2M
-  float2* Y = ti + N2;                           // M bins
-  float* x = reinterpret_cast<float*>(Y + M);    // N windowed samples
-  const float2* twg = reinterpret_cast<const float2*>(fl + g.tw);
-  const float2* tig = reinterpret_cast<const float2*>(fl + g.tws);
-  for (int t = threadIdx.x; t < N; t += SG_FFT_THREADS) tw[t] = twg[t];
-  for (int t = threadIdx.x; t < N2; t += SG_FFT_THREADS) ti[t] = tig[t];
+  const int T = max(g.cd[0].L ? g.cd[0].L : g.cd[0].n, g.cd[1].L ? g.cd[1].L : g.cd[1].n);
+  float2* B = reinterpret_cast<float2*>(lds4);  // N points
+  float2* Z = B + N;                            // Bluestein work buffer
+  float2* tw = Z + T;                           // FFT twiddles
   const SgFrame F = frames[G.f0];
   const float* ham = fl + g.win;
   const float* han = ham + N;
+  // Y_k (k < M) into B[k], then the Hermitian extension in place (B[M + 1 ..] hold
+  // bins >= M of the forward transform, which nothing reads)
   if (G.mode == SG_FRAME_FILTER) {
     const float* s = fs + F.src;
-    for (int n = threadIdx.x; n < N; n += SG_FFT_THREADS) x[n] = s[n] * ham[n];
+    for (int n = threadIdx.x; n < N; n += SG_FFT_THREADS) B[n] = make_float2(s[n] * ham[n], 0.f);
     __syncthreads();
+    cdft<false>(B, g.cd[0], geoms, fl, Z, tw);
     const float* env = fl + F.env;
     const float invN = 1.f / (float)N;
     for (int k = threadIdx.x; k < M; k += SG_FFT_THREADS) {
-      float2 acc = make_float2(0.f, 0.f);
-      int e = 0;
-      for (int n = 0; n < N; ++n) {
-        acc.x = fmaf(x[n], tw[e].x, acc.x);
-        acc.y = fmaf(x[n], tw[e].y, acc.y);
-        e += k;
-        if (e >= N) e -= N;
-      }
       const float sc = invN * env[k];
-      Y[k] = make_float2(acc.x * sc, acc.y * sc);
+      const float2 y = make_float2(B[k].x * sc, B[k].y * sc);
+      B[k] = y;
+      if (k > 0) B[N2 - k] = cconj(y);
+      if (k == M - 1) B[M] = make_float2(y.x, 0.f);
     }
   } else {  // SG_FRAME_NOISE: real spectrum u * filter
     const float* u = fl + F.src;
     const float* flt = fl + F.env;
-    for (int k = threadIdx.x; k < M; k += SG_FFT_THREADS) Y[k] = make_float2(u[k] * flt[k], 0.f);
+    for (int k = threadIdx.x; k < M; k += SG_FFT_THREADS) {
+      const float2 y = make_float2(u[k] * flt[k], 0.f);
+      B[k] = y;
+      if (k > 0) B[N2 - k] = y;
+      if (k == M - 1) B[M] = y;
+    }
   }
   __syncthreads();
+  cdft<true>(B, g.cd[1], geoms, fl, Z, tw);
   const float invN2 = 1.f / (float)N2;
   float* d = fs + F.dst;
-  for (int i = threadIdx.x; i < N; i += SG_FFT_THREADS) {
-    const int n = i < N2 ? i : i - N2;
-    float acc = Y[0].x + ((n & 1) ? -Y[M - 1].x : Y[M - 1].x);
-    float part = 0.f;
-    int e = n;
-    for (int k = 1; k < M; ++k) {
-      part = fmaf(Y[k].x, ti[e].x, part);
-      part = fmaf(-Y[k].y, ti[e].y, part);
-      e += n;
-      if (e >= N2) e -= N2;
-    }
-    acc = fmaf(2.f, part, acc);
-    d[i] = acc * invN2 * han[i];
-  }
+  for (int i = threadIdx.x; i < N; i += SG_FFT_THREADS) d[i] = B[i < N2 ? i : i - N2].x * invN2 * han[i];
 }
 
 }  // namespace
@@ -491,14 +512,15 @@ extern "C" __global__ __launch_bounds__(SG_FFT_THREADS) void sg_fft_frames(
   const SgFrameGroup G = groups[blockIdx.x];
   const SgFftGeom& g = geoms[G.geom];
   if (g.kind == SG_FFT_ODD) {  // workgroup-uniform
-    odd_frame(G, frames, g, fl, fs, lds4);
+    odd_frame(G, frames, g, geoms, fl, fs, lds4);
     return;
   }
   const int M = g.M, N = g.wl, fb = G.nf;
   const float2* twg = reinterpret_cast<const float2*>(fl + g.tw);
   const float2* twN = twg + M;  // L1/L2 resident (one read per bin pair)
-  float2* twM = A + fb * M;     // W_M table in LDS behind the frames
-  for (int t = threadIdx.x; t < M; t += SG_FFT_THREADS) twM[t] = twg[t];
+  float2* twM = A + fb * M;     // W_M table in LDS behind the frames (SG_FFT_DFT: the Bluestein buffers)
+  if (g.kind != SG_FFT_DFT)
+    for (int t = threadIdx.x; t < M; t += SG_FFT_THREADS) twM[t] = twg[t];
   if (threadIdx.x < fb) fr[threadIdx.x] = frames[G.f0 + threadIdx.x];
   __syncthreads();
   const float* ham = fl + g.win;
@@ -514,7 +536,7 @@ extern "C" __global__ __launch_bounds__(SG_FFT_THREADS) void sg_fft_frames(
       A[idx] = make_float2(s[2 * n] * ham[2 * n], s[2 * n + 1] * ham[2 * n + 1]);
     }
     __syncthreads();
-    if (g.kind == SG_FFT_DFT) dft_ip<false>(A, twM + M, twM, M);
+    if (g.kind == SG_FFT_DFT) cdft<false>(A, g.cd[0], geoms, fl, twM, twM + g.cd[0].L);
     else fft_ip<false>(A, g, twM, fb);
     // untangle the real transform: X[k] = E + W_N^k O, E = (Z_k + conj Z_{M-k})/2,
     // O = -i (Z_k - conj Z_{M-k}) / 2; Y = X / N * env; pack for the inverse
@@ -596,7 +618,7 @@ extern "C" __global__ __launch_bounds__(SG_FFT_THREADS) void sg_fft_frames(
     }
     __syncthreads();
   }
-  if (g.kind == SG_FFT_DFT) dft_ip<true>(A, twM + M, twM, M);
+  if (g.kind == SG_FFT_DFT) cdft<true>(A, g.cd[0], geoms, fl, twM, twM + g.cd[0].L);
   else fft_ip<true>(A, g, twM, fb);
   // windowed frame: Re(ifft)/N x hann, y[2n] = Re z[n], y[2n+1] = Im z[n]
   for (int idx = threadIdx.x; idx < fb * M; idx += SG_FFT_THREADS) {
@@ -614,10 +636,15 @@ extern "C" __global__ __launch_bounds__(SG_FFT_THREADS) void sg_fft_frames(
 //   FILTER: s[i] = sound (y[2n], y[2n+1]), n = 64 i + lane; a[i] = envelope
 //           (env[k], env[M - k]) with k = 64 i + lane (k = 0: env[0], env[M-1]); xh = env[half]
 //   NOISE:  a[i] = uniforms (u[k], u[M - k]), b[i] = filter (f[k], f[M - k]) (k = 0: M - 1); xh, xh2 at half
+// NOISE's filter pairs share the FILTER sound registers (b[i] = s[i]): the mode is
+// wave-uniform but not a compile-time constant, so separate arrays would both be allocated
+static_assert(SG_PF_PAIR <= SG_PF_SRC, "noise filter pairs alias the sound pairs");
 struct FramePf {
   float2 s[SG_PF_SRC];
-  float2 a[SG_PF_PAIR], b[SG_PF_PAIR];
+  float2 a[SG_PF_PAIR];
   float xh, xh2;
+  __device__ __forceinline__ float2& b(int i) { return s[i]; }
+  __device__ __forceinline__ const float2& b(int i) const { return s[i]; }
 };
 
 __device__ __forceinline__ void frame_prefetch(FramePf& P, const SgFrame& F, int mode, int M,
@@ -646,7 +673,7 @@ __device__ __forceinline__ void frame_prefetch(FramePf& P, const SgFrame& F, int
       if (k <= half) {
         const int km = k == 0 ? M - 1 : M - k;
         P.a[i] = make_float2(u[k], u[km]);
-        P.b[i] = make_float2(flt[k], flt[km]);
+        P.b(i) = make_float2(flt[k], flt[km]);
       }
     }
     P.xh = u[half];
@@ -657,10 +684,11 @@ __device__ __forceinline__ void frame_prefetch(FramePf& P, const SgFrame& F, int
 // Consume P: the frame's packed inverse-FFT input lands in A (FILTER: sound x
 // hamming -> forward FFT -> untangle, /wl x envelope, seewave's Hermitian
 // mirror; NOISE: uniforms x filter). Tables in LDS: ham (wl floats), twN (M pairs).
+template <int CM, int R0, int R1, int R2>
 __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mode, const SgFftGeom& g,
                                             const float2* twS, const float2* twN, const float* ham, int lane SG_ST_PARAMS) {
-  int M = g.M, N = g.wl;
-  __asm__ __volatile__("" : "+s"(M), "+s"(N));  // opaque: no hoisting across the caller's frame loop
+  int M = CM ? CM : g.M, N = CM ? 2 * CM : g.wl;
+  if (!CM) __asm__ __volatile__("" : "+s"(M), "+s"(N));  // opaque: no hoisting across the caller's frame loop
   const float invN = 1.f / (float)N;
   const int half = M / 2;
   if (mode == SG_FRAME_FILTER) {
@@ -671,7 +699,8 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
     }
     sg_wave_fence();
     SG_ST(0);
-    fft_w<false>(A, g, twS, lane SG_ST_ARGS);
+    if constexpr (CM != 0) fft_wc<false, CM, R0, R1, R2>(A, twS, lane SG_ST_ARGS);
+    else fft_w<false>(A, g, twS, lane SG_ST_ARGS);
     // untangle X[k] = E + W_N^k O (E, O from Z_k, conj Z_{M-k}), Y = X / wl x env,
     // pack for the inverse; pair k owns slots k and M - k, the k = 0 lane also
     // reads slots 1, M - 1 and half; every read of an iteration precedes its writes
@@ -731,7 +760,7 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
       const int k = 64 * i + lane;
       if (k > half) continue;
       if (k == 0) {
-        const float y0 = P.a[i].x * P.b[i].x, nyq = P.a[i].y * P.b[i].y;
+        const float y0 = P.a[i].x * P.b(i).x, nyq = P.a[i].y * P.b(i).y;
         A[0] = make_float2(y0 + nyq, y0 - nyq);
         if (M % 2 == 0) {
           const float2 yk = make_float2(P.xh * P.xh2, 0.f);
@@ -740,7 +769,7 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
           A[half] = a;
         }
       } else if (k < M - k) {
-        const float2 yk = make_float2(P.a[i].x * P.b[i].x, 0.f), ym = make_float2(P.a[i].y * P.b[i].y, 0.f);
+        const float2 yk = make_float2(P.a[i].x * P.b(i).x, 0.f), ym = make_float2(P.a[i].y * P.b(i).y, 0.f);
         float2 a, b;
         pack_pair(yk, ym, twN[k], a, b);
         A[k] = a;
@@ -763,32 +792,14 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
 // registers while this frame's inverse FFT runs. Frames never leave LDS;
 // summation is in frame order, so results are deterministic.
 // LDS: twS (M pairs), twN (M pairs), ham + han (M pairs each), SG_FFT_WAVES slices (M pairs each).
-extern "C" __global__ __launch_bounds__(SG_FFT_WAVES * 64) __attribute__((amdgpu_waves_per_eu(SG_FFT_WPE))) void sg_stft_ola(
-    const SgSegment* __restrict__ segs, const SgOla* __restrict__ olas, const SgFrame* __restrict__ frames,
-    const SgFftGeom* __restrict__ geoms, const float* __restrict__ fl, float* __restrict__ fs,
-    float* __restrict__ slotmax) {
-  constexpr int W = SG_FFT_WAVES, NT = W * 64;
-  extern __shared__ float4 lds4[];
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // w wave-uniform
-  const SgFftGeom& g = geoms[segs[blockIdx.x * W].geom];  // the planner groups segments by geometry
-  const int M = g.M, N = g.wl;
-  float2* twS = reinterpret_cast<float2*>(lds4);
-  float2* twN = twS + M;
-  float* ham = reinterpret_cast<float*>(twN + M);
-  float* han = ham + N;
-  {
-    const float2* tsg = reinterpret_cast<const float2*>(fl + g.tws);
-    const float2* tng = reinterpret_cast<const float2*>(fl + g.tw) + M;
-    const float* wg = fl + g.win;
-    for (int t = threadIdx.x; t < M; t += NT) {
-      if (t < M - 1) twS[t] = tsg[t];
-      twN[t] = tng[t];
-    }
-    for (int t = threadIdx.x; t < 2 * N; t += NT) ham[t] = wg[t];  // hamming then hanning
-  }
-  __syncthreads();
-  const SgSegment S = segs[blockIdx.x * W + w];
-  if (S.nf <= 0) return;  // padding segment
+// One segment of sg_stft_ola (CM > 0: the M = CM geometry with radices R0 x R1 x R2, sizes folded)
+template <int CM, int R0, int R1, int R2>
+__device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __restrict__ olas,
+                                             const SgFrame* __restrict__ frames, const SgFftGeom& g,
+                                             const float* __restrict__ fl, float* __restrict__ fs,
+                                             float* __restrict__ slotmax, float2* twS, const float2* twN,
+                                             const float* ham, const float* han, int w, int lane) {
+  const int M = CM ? CM : g.M, N = CM ? 2 * CM : g.wl;
   const SgOla& O = olas[S.ola];
   float2* A = twS + M * (4 + w);
   const float* Af = reinterpret_cast<const float*>(A);
@@ -811,17 +822,35 @@ extern "C" __global__ __launch_bounds__(SG_FFT_WAVES * 64) __attribute__((amdgpu
   uint64_t* st_last = &st_lastv;
 #endif
   int bf = bstart(S.f0);
+#if SG_PF_AHEAD
+  {
+    int Mk = M;
+    if (!CM) __asm__ __volatile__("" : "+s"(Mk));
+    frame_prefetch(P, frames[S.fdev], S.mode, Mk, fl, fs, lane);
+  }
+#endif
   for (int k = 0; k < S.nf; ++k) {
+#if !SG_PF_AHEAD
     {
       int Mk = M;
-      __asm__ __volatile__("" : "+s"(Mk));
+      if (!CM) __asm__ __volatile__("" : "+s"(Mk));
       frame_prefetch(P, frames[S.fdev + k], S.mode, Mk, fl, fs, lane);
     }
-    frame_front(A, P, S.mode, g, twS, twN, ham, lane SG_ST_ARGS);
+#endif
+    frame_front<CM, R0, R1, R2>(A, P, S.mode, g, twS, twN, ham, lane SG_ST_ARGS);
+#if SG_PF_AHEAD
+    // the next frame's inputs are in flight during this frame's inverse FFT and overlap-add
+    if (k + 1 < S.nf) {
+      int Mk = M;
+      if (!CM) __asm__ __volatile__("" : "+s"(Mk));
+      frame_prefetch(P, frames[S.fdev + k + 1], S.mode, Mk, fl, fs, lane);
+    }
+#endif
     SG_ST(4);
-    fft_w<true>(A, g, twS, lane SG_ST_ARGS);
+    if constexpr (CM != 0) fft_wc<true, CM, R0, R1, R2>(A, twS, lane SG_ST_ARGS);
+    else fft_w<true>(A, g, twS, lane SG_ST_ARGS);
     int Mk = M, Nk = N;
-    __asm__ __volatile__("" : "+s"(Mk), "+s"(Nk));
+    if (!CM) __asm__ __volatile__("" : "+s"(Mk), "+s"(Nk));
     // window (/wl x hanning) and add the carry (pairs n = 64 r + lane)
 #pragma unroll
     for (int r = 0; r < SG_CARRY_PAIRS; ++r) {
@@ -880,6 +909,40 @@ extern "C" __global__ __launch_bounds__(SG_FFT_WAVES * 64) __attribute__((amdgpu
     }
   m = sgd::wave_max(m);
   if (lane == 0) slotmax[S.slot] = m;
+}
+
+extern "C" __global__ __launch_bounds__(SG_FFT_WAVES * 64) __attribute__((amdgpu_waves_per_eu(SG_FFT_WPE))) void sg_stft_ola(
+    const SgSegment* __restrict__ segs, const SgOla* __restrict__ olas, const SgFrame* __restrict__ frames,
+    const SgFftGeom* __restrict__ geoms, const float* __restrict__ fl, float* __restrict__ fs,
+    float* __restrict__ slotmax) {
+  constexpr int W = SG_FFT_WAVES, NT = W * 64;
+  extern __shared__ float4 lds4[];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // w wave-uniform
+  const SgFftGeom& g = geoms[segs[blockIdx.x * W].geom];  // the planner groups segments by geometry
+  const int M = g.M, N = g.wl;
+  float2* twS = reinterpret_cast<float2*>(lds4);
+  float2* twN = twS + M;
+  float* ham = reinterpret_cast<float*>(twN + M);
+  float* han = ham + N;
+  {
+    const float2* tsg = reinterpret_cast<const float2*>(fl + g.tws);
+    const float2* tng = reinterpret_cast<const float2*>(fl + g.tw) + M;
+    const float* wg = fl + g.win;
+    for (int t = threadIdx.x; t < M; t += NT) {
+      if (t < M - 1) twS[t] = tsg[t];
+      twN[t] = tng[t];
+    }
+    for (int t = threadIdx.x; t < 2 * N; t += NT) ham[t] = wg[t];  // hamming then hanning
+  }
+  __syncthreads();
+  const SgSegment S = segs[blockIdx.x * W + w];
+  if (S.nf <= 0) return;  // padding segment
+#if SG_STFT_SPEC
+  if (M == 1102 && g.nstages == 3 && g.radix[0] == 2 && g.radix[1] == 19 && g.radix[2] == 29)
+    stft_segment<1102, 2, 19, 29>(S, olas, frames, g, fl, fs, slotmax, twS, twN, ham, han, w, lane);
+  else
+#endif
+    stft_segment<0, 0, 0, 0>(S, olas, frames, g, fl, fs, slotmax, twS, twN, ham, han, w, lane);
 }
 
 // Test probe: wavefront w transforms frame w (M complex points, in place) with

@@ -306,8 +306,150 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank(
   }
 }
 
-// The tasks with more than SG_ROWS_F32 rows (listed in idx): fp64 sincospi of the
-// reduced phase and fp64 Clenshaw chains, one task per wave.
+// ---------------------------------------------- tall tasks, fp32 Reinsch
+// Plain Clenshaw in fp32 loses ~R^2 eps when cos(theta) is near +-1 (a sideband
+// grid's angle is small: theta = 2 pi subFreq / fs): 2 cos(theta) is then known
+// only to eps absolutely, which misplaces the angle by eps / theta. Reinsch's
+// modification carries d_k = b_k - sg b_{k+1} (sg = sign cos theta) and enters the
+// angle through u = 2 cos(theta) - 2 sg = -4 sin^2(theta/2) (sg = 1) or
+// 4 cos^2(theta/2) (sg = -1), both known to a few eps RELATIVE:
+//   d_k = a_k + u b_{k+1} + sg d_{k+1},   b_k = d_k + sg b_{k+1},   S = b_1 sin(theta)
+// (3 FMAs per row and chain; samples in packed pairs). sin/cos of the half angle
+// come from fp32 Taylor polynomials on [-pi/2, pi/2] (relative error < 1e-9 before
+// rounding), not from v_sin / v_cos, whose error is absolute.
+#ifndef SG_TALL_F32
+#define SG_TALL_F32 0  // build knob: 1 = fp32 Reinsch chains (measured equal time on C5: the tall kernel is latency-bound)
+#endif
+
+__device__ __forceinline__ void rs_setup(const SgWTask& T, int l, bool two, float& t, float& u, float& sg, float& sn) {
+  t = two ? fmaf((float)l, T.xby, T.tc0) * T.rdx : 0.f;
+  const double m = (double)(T.mbase + l);
+  const double P = fma(m, fma(m, fma(m, fma(m, T.c4, T.c3), T.c2), T.c1), T.c0);
+  const float x = (float)(P - rint(P));  // revolutions, |x| <= 1/2
+  const float h = 3.14159265358979f * x;  // theta / 2
+  const float h2 = h * h;
+  float s = fmaf(h2, 1.6059043836821614e-10f, -2.5052108385441720e-08f);
+  s = fmaf(h2, s, 2.7557319223985893e-06f);
+  s = fmaf(h2, s, -1.9841269841269841e-04f);
+  s = fmaf(h2, s, 8.3333333333333333e-03f);
+  s = fmaf(h2, s, -1.6666666666666667e-01f);
+  s = fmaf(h2 * s, h, h);  // sin(theta / 2)
+  float c = fmaf(h2, -1.1470745597729725e-11f, 2.0876756987868099e-09f);
+  c = fmaf(h2, c, -2.7557319223985891e-07f);
+  c = fmaf(h2, c, 2.4801587301587302e-05f);
+  c = fmaf(h2, c, -1.3888888888888889e-03f);
+  c = fmaf(h2, c, 4.1666666666666667e-02f);
+  c = fmaf(h2, c, -0.5f);
+  c = fmaf(h2, c, 1.f);  // cos(theta / 2)
+  sn = 2.f * s * c;
+  const bool pos = fabsf(x) <= 0.25f;  // cos(theta) >= 0
+  sg = pos ? 1.f : -1.f;
+  u = pos ? -4.f * s * s : 4.f * c * c;
+}
+
+#define SG_RROW(a, dd)                                   \
+  {                                                      \
+    _Pragma("unroll") for (int p = 0; p < NP; ++p) {     \
+      f2 q = vfma(sg[p], d[p], f2{(a), (a)});            \
+      q = vfma(u[p], b[p], q);                           \
+      b[p] = vfma(sg[p], b[p], q);                       \
+      d[p] = q;                                          \
+      if (TWO) {                                         \
+        f2 r = vfma(sg[p], g[p], f2{(dd), (dd)});        \
+        r = vfma(u[p], e[p], r);                         \
+        e[p] = vfma(sg[p], e[p], r);                     \
+        g[p] = r;                                        \
+      }                                                  \
+    }                                                    \
+  }
+// rows n-1 .. 0 (n a multiple of 4) of the staged chunk, continuing (b, d) and (e, g)
+template <int NP, bool TWO>
+__device__ __forceinline__ void reinsch_lds(const float* __restrict__ la, const float* __restrict__ ld, int n,
+                                            const f2 (&u)[NP], const f2 (&sg)[NP], f2 (&b)[NP], f2 (&d)[NP],
+                                            f2 (&e)[NP], f2 (&g)[NP]) {
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 1
+  for (int r = n - 4; r >= 0; r -= 4) {
+    const float4 A4 = *reinterpret_cast<const float4*>(la + r);
+    const float4 D4 = TWO ? *reinterpret_cast<const float4*>(ld + r) : z4;
+    SG_RROW(A4.w, D4.w)
+    SG_RROW(A4.z, D4.z)
+    SG_RROW(A4.y, D4.y)
+    SG_RROW(A4.x, D4.x)
+  }
+}
+#undef SG_RROW
+
+// NP packed pairs per lane: pair p holds samples l0 + 128 p + lane and l0 + 128 p + 64 + lane
+template <int NP, bool TWO, bool ENV>
+__device__ __forceinline__ void run_pairs_rs(const SgWTask& T, bool staged, float* __restrict__ la,
+                                             float* __restrict__ ld, const float* __restrict__ amps,
+                                             const SgSyllable* __restrict__ syls, const double* __restrict__ cknots,
+                                             float* __restrict__ W, int l0, int lane, float& tmax) {
+  constexpr int NS = 2 * NP;
+  float t[NS], uu[NS], ss[NS], sn[NS];
+  int l[NS];
+  bool valid[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    l[s] = l0 + 64 * s + lane;
+    valid[s] = l[s] < T.len;
+    rs_setup(T, valid[s] ? l[s] : 0, TWO, t[s], uu[s], ss[s], sn[s]);
+  }
+  f2 u[NP], sg[NP], b[NP], d[NP], e[NP], g[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    u[p] = f2{uu[2 * p], uu[2 * p + 1]};
+    sg[p] = f2{ss[2 * p], ss[2 * p + 1]};
+    b[p] = d[p] = e[p] = g[p] = f2{0.f, 0.f};
+  }
+  if (staged) {
+    reinsch_lds<NP, TWO>(la, ld, T.R, u, sg, b, d, e, g);
+  } else {  // more than SG_LDS_ROWS rows: 256-row chunks, top first
+    for (int r0 = (T.R - 1) / SG_LDS_ROWS * SG_LDS_ROWS; r0 >= 0; r0 -= SG_LDS_ROWS) {
+      const int n = T.R - r0 < SG_LDS_ROWS ? T.R - r0 : SG_LDS_ROWS;
+      stage_rows<TWO>(la, ld, amps + T.a_off, amps + T.d_off, r0, n, lane);
+      reinsch_lds<NP, TWO>(la, ld, n, u, sg, b, d, e, g);
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const float bs = (s & 1) ? b[s >> 1].y : b[s >> 1].x;
+    const float es = (s & 1) ? e[s >> 1].y : e[s >> 1].x;
+    const float y = (TWO ? fmaf(t[s], es, bs) : bs) * sn[s];
+    const int j = T.j0 + l[s];
+    if (valid[s]) W[T.w_off + j] = y;
+    const bool in = valid[s] && j >= T.dj0 && j < T.dj1;
+    if (!ENV) {
+      tmax = in ? fmaxf(tmax, y) : tmax;
+    } else if (in) {
+      const SgSyllable& sy = syls[T.syl];
+      tmax = fmaxf(tmax, (float)((double)y * contour_at(sy.env, cknots, sy.L, T.dk0 + j)));
+    }
+  }
+}
+
+template <bool TWO, bool ENV>
+__device__ __forceinline__ float run_task_rs(const SgWTask& T, float* __restrict__ la, float* __restrict__ ld,
+                                             const float* __restrict__ amps, const SgSyllable* __restrict__ syls,
+                                             const double* __restrict__ cknots, float* __restrict__ W, int lane) {
+  const bool staged = T.R <= SG_LDS_ROWS;
+  if (staged) stage_rows<TWO>(la, ld, amps + T.a_off, amps + T.d_off, 0, T.R, lane);
+  float tmax = 0.f;
+  int l0 = 0;
+#pragma unroll 1
+  for (; T.len - l0 > 256; l0 += 512)
+    run_pairs_rs<4, TWO, ENV>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax);
+  if (T.len - l0 > 128) {
+    run_pairs_rs<2, TWO, ENV>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax);
+    l0 += 256;
+  }
+  if (l0 < T.len) run_pairs_rs<1, TWO, ENV>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax);
+  return tmax;
+}
+
+// The tasks with more than SG_ROWS_F32 rows (listed in idx), one task per wave:
+// fp32 Reinsch chains (SG_TALL_F32), else fp64 sincospi and fp64 Clenshaw chains.
 extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_tall(
     const int32_t* __restrict__ idx, int64_t n, const SgWTask* __restrict__ tasks, const float* __restrict__ amps,
     const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, float* __restrict__ W,
@@ -322,12 +464,21 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_tall(
   float* la = rows[wave][0];
   float* ld = rows[wave][1];
   float tmax;
+#if SG_TALL_F32
+  if (T.flags & SG_TASK_ENV)
+    tmax = (T.flags & SG_TASK_CONST) ? run_task_rs<false, true>(T, la, ld, amps, syls, cknots, W, lane)
+                                     : run_task_rs<true, true>(T, la, ld, amps, syls, cknots, W, lane);
+  else
+    tmax = (T.flags & SG_TASK_CONST) ? run_task_rs<false, false>(T, la, ld, amps, syls, cknots, W, lane)
+                                     : run_task_rs<true, false>(T, la, ld, amps, syls, cknots, W, lane);
+#else
   if (T.flags & SG_TASK_ENV)
     tmax = (T.flags & SG_TASK_CONST) ? run_task<false, true, false, double>(T, la, ld, amps, syls, cknots, W, lane)
                                      : run_task<true, true, false, double>(T, la, ld, amps, syls, cknots, W, lane);
   else
     tmax = (T.flags & SG_TASK_CONST) ? run_task<false, false, false, double>(T, la, ld, amps, syls, cknots, W, lane)
                                      : run_task<true, false, false, double>(T, la, ld, amps, syls, cknots, W, lane);
+#endif
   const float wm = wave_max(tmax);
   if (lane == 0) taskmax[ti] = wm;
 }

@@ -6,6 +6,7 @@
 // R's operation order; per-sample work runs in sg_fft.hip.
 #include <algorithm>
 #include <cmath>
+#include <complex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -47,31 +48,93 @@ static int64_t push_windows(Batch& B, int wl) {
   return fl_push(B, win.data(), (int64_t)win.size());
 }
 
+// ---- complex DFTs of any length for sg_fft_frames (SgCdft, sg_dev.h)
+static bool smooth31(int n) {
+  for (int r : kRadices)
+    while (n % r == 0) n /= r;
+  return n == 1;
+}
+// n-point DFT in fp64 (n 5-smooth), recursive decimation in time; exponents reduced mod n exactly
+static void dft_smooth(const std::vector<std::complex<double>>& x, std::vector<std::complex<double>>& y) {
+  const int n = (int)x.size();
+  y.assign((size_t)n, 0.0);
+  if (n == 1) {
+    y[0] = x[0];
+    return;
+  }
+  int p = 2;
+  while (n % p) ++p;
+  const int m = n / p;
+  std::vector<std::vector<std::complex<double>>> sub((size_t)p);
+  for (int r = 0; r < p; ++r) {
+    std::vector<std::complex<double>> xs((size_t)m);
+    for (int j = 0; j < m; ++j) xs[j] = x[(size_t)j * p + r];
+    dft_smooth(xs, sub[r]);
+  }
+  for (int k = 0; k < n; ++k) {
+    std::complex<double> acc = 0.0;
+    for (int r = 0; r < p; ++r) {
+      const double a = -2.0 * M_PI * (double)(((int64_t)r * k) % n) / (double)n;
+      acc += std::complex<double>(std::cos(a), std::sin(a)) * sub[r][k % m];
+    }
+    y[k] = acc;
+  }
+}
+static SgCdft make_cdft(Batch& B, int n) {
+  SgCdft c{};
+  c.n = n;
+  if (smooth31(n)) {
+    c.geom = geometry(B, 2 * n);  // its M = n: radices, magic numbers, W_n table
+    return c;
+  }
+  int L = 2 * n - 1;
+  for (;; ++L) {
+    int m = L;
+    for (int r : {2, 3, 5})
+      while (m % r == 0) m /= r;
+    if (m == 1) break;
+  }
+  if (L > kFftSlots) throw SgError(SG_E_UNSUPPORTED, "FFT: Bluestein length " + std::to_string(L) + " exceeds LDS");
+  c.L = L;
+  c.geom = geometry(B, 2 * L);
+  vec ch(2 * (size_t)n);
+  std::vector<std::complex<double>> b((size_t)L, 0.0), bf;
+  for (int m = 0; m < n; ++m) {
+    const double a = -M_PI * (double)(((int64_t)m * m) % (2 * (int64_t)n)) / (double)n;
+    ch[2 * m] = std::cos(a);
+    ch[2 * m + 1] = std::sin(a);
+    b[m] = std::complex<double>(ch[2 * m], -ch[2 * m + 1]);
+    if (m > 0) b[L - m] = b[m];
+  }
+  dft_smooth(b, bf);
+  vec bv(2 * (size_t)L);
+  for (int k = 0; k < L; ++k) {
+    bv[2 * k] = bf[k].real() / L;
+    bv[2 * k + 1] = bf[k].imag() / L;
+  }
+  c.chirp = fl_push(B, ch.data(), (int64_t)ch.size());
+  c.bf = fl_push(B, bv.data(), (int64_t)bv.size());
+  return c;
+}
+static int cdft_size(const SgCdft& c) { return c.L ? c.L : c.n; }
+
 // odd window length (SG_FFT_ODD, sg_dev.h): forward wl-point and inverse
-// (wl - 1)-point direct DFT tables
+// (wl - 1)-point complex DFTs
 static int geometry_odd(Batch& B, int wl) {
   SgFftGeom g{};
   g.wl = wl;
   g.M = wl / 2;
   g.kind = SG_FFT_ODD;
   g.fb = 1;
-  // tables W_wl (wl pairs) and the inverse (2M pairs), M bins, the wl-point frame
-  g.lds_bytes = (int32_t)(((int64_t)wl * 8 + (int64_t)2 * g.M * 8 + (int64_t)g.M * 8 + (int64_t)wl * 4 + 15) / 16 * 16);
+  g.cd[0] = make_cdft(B, wl);
+  g.cd[1] = make_cdft(B, 2 * g.M);
+  // the wl-point frame buffer, the Bluestein work buffer and the FFT twiddle table
+  const int T = std::max(cdft_size(g.cd[0]), cdft_size(g.cd[1]));
+  g.lds_bytes = (int32_t)(((int64_t)wl + 2 * (int64_t)T) * 8);
   if (g.lds_bytes > 160 * 1024) throw SgError(SG_E_UNSUPPORTED, "FFT: odd window length exceeds the LDS budget");
-  vec tw(2 * (size_t)wl), ti(2 * (size_t)(2 * g.M));
-  for (int t = 0; t < wl; ++t) {
-    const double a = -2.0 * M_PI * (double)t / (double)wl;
-    tw[2 * t] = std::cos(a);
-    tw[2 * t + 1] = std::sin(a);
-  }
-  for (int t = 0; t < 2 * g.M; ++t) {
-    const double a = 2.0 * M_PI * (double)t / (double)(2 * g.M);
-    ti[2 * t] = std::cos(a);
-    ti[2 * t + 1] = std::sin(a);
-  }
-  g.tw = fl_push(B, tw.data(), (int64_t)tw.size());
-  g.tws = fl_push(B, ti.data(), (int64_t)ti.size());
   g.win = push_windows(B, wl);
+  for (size_t i = 0; i < B.geoms.size(); ++i)  // the sub-geometries were pushed first
+    if (B.geoms[i].wl == wl) return (int)i;
   B.geoms.push_back(g);
   return (int)B.geoms.size() - 1;
 }
@@ -97,9 +160,9 @@ int geometry(Batch& B, int wl) {
   const bool dft = m != 1;
   if (dft) {
     g.nstages = 0;
-    if ((int64_t)3 * g.M * 8 > 160 * 1024)
-      throw SgError(SG_E_UNSUPPORTED, "FFT: window length " + std::to_string(wl) + " has a prime factor > 31 and "
-                    "exceeds the direct-DFT LDS budget");
+    g.cd[0] = make_cdft(B, g.M);  // Bluestein (pushes its L-point sub-geometry first)
+    for (size_t i = 0; i < B.geoms.size(); ++i)
+      if (B.geoms[i].wl == wl) return (int)i;
   }
   // twiddles W_M^t (t < M), W_N^k (k < M), fp64 -> fp32
   vec tw(4 * (size_t)g.M);
@@ -148,7 +211,8 @@ int geometry(Batch& B, int wl) {
     g.lds_bytes = (SG_FFT_WAVES + 4) * g.M * 8;
   } else if (g.kind == SG_FFT_DFT) {
     g.fb = 1;
-    g.lds_bytes = 3 * g.M * 8;  // frame, W_M table, DFT output
+    g.lds_bytes = (g.M + 2 * g.cd[0].L) * 8;  // frame, Bluestein work buffer, W_L table
+    if (g.lds_bytes > 160 * 1024) throw SgError(SG_E_UNSUPPORTED, "FFT: Bluestein frame exceeds the LDS budget");
   } else {
     g.fb = std::max(1, std::min(16, kFftSlots / g.M));
     if (g.fb * g.M > kFftSlots) throw SgError(SG_E_UNSUPPORTED, "FFT: window too long for LDS (wl > 16384)");
@@ -777,6 +841,15 @@ void finalize_spec(Batch& B) {
       for (int s = 0; s < g.nstages; ++s) rs += (s ? "x" : "") + std::to_string(g.radix[s]);
       std::fprintf(stderr, "sg plan: geom wl=%d M=%d radices %s: %lld frames\n", g.wl, g.M, rs.c_str(),
                    (long long)gs[i].first);
+    }
+    std::map<int32_t, int64_t> gun;  // unfused (sg_fft_frames) frames per geometry
+    for (const SgFrameGroup& fg : B.fgroups) gun[fg.geom] += fg.nf;
+    for (const auto& kv : gun) {
+      const SgFftGeom& g = B.geoms[kv.first];
+      std::string rs;
+      for (int s = 0; s < g.nstages; ++s) rs += (s ? "x" : "") + std::to_string(g.radix[s]);
+      std::fprintf(stderr, "sg plan: unfused geom wl=%d M=%d kind %d radices %s: %lld frames\n", g.wl, g.M, g.kind,
+                   rs.c_str(), (long long)kv.second);
     }
     std::fprintf(stderr, "sg plan: %lld fused segments (%lld slots incl. padding), %lld frames owned, %lld computed (%.1f%% recomputed)\n",
                  (long long)real, (long long)B.olasegs.size(), (long long)owned, (long long)run,
