@@ -15,11 +15,16 @@
 // Each chunk ends with 64 consecutive fp32 stores (coalesced).
 //
 // Work per active (chunk, track): 2 fp64 FMA + cvt + v_exp_f32 + FMA + select,
-// plus 7 lane broadcasts. Output 4 B per bin and column, ~48 B per track and
+// the track's parameters from scalar loads (v_readlane broadcasts were 7 more VALU
+// instructions per pair, and the kernel is VALU-bound: PMC ~94 % VALU-busy SIMDs). Output 4 B per bin and column, ~48 B per track and
 // column read once: VALU/issue-bound, not HBM-bound.
 #include <hip/hip_runtime.h>
 
 #include "sg_dev.h"
+
+#ifndef SG_ENV_SMEM
+#define SG_ENV_SMEM 1  // build knob: a selected track's parameters by scalar loads (0: v_readlane broadcasts)
+#endif
 
 __device__ __forceinline__ double bcast(double v, int lane) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
@@ -39,7 +44,7 @@ extern "C" __global__ __launch_bounds__(256) void sg_spec_env(const SgEnvTask* _
   const SgEnvTask T = tasks[w];
   const SgEnvJob J = jobs[T.job];
   const int c1 = T.c0 + SG_ENV_COLS < J.nc ? T.c0 + SG_ENV_COLS : J.nc;
-  const double thr = -SG_ENV_CUT;  // log2 units
+  const float thrf = -SG_ENV_CUT;  // log2 units
 #pragma unroll 1
   for (int c = T.c0; c < c1; ++c) {
     const SgEnvTerm* __restrict__ tm = terms + J.term0 + (int64_t)c * J.ntr;
@@ -52,7 +57,10 @@ extern "C" __global__ __launch_bounds__(256) void sg_spec_env(const SgEnvTask* _
       const int t = g * 64 + lane;
       const bool in = t < J.ntr;
       const SgEnvTerm& e = tm[in ? t : 0];
-      A[g] = e.A; Rr[g] = e.Rr; Lm[g] = e.Lm; amp[g] = (float)e.amp;
+      if (!SG_ENV_SMEM) {
+        A[g] = e.A; Rr[g] = e.Rr; Lm[g] = e.Lm;
+      }
+      amp[g] = (float)e.amp;
       klo[g] = in ? e.klo : 1 << 30;
       khi[g] = in ? e.khi : -1;
     }
@@ -70,10 +78,17 @@ extern "C" __global__ __launch_bounds__(256) void sg_spec_env(const SgEnvTask* _
         while (m) {
           const int t = __builtin_ctzll(m);
           m &= m - 1;
+#if SG_ENV_SMEM
+          const SgEnvTerm* __restrict__ e = tm + g * 64 + t;  // wave-uniform: scalar loads into SGPRs
+          const double a = e->A, r = e->Rr, l = e->Lm;
+#else
           const double a = bcast(A[g], t), r = bcast(Rr[g], t), l = bcast(Lm[g], t);
+#endif
           const float am = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amp[g]), t));
           const double d = fma(a, lx, fma(-r, x, -l));
-          if (d > thr) acc = fmaf(am, exp2f((float)d), acc);
+          // d > thr >= -126: the raw v_exp_f32 is exact enough and never denormal
+          const float df = (float)d;
+          if (df > thrf) acc = fmaf(am, __builtin_amdgcn_exp2f(df), acc);
         }
       }
       const float lxf = (float)lx;

@@ -127,11 +127,15 @@ void finalize_plan(Batch& B) {
     double terms[2] = {0, 0};
     int64_t ntask[2] = {0, 0}, rmax = 0, samples[2] = {0, 0};
     std::map<int, int64_t> rh;
+    int64_t nshort[2] = {0, 0}, lh[2][5] = {{0}};
+    double sterms[2] = {0, 0};
     for (const SgWTask& t : B.tasks) {
       const int k = t.R > SG_ROWS_F32 ? 1 : 0;
       terms[k] += (double)t.R * t.len * ((t.flags & SG_TASK_CONST) ? 1 : 2);
       ++ntask[k];
       samples[k] += t.len;
+      if (t.len <= 64) { ++nshort[k]; sterms[k] += (double)t.R * t.len * ((t.flags & SG_TASK_CONST) ? 1 : 2); }
+      lh[k][t.len <= 64 ? 0 : t.len <= 128 ? 1 : t.len <= 256 ? 2 : t.len <= 512 ? 3 : 4]++;
       if (k) {
         rmax = std::max<int64_t>(rmax, t.R);
         rh[t.R < 256 ? 0 : t.R < 512 ? 1 : t.R < 1024 ? 2 : t.R < 2048 ? 3 : 4]++;
@@ -140,6 +144,10 @@ void finalize_plan(Batch& B) {
     std::fprintf(stderr, "sg plan: sine tasks fp32 %lld (%lld samples, %.3g chain terms), tall %lld (%lld samples, %.3g chain terms, max R %lld; R<256 %lld, <512 %lld, <1024 %lld, <2048 %lld, more %lld)\n",
                  (long long)ntask[0], (long long)samples[0], terms[0], (long long)ntask[1], (long long)samples[1], terms[1],
                  (long long)rmax, (long long)rh[0], (long long)rh[1], (long long)rh[2], (long long)rh[3], (long long)rh[4]);
+    for (int k = 0; k < 2; ++k)
+      std::fprintf(stderr, "sg plan: %s tasks <= 64 samples: %lld (%.3g chain terms); len <=64/128/256/512/more: %lld %lld %lld %lld %lld\n",
+                   k ? "tall" : "fp32", (long long)nshort[k], sterms[k], (long long)lh[k][0], (long long)lh[k][1],
+                   (long long)lh[k][2], (long long)lh[k][3], (long long)lh[k][4]);
   }
   B.ptiles.clear();
   for (size_t s = 0; s < B.syls.size(); ++s) {

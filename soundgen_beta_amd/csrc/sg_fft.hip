@@ -942,7 +942,11 @@ extern "C" __global__ __launch_bounds__(SG_FFT_WAVES * 64) __attribute__((amdgpu
     stft_segment<1102, 2, 19, 29>(S, olas, frames, g, fl, fs, slotmax, twS, twN, ham, han, w, lane);
   else
 #endif
+#ifndef SG_STFT_ONLY_SPEC  // diagnostic: the specialised path alone (register budget)
     stft_segment<0, 0, 0, 0>(S, olas, frames, g, fl, fs, slotmax, twS, twN, ham, han, w, lane);
+#else
+    ;
+#endif
 }
 
 // Test probe: wavefront w transforms frame w (M complex points, in place) with

@@ -268,6 +268,80 @@ __device__ __forceinline__ float run_task(const SgWTask& T, float* __restrict__ 
   return tmax;
 }
 
+// One task on its own wave pass (any length, envelope, linear or general phase)
+__device__ __forceinline__ float run_one(const SgWTask& T, float* __restrict__ la, float* __restrict__ ld,
+                                         const float* __restrict__ amps, const SgSyllable* __restrict__ syls,
+                                         const double* __restrict__ cknots, float* __restrict__ W, int lane) {
+  if (T.flags & SG_TASK_ENV)  // amplAnchors envelope: rare, kept out of the hot variants
+    return (T.flags & SG_TASK_CONST) ? run_task<false, true, false>(T, la, ld, amps, syls, cknots, W, lane)
+                                     : run_task<true, true, false>(T, la, ld, amps, syls, cknots, W, lane);
+  if (T.flags & SG_TASK_LIN)  // constant pitch over the phase segment
+    return (T.flags & SG_TASK_CONST) ? run_task<false, false, true>(T, la, ld, amps, syls, cknots, W, lane)
+                                     : run_task<true, false, true>(T, la, ld, amps, syls, cknots, W, lane);
+  return (T.flags & SG_TASK_CONST) ? run_task<false, false, false>(T, la, ld, amps, syls, cknots, W, lane)
+                                   : run_task<true, false, false>(T, la, ld, amps, syls, cknots, W, lane);
+}
+
+#ifndef SG_PAIR
+#define SG_PAIR 1  // build knob: two short tasks per wave in the halves of packed pairs
+#endif
+// Two tasks of <= 64 samples (most of C5's: one glottal cycle each) in one
+// wave: lane l runs sample l of task P in the low and of task Q in the high half
+// of packed fp32 pairs, so each row costs the 2 packed ops per chain of ONE
+// task. Their rows interleave in LDS (la[2r] = A_P[r], la[2r + 1] = A_Q[r],
+// zero above a task's R; the dA rows likewise, zero for a CONST task), and one
+// broadcast ds_read_b128 yields rows r, r + 1 of both.
+template <bool TWO>
+__device__ __forceinline__ void run_pair(const SgWTask& P, const SgWTask& Q, float* __restrict__ la,
+                                         float* __restrict__ ld, const float* __restrict__ amps,
+                                         float* __restrict__ W, int lane, float& mp, float& mq) {
+  const int R = P.R > Q.R ? P.R : Q.R;  // multiples of 16
+  for (int r = lane; r < R; r += 64) {
+    *reinterpret_cast<float2*>(la + 2 * r) = make_float2(r < P.R ? amps[P.a_off + r] : 0.f, r < Q.R ? amps[Q.a_off + r] : 0.f);
+    if (TWO)
+      *reinterpret_cast<float2*>(ld + 2 * r) =
+          make_float2(r < P.R && !(P.flags & SG_TASK_CONST) ? amps[P.d_off + r] : 0.f,
+                      r < Q.R && !(Q.flags & SG_TASK_CONST) ? amps[Q.d_off + r] : 0.f);
+  }
+  const bool vp = lane < P.len, vq = lane < Q.len;
+  float tp, alp, snp, tq, alq, snq;
+  sample_setup<TWO, false>(P, vp ? lane : 0, tp, alp, snp);
+  sample_setup<TWO, false>(Q, vq ? lane : 0, tq, alq, snq);
+  const f2 al{alp, alq};
+  f2 b1{0.f, 0.f}, b2{0.f, 0.f}, e1{0.f, 0.f}, e2{0.f, 0.f};
+#define SG_PROW(a, d)                      \
+  {                                        \
+    const f2 b = vfma(al, b1, (a) - b2);   \
+    b2 = b1;                               \
+    b1 = b;                                \
+    if (TWO) {                             \
+      const f2 e = vfma(al, e1, (d) - e2); \
+      e2 = e1;                             \
+      e1 = e;                              \
+    }                                      \
+  }
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 1
+  for (int r = R - 4; r >= 0; r -= 4) {  // rows r + 3 .. r
+    const float4 A1 = *reinterpret_cast<const float4*>(la + 2 * r + 4);
+    const float4 A0 = *reinterpret_cast<const float4*>(la + 2 * r);
+    const float4 D1 = TWO ? *reinterpret_cast<const float4*>(ld + 2 * r + 4) : z4;
+    const float4 D0 = TWO ? *reinterpret_cast<const float4*>(ld + 2 * r) : z4;
+    SG_PROW((f2{A1.z, A1.w}), (f2{D1.z, D1.w}))
+    SG_PROW((f2{A1.x, A1.y}), (f2{D1.x, D1.y}))
+    SG_PROW((f2{A0.z, A0.w}), (f2{D0.z, D0.w}))
+    SG_PROW((f2{A0.x, A0.y}), (f2{D0.x, D0.y}))
+  }
+#undef SG_PROW
+  const float yp = (TWO ? fmaf(tp, e1.x, b1.x) : b1.x) * snp;
+  const float yq = (TWO ? fmaf(tq, e1.y, b1.y) : b1.y) * snq;
+  const int jp = P.j0 + lane, jq = Q.j0 + lane;
+  if (vp) W[P.w_off + jp] = yp;
+  if (vq) W[Q.w_off + jq] = yq;
+  mp = vp && jp >= P.dj0 && jp < P.dj1 ? yp : 0.f;
+  mq = vq && jq >= Q.dj0 && jq < Q.dj1 ? yq : 0.f;
+}
+
 extern "C" __global__ __launch_bounds__(256) void sg_sine_bank(
     const SgWTask* __restrict__ tasks, int64_t ntasks, const float* __restrict__ amps,
     const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, float* __restrict__ W,
@@ -277,6 +351,40 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank(
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float* la = rows[wave][0];
   float* ld = rows[wave][1];
+#if SG_PAIR
+  // wave w takes tasks 2w and 2w + 1 (consecutive cycles of one epoch, as a rule)
+  const int64_t t0 = ((int64_t)blockIdx.x * 4 + wave) * 2;
+  if (t0 >= ntasks) return;
+  const SgWTask P = tasks[t0];
+  const bool has_q = t0 + 1 < ntasks;
+  const SgWTask Q = tasks[has_q ? t0 + 1 : t0];
+  const bool okp = P.R <= SG_ROWS_F32, okq = has_q && Q.R <= SG_ROWS_F32;  // others: sg_sine_bank_tall
+  // a short task ALWAYS runs the pair arithmetic (with itself as the partner when
+  // its neighbour is not short), so its bytes never depend on the batch around it
+  const bool ep = okp && P.len <= 64 && !(P.flags & SG_TASK_ENV);
+  const bool eq = okq && Q.len <= 64 && !(Q.flags & SG_TASK_ENV);
+  if (ep || eq) {
+    const SgWTask& X = ep ? P : Q;
+    const SgWTask& Y = eq ? Q : X;
+    float mx, my;
+    if ((X.flags & Y.flags) & SG_TASK_CONST) run_pair<false>(X, Y, la, ld, amps, W, lane, mx, my);
+    else run_pair<true>(X, Y, la, ld, amps, W, lane, mx, my);
+    mx = wave_max(mx);
+    my = wave_max(my);
+    if (lane == 0) {
+      if (ep) taskmax[t0] = mx;
+      if (eq) taskmax[t0 + 1] = my;
+    }
+  }
+  if (okp && !ep) {
+    const float wm = wave_max(run_one(P, la, ld, amps, syls, cknots, W, lane));
+    if (lane == 0) taskmax[t0] = wm;
+  }
+  if (okq && !eq) {
+    const float wm = wave_max(run_one(Q, la, ld, amps, syls, cknots, W, lane));
+    if (lane == 0) taskmax[t0 + 1] = wm;
+  }
+#else
 #if SG_SINE_PERSIST
   // persistent waves: wave w of the grid takes tasks w, w + 4 gridDim.x, ...
   const int64_t stride = (int64_t)gridDim.x * 4;
@@ -291,19 +399,10 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank(
 #endif
     const SgWTask T = tasks[ti];
     if (T.R > SG_ROWS_F32) continue;  // sg_sine_bank_tall
-    float tmax;
-    if (T.flags & SG_TASK_ENV)  // amplAnchors envelope: rare, kept out of the hot variants
-      tmax = (T.flags & SG_TASK_CONST) ? run_task<false, true, false>(T, la, ld, amps, syls, cknots, W, lane)
-                                       : run_task<true, true, false>(T, la, ld, amps, syls, cknots, W, lane);
-    else if (T.flags & SG_TASK_LIN)  // constant pitch over the phase segment
-      tmax = (T.flags & SG_TASK_CONST) ? run_task<false, false, true>(T, la, ld, amps, syls, cknots, W, lane)
-                                       : run_task<true, false, true>(T, la, ld, amps, syls, cknots, W, lane);
-    else
-      tmax = (T.flags & SG_TASK_CONST) ? run_task<false, false, false>(T, la, ld, amps, syls, cknots, W, lane)
-                                       : run_task<true, false, false>(T, la, ld, amps, syls, cknots, W, lane);
-    const float wm = wave_max(tmax);
+    const float wm = wave_max(run_one(T, la, ld, amps, syls, cknots, W, lane));
     if (lane == 0) taskmax[ti] = wm;
   }
+#endif
 }
 
 // ---------------------------------------------- tall tasks, fp32 Reinsch
@@ -448,6 +547,90 @@ __device__ __forceinline__ float run_task_rs(const SgWTask& T, float* __restrict
   return tmax;
 }
 
+#ifndef SG_TALL_PAIR
+#define SG_TALL_PAIR 1  // build knob: two short tall tasks per wave, fp32 Reinsch in packed halves
+#endif
+// Two tall tasks of <= 64 samples in one wave (as run_pair: task P in the low,
+// Q in the high half of packed pairs), Reinsch chains, rows staged interleaved
+// in 128-row chunks from the top.
+template <bool TWO>
+__device__ __forceinline__ void run_pair_rs(const SgWTask& P, const SgWTask& Q, float* __restrict__ la,
+                                            float* __restrict__ ld, const float* __restrict__ amps,
+                                            float* __restrict__ W, int lane, float& mp, float& mq) {
+  const int R = P.R > Q.R ? P.R : Q.R;
+  const bool vp = lane < P.len, vq = lane < Q.len;
+  float tp, up, sgp, snp, tq, uq, sgq, snq;
+  rs_setup(P, vp ? lane : 0, TWO, tp, up, sgp, snp);
+  rs_setup(Q, vq ? lane : 0, TWO, tq, uq, sgq, snq);
+  const f2 u{up, uq}, sg{sgp, sgq};
+  f2 b{0.f, 0.f}, d{0.f, 0.f}, e{0.f, 0.f}, g{0.f, 0.f};
+#define SG_RPROW(a, dd)                  \
+  {                                      \
+    f2 q = vfma(sg, d, (a));             \
+    q = vfma(u, b, q);                   \
+    b = vfma(sg, b, q);                  \
+    d = q;                               \
+    if (TWO) {                           \
+      f2 w = vfma(sg, g, (dd));          \
+      w = vfma(u, e, w);                 \
+      e = vfma(sg, e, w);                \
+      g = w;                             \
+    }                                    \
+  }
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  constexpr int CH = SG_LDS_ROWS / 2;  // rows per interleaved chunk
+#pragma unroll 1
+  for (int r0 = (R - 1) / CH * CH; r0 >= 0; r0 -= CH) {
+    const int n = R - r0 < CH ? R - r0 : CH;  // multiple of 16
+    for (int r = lane; r < n; r += 64) {
+      const int rr = r0 + r;
+      *reinterpret_cast<float2*>(la + 2 * r) =
+          make_float2(rr < P.R ? amps[P.a_off + rr] : 0.f, rr < Q.R ? amps[Q.a_off + rr] : 0.f);
+      if (TWO)
+        *reinterpret_cast<float2*>(ld + 2 * r) =
+            make_float2(rr < P.R && !(P.flags & SG_TASK_CONST) ? amps[P.d_off + rr] : 0.f,
+                        rr < Q.R && !(Q.flags & SG_TASK_CONST) ? amps[Q.d_off + rr] : 0.f);
+    }
+#pragma unroll 1
+    for (int r = n - 4; r >= 0; r -= 4) {
+      const float4 A1 = *reinterpret_cast<const float4*>(la + 2 * r + 4);
+      const float4 A0 = *reinterpret_cast<const float4*>(la + 2 * r);
+      const float4 D1 = TWO ? *reinterpret_cast<const float4*>(ld + 2 * r + 4) : z4;
+      const float4 D0 = TWO ? *reinterpret_cast<const float4*>(ld + 2 * r) : z4;
+      SG_RPROW((f2{A1.z, A1.w}), (f2{D1.z, D1.w}))
+      SG_RPROW((f2{A1.x, A1.y}), (f2{D1.x, D1.y}))
+      SG_RPROW((f2{A0.z, A0.w}), (f2{D0.z, D0.w}))
+      SG_RPROW((f2{A0.x, A0.y}), (f2{D0.x, D0.y}))
+    }
+  }
+#undef SG_RPROW
+  const float yp = (TWO ? fmaf(tp, e.x, b.x) : b.x) * snp;
+  const float yq = (TWO ? fmaf(tq, e.y, b.y) : b.y) * snq;
+  const int jp = P.j0 + lane, jq = Q.j0 + lane;
+  if (vp) W[P.w_off + jp] = yp;
+  if (vq) W[Q.w_off + jq] = yq;
+  mp = vp && jp >= P.dj0 && jp < P.dj1 ? yp : 0.f;
+  mq = vq && jq >= Q.dj0 && jq < Q.dj1 ? yq : 0.f;
+}
+
+__device__ __forceinline__ float run_one_tall(const SgWTask& T, float* __restrict__ la, float* __restrict__ ld,
+                                              const float* __restrict__ amps, const SgSyllable* __restrict__ syls,
+                                              const double* __restrict__ cknots, float* __restrict__ W, int lane) {
+#if SG_TALL_F32
+  if (T.flags & SG_TASK_ENV)
+    return (T.flags & SG_TASK_CONST) ? run_task_rs<false, true>(T, la, ld, amps, syls, cknots, W, lane)
+                                     : run_task_rs<true, true>(T, la, ld, amps, syls, cknots, W, lane);
+  return (T.flags & SG_TASK_CONST) ? run_task_rs<false, false>(T, la, ld, amps, syls, cknots, W, lane)
+                                   : run_task_rs<true, false>(T, la, ld, amps, syls, cknots, W, lane);
+#else
+  if (T.flags & SG_TASK_ENV)
+    return (T.flags & SG_TASK_CONST) ? run_task<false, true, false, double>(T, la, ld, amps, syls, cknots, W, lane)
+                                     : run_task<true, true, false, double>(T, la, ld, amps, syls, cknots, W, lane);
+  return (T.flags & SG_TASK_CONST) ? run_task<false, false, false, double>(T, la, ld, amps, syls, cknots, W, lane)
+                                   : run_task<true, false, false, double>(T, la, ld, amps, syls, cknots, W, lane);
+#endif
+}
+
 // The tasks with more than SG_ROWS_F32 rows (listed in idx), one task per wave:
 // fp32 Reinsch chains (SG_TALL_F32), else fp64 sincospi and fp64 Clenshaw chains.
 extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_tall(
@@ -457,30 +640,48 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_tall(
   __shared__ __attribute__((aligned(16))) float rows[4][2][SG_LDS_ROWS];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float* la = rows[wave][0];
+  float* ld = rows[wave][1];
+#if SG_TALL_PAIR
+  const int64_t k = ((int64_t)blockIdx.x * 4 + wave) * 2;
+  if (k >= n) return;
+  const int64_t tp = idx[k];
+  const bool has_q = k + 1 < n;
+  const int64_t tq = has_q ? idx[k + 1] : tp;
+  const SgWTask P = tasks[tp];
+  const SgWTask Q = tasks[tq];
+  // short tasks always take the pair arithmetic (see sg_sine_bank)
+  const bool ep = P.len <= 64 && !(P.flags & SG_TASK_ENV);
+  const bool eq = has_q && Q.len <= 64 && !(Q.flags & SG_TASK_ENV);
+  if (ep || eq) {
+    const SgWTask& X = ep ? P : Q;
+    const SgWTask& Y = eq ? Q : X;
+    float mx, my;
+    if ((X.flags & Y.flags) & SG_TASK_CONST) run_pair_rs<false>(X, Y, la, ld, amps, W, lane, mx, my);
+    else run_pair_rs<true>(X, Y, la, ld, amps, W, lane, mx, my);
+    mx = wave_max(mx);
+    my = wave_max(my);
+    if (lane == 0) {
+      if (ep) taskmax[tp] = mx;
+      if (eq) taskmax[tq] = my;
+    }
+  }
+  if (!ep) {
+    const float wm = wave_max(run_one_tall(P, la, ld, amps, syls, cknots, W, lane));
+    if (lane == 0) taskmax[tp] = wm;
+  }
+  if (has_q && !eq) {
+    const float wm = wave_max(run_one_tall(Q, la, ld, amps, syls, cknots, W, lane));
+    if (lane == 0) taskmax[tq] = wm;
+  }
+#else
   const int64_t k = (int64_t)blockIdx.x * 4 + wave;
   if (k >= n) return;
   const int64_t ti = idx[k];
   const SgWTask T = tasks[ti];
-  float* la = rows[wave][0];
-  float* ld = rows[wave][1];
-  float tmax;
-#if SG_TALL_F32
-  if (T.flags & SG_TASK_ENV)
-    tmax = (T.flags & SG_TASK_CONST) ? run_task_rs<false, true>(T, la, ld, amps, syls, cknots, W, lane)
-                                     : run_task_rs<true, true>(T, la, ld, amps, syls, cknots, W, lane);
-  else
-    tmax = (T.flags & SG_TASK_CONST) ? run_task_rs<false, false>(T, la, ld, amps, syls, cknots, W, lane)
-                                     : run_task_rs<true, false>(T, la, ld, amps, syls, cknots, W, lane);
-#else
-  if (T.flags & SG_TASK_ENV)
-    tmax = (T.flags & SG_TASK_CONST) ? run_task<false, true, false, double>(T, la, ld, amps, syls, cknots, W, lane)
-                                     : run_task<true, true, false, double>(T, la, ld, amps, syls, cknots, W, lane);
-  else
-    tmax = (T.flags & SG_TASK_CONST) ? run_task<false, false, false, double>(T, la, ld, amps, syls, cknots, W, lane)
-                                     : run_task<true, false, false, double>(T, la, ld, amps, syls, cknots, W, lane);
-#endif
-  const float wm = wave_max(tmax);
+  const float wm = wave_max(run_one_tall(T, la, ld, amps, syls, cknots, W, lane));
   if (lane == 0) taskmax[ti] = wm;
+#endif
 }
 
 // per-syllable max over its task slots and crossfade-piece slots
@@ -732,7 +933,7 @@ void launch_sine_bank(const DevicePlan& D, int64_t t0, int64_t n_tasks, hipStrea
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   const int64_t blocks = std::min<int64_t>((n_tasks + 3) / 4, (int64_t)ncu * SG_SINE_PERSIST);
 #else
-  const int64_t blocks = (n_tasks + SG_TASKS_PER_BLOCK - 1) / SG_TASKS_PER_BLOCK;
+  const int64_t blocks = SG_PAIR ? (n_tasks + 7) / 8 : (n_tasks + SG_TASKS_PER_BLOCK - 1) / SG_TASKS_PER_BLOCK;
 #endif
   hipLaunchKernelGGL(sg_sine_bank, dim3((unsigned)blocks), dim3(256), 0, s, D.tasks + t0, n_tasks, D.amps, D.syls,
                      D.cknots, D.W, D.taskmax + t0);
@@ -740,7 +941,7 @@ void launch_sine_bank(const DevicePlan& D, int64_t t0, int64_t n_tasks, hipStrea
 }
 void launch_sine_bank_tall(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(sg_sine_bank_tall, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, D.tall + k0, n, D.tasks,
+  hipLaunchKernelGGL(sg_sine_bank_tall, dim3((unsigned)(SG_TALL_PAIR ? (n + 7) / 8 : (n + 3) / 4)), dim3(256), 0, s, D.tall + k0, n, D.tasks,
                      D.amps, D.syls, D.cknots, D.W, D.taskmax);
   SG_LAUNCHED("sg_sine_bank_tall");
 }
