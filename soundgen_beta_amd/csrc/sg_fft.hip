@@ -793,13 +793,14 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
 // summation is in frame order, so results are deterministic.
 // LDS: twS (M pairs), twN (M pairs), ham + han (M pairs each), SG_FFT_WAVES slices (M pairs each).
 // One segment of sg_stft_ola (CM > 0: the M = CM geometry with radices R0 x R1 x R2, sizes folded)
-template <int CM, int R0, int R1, int R2>
+template <int CM, int R0, int R1, int R2, int MODE>
 __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __restrict__ olas,
                                              const SgFrame* __restrict__ frames, const SgFftGeom& g,
                                              const float* __restrict__ fl, float* __restrict__ fs,
                                              float* __restrict__ slotmax, float2* twS, const float2* twN,
                                              const float* ham, const float* han, int w, int lane) {
   const int M = CM ? CM : g.M, N = CM ? 2 * CM : g.wl;
+  const int mode = MODE;  // the launch's phase fixes it (noise: phase 0, filter: phase 1)
   const SgOla& O = olas[S.ola];
   float2* A = twS + M * (4 + w);
   const float* Af = reinterpret_cast<const float*>(A);
@@ -826,7 +827,7 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
   {
     int Mk = M;
     if (!CM) __asm__ __volatile__("" : "+s"(Mk));
-    frame_prefetch(P, frames[S.fdev], S.mode, Mk, fl, fs, lane);
+    frame_prefetch(P, frames[S.fdev], mode, Mk, fl, fs, lane);
   }
 #endif
   for (int k = 0; k < S.nf; ++k) {
@@ -834,16 +835,16 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
     {
       int Mk = M;
       if (!CM) __asm__ __volatile__("" : "+s"(Mk));
-      frame_prefetch(P, frames[S.fdev + k], S.mode, Mk, fl, fs, lane);
+      frame_prefetch(P, frames[S.fdev + k], mode, Mk, fl, fs, lane);
     }
 #endif
-    frame_front<CM, R0, R1, R2>(A, P, S.mode, g, twS, twN, ham, lane SG_ST_ARGS);
+    frame_front<CM, R0, R1, R2>(A, P, mode, g, twS, twN, ham, lane SG_ST_ARGS);
 #if SG_PF_AHEAD
     // the next frame's inputs are in flight during this frame's inverse FFT and overlap-add
     if (k + 1 < S.nf) {
       int Mk = M;
       if (!CM) __asm__ __volatile__("" : "+s"(Mk));
-      frame_prefetch(P, frames[S.fdev + k + 1], S.mode, Mk, fl, fs, lane);
+      frame_prefetch(P, frames[S.fdev + k + 1], mode, Mk, fl, fs, lane);
     }
 #endif
     SG_ST(4);
@@ -911,7 +912,8 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
   if (lane == 0) slotmax[S.slot] = m;
 }
 
-extern "C" __global__ __launch_bounds__(SG_FFT_WAVES * 64) __attribute__((amdgpu_waves_per_eu(SG_FFT_WPE))) void sg_stft_ola(
+template <int MODE>
+__device__ __forceinline__ void stft_ola_body(
     const SgSegment* __restrict__ segs, const SgOla* __restrict__ olas, const SgFrame* __restrict__ frames,
     const SgFftGeom* __restrict__ geoms, const float* __restrict__ fl, float* __restrict__ fs,
     float* __restrict__ slotmax) {
@@ -939,14 +941,28 @@ extern "C" __global__ __launch_bounds__(SG_FFT_WAVES * 64) __attribute__((amdgpu
   if (S.nf <= 0) return;  // padding segment
 #if SG_STFT_SPEC
   if (M == 1102 && g.nstages == 3 && g.radix[0] == 2 && g.radix[1] == 19 && g.radix[2] == 29)
-    stft_segment<1102, 2, 19, 29>(S, olas, frames, g, fl, fs, slotmax, twS, twN, ham, han, w, lane);
+    stft_segment<1102, 2, 19, 29, MODE>(S, olas, frames, g, fl, fs, slotmax, twS, twN, ham, han, w, lane);
   else
 #endif
 #ifndef SG_STFT_ONLY_SPEC  // diagnostic: the specialised path alone (register budget)
-    stft_segment<0, 0, 0, 0>(S, olas, frames, g, fl, fs, slotmax, twS, twN, ham, han, w, lane);
+    stft_segment<0, 0, 0, 0, MODE>(S, olas, frames, g, fl, fs, slotmax, twS, twN, ham, han, w, lane);
 #else
     ;
 #endif
+}
+
+extern "C" __global__ __launch_bounds__(SG_FFT_WAVES * 64) __attribute__((amdgpu_waves_per_eu(SG_FFT_WPE))) void sg_stft_ola(
+    const SgSegment* __restrict__ segs, const SgOla* __restrict__ olas, const SgFrame* __restrict__ frames,
+    const SgFftGeom* __restrict__ geoms, const float* __restrict__ fl, float* __restrict__ fs,
+    float* __restrict__ slotmax) {
+  stft_ola_body<SG_FRAME_FILTER>(segs, olas, frames, geoms, fl, fs, slotmax);
+}
+// generateNoise()'s istft (phase 0): the noise mode only
+extern "C" __global__ __launch_bounds__(SG_FFT_WAVES * 64) __attribute__((amdgpu_waves_per_eu(SG_FFT_WPE))) void sg_stft_ola_noise(
+    const SgSegment* __restrict__ segs, const SgOla* __restrict__ olas, const SgFrame* __restrict__ frames,
+    const SgFftGeom* __restrict__ geoms, const float* __restrict__ fl, float* __restrict__ fs,
+    float* __restrict__ slotmax) {
+  stft_ola_body<SG_FRAME_NOISE>(segs, olas, frames, geoms, fl, fs, slotmax);
 }
 
 // Test probe: wavefront w transforms frame w (M complex points, in place) with
@@ -1162,10 +1178,11 @@ void launch_fft_frames(const DevicePlan& D, int64_t g0, int64_t n_groups, int ld
                      D.geoms, D.fl, D.fs);
   SG_LAUNCHED("sg_fft_frames");
 }
-void launch_stft_ola(const DevicePlan& D, int64_t s0, int64_t n_segs, int lds_bytes, hipStream_t s) {
+void launch_stft_ola(const DevicePlan& D, int phase, int64_t s0, int64_t n_segs, int lds_bytes, hipStream_t s) {
   if (n_segs <= 0) return;
-  lds_opt_in(reinterpret_cast<const void*>(&sg_stft_ola), lds_bytes, "sg_stft_ola");
-  hipLaunchKernelGGL(sg_stft_ola, dim3((unsigned)(n_segs / SG_FFT_WAVES)), dim3(SG_FFT_WAVES * 64), lds_bytes, s,
+  auto* k = phase == 0 ? &sg_stft_ola_noise : &sg_stft_ola;
+  lds_opt_in(reinterpret_cast<const void*>(k), lds_bytes, phase == 0 ? "sg_stft_ola_noise" : "sg_stft_ola");
+  hipLaunchKernelGGL(k, dim3((unsigned)(n_segs / SG_FFT_WAVES)), dim3(SG_FFT_WAVES * 64), lds_bytes, s,
                      D.olasegs + s0,
                      D.olas, D.frames, D.geoms, D.fl, D.fs, D.olatilemax);
   SG_LAUNCHED("sg_stft_ola");
