@@ -218,8 +218,9 @@ def traffic_from_profiles(config, kernel, launches_per_step):
         return None, None
     d = json.load(open(files[-1]))
     ex = d.get("executes")
+    names = (kernel, kernel + "_noise")  # sg_stft_ola: the filter and the noise (phase 0) kernels
     hits = [(v["hbm_bytes"], v.get("launches")) for k, v in d.get("kernels", {}).items()
-            if k.split(" ")[0] == kernel and "hbm_bytes" in v]
+            if k.split(" ")[0] in names and "hbm_bytes" in v]
     if not hits or not ex or any(n is None for _, n in hits):
         return None, None
     per_step = sum(b * n for b, n in hits) / ex
