@@ -1056,6 +1056,10 @@ __device__ __forceinline__ float sigmoid_at(const float* __restrict__ tab, int l
   return r < lo ? tab[r] : tab[2 * lo - 1 - r];
 }
 
+#ifndef SG_MIX_LDS_SPLINE
+#define SG_MIX_LDS_SPLINE 1  // build knob: sg_mix evaluates spline contours from LDS-staged knots
+#endif
+[[maybe_unused]] constexpr int SG_MIX_KMAX = 32;  // knots of an LDS-staged contour
 __device__ __forceinline__ float fade_in_out(int lf, int64_t L, int64_t k) {  // fadeInOut(), R/utilities_soundgen.R:440-459
   float f = 1.f;
   if (lf < 2) return f;
@@ -1087,6 +1091,21 @@ extern "C" __global__ __launch_bounds__(256) void sg_mix(const SgMixTile* __rest
   __shared__ int curs[NC][256];
   for (int i = 0; i < NC && i < X.nitems; ++i) curs[i][threadIdx.x] = -1;
   int mcur = -1;
+#if SG_MIX_LDS_SPLINE
+  // spline contours (kind 3, <= SG_MIX_KMAX knots) of the mult envelope (slot NC) and
+  // the first NC items staged in LDS: the per-sample interval walk and the five
+  // coefficient loads then hit LDS instead of a dependent chain of global loads
+  __shared__ double cks[NC + 1][5 * SG_MIX_KMAX];
+  auto lds_ok = [&](const SgContour& c) { return c.kind == 3 && c.nk <= SG_MIX_KMAX; };
+  for (int i = 0; i <= NC; ++i) {
+    if (i < NC && i >= X.nitems) continue;
+    const SgContour& c = i == NC ? X.mult : items[X.item0 + i].strength;
+    if (!lds_ok(c)) continue;
+    const double* src = cknots + c.k_off;
+    for (int j = threadIdx.x; j < 5 * c.nk; j += 256) cks[i][j] = src[j];
+  }
+  __syncthreads();
+#endif
 #pragma unroll 1
   for (int64_t kc = T.k0; kc < kend; kc += E * 256) {
     float v[E];
@@ -1120,8 +1139,16 @@ extern "C" __global__ __launch_bounds__(256) void sg_mix(const SgMixTile* __rest
         if (k >= kend || j < 0 || j >= it.len) continue;
         float nv = raw[e] * nscale;
         if (flat) nv *= sflat;
-        else if (it.strength.kind != 0)
-          nv = (float)((double)nv * sgd::contour_at_cursor(it.strength, cknots, it.len, j, cur));
+        else if (it.strength.kind != 0) {
+#if SG_MIX_LDS_SPLINE
+          if (i < NC && lds_ok(it.strength)) {
+            SgContour cl = it.strength;
+            cl.k_off = 0;
+            nv = (float)((double)nv * sgd::contour_at_cursor(cl, &cks[i][0], it.len, j, cur));
+          } else
+#endif
+            nv = (float)((double)nv * sgd::contour_at_cursor(it.strength, cknots, it.len, j, cur));
+        }
         nv *= fade_in_out(it.fade, it.len, j);
         v[e] += nv;
       }
@@ -1130,8 +1157,16 @@ extern "C" __global__ __launch_bounds__(256) void sg_mix(const SgMixTile* __rest
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int64_t k = kc + e * 256 + threadIdx.x;
-      if (X.mult.kind != 0 && k < kend)
-        v[e] = (float)((double)v[e] * sgd::contour_at_cursor(X.mult, cknots, X.len, k, mcur));
+      if (X.mult.kind != 0 && k < kend) {
+#if SG_MIX_LDS_SPLINE
+        if (lds_ok(X.mult)) {
+          SgContour cl = X.mult;
+          cl.k_off = 0;
+          v[e] = (float)((double)v[e] * sgd::contour_at_cursor(cl, &cks[NC][0], X.len, k, mcur));
+        } else
+#endif
+          v[e] = (float)((double)v[e] * sgd::contour_at_cursor(X.mult, cknots, X.len, k, mcur));
+      }
       if (X.am_lo > 0) v[e] *= 1.f - sigmoid_at(fl + X.am_tab, X.am_lo, k) * X.am_dep / 100.f;
     }
 #pragma unroll

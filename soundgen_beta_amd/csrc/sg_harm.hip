@@ -81,6 +81,9 @@ __device__ __forceinline__ void clenshaw_lds(const float* __restrict__ la, const
                                              const Acc (&al)[NS], Acc (&b1)[NS], Acc (&b2)[NS],
                                              Acc (&e1)[NS], Acc (&e2)[NS]) {
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#ifdef SG_DIAG_NOROWS  // diagnostic timing build only: no row work
+  n = 0;
+#endif
   if (SG_ROWS_IT == 8 && (n & 4)) {  // odd group of 4 on top
     const float4 A4 = *reinterpret_cast<const float4*>(la + n - 4);
     const float4 D4 = TWO ? *reinterpret_cast<const float4*>(ld + n - 4) : z4;
@@ -252,6 +255,16 @@ __device__ __forceinline__ float run_task(const SgWTask& T, float* __restrict__ 
 #pragma unroll
     for (int k = 0; k < 8; ++k) rc[k] = rs[k] = 0.f;
   }
+#ifndef SG_F64_NS_MAX
+#define SG_F64_NS_MAX 2  // build knob: widest fp64 slot pass (tall tasks; fewer VGPRs, higher occupancy)
+#endif
+  if constexpr (!F32 && SG_F64_NS_MAX < 4) {
+#pragma unroll 1
+    for (; T.len - l0 > 64; l0 += 128)
+      run_slots<2, TWO, ENV, LIN, Acc>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax, rc, rs);
+    if (l0 < T.len) run_slots<1, TWO, ENV, LIN, Acc>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax, rc, rs);
+    return tmax;
+  }
   if (F32 && (!TWO || SG_NS8_TWO) && SG_NS_MAX >= 8) {
 #pragma unroll 1
     for (; T.len - l0 > 448; l0 += 512)
@@ -268,13 +281,28 @@ __device__ __forceinline__ float run_task(const SgWTask& T, float* __restrict__ 
   return tmax;
 }
 
+#ifndef SG_ENV_NOINLINE
+#define SG_ENV_NOINLINE 0  // build knob: amplitude-envelope tasks (rare) out of line, a smaller hot kernel
+#endif
+#if SG_ENV_NOINLINE
+__device__ __noinline__ float run_env(const SgWTask& T, float* __restrict__ la, float* __restrict__ ld,
+                                      const float* __restrict__ amps, const SgSyllable* __restrict__ syls,
+                                      const double* __restrict__ cknots, float* __restrict__ W, int lane) {
+  return (T.flags & SG_TASK_CONST) ? run_task<false, true, false>(T, la, ld, amps, syls, cknots, W, lane)
+                                   : run_task<true, true, false>(T, la, ld, amps, syls, cknots, W, lane);
+}
+#endif
 // One task on its own wave pass (any length, envelope, linear or general phase)
 __device__ __forceinline__ float run_one(const SgWTask& T, float* __restrict__ la, float* __restrict__ ld,
                                          const float* __restrict__ amps, const SgSyllable* __restrict__ syls,
                                          const double* __restrict__ cknots, float* __restrict__ W, int lane) {
+#if SG_ENV_NOINLINE
+  if (T.flags & SG_TASK_ENV) return run_env(T, la, ld, amps, syls, cknots, W, lane);
+#else
   if (T.flags & SG_TASK_ENV)  // amplAnchors envelope: rare, kept out of the hot variants
     return (T.flags & SG_TASK_CONST) ? run_task<false, true, false>(T, la, ld, amps, syls, cknots, W, lane)
                                      : run_task<true, true, false>(T, la, ld, amps, syls, cknots, W, lane);
+#endif
   if (T.flags & SG_TASK_LIN)  // constant pitch over the phase segment
     return (T.flags & SG_TASK_CONST) ? run_task<false, false, true>(T, la, ld, amps, syls, cknots, W, lane)
                                      : run_task<true, false, true>(T, la, ld, amps, syls, cknots, W, lane);
@@ -295,7 +323,11 @@ template <bool TWO>
 __device__ __forceinline__ void run_pair(const SgWTask& P, const SgWTask& Q, float* __restrict__ la,
                                          float* __restrict__ ld, const float* __restrict__ amps,
                                          float* __restrict__ W, int lane, float& mp, float& mq) {
+#ifdef SG_DIAG_NOROWS
+  const int R = 0;
+#else
   const int R = P.R > Q.R ? P.R : Q.R;  // multiples of 16
+#endif
   for (int r = lane; r < R; r += 64) {
     *reinterpret_cast<float2*>(la + 2 * r) = make_float2(r < P.R ? amps[P.a_off + r] : 0.f, r < Q.R ? amps[Q.a_off + r] : 0.f);
     if (TWO)
@@ -812,11 +844,31 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_copy(const SgCopyTile*
 
 // General path: the tiles the planner did not give to sg_harm_copy (crossfade
 // pieces, amplitude envelope, drift, misaligned slots).
+#ifndef SG_FIN_LDS_ENV
+#define SG_FIN_LDS_ENV 2  // build knob: envelope spline by interval cursors (2), also from LDS-staged knots (1; the
+                          // per-tile barriers cost more than they save: 5.98 -> 6.27 ms on C5), bisection per sample (0)
+#endif
+#ifndef SG_FIN_WAVE_TILE
+#define SG_FIN_WAVE_TILE 0  // build knob: one wave per 1024-sample tile (its 4 quarters in turn)
+#endif
+static_assert(!(SG_FIN_WAVE_TILE && SG_FIN_LDS_ENV == 1), "LDS envelope staging needs all waves on one tile");
+constexpr int SG_FIN_KMAX = 32;  // knots of an LDS-staged envelope
 __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece* __restrict__ pieces,
                                               const SgSyllable* __restrict__ syls, const double* __restrict__ cknots,
                                               const float* __restrict__ W, const float* __restrict__ maxes,
-                                              float* __restrict__ out_buf, float* __restrict__ fs) {
+                                              float* __restrict__ out_buf, float* __restrict__ fs, double* lenv,
+                                              int wv) {
   const SgSyllable& sy = syls[tl.syl];
+#if SG_FIN_LDS_ENV == 1
+  // the syllable's envelope knots (x, y, b, c, d) in LDS for this tile (all waves
+  // of the workgroup work on the same tile: sync before overwriting, sync after)
+  const bool envl = sy.env.kind == 3 && sy.env.nk <= SG_FIN_KMAX;
+  __syncthreads();
+  if (envl)
+    for (int j = threadIdx.x; j < 5 * sy.env.nk; j += 256) lenv[j] = cknots[sy.env.k_off + j];
+  __syncthreads();
+#endif
+  int ecur = -1;  // a lane's samples increase: the envelope interval is found by stepping
   float* __restrict__ out = sy.dst_fs ? fs : out_buf;
   const float inv_max = 1.f / maxes[sy.max_slot];
   const int pend = sy.piece0 + sy.npiece;
@@ -826,7 +878,7 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
   // drift-knot interval of its first sample; up to 8 knots from there are
   // held as wave-uniform values and each lane picks its interval by compares
   // (no dependent loads); chunks spanning more knots or pieces step per lane.
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63;
   const int64_t c0 = tl.k0 + 256 * wv;
   if (c0 >= tile_end) return;
   const int64_t c1 = c0 + 256 < tile_end ? c0 + 256 : tile_end;
@@ -871,7 +923,20 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
       const SgPiece& pc = pieces[p];
       x = pc.nterms == 0 ? 0.f : piece_value(pc, W, k - pc.start);
     }
-    if (sy.env.kind != 0) x = (float)((double)x * contour_at(sy.env, cknots, sy.L, k));
+    if (sy.env.kind != 0) {
+#if SG_FIN_LDS_ENV == 1
+      if (envl) {
+        SgContour cl = sy.env;
+        cl.k_off = 0;
+        x = (float)((double)x * sgd::contour_at_cursor(cl, lenv, sy.L, k, ecur));
+      } else
+        x = (float)((double)x * sgd::contour_at_cursor(sy.env, cknots, sy.L, k, ecur));
+#elif SG_FIN_LDS_ENV == 2
+      x = (float)((double)x * sgd::contour_at_cursor(sy.env, cknots, sy.L, k, ecur));
+#else
+      x = (float)((double)x * contour_at(sy.env, cknots, sy.L, k));
+#endif
+    }
     x *= inv_max;
     if (sy.fade >= 2) x *= fade_at(sy.fade, sy.L, k);
     if (drift) {
@@ -909,12 +974,23 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize(
     const SgSylTile* __restrict__ stiles, int64_t ntiles, const SgPiece* __restrict__ pieces,
     const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, const float* __restrict__ W,
     const float* __restrict__ maxes, float* __restrict__ out_buf, float* __restrict__ fs) {
+  __shared__ double lenv[5 * SG_FIN_KMAX];
+#if SG_FIN_WAVE_TILE
+  // wave w takes tile 4 b + w whole (its quarters in turn): one descriptor chain per 1024 samples
+  const int64_t t = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (t >= ntiles) return;
+  const SgSylTile tl = stiles[t];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) finalize_tile(tl, pieces, syls, cknots, W, maxes, out_buf, fs, lenv, q);
+#else
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #pragma unroll 1
   for (int i = 0; i < SG_FIN_TILES; ++i) {
     const int64_t t = (int64_t)blockIdx.x * SG_FIN_TILES + i;
     if (t >= ntiles) break;
-    finalize_tile(stiles[t], pieces, syls, cknots, W, maxes, out_buf, fs);
+    finalize_tile(stiles[t], pieces, syls, cknots, W, maxes, out_buf, fs, lenv, wv);
   }
+#endif
 }
 
 // ---------------------------------------------------------------- launchers
@@ -965,7 +1041,8 @@ void launch_harm_copy(const DevicePlan& D, int64_t c0, int64_t n_ctiles, float* 
 }
 void launch_harm_finalize(const DevicePlan& D, int64_t f0, int64_t n_stiles, float* out, hipStream_t s) {
   if (n_stiles <= 0) return;
-  hipLaunchKernelGGL(sg_harm_finalize, dim3((unsigned)((n_stiles + SG_FIN_TILES - 1) / SG_FIN_TILES)), dim3(256), 0, s,
+  const int64_t per_block = SG_FIN_WAVE_TILE ? 4 : SG_FIN_TILES;
+  hipLaunchKernelGGL(sg_harm_finalize, dim3((unsigned)((n_stiles + per_block - 1) / per_block)), dim3(256), 0, s,
                      D.syl_tiles + f0, n_stiles, D.pieces, D.syls,
                      D.cknots, D.W, D.maxes, out, D.fs);
   SG_LAUNCHED("sg_harm_finalize");
