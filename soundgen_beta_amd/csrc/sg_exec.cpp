@@ -288,18 +288,29 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   D.uploaded = true;
 }
 
+// The harmonic source (sine banks -> maxima -> finalize) and the noise phase
+// (envelopes -> noise STFT/OLA) read and write disjoint buffers, so they run
+// concurrently: the harmonic chain on s2, the noise phase on s; the pre-filter
+// mixes wait for both. SG_OVERLAP=0 runs everything on s (measurement knob).
+static bool overlap_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("SG_OVERLAP");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 void device_execute(const Batch& B, DevicePlan& D, float* d_out, hipStream_t s, hipStream_t s2,
                     std::vector<SgProfEvent>* prof) {
   if (B.slices.empty()) {  // no harmonic syllables: spectral phases only
-    device_execute_spec(B, D, d_out, s, prof);
+    device_execute_spec(B, D, d_out, s, prof, false);
     return;
   }
-  const bool two = B.slices.size() > 1;
-  if (!two) s2 = s;
-  // fork: s2 starts after everything already queued on s
-  if (two) {
+  const bool ovl = overlap_on() && s2 != nullptr && s2 != s;
+  hipStream_t h = ovl ? s2 : s;  // the harmonic chain's stream
+  if (ovl) {  // fork: h starts after everything already queued on s
     HIPCHK(hipEventRecord(D.ev_fork, s));
-    HIPCHK(hipStreamWaitEvent(s2, D.ev_fork, 0));
+    HIPCHK(hipStreamWaitEvent(h, D.ev_fork, 0));
   }
   for (size_t c = 0; c < B.slices.size(); ++c) {
     const Slice& sl = B.slices[c];
@@ -307,39 +318,37 @@ void device_execute(const Batch& B, DevicePlan& D, float* d_out, hipStream_t s, 
     if (prof) {
       HIPCHK(hipEventCreate(&e0));
       HIPCHK(hipEventCreate(&e1));
-      HIPCHK(hipEventRecord(e0, s));
+      HIPCHK(hipEventRecord(e0, h));
     }
-    launch_sine_bank(D, sl.t0, sl.t1 - sl.t0, s);
+    launch_sine_bank(D, sl.t0, sl.t1 - sl.t0, h);
     {  // tall tasks of the slice (ascending indices)
       const auto lo = std::lower_bound(D.tall_host.begin(), D.tall_host.end(), (int32_t)sl.t0);
       const auto hi = std::lower_bound(D.tall_host.begin(), D.tall_host.end(), (int32_t)sl.t1);
-      launch_sine_bank_tall(D, lo - D.tall_host.begin(), hi - lo, s);
+      launch_sine_bank_tall(D, lo - D.tall_host.begin(), hi - lo, h);
     }
     if (prof) {
-      HIPCHK(hipEventRecord(e1, s));
+      HIPCHK(hipEventRecord(e1, h));
       prof->push_back({SG_PROF_SINE_BANK, e0, e1});
     }
-    launch_piece_max(D, sl.p0, sl.p1 - sl.p0, s);
-    launch_syl_max(D, sl.s0, sl.s1 - sl.s0, s);
-    if (two) {
-      HIPCHK(hipEventRecord(D.ev_slice[c], s));
-      HIPCHK(hipStreamWaitEvent(s2, D.ev_slice[c], 0));
-    }
-    launch_harm_copy(D, sl.c0, sl.c1 - sl.c0, d_out, s2);
-    launch_harm_finalize(D, sl.f0, sl.f1 - sl.f0, d_out, s2);
+    launch_piece_max(D, sl.p0, sl.p1 - sl.p0, h);
+    launch_syl_max(D, sl.s0, sl.s1 - sl.s0, h);
+    launch_harm_copy(D, sl.c0, sl.c1 - sl.c0, d_out, h);
+    launch_harm_finalize(D, sl.f0, sl.f1 - sl.f0, d_out, h);
   }
-  if (two) {  // join
-    HIPCHK(hipEventRecord(D.ev_join, s2));
-    HIPCHK(hipStreamWaitEvent(s, D.ev_join, 0));
+  if (ovl) {
+    // the noise phase runs on s meanwhile; the pre-filter mixes join the harmonic chain
+    HIPCHK(hipEventRecord(D.ev_join, h));
+    device_execute_spec(B, D, d_out, s, prof, true, D.ev_join);
+  } else {
+    device_execute_spec(B, D, d_out, s, prof, false);
   }
-  device_execute_spec(B, D, d_out, s, prof);
   HIPCHK(hipGetLastError());
 }
 
 // Spectral phases after the harmonic syllables: noise frames -> noise OLA,
 // pre-filter mixes (sounds), filter frames -> filter OLA, final mixes.
 void device_execute_spec(const Batch& B, const DevicePlan& D, float* d_out, hipStream_t s,
-                         std::vector<SgProfEvent>* prof) {
+                         std::vector<SgProfEvent>* prof, bool join, hipEvent_t harm_done) {
   launch_spec_env(D, B, s);  // envelopes and noise filters read by both phases
   // phase: fused STFT/ISTFT/OLA segments, unfused frame groups + OLA tiles, per-OLA maxima
   auto phase = [&](int ph) {
@@ -365,6 +374,7 @@ void device_execute_spec(const Batch& B, const DevicePlan& D, float* d_out, hipS
   phase(0);
   for (const Batch::Copy& c : B.copies)
     HIPCHK(hipMemcpyAsync(D.fs + c.fs_off, D.fl + c.fl_off, (size_t)c.n * sizeof(float), hipMemcpyDeviceToDevice, s));
+  if (join) HIPCHK(hipStreamWaitEvent(s, harm_done, 0));  // the harmonic syllables (fs, out) are final
   launch_mix(D, 0, B.mixtile_split, d_out, s);
   phase(1);
   launch_mix(D, B.mixtile_split, (int64_t)B.mixtiles.size() - B.mixtile_split, d_out, s);

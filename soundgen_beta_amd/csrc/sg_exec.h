@@ -79,7 +79,7 @@ struct SgProfEvent {
 void device_execute(const Batch& B, DevicePlan& D, float* d_out, hipStream_t s, hipStream_t s2,
                     std::vector<SgProfEvent>* prof);
 void device_execute_spec(const Batch& B, const DevicePlan& D, float* d_out, hipStream_t s,
-                         std::vector<SgProfEvent>* prof = nullptr);
+                         std::vector<SgProfEvent>* prof, bool join = false, hipEvent_t harm_done = nullptr);
 
 // launchers (sg_harm.hip)
 void launch_sine_bank(const DevicePlan& D, int64_t t0, int64_t n_tasks, hipStream_t s);

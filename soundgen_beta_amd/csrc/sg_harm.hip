@@ -852,12 +852,15 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_copy(const SgCopyTile*
 #define SG_FIN_WAVE_TILE 0  // build knob: one wave per 1024-sample tile (its 4 quarters in turn)
 #endif
 static_assert(!(SG_FIN_WAVE_TILE && SG_FIN_LDS_ENV == 1), "LDS envelope staging needs all waves on one tile");
+#ifndef SG_FIN_DRIFT_LDS
+#define SG_FIN_DRIFT_LDS 1  // build knob: drift interval by index from per-wave LDS (x, y, slope) rows
+#endif
 constexpr int SG_FIN_KMAX = 32;  // knots of an LDS-staged envelope
 __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece* __restrict__ pieces,
                                               const SgSyllable* __restrict__ syls, const double* __restrict__ cknots,
                                               const float* __restrict__ W, const float* __restrict__ maxes,
                                               float* __restrict__ out_buf, float* __restrict__ fs, double* lenv,
-                                              int wv) {
+                                              int wv, double* lkw) {
   const SgSyllable& sy = syls[tl.syl];
 #if SG_FIN_LDS_ENV == 1
   // the syllable's envelope knots (x, y, b, c, d) in LDS for this tile (all waves
@@ -867,6 +870,16 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
   if (envl)
     for (int j = threadIdx.x; j < 5 * sy.env.nk; j += 256) lenv[j] = cknots[sy.env.k_off + j];
   __syncthreads();
+#elif SG_FIN_LDS_ENV == 3
+  // the same per wave (its own copy, no workgroup barrier)
+  const bool envl = sy.env.kind == 3 && sy.env.nk <= SG_FIN_KMAX;
+  if (envl) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // earlier reads of the slot come first
+    __builtin_amdgcn_wave_barrier();
+    for (int j = threadIdx.x & 63; j < 5 * sy.env.nk; j += 64) lenv[j] = cknots[sy.env.k_off + j];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
 #endif
   int ecur = -1;  // a lane's samples increase: the envelope interval is found by stepping
   float* __restrict__ out = sy.dst_fs ? fs : out_buf;
@@ -906,6 +919,24 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
     }
     // every sample of the chunk lies in intervals d0 .. d0 + KW - 2
     local_knots = d0 + KW - 1 >= dr.nk - 1 || u_at(c1 - 1) < xs[KW - 1];
+#if SG_FIN_DRIFT_LDS
+    // per interval (x_t, y_t, slope_t) in the wave's LDS slot: a lane then reads its
+    // interval by index instead of selecting four doubles through KW - 2 compares,
+    // and multiplies by the slope instead of dividing (a few fp64 ulps from approx()'s
+    // (y_j - y_i) * ((u - x_i) / (x_j - x_i)), far below the fp32 output)
+    if (lane < KW - 1) {
+      double xv = xs[0], yv = ys[0], x1 = xs[1], y1 = ys[1];
+#pragma unroll
+      for (int t = 1; t < KW - 1; ++t)
+        if (lane == t) { xv = xs[t]; yv = ys[t]; x1 = xs[t + 1]; y1 = ys[t + 1]; }
+      lkw[3 * lane] = xv;
+      lkw[3 * lane + 1] = yv;
+      lkw[3 * lane + 2] = x1 > xv ? (y1 - yv) / (x1 - xv) : 0.0;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
   }
   int p = pu, di = d0;
   float res[4];  // every load of the chunk before its stores
@@ -924,7 +955,7 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
       x = pc.nterms == 0 ? 0.f : piece_value(pc, W, k - pc.start);
     }
     if (sy.env.kind != 0) {
-#if SG_FIN_LDS_ENV == 1
+#if SG_FIN_LDS_ENV == 1 || SG_FIN_LDS_ENV == 3
       if (envl) {
         SgContour cl = sy.env;
         cl.k_off = 0;
@@ -943,11 +974,19 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
       double dm;
       if (local_knots) {  // linear_at's interval and arithmetic, knots from registers
         const double u = u_at(k);
+#if SG_FIN_DRIFT_LDS
+        int t = 0;  // the conditions hold for a prefix of t: their count is the interval
+#pragma unroll
+        for (int q = 1; q < KW - 1; ++q) t += (d0 + q <= dr.nk - 2 && xs[q] <= u) ? 1 : 0;
+        const double xi = lkw[3 * t], yi = lkw[3 * t + 1], sl = lkw[3 * t + 2];
+        dm = u == xi ? yi : fma(sl, u - xi, yi);
+#else
         double xi = xs[0], xj = xs[1], yi = ys[0], yj = ys[1];
 #pragma unroll
         for (int t = 1; t < KW - 1; ++t)
           if (d0 + t <= dr.nk - 2 && xs[t] <= u) { xi = xs[t]; xj = xs[t + 1]; yi = ys[t]; yj = ys[t + 1]; }
         dm = u == xj ? yj : (u == xi ? yi : yi + (yj - yi) * ((u - xi) / (xj - xi)));
+#endif
       } else {
         dm = sgd::linear_at_cursor(dr, cknots, sy.L, k, di);
       }
@@ -974,21 +1013,28 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize(
     const SgSylTile* __restrict__ stiles, int64_t ntiles, const SgPiece* __restrict__ pieces,
     const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, const float* __restrict__ W,
     const float* __restrict__ maxes, float* __restrict__ out_buf, float* __restrict__ fs) {
+#if SG_FIN_LDS_ENV == 3
+  __shared__ double lenv_w[4][5 * SG_FIN_KMAX];  // per wave
+  double* lenv = lenv_w[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
+#else
   __shared__ double lenv[5 * SG_FIN_KMAX];
+#endif
+  __shared__ double lk[4][3 * 8];  // per wave: drift intervals (x, y, slope)
+  double* lkw = lk[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
 #if SG_FIN_WAVE_TILE
   // wave w takes tile 4 b + w whole (its quarters in turn): one descriptor chain per 1024 samples
   const int64_t t = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (t >= ntiles) return;
   const SgSylTile tl = stiles[t];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) finalize_tile(tl, pieces, syls, cknots, W, maxes, out_buf, fs, lenv, q);
+  for (int q = 0; q < 4; ++q) finalize_tile(tl, pieces, syls, cknots, W, maxes, out_buf, fs, lenv, q, lkw);
 #else
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #pragma unroll 1
   for (int i = 0; i < SG_FIN_TILES; ++i) {
     const int64_t t = (int64_t)blockIdx.x * SG_FIN_TILES + i;
     if (t >= ntiles) break;
-    finalize_tile(stiles[t], pieces, syls, cknots, W, maxes, out_buf, fs, lenv, wv);
+    finalize_tile(stiles[t], pieces, syls, cknots, W, maxes, out_buf, fs, lenv, wv, lkw);
   }
 #endif
 }

@@ -12,7 +12,12 @@ if [ -n "$PYTEST_K" ]; then
   tail -2 gpurun_out/pytest_$TAG.log
 fi
 for v in default ${VARIANTS}; do
-  if [ "$v" = default ]; then unset SG_HIP_LIB; else export SG_HIP_LIB=$R/soundgen_beta_amd/lib/exp_$v.so; fi
+  unset SG_OVERLAP
+  case "$v" in
+    default) unset SG_HIP_LIB ;;
+    nooverlap) unset SG_HIP_LIB; export SG_OVERLAP=0 ;;
+    *) export SG_HIP_LIB=$R/soundgen_beta_amd/lib/exp_$v.so ;;
+  esac
   cd /tmp
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/pk_${TAG}_$v" -o run -- python "$R/bench.py" --config c5 --calls ${CALLS:-16384} --steps 3 --warmup 1 --host-steps 0 --no-cpu-baseline > "$R/gpurun_out/pk_${TAG}_$v.log" 2>&1 || { tail -20 "$R/gpurun_out/pk_${TAG}_$v.log"; exit 1; }
   cd "$R"
