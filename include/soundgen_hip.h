@@ -198,7 +198,9 @@ int sg_execute(sg_ctx* ctx, sg_plan* plan, float* d_out, void* stream);
  * per batch slice) and every sg_stft_ola launch with HIP events on the launch
  * stream; sg_profile_read
  * returns the average launch duration (ms) and the number of launches
- * recorded, and clears them. */
+ * recorded, and clears them. While profiling is on, the harmonic chain and
+ * the noise phase (otherwise concurrent on the context's two streams) run one
+ * after the other, so each recorded duration is the launch's own. */
 int sg_set_profiling(sg_ctx* ctx, int on);
 int sg_profile_read(sg_ctx* ctx, double* sine_ms_avg, int64_t* n);
 /* Same for one kernel: SG_PROF_SINE_BANK (sg_sine_bank, generateHarmonics'

@@ -306,7 +306,8 @@ void device_execute(const Batch& B, DevicePlan& D, float* d_out, hipStream_t s, 
     device_execute_spec(B, D, d_out, s, prof, false);
     return;
   }
-  const bool ovl = overlap_on() && s2 != nullptr && s2 != s;
+  // profiling (per-kernel events) serialises the two chains: each launch's time is its own
+  const bool ovl = overlap_on() && prof == nullptr && s2 != nullptr && s2 != s;
   hipStream_t h = ovl ? s2 : s;  // the harmonic chain's stream
   if (ovl) {  // fork: h starts after everything already queued on s
     HIPCHK(hipEventRecord(D.ev_fork, s));
