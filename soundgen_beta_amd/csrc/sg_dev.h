@@ -76,6 +76,12 @@ struct SgWTask {
   int32_t pad;
 };
 static_assert(sizeof(SgWTask) == 128, "SgWTask layout");
+#ifndef SG_PAIR
+#define SG_PAIR 1  // build knob: short fp32 tasks (<= 64 samples) two per wave in the halves of packed pairs
+#endif
+#ifndef SG_TALL_PAIR
+#define SG_TALL_PAIR 1  // build knob: short tall tasks two per wave, fp32 Reinsch in packed halves
+#endif
 #ifndef SG_TASKS_PER_BLOCK
 #define SG_TASKS_PER_BLOCK 4  // 4 waves x 1 task (build knob; measured better than 2 per wave)
 #endif

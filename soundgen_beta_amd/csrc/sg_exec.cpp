@@ -22,7 +22,7 @@ constexpr size_t ALIGN = 256;
 size_t up(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
 struct Layout {
-  size_t tall;
+  size_t tall, tlong, tshort, tallp;
   size_t segs, epochs, knots, amps, tasks, pieces, syls, syl_tiles, copy_tiles, ptiles, cknots, W, taskmax, ptilemax, maxes, total;
   size_t geoms, frames, fgroups, olas, olatiles, olasegs, olatilemax, olamax, items, mixes, mixtiles, fl, fs;
   size_t eterms, ecols, envjobs, envtasks, elog2;
@@ -35,6 +35,9 @@ struct Layout {
     amps = take(B.amps.size() * sizeof(float) + 64 * sizeof(float));
     tasks = take(B.tasks.size() * sizeof(SgWTask));
     tall = take(B.tasks.size() * sizeof(int32_t));
+    tlong = take(B.tasks.size() * sizeof(int32_t));
+    tshort = take(B.tasks.size() * sizeof(int32_t));
+    tallp = take(B.tasks.size() * sizeof(int32_t));
     pieces = take(B.pieces.size() * sizeof(SgPiece));
     syls = take(B.syls.size() * sizeof(SgSyllable));
     syl_tiles = take(B.fin_tiles.size() * sizeof(SgSylTile));
@@ -215,6 +218,9 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   D.amps = (float*)(a + L.amps);
   D.tasks = (SgWTask*)(a + L.tasks);
   D.tall = (int32_t*)(a + L.tall);
+  D.tlong = (int32_t*)(a + L.tlong);
+  D.tshort = (int32_t*)(a + L.tshort);
+  D.tallp = (int32_t*)(a + L.tallp);
   D.pieces = (SgPiece*)(a + L.pieces);
   D.syls = (SgSyllable*)(a + L.syls);
   D.syl_tiles = (SgSylTile*)(a + L.syl_tiles);
@@ -251,10 +257,23 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   cp(D.knots, B.knots.data(), B.knots.size() * sizeof(double));
   cp(D.amps, B.amps.data(), B.amps.size() * sizeof(float));
   cp(D.tasks, B.tasks.data(), B.tasks.size() * sizeof(SgWTask));
+  // task classes (each task's class depends on the task alone): tall (sg_sine_bank_tall),
+  // short fp32 (two per wave, sg_sine_bank_pairs), other fp32 (sg_sine_bank)
   D.tall_host.clear();
-  for (size_t i = 0; i < B.tasks.size(); ++i)
-    if (B.tasks[i].R > SG_ROWS_F32) D.tall_host.push_back((int32_t)i);
+  D.tlong_host.clear();
+  D.tshort_host.clear();
+  D.tallp_host.clear();
+  for (size_t i = 0; i < B.tasks.size(); ++i) {
+    const SgWTask& t = B.tasks[i];
+    const bool shrt = t.len <= 64 && !(t.flags & SG_TASK_ENV);
+    if (t.R > SG_ROWS_F32) (SG_TALL_PAIR && shrt ? D.tallp_host : D.tall_host).push_back((int32_t)i);
+    else if (SG_PAIR && t.len <= 64 && !(t.flags & SG_TASK_ENV)) D.tshort_host.push_back((int32_t)i);
+    else D.tlong_host.push_back((int32_t)i);
+  }
   cp(D.tall, D.tall_host.data(), D.tall_host.size() * sizeof(int32_t));
+  cp(D.tlong, D.tlong_host.data(), D.tlong_host.size() * sizeof(int32_t));
+  cp(D.tshort, D.tshort_host.data(), D.tshort_host.size() * sizeof(int32_t));
+  cp(D.tallp, D.tallp_host.data(), D.tallp_host.size() * sizeof(int32_t));
   cp(D.pieces, B.pieces.data(), B.pieces.size() * sizeof(SgPiece));
   cp(D.syls, B.syls.data(), B.syls.size() * sizeof(SgSyllable));
   cp(D.syl_tiles, B.fin_tiles.data(), B.fin_tiles.size() * sizeof(SgSylTile));
@@ -321,11 +340,22 @@ void device_execute(const Batch& B, DevicePlan& D, float* d_out, hipStream_t s, 
       HIPCHK(hipEventCreate(&e1));
       HIPCHK(hipEventRecord(e0, h));
     }
-    launch_sine_bank(D, sl.t0, sl.t1 - sl.t0, h);
-    {  // tall tasks of the slice (ascending indices)
-      const auto lo = std::lower_bound(D.tall_host.begin(), D.tall_host.end(), (int32_t)sl.t0);
-      const auto hi = std::lower_bound(D.tall_host.begin(), D.tall_host.end(), (int32_t)sl.t1);
-      launch_sine_bank_tall(D, lo - D.tall_host.begin(), hi - lo, h);
+    {  // the slice's tasks of each class (ascending indices)
+      auto range = [&](const std::vector<int32_t>& v, int64_t& k0) {
+        const auto lo = std::lower_bound(v.begin(), v.end(), (int32_t)sl.t0);
+        const auto hi = std::lower_bound(v.begin(), v.end(), (int32_t)sl.t1);
+        k0 = lo - v.begin();
+        return (int64_t)(hi - lo);
+      };
+      int64_t k0 = 0, n = 0;
+      n = range(D.tlong_host, k0);
+      launch_sine_bank(D, k0, n, h);
+      n = range(D.tshort_host, k0);
+      launch_sine_bank_pairs(D, k0, n, h);
+      n = range(D.tall_host, k0);
+      launch_sine_bank_tall(D, k0, n, h);
+      n = range(D.tallp_host, k0);
+      launch_sine_bank_tall_pairs(D, k0, n, h);
     }
     if (prof) {
       HIPCHK(hipEventRecord(e1, h));

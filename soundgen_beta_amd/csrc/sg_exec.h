@@ -32,6 +32,12 @@ struct DevicePlan {
   SgWTask* tasks = nullptr;
   int32_t* tall = nullptr;           // indices of tasks with R > SG_ROWS_F32 (sg_sine_bank_tall)
   std::vector<int32_t> tall_host;
+  int32_t* tlong = nullptr;          // fp32 tasks run one per wave (sg_sine_bank)
+  std::vector<int32_t> tlong_host;
+  int32_t* tshort = nullptr;         // fp32 tasks of <= 64 samples, two per wave (sg_sine_bank_pairs)
+  std::vector<int32_t> tshort_host;
+  int32_t* tallp = nullptr;          // tall tasks of <= 64 samples, two per wave (sg_sine_bank_tall_pairs)
+  std::vector<int32_t> tallp_host;
   SgPiece* pieces = nullptr;
   SgSyllable* syls = nullptr;
   SgSylTile* syl_tiles = nullptr;    // general-path finalize tiles (Batch::fin_tiles)
@@ -82,8 +88,10 @@ void device_execute_spec(const Batch& B, const DevicePlan& D, float* d_out, hipS
                          std::vector<SgProfEvent>* prof, bool join = false, hipEvent_t harm_done = nullptr);
 
 // launchers (sg_harm.hip)
-void launch_sine_bank(const DevicePlan& D, int64_t t0, int64_t n_tasks, hipStream_t s);
+void launch_sine_bank(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s);
+void launch_sine_bank_pairs(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s);
 void launch_sine_bank_tall(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s);
+void launch_sine_bank_tall_pairs(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s);
 void launch_syl_max(const DevicePlan& D, int64_t s0, int64_t n_syls, hipStream_t s);
 void launch_piece_max(const DevicePlan& D, int64_t p0, int64_t n_ptiles, hipStream_t s);
 void launch_harm_finalize(const DevicePlan& D, int64_t f0, int64_t n_stiles, float* out, hipStream_t s);

@@ -38,9 +38,7 @@ constexpr int SG_LDS_ROWS = 256;
 #ifndef SG_NS_MAX
 #define SG_NS_MAX 8  // build knob: largest slot pass (8 or 4)
 #endif
-#ifndef SG_SINE_PERSIST
-#define SG_SINE_PERSIST 0  // build knob: > 0 = persistent grid of that many blocks per CU
-#endif  // rows staged per wave; taller tasks stream 256-row chunks
+
 
 template <bool TWO>
 __device__ __forceinline__ void stage_rows(float* __restrict__ la, float* __restrict__ ld, const float* __restrict__ A,
@@ -310,9 +308,6 @@ __device__ __forceinline__ float run_one(const SgWTask& T, float* __restrict__ l
                                    : run_task<true, false, false>(T, la, ld, amps, syls, cknots, W, lane);
 }
 
-#ifndef SG_PAIR
-#define SG_PAIR 1  // build knob: two short tasks per wave in the halves of packed pairs
-#endif
 // Two tasks of <= 64 samples (most of C5's: one glottal cycle each) in one
 // wave: lane l runs sample l of task P in the low and of task Q in the high half
 // of packed fp32 pairs, so each row costs the 2 packed ops per chain of ONE
@@ -374,67 +369,47 @@ __device__ __forceinline__ void run_pair(const SgWTask& P, const SgWTask& Q, flo
   mq = vq && jq >= Q.dj0 && jq < Q.dj1 ? yq : 0.f;
 }
 
+// Tasks of the fp32 class (listed in idx), one per wave.
 extern "C" __global__ __launch_bounds__(256) void sg_sine_bank(
-    const SgWTask* __restrict__ tasks, int64_t ntasks, const float* __restrict__ amps,
+    const int32_t* __restrict__ idx, int64_t n, const SgWTask* __restrict__ tasks, const float* __restrict__ amps,
     const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, float* __restrict__ W,
     float* __restrict__ taskmax) {
   __shared__ __attribute__((aligned(16))) float rows[4][2][SG_LDS_ROWS];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  float* la = rows[wave][0];
-  float* ld = rows[wave][1];
-#if SG_PAIR
-  // wave w takes tasks 2w and 2w + 1 (consecutive cycles of one epoch, as a rule)
-  const int64_t t0 = ((int64_t)blockIdx.x * 4 + wave) * 2;
-  if (t0 >= ntasks) return;
-  const SgWTask P = tasks[t0];
-  const bool has_q = t0 + 1 < ntasks;
-  const SgWTask Q = tasks[has_q ? t0 + 1 : t0];
-  const bool okp = P.R <= SG_ROWS_F32, okq = has_q && Q.R <= SG_ROWS_F32;  // others: sg_sine_bank_tall
-  // a short task ALWAYS runs the pair arithmetic (with itself as the partner when
-  // its neighbour is not short), so its bytes never depend on the batch around it
-  const bool ep = okp && P.len <= 64 && !(P.flags & SG_TASK_ENV);
-  const bool eq = okq && Q.len <= 64 && !(Q.flags & SG_TASK_ENV);
-  if (ep || eq) {
-    const SgWTask& X = ep ? P : Q;
-    const SgWTask& Y = eq ? Q : X;
-    float mx, my;
-    if ((X.flags & Y.flags) & SG_TASK_CONST) run_pair<false>(X, Y, la, ld, amps, W, lane, mx, my);
-    else run_pair<true>(X, Y, la, ld, amps, W, lane, mx, my);
-    mx = wave_max(mx);
-    my = wave_max(my);
-    if (lane == 0) {
-      if (ep) taskmax[t0] = mx;
-      if (eq) taskmax[t0 + 1] = my;
-    }
+  const int64_t k = (int64_t)blockIdx.x * 4 + wave;
+  if (k >= n) return;
+  const int64_t ti = idx[k];
+  const SgWTask T = tasks[ti];
+  const float wm = wave_max(run_one(T, rows[wave][0], rows[wave][1], amps, syls, cknots, W, lane));
+  if (lane == 0) taskmax[ti] = wm;
+}
+
+// Short fp32 tasks (<= 64 samples, no envelope; listed in idx), two per wave in
+// the halves of packed pairs (run_pair). The arithmetic of a task does not
+// depend on its partner (the last odd one pairs with itself).
+extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_pairs(
+    const int32_t* __restrict__ idx, int64_t n, const SgWTask* __restrict__ tasks, const float* __restrict__ amps,
+    float* __restrict__ W, float* __restrict__ taskmax) {
+  __shared__ __attribute__((aligned(16))) float rows[4][2][SG_LDS_ROWS];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t k = ((int64_t)blockIdx.x * 4 + wave) * 2;
+  if (k >= n) return;
+  const int64_t tp = idx[k];
+  const bool has_q = k + 1 < n;
+  const int64_t tq = has_q ? idx[k + 1] : tp;
+  const SgWTask P = tasks[tp];
+  const SgWTask Q = tasks[tq];
+  float mp, mq;
+  if ((P.flags & Q.flags) & SG_TASK_CONST) run_pair<false>(P, Q, rows[wave][0], rows[wave][1], amps, W, lane, mp, mq);
+  else run_pair<true>(P, Q, rows[wave][0], rows[wave][1], amps, W, lane, mp, mq);
+  mp = wave_max(mp);
+  mq = wave_max(mq);
+  if (lane == 0) {
+    taskmax[tp] = mp;
+    if (has_q) taskmax[tq] = mq;
   }
-  if (okp && !ep) {
-    const float wm = wave_max(run_one(P, la, ld, amps, syls, cknots, W, lane));
-    if (lane == 0) taskmax[t0] = wm;
-  }
-  if (okq && !eq) {
-    const float wm = wave_max(run_one(Q, la, ld, amps, syls, cknots, W, lane));
-    if (lane == 0) taskmax[t0 + 1] = wm;
-  }
-#else
-#if SG_SINE_PERSIST
-  // persistent waves: wave w of the grid takes tasks w, w + 4 gridDim.x, ...
-  const int64_t stride = (int64_t)gridDim.x * 4;
-#pragma unroll 1
-  for (int64_t ti = (int64_t)blockIdx.x * 4 + wave; ti < ntasks; ti += stride) {
-#else
-  const int64_t tbase = (int64_t)blockIdx.x * SG_TASKS_PER_BLOCK;
-#pragma unroll 1
-  for (int q = wave; q < SG_TASKS_PER_BLOCK; q += 4) {
-    const int64_t ti = tbase + q;
-    if (ti >= ntasks) break;
-#endif
-    const SgWTask T = tasks[ti];
-    if (T.R > SG_ROWS_F32) continue;  // sg_sine_bank_tall
-    const float wm = wave_max(run_one(T, la, ld, amps, syls, cknots, W, lane));
-    if (lane == 0) taskmax[ti] = wm;
-  }
-#endif
 }
 
 // ---------------------------------------------- tall tasks, fp32 Reinsch
@@ -579,9 +554,6 @@ __device__ __forceinline__ float run_task_rs(const SgWTask& T, float* __restrict
   return tmax;
 }
 
-#ifndef SG_TALL_PAIR
-#define SG_TALL_PAIR 1  // build knob: two short tall tasks per wave, fp32 Reinsch in packed halves
-#endif
 // Two tall tasks of <= 64 samples in one wave (as run_pair: task P in the low,
 // Q in the high half of packed pairs), Reinsch chains, rows staged interleaved
 // in 128-row chunks from the top.
@@ -665,6 +637,8 @@ __device__ __forceinline__ float run_one_tall(const SgWTask& T, float* __restric
 
 // The tasks with more than SG_ROWS_F32 rows (listed in idx), one task per wave:
 // fp32 Reinsch chains (SG_TALL_F32), else fp64 sincospi and fp64 Clenshaw chains.
+// Tall tasks (listed in idx): SG_TALL_PAIR lists the short ones (<= 64 samples, no
+// envelope) separately for sg_sine_bank_tall_pairs; these run one per wave.
 extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_tall(
     const int32_t* __restrict__ idx, int64_t n, const SgWTask* __restrict__ tasks, const float* __restrict__ amps,
     const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, float* __restrict__ W,
@@ -672,9 +646,22 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_tall(
   __shared__ __attribute__((aligned(16))) float rows[4][2][SG_LDS_ROWS];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  float* la = rows[wave][0];
-  float* ld = rows[wave][1];
-#if SG_TALL_PAIR
+  const int64_t k = (int64_t)blockIdx.x * 4 + wave;
+  if (k >= n) return;
+  const int64_t ti = idx[k];
+  const SgWTask T = tasks[ti];
+  const float wm = wave_max(run_one_tall(T, rows[wave][0], rows[wave][1], amps, syls, cknots, W, lane));
+  if (lane == 0) taskmax[ti] = wm;
+}
+
+// Short tall tasks, two per wave, fp32 Reinsch (run_pair_rs); a task's arithmetic
+// does not depend on its partner.
+extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_tall_pairs(
+    const int32_t* __restrict__ idx, int64_t n, const SgWTask* __restrict__ tasks, const float* __restrict__ amps,
+    float* __restrict__ W, float* __restrict__ taskmax) {
+  __shared__ __attribute__((aligned(16))) float rows[4][2][SG_LDS_ROWS];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t k = ((int64_t)blockIdx.x * 4 + wave) * 2;
   if (k >= n) return;
   const int64_t tp = idx[k];
@@ -682,38 +669,15 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_tall(
   const int64_t tq = has_q ? idx[k + 1] : tp;
   const SgWTask P = tasks[tp];
   const SgWTask Q = tasks[tq];
-  // short tasks always take the pair arithmetic (see sg_sine_bank)
-  const bool ep = P.len <= 64 && !(P.flags & SG_TASK_ENV);
-  const bool eq = has_q && Q.len <= 64 && !(Q.flags & SG_TASK_ENV);
-  if (ep || eq) {
-    const SgWTask& X = ep ? P : Q;
-    const SgWTask& Y = eq ? Q : X;
-    float mx, my;
-    if ((X.flags & Y.flags) & SG_TASK_CONST) run_pair_rs<false>(X, Y, la, ld, amps, W, lane, mx, my);
-    else run_pair_rs<true>(X, Y, la, ld, amps, W, lane, mx, my);
-    mx = wave_max(mx);
-    my = wave_max(my);
-    if (lane == 0) {
-      if (ep) taskmax[tp] = mx;
-      if (eq) taskmax[tq] = my;
-    }
+  float mp, mq;
+  if ((P.flags & Q.flags) & SG_TASK_CONST) run_pair_rs<false>(P, Q, rows[wave][0], rows[wave][1], amps, W, lane, mp, mq);
+  else run_pair_rs<true>(P, Q, rows[wave][0], rows[wave][1], amps, W, lane, mp, mq);
+  mp = wave_max(mp);
+  mq = wave_max(mq);
+  if (lane == 0) {
+    taskmax[tp] = mp;
+    if (has_q) taskmax[tq] = mq;
   }
-  if (!ep) {
-    const float wm = wave_max(run_one_tall(P, la, ld, amps, syls, cknots, W, lane));
-    if (lane == 0) taskmax[tp] = wm;
-  }
-  if (has_q && !eq) {
-    const float wm = wave_max(run_one_tall(Q, la, ld, amps, syls, cknots, W, lane));
-    if (lane == 0) taskmax[tq] = wm;
-  }
-#else
-  const int64_t k = (int64_t)blockIdx.x * 4 + wave;
-  if (k >= n) return;
-  const int64_t ti = idx[k];
-  const SgWTask T = tasks[ti];
-  const float wm = wave_max(run_one_tall(T, la, ld, amps, syls, cknots, W, lane));
-  if (lane == 0) taskmax[ti] = wm;
-#endif
 }
 
 // per-syllable max over its task slots and crossfade-piece slots
@@ -1048,24 +1012,29 @@ namespace sg {
     if (_e != hipSuccess) throw SgError(SG_E_DEVICE, std::string("launch " name ": ") + hipGetErrorString(_e)); \
   } while (0)
 
-void launch_sine_bank(const DevicePlan& D, int64_t t0, int64_t n_tasks, hipStream_t s) {
-  if (n_tasks <= 0) return;
-#if SG_SINE_PERSIST
-  int dev = 0, ncu = 256;
-  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  const int64_t blocks = std::min<int64_t>((n_tasks + 3) / 4, (int64_t)ncu * SG_SINE_PERSIST);
-#else
-  const int64_t blocks = SG_PAIR ? (n_tasks + 7) / 8 : (n_tasks + SG_TASKS_PER_BLOCK - 1) / SG_TASKS_PER_BLOCK;
-#endif
-  hipLaunchKernelGGL(sg_sine_bank, dim3((unsigned)blocks), dim3(256), 0, s, D.tasks + t0, n_tasks, D.amps, D.syls,
-                     D.cknots, D.W, D.taskmax + t0);
+void launch_sine_bank(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(sg_sine_bank, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, D.tlong + k0, n, D.tasks, D.amps,
+                     D.syls, D.cknots, D.W, D.taskmax);
   SG_LAUNCHED("sg_sine_bank");
+}
+void launch_sine_bank_pairs(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(sg_sine_bank_pairs, dim3((unsigned)((n + 7) / 8)), dim3(256), 0, s, D.tshort + k0, n, D.tasks,
+                     D.amps, D.W, D.taskmax);
+  SG_LAUNCHED("sg_sine_bank_pairs");
 }
 void launch_sine_bank_tall(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(sg_sine_bank_tall, dim3((unsigned)(SG_TALL_PAIR ? (n + 7) / 8 : (n + 3) / 4)), dim3(256), 0, s, D.tall + k0, n, D.tasks,
+  hipLaunchKernelGGL(sg_sine_bank_tall, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, D.tall + k0, n, D.tasks,
                      D.amps, D.syls, D.cknots, D.W, D.taskmax);
   SG_LAUNCHED("sg_sine_bank_tall");
+}
+void launch_sine_bank_tall_pairs(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(sg_sine_bank_tall_pairs, dim3((unsigned)((n + 7) / 8)), dim3(256), 0, s, D.tallp + k0, n,
+                     D.tasks, D.amps, D.W, D.taskmax);
+  SG_LAUNCHED("sg_sine_bank_tall_pairs");
 }
 void launch_piece_max(const DevicePlan& D, int64_t p0, int64_t n_ptiles, hipStream_t s) {
   if (n_ptiles <= 0) return;
