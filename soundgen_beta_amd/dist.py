@@ -11,6 +11,7 @@ link to rank 0, so the transfers do not serialise on a ring).
 Assignment is LPT (longest processing time first) over an analytic cost per
 call, identical on every rank (no communication needed to agree on it).
 """
+import os
 import math
 
 import numpy as np
@@ -132,11 +133,14 @@ def gather_to_root(outputs, owner, rank, world, device="cpu", root=0):
     return result
 
 
-def synthesize_sharded(calls, rank, world, device=0, synth=None, root=0, comm_device=None):
+def synthesize_sharded(calls, rank, world, device=None, synth=None, root=0, comm_device=None):
     """Every rank synthesizes its LPT shard (on its GPU) and the root gathers
     the batch in call order. `synth` (default batch.synthesize) maps a list of
-    calls to a list of outputs; `comm_device` is where the exchange tensors
-    live ("cpu" for gloo, "cuda:<local>" for RCCL)."""
+    calls to a list of outputs; `device` defaults to the rank's LOCAL_RANK GPU;
+    `comm_device` is where the exchange tensors live ("cpu" for gloo,
+    "cuda:<local>" for RCCL)."""
+    if device is None:
+        device = int(os.environ.get("LOCAL_RANK", "0"))
     if synth is None:
         from . import batch
 
