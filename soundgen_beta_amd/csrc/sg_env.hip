@@ -32,69 +32,102 @@ __device__ __forceinline__ double bcast(double v, int lane) {
   return __hiloint2double(hi, lo);
 }
 
+#ifndef SG_ENV_LG_LDS
+#define SG_ENV_LG_LDS 2048  // build knob: log2(k) table entries staged in LDS per workgroup (0: read from HBM)
+#endif
+
+// One column of a job: per 64-bin chunk, the tracks whose bands reach it (ballot),
+// their parameters by scalar loads; LG: log2(k) from the LDS copy.
+template <bool LG>
+__device__ __forceinline__ void env_column(const SgEnvJob& J, int c, const SgEnvTerm* __restrict__ tm,
+                                           const SgEnvCol& C, const double* __restrict__ lg2, const double* lgs,
+                                           float* __restrict__ fe, int lane) {
+  const float thrf = -SG_ENV_CUT;  // log2 units
+  // lane t: term t (group 0) and term 64 + t (group 1); absent terms get an empty range
+  double A[2], Rr[2], Lm[2];
+  float amp[2];
+  int klo[2], khi[2];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int t = g * 64 + lane;
+    const bool in = t < J.ntr;
+    const SgEnvTerm& e = tm[in ? t : 0];
+    if (!SG_ENV_SMEM) {
+      A[g] = e.A; Rr[g] = e.Rr; Lm[g] = e.Lm;
+    }
+    amp[g] = (float)e.amp;
+    klo[g] = in ? e.klo : 1 << 30;
+    khi[g] = in ? e.khi : -1;
+  }
+  float* __restrict__ dst = fe + J.out + (int64_t)c * J.nr;
+#pragma unroll 1
+  for (int k0 = 0; k0 < J.nr; k0 += 64) {
+    const int k = k0 + lane;
+    const double x = (double)(k + 1);
+    const double lx = LG ? lgs[k] : lg2[k];
+    float acc = 0.f;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      uint64_t m = __ballot(klo[g] <= k0 + 64 && khi[g] >= k0 + 1);
+      while (m) {
+        const int t = __builtin_ctzll(m);
+        m &= m - 1;
+#if SG_ENV_SMEM
+        const SgEnvTerm* __restrict__ e = tm + g * 64 + t;  // wave-uniform: scalar loads into SGPRs
+        const double a = e->A, r = e->Rr, l = e->Lm;
+#else
+        const double a = bcast(A[g], t), r = bcast(Rr[g], t), l = bcast(Lm[g], t);
+#endif
+        const float am = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amp[g]), t));
+        const double d = fma(a, lx, fma(-r, x, -l));
+        // d > thr >= -126: the raw v_exp_f32 is exact enough and never denormal
+        const float df = (float)d;
+        if (df > thrf) acc = fmaf(am, __builtin_amdgcn_exp2f(df), acc);
+      }
+    }
+    const float lxf = (float)lx;
+    const float v = fmaf(fmaf(C.lip, lxf, acc), C.boost, J.slope * lxf);
+    if (k < J.nr) dst[k] = exp2f(v * 0.1f);
+  }
+}
+
 extern "C" __global__ __launch_bounds__(256) void sg_spec_env(const SgEnvTask* __restrict__ tasks, int64_t ntask,
                                                               const SgEnvJob* __restrict__ jobs,
                                                               const SgEnvTerm* __restrict__ terms,
                                                               const SgEnvCol* __restrict__ cols,
-                                                              const double* __restrict__ lg2,
+                                                              const double* __restrict__ lg2, int64_t nlg,
                                                               float* __restrict__ fe) {
   const int64_t w = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (w >= ntask) return;
   const int lane = threadIdx.x & 63;
-  const SgEnvTask T = tasks[w];
+  const SgEnvTask T = tasks[w < ntask ? w : ntask - 1];
   const SgEnvJob J = jobs[T.job];
+#if SG_ENV_LG_LDS
+  // the log2(k) table is common to every job: one LDS copy per workgroup, as far
+  // as the workgroup's longest column reaches (whole 64-bin chunks)
+  __shared__ double lgs[SG_ENV_LG_LDS];
+  __shared__ int nrw[4];
+  if (lane == 0) nrw[threadIdx.x >> 6] = (J.nr + 63) / 64 * 64;
+  __syncthreads();
+  int need = nrw[0] > nrw[1] ? nrw[0] : nrw[1];
+  need = need > nrw[2] ? need : nrw[2];
+  need = need > nrw[3] ? need : nrw[3];
+  const int cap = nlg < SG_ENV_LG_LDS ? (int)nlg : SG_ENV_LG_LDS;
+  const int nst = need < cap ? need : cap;
+  for (int i = threadIdx.x; i < nst; i += 256) lgs[i] = lg2[i];
+  __syncthreads();
+#else
+  const double* lgs = nullptr;
+  const int nst = 0;
+#endif
+  if (w >= ntask) return;
   const int c1 = T.c0 + SG_ENV_COLS < J.nc ? T.c0 + SG_ENV_COLS : J.nc;
-  const float thrf = -SG_ENV_CUT;  // log2 units
+  const bool lds = (J.nr + 63) / 64 * 64 <= nst;  // every chunk's k inside the staged table
 #pragma unroll 1
   for (int c = T.c0; c < c1; ++c) {
     const SgEnvTerm* __restrict__ tm = terms + J.term0 + (int64_t)c * J.ntr;
-    // lane t: term t (group 0) and term 64 + t (group 1); absent terms get an empty range
-    double A[2], Rr[2], Lm[2];
-    float amp[2];
-    int klo[2], khi[2];
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      const int t = g * 64 + lane;
-      const bool in = t < J.ntr;
-      const SgEnvTerm& e = tm[in ? t : 0];
-      if (!SG_ENV_SMEM) {
-        A[g] = e.A; Rr[g] = e.Rr; Lm[g] = e.Lm;
-      }
-      amp[g] = (float)e.amp;
-      klo[g] = in ? e.klo : 1 << 30;
-      khi[g] = in ? e.khi : -1;
-    }
     const SgEnvCol C = cols[J.col0 + c];
-    float* __restrict__ dst = fe + J.out + (int64_t)c * J.nr;
-#pragma unroll 1
-    for (int k0 = 0; k0 < J.nr; k0 += 64) {
-      const int k = k0 + lane;
-      const double x = (double)(k + 1);
-      const double lx = lg2[k];
-      float acc = 0.f;
-#pragma unroll
-      for (int g = 0; g < 2; ++g) {
-        uint64_t m = __ballot(klo[g] <= k0 + 64 && khi[g] >= k0 + 1);
-        while (m) {
-          const int t = __builtin_ctzll(m);
-          m &= m - 1;
-#if SG_ENV_SMEM
-          const SgEnvTerm* __restrict__ e = tm + g * 64 + t;  // wave-uniform: scalar loads into SGPRs
-          const double a = e->A, r = e->Rr, l = e->Lm;
-#else
-          const double a = bcast(A[g], t), r = bcast(Rr[g], t), l = bcast(Lm[g], t);
-#endif
-          const float am = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amp[g]), t));
-          const double d = fma(a, lx, fma(-r, x, -l));
-          // d > thr >= -126: the raw v_exp_f32 is exact enough and never denormal
-          const float df = (float)d;
-          if (df > thrf) acc = fmaf(am, __builtin_amdgcn_exp2f(df), acc);
-        }
-      }
-      const float lxf = (float)lx;
-      const float v = fmaf(fmaf(C.lip, lxf, acc), C.boost, J.slope * lxf);
-      if (k < J.nr) dst[k] = exp2f(v * 0.1f);
-    }
+    if (lds) env_column<true>(J, c, tm, C, lg2, lgs, fe, lane);
+    else env_column<false>(J, c, tm, C, lg2, lgs, fe, lane);
   }
 }
 
@@ -105,7 +138,7 @@ void launch_spec_env(const DevicePlan& D, const Batch& B, hipStream_t s) {
   const int64_t n = (int64_t)B.envtasks.size();
   if (n <= 0) return;
   hipLaunchKernelGGL(sg_spec_env, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, D.envtasks, n, D.envjobs, D.eterms,
-                     D.ecols, D.elog2, D.fl + B.fe_base);
+                     D.ecols, D.elog2, (int64_t)B.elog2.size(), D.fl + B.fe_base);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw SgError(SG_E_DEVICE, std::string("launch sg_spec_env: ") + hipGetErrorString(e));
 }

@@ -12,7 +12,7 @@ if [ -n "$PYTEST_K" ]; then
   tail -2 gpurun_out/pytest_$TAG.log
 fi
 for v in default ${VARIANTS}; do
-  unset SG_OVERLAP
+  export SG_OVERLAP=${ABK_OVERLAP:-1}
   case "$v" in
     default) unset SG_HIP_LIB ;;
     nooverlap) unset SG_HIP_LIB; export SG_OVERLAP=0 ;;
