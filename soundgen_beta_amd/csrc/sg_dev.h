@@ -227,6 +227,13 @@ constexpr int SG_WAVE_STATE = 24;  // complex butterfly points a lane holds per 
 #define SG_FFT_WAVES_N 8  // build knob
 #endif
 constexpr int SG_FFT_WAVES = SG_FFT_WAVES_N;    // wavefronts (segments) per sg_stft_ola workgroup: one workgroup per CU
+#ifndef SG_FFT_WAVES_NOISE_N
+#define SG_FFT_WAVES_NOISE_N 12  // build knob
+#endif
+// sg_stft_ola_noise (no forward FFT: its specialised path fits 168 VGPRs, 3 waves per
+// SIMD, and (12 + 4) M pairs of LDS fit 160 KB for every M <= 64 SG_PF_SRC)
+constexpr int SG_FFT_WAVES_NOISE = SG_FFT_WAVES_NOISE_N;
+constexpr int sg_fft_waves(int phase) { return phase == 0 ? SG_FFT_WAVES_NOISE : SG_FFT_WAVES; }
 constexpr int SG_PF_SRC = 20;      // sg_stft_ola register prefetch: sound pairs per lane (M <= 1280)
 constexpr int SG_PF_PAIR = 10;     // bin pairs per lane (M / 2 + 1 <= 640)
 
@@ -276,6 +283,7 @@ constexpr int SG_SEG_LAST = 2;
 constexpr int SG_SEG_FRAMES = 48;   // target frames owned per segment (one wavefront each)
 constexpr int SG_SEG_MIN_FRAMES = 8;  // shortest segment the planner picks (3 recomputed frames each)
 constexpr int64_t SG_RESIDENT_WAVES = 256 * SG_FFT_WAVES;  // sg_stft_ola waves resident on a 256-CU MI355X
+constexpr int64_t sg_resident_waves(int phase) { return 256 * (int64_t)sg_fft_waves(phase); }
 constexpr int SG_CARRY_PAIRS = 16;  // sg_stft_ola carry registers: wl - floor(hop) <= 128 * 16 samples
 struct SgOlaTile {
   int32_t ola, pad;

@@ -22,6 +22,9 @@
 #ifndef SG_FFT_WPE
 #define SG_FFT_WPE 2  // build knob: waves per SIMD for sg_stft_ola
 #endif
+#ifndef SG_FFT_WPE_NOISE
+#define SG_FFT_WPE_NOISE (SG_FFT_WAVES_NOISE_N > 8 ? 3 : 2)  // waves per SIMD for sg_stft_ola_noise
+#endif
 #ifndef SG_PF_AHEAD
 #define SG_PF_AHEAD 0  // build knob: issue the next frame's input loads before this frame's inverse FFT
 #endif
@@ -917,7 +920,7 @@ __device__ __forceinline__ void stft_ola_body(
     const SgSegment* __restrict__ segs, const SgOla* __restrict__ olas, const SgFrame* __restrict__ frames,
     const SgFftGeom* __restrict__ geoms, const float* __restrict__ fl, float* __restrict__ fs,
     float* __restrict__ slotmax) {
-  constexpr int W = SG_FFT_WAVES, NT = W * 64;
+  constexpr int W = MODE == SG_FRAME_NOISE ? SG_FFT_WAVES_NOISE : SG_FFT_WAVES, NT = W * 64;
   extern __shared__ float4 lds4[];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // w wave-uniform
   const SgFftGeom& g = geoms[segs[blockIdx.x * W].geom];  // the planner groups segments by geometry
@@ -958,7 +961,7 @@ extern "C" __global__ __launch_bounds__(SG_FFT_WAVES * 64) __attribute__((amdgpu
   stft_ola_body<SG_FRAME_FILTER>(segs, olas, frames, geoms, fl, fs, slotmax);
 }
 // generateNoise()'s istft (phase 0): the noise mode only
-extern "C" __global__ __launch_bounds__(SG_FFT_WAVES * 64) __attribute__((amdgpu_waves_per_eu(SG_FFT_WPE))) void sg_stft_ola_noise(
+extern "C" __global__ __launch_bounds__(SG_FFT_WAVES_NOISE * 64) __attribute__((amdgpu_waves_per_eu(SG_FFT_WPE_NOISE))) void sg_stft_ola_noise(
     const SgSegment* __restrict__ segs, const SgOla* __restrict__ olas, const SgFrame* __restrict__ frames,
     const SgFftGeom* __restrict__ geoms, const float* __restrict__ fl, float* __restrict__ fs,
     float* __restrict__ slotmax) {
@@ -1217,7 +1220,9 @@ void launch_stft_ola(const DevicePlan& D, int phase, int64_t s0, int64_t n_segs,
   if (n_segs <= 0) return;
   auto* k = phase == 0 ? &sg_stft_ola_noise : &sg_stft_ola;
   lds_opt_in(reinterpret_cast<const void*>(k), lds_bytes, phase == 0 ? "sg_stft_ola_noise" : "sg_stft_ola");
-  hipLaunchKernelGGL(k, dim3((unsigned)(n_segs / SG_FFT_WAVES)), dim3(SG_FFT_WAVES * 64), lds_bytes, s,
+  const int W = sg_fft_waves(phase);
+  if (n_segs % W) throw SgError(SG_E_DEVICE, "sg_stft_ola: segment count not a multiple of the workgroup's waves");
+  hipLaunchKernelGGL(k, dim3((unsigned)(n_segs / W)), dim3(W * 64), lds_bytes, s,
                      D.olasegs + s0,
                      D.olas, D.frames, D.geoms, D.fl, D.fs, D.olatilemax);
   SG_LAUNCHED("sg_stft_ola");

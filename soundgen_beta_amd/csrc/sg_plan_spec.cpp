@@ -676,7 +676,7 @@ void finalize_spec(Batch& B) {
       const int gi = fg[i];
       const SgFftGeom& g = B.geoms[gi];
       if (g.kind == SG_FFT_WAVE) {  // transformed inside sg_stft_ola
-        B.fgroup_lds[ph][0] = std::max(B.fgroup_lds[ph][0], g.lds_bytes);
+        B.fgroup_lds[ph][0] = std::max(B.fgroup_lds[ph][0], (sg_fft_waves(ph) + 4) * g.M * 8);
         ++i;
         continue;
       }
@@ -718,7 +718,8 @@ void finalize_spec(Batch& B) {
     B.seg_range[ph][0] = (int64_t)B.olasegs.size();
     const size_t o_lo = ph == 0 ? 0 : (size_t)B.ola_split, o_hi = ph == 0 ? (size_t)B.ola_split : B.olas_dev.size();
     const int32_t fbase = ph == 0 ? 0 : (int32_t)B.frames[0].size();
-    // fused OLAs of the phase ordered by geometry; a workgroup's SG_FFT_WAVES
+    const int WPH = sg_fft_waves(ph);
+    // fused OLAs of the phase ordered by geometry; a workgroup's WPH (sg_fft_waves)
     // segments share one geometry (padding segments have nf = 0)
     std::vector<size_t> order;
     for (size_t oi = o_lo; oi < o_hi; ++oi)
@@ -727,7 +728,7 @@ void finalize_spec(Batch& B) {
     std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return geom_of(a) < geom_of(b); });
     // Segment length: SG_SEG_FRAMES frames would leave a partial last round of
     // workgroups (one per CU), so pick the length that packs the segments into
-    // whole rounds of SG_RESIDENT_WAVES (the fewest rounds SG_SEG_FRAMES needs).
+    // whole rounds of sg_resident_waves(ph) (the fewest rounds SG_SEG_FRAMES needs).
     int64_t seg_frames = SG_SEG_FRAMES;
     {
       auto segs_at = [&](int64_t S) {
@@ -736,7 +737,7 @@ void finalize_spec(Batch& B) {
         for (size_t oi : order) {
           const int g = geom_of(oi);
           if (g != prev) {
-            tot += (SG_FFT_WAVES - run % SG_FFT_WAVES) % SG_FFT_WAVES;  // padding of the previous geometry
+            tot += (WPH - run % WPH) % WPH;  // padding of the previous geometry
             run = 0;
             prev = g;
           }
@@ -744,17 +745,17 @@ void finalize_spec(Batch& B) {
           tot += k;
           run += k;
         }
-        return tot + (SG_FFT_WAVES - run % SG_FFT_WAVES) % SG_FFT_WAVES;
+        return tot + (WPH - run % WPH) % WPH;
       };
       const int64_t base = segs_at(SG_SEG_FRAMES);
-      const int64_t rounds = (base + SG_RESIDENT_WAVES - 1) / SG_RESIDENT_WAVES;
+      const int64_t rounds = (base + sg_resident_waves(ph) - 1) / sg_resident_waves(ph);
       int64_t S = SG_SEG_MIN_FRAMES;
-      while (S < SG_SEG_FRAMES && segs_at(S) > rounds * SG_RESIDENT_WAVES) S = std::max(S + 1, S * 9 / 8);
+      while (S < SG_SEG_FRAMES && segs_at(S) > rounds * sg_resident_waves(ph)) S = std::max(S + 1, S * 9 / 8);
       seg_frames = std::min<int64_t>(S, SG_SEG_FRAMES);
     }
     int cur_geom = -1;
     auto pad = [&]() {
-      while (B.olasegs.size() % SG_FFT_WAVES) {
+      while (((int64_t)B.olasegs.size() - B.seg_range[ph][0]) % WPH) {
         SgSegment d{};
         d.geom = cur_geom;
         B.olasegs.push_back(d);
