@@ -194,6 +194,14 @@ int sg_plan_release_host(sg_plan* plan);
  * writing fp32 samples into device buffer d_out (packed, offsets as above).
  * No host synchronisation inside; graph-capturable. */
 int sg_execute(sg_ctx* ctx, sg_plan* plan, float* d_out, void* stream);
+/* Several uploaded plans executed as ONE batch on `stream` (the outputs of
+ * plan i go to d_outs[i], exactly as sg_execute(plans[i], d_outs[i]) would
+ * write them): the harmonic chains of all plans run back to back on the
+ * context's second stream, overlapping the spectral phases of the earlier
+ * plans; everything is ordered after prior work on `stream` and joined back
+ * to it. A plan may appear once. Replaces a loop of sg_execute over the 16k-call
+ * chunks of one soundgen() batch (R/soundgen.R:208-862 per call). */
+int sg_execute_plans(sg_ctx* ctx, sg_plan* const* plans, float* const* d_outs, int n, void* stream);
 /* Profiling: when enabled, sg_execute brackets every sine-bank launch (one
  * per batch slice) and every sg_stft_ola launch with HIP events on the launch
  * stream; sg_profile_read

@@ -99,6 +99,19 @@ class Plan:
             pass
 
 
+def execute_plans(ctx, plans, d_out_ptrs, stream_ptr=None):
+    """Run several uploaded plans as one batch (sg_execute_plans): plan i writes
+    its calls to device pointer d_out_ptrs[i]; the harmonic chains of later plans
+    overlap the spectral phases of earlier ones on the context's second stream."""
+    n = len(plans)
+    if n == 0:
+        return
+    P = (C.c_void_p * n)(*[p.ptr for p in plans])
+    O = (C.c_void_p * n)(*[C.c_void_p(o) for o in d_out_ptrs])
+    native.check(native.lib().sg_execute_plans(ctx.ptr, P, O, n, C.c_void_p(stream_ptr) if stream_ptr else None),
+                 ctx.ptr)
+
+
 def synthesize_to_wav(calls, paths, sampling_rates, device=0):
     """soundgen(..., savePath = path) for a batch: synthesize on the GPU, convert
     every call to 16-bit PCM on the GPU (half the bytes cross PCIe), write one

@@ -462,6 +462,23 @@ int sg_execute(sg_ctx* ctx, sg_plan* plan, float* d_out, void* stream) {
   });
 }
 
+int sg_execute_plans(sg_ctx* ctx, sg_plan* const* plans, float* const* d_outs, int n, void* stream) {
+  return guarded(ctx, [&]() {
+    HIPCHK(hipSetDevice(ctx->device));
+    if (n < 0 || (n > 0 && (!plans || !d_outs))) throw sg::SgError(SG_E_ARG, "sg_execute_plans: bad plan list");
+    std::vector<sg::PlanRun> runs;
+    for (int i = 0; i < n; ++i) {
+      if (!plans[i] || !plans[i]->D.uploaded) throw sg::SgError(SG_E_ARG, "sg_execute_plans: plan not uploaded");
+      for (int j = 0; j < i; ++j)
+        if (plans[j] == plans[i]) throw sg::SgError(SG_E_ARG, "sg_execute_plans: a plan listed twice");
+      runs.push_back(sg::PlanRun{&plans[i]->B, &plans[i]->D, d_outs[i]});
+    }
+    if (runs.empty()) return SG_OK;
+    sg::device_execute_many(runs, (hipStream_t)stream, ctx->aux, ctx->profiling ? &ctx->prof_events : nullptr);
+    return SG_OK;
+  });
+}
+
 int sg_set_profiling(sg_ctx* ctx, int on) {
   ctx->profiling = on != 0;
   return SG_OK;

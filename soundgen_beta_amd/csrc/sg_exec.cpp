@@ -307,31 +307,10 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   D.uploaded = true;
 }
 
-// The harmonic source (sine banks -> maxima -> finalize) and the noise phase
-// (envelopes -> noise STFT/OLA) read and write disjoint buffers, so they run
-// concurrently: the harmonic chain on s2, the noise phase on s; the pre-filter
-// mixes wait for both. SG_OVERLAP=0 runs everything on s (measurement knob).
-static bool overlap_on() {
-  static const bool on = [] {
-    const char* e = std::getenv("SG_OVERLAP");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-void device_execute(const Batch& B, DevicePlan& D, float* d_out, hipStream_t s, hipStream_t s2,
-                    std::vector<SgProfEvent>* prof) {
-  if (B.slices.empty()) {  // no harmonic syllables: spectral phases only
-    device_execute_spec(B, D, d_out, s, prof, false);
-    return;
-  }
-  // profiling (per-kernel events) serialises the two chains: each launch's time is its own
-  const bool ovl = overlap_on() && prof == nullptr && s2 != nullptr && s2 != s;
-  hipStream_t h = ovl ? s2 : s;  // the harmonic chain's stream
-  if (ovl) {  // fork: h starts after everything already queued on s
-    HIPCHK(hipEventRecord(D.ev_fork, s));
-    HIPCHK(hipStreamWaitEvent(h, D.ev_fork, 0));
-  }
+// the harmonic chain of one plan on stream h: sine banks (four task classes),
+// maxima, finalize
+static void device_execute_harm(const Batch& B, DevicePlan& D, float* d_out, hipStream_t h,
+                                std::vector<SgProfEvent>* prof) {
   for (size_t c = 0; c < B.slices.size(); ++c) {
     const Slice& sl = B.slices[c];
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -366,13 +345,52 @@ void device_execute(const Batch& B, DevicePlan& D, float* d_out, hipStream_t s, 
     launch_harm_copy(D, sl.c0, sl.c1 - sl.c0, d_out, h);
     launch_harm_finalize(D, sl.f0, sl.f1 - sl.f0, d_out, h);
   }
-  if (ovl) {
-    // the noise phase runs on s meanwhile; the pre-filter mixes join the harmonic chain
-    HIPCHK(hipEventRecord(D.ev_join, h));
-    device_execute_spec(B, D, d_out, s, prof, true, D.ev_join);
-  } else {
-    device_execute_spec(B, D, d_out, s, prof, false);
+}
+
+// The harmonic source (sine banks -> maxima -> finalize) and the noise phase
+// (envelopes -> noise STFT/OLA) read and write disjoint buffers, so they run
+// concurrently: the harmonic chain on s2, the noise phase on s; the pre-filter
+// mixes wait for both. SG_OVERLAP=0 runs everything on s (measurement knob).
+static bool overlap_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("SG_OVERLAP");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+void device_execute(const Batch& B, DevicePlan& D, float* d_out, hipStream_t s, hipStream_t s2,
+                    std::vector<SgProfEvent>* prof) {
+  std::vector<PlanRun> one{PlanRun{&B, &D, d_out}};
+  device_execute_many(one, s, s2, prof);
+}
+
+// Plans executed as one batch: one fork, every plan's harmonic chain queued on s2
+// back to back, and on s per plan: envelopes, noise phase, wait for that plan's
+// harmonic chain, pre-filter mixes, filter phase, final mixes. Plan p + 1's
+// harmonic chain thus overlaps plan p's filter phase as well as its own noise
+// phase. The plans own disjoint arenas and output slots. Profiling (per-kernel
+// events) serialises everything on s.
+void device_execute_many(const std::vector<PlanRun>& runs, hipStream_t s, hipStream_t s2,
+                         std::vector<SgProfEvent>* prof) {
+  const bool ovl = overlap_on() && prof == nullptr && s2 != nullptr && s2 != s;
+  if (!ovl) {
+    for (const PlanRun& r : runs) {
+      device_execute_harm(*r.B, *r.D, r.out, s, prof);
+      device_execute_spec(*r.B, *r.D, r.out, s, prof, false);
+    }
+    HIPCHK(hipGetLastError());
+    return;
   }
+  // fork: s2 starts after everything already queued on s
+  DevicePlan& D0 = *runs[0].D;
+  HIPCHK(hipEventRecord(D0.ev_fork, s));
+  HIPCHK(hipStreamWaitEvent(s2, D0.ev_fork, 0));
+  for (const PlanRun& r : runs) {
+    device_execute_harm(*r.B, *r.D, r.out, s2, nullptr);
+    HIPCHK(hipEventRecord(r.D->ev_join, s2));
+  }
+  for (const PlanRun& r : runs) device_execute_spec(*r.B, *r.D, r.out, s, nullptr, true, r.D->ev_join);
   HIPCHK(hipGetLastError());
 }
 

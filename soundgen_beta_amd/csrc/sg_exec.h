@@ -84,6 +84,13 @@ struct SgProfEvent {
 // (optional) receives one event pair per sine-bank and sg_stft_ola launch.
 void device_execute(const Batch& B, DevicePlan& D, float* d_out, hipStream_t s, hipStream_t s2,
                     std::vector<SgProfEvent>* prof);
+struct PlanRun {
+  const Batch* B;
+  DevicePlan* D;
+  float* out;
+};
+void device_execute_many(const std::vector<PlanRun>& runs, hipStream_t s, hipStream_t s2,
+                         std::vector<SgProfEvent>* prof);
 void device_execute_spec(const Batch& B, const DevicePlan& D, float* d_out, hipStream_t s,
                          std::vector<SgProfEvent>* prof, bool join = false, hipEvent_t harm_done = nullptr);
 

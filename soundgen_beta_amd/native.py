@@ -67,6 +67,7 @@ def lib():
     L.sg_plan_upload.argtypes = [vp, vp]
     L.sg_plan_release_host.argtypes = [vp]
     L.sg_execute.argtypes = [vp, vp, vp, vp]
+    L.sg_execute_plans.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), C.c_int, vp]
     L.sg_set_profiling.argtypes = [vp, C.c_int]
     L.sg_profile_read.argtypes = [vp, dp, i64p]
     L.sg_profile_read_kernel.argtypes = [vp, C.c_int, dp, i64p]

@@ -181,3 +181,36 @@ def test_sharded_batch_byte_equal():
         assert 0 < len(idx) < len(calls)
         for i, y in zip(idx, run(mine)):
             assert np.array_equal(y.view(np.uint32), whole[i].view(np.uint32)), (r, int(i))
+
+
+def test_execute_plans_equals_per_plan_execute():
+    """sg_execute_plans (several uploaded plans as one batch, the harmonic chains of
+    later plans overlapping the spectral phases of earlier ones on the context's
+    second stream) writes exactly the bytes of a loop of sg_execute; the overlap
+    knob (SG_OVERLAP, read once per process) does not enter the comparison."""
+    import os
+    import sys
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from soundgen_beta_amd import batch, native
+    calls = bench.c5_calls(96)
+    chunks = [calls[0:40], calls[40:41], calls[41:96]]
+    ctx = native.default_context(0)
+    plans = [batch.Plan(c, ctx) for c in chunks]
+    for p in plans:
+        assert (p.status == 0).all()
+        p.upload()
+    outs = [torch.zeros(max(p.total, 1), dtype=torch.float32, device="cuda") for p in plans]
+    ref = [torch.zeros_like(o) for o in outs]
+    sptr = torch.cuda.current_stream().cuda_stream
+    for p, o in zip(plans, ref):
+        p.execute(o.data_ptr(), sptr)
+    batch.execute_plans(ctx, plans, [o.data_ptr() for o in outs], sptr)
+    torch.cuda.synchronize()
+    for o, r in zip(outs, ref):
+        assert torch.equal(o.view(torch.int32), r.view(torch.int32))
+    with pytest.raises(native.SoundgenError):  # a plan listed twice is refused
+        batch.execute_plans(ctx, [plans[0], plans[0]], [outs[0].data_ptr()] * 2, sptr)
+    for p in plans:
+        p.close()

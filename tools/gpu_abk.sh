@@ -13,9 +13,11 @@ if [ -n "$PYTEST_K" ]; then
 fi
 for v in default ${VARIANTS}; do
   export SG_OVERLAP=${ABK_OVERLAP:-1}
+  unset SG_EXEC_EACH
   case "$v" in
     default) unset SG_HIP_LIB ;;
     nooverlap) unset SG_HIP_LIB; export SG_OVERLAP=0 ;;
+    each) unset SG_HIP_LIB; export SG_EXEC_EACH=1 ;;
     *) export SG_HIP_LIB=$R/soundgen_beta_amd/lib/exp_$v.so ;;
   esac
   cd /tmp
