@@ -815,7 +815,11 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_copy(const SgCopyTile*
 #ifndef SG_FIN_WAVE_TILE
 #define SG_FIN_WAVE_TILE 0  // build knob: one wave per 1024-sample tile (its 4 quarters in turn)
 #endif
-static_assert(!(SG_FIN_WAVE_TILE && SG_FIN_LDS_ENV == 1), "LDS envelope staging needs all waves on one tile");
+#ifndef SG_FIN_DIRECT
+#define SG_FIN_DIRECT 0  // build knob: whole-tile path for tiles inside one direct piece (16 samples per lane;
+                         // measured 5.93 -> 7.82 ms on C5: 108 VGPRs and per-sample fp64 drift division)
+#endif
+static_assert(!((SG_FIN_WAVE_TILE || SG_FIN_DIRECT) && SG_FIN_LDS_ENV == 1), "LDS envelope staging needs all waves on one tile");
 #ifndef SG_FIN_DRIFT_LDS
 #define SG_FIN_DRIFT_LDS 1  // build knob: drift interval by index from per-wave LDS (x, y, slope) rows
 #endif
@@ -973,6 +977,60 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
 #define SG_FIN_TILES_N 4  // build knob
 #endif
 constexpr int SG_FIN_TILES = SG_FIN_TILES_N;
+// A tile lying inside ONE direct piece (the epoch waveform itself, no crossfade
+// terms), taken by one wave: lane l loads samples k0 + 256 j + 4 l + e (j, e < 4),
+// all sixteen before any store (the general path keeps four per lane in flight
+// and is memory-latency-bound), then envelope, 1/max, fades and drift per
+// sample in the general path's order (drift by the cursor form of approx()).
+// Returns false (nothing written) when the tile is not of that kind.
+__device__ __forceinline__ bool finalize_tile_direct(const SgSylTile& tl, const SgPiece* __restrict__ pieces,
+                                                     const SgSyllable* __restrict__ syls,
+                                                     const double* __restrict__ cknots, const float* __restrict__ W,
+                                                     const float* __restrict__ maxes, float* __restrict__ out_buf,
+                                                     float* __restrict__ fs) {
+  const SgSyllable& sy = syls[tl.syl];
+  const int64_t tile_end = tl.k0 + 1024 < sy.L ? tl.k0 + 1024 : sy.L;
+  const int pu = tl.wpiece[0];
+  const int pend = sy.piece0 + sy.npiece;
+  const SgPiece& pc = pieces[pu];
+  if (pc.nterms >= 0 || pc.start > tl.k0 || (pu + 1 < pend && pieces[pu + 1].start < tile_end)) return false;
+  const int lane = threadIdx.x & 63;
+  const float* __restrict__ src = W + (pc.t[0].src - pc.start);  // sample k -> src[k]
+  float* __restrict__ out = (sy.dst_fs ? fs : out_buf) + sy.out_off;
+  float x[16];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t k = tl.k0 + 256 * j + 4 * lane + e;
+      x[4 * j + e] = src[k < tile_end ? k : tl.k0];
+    }
+  const float inv_max = 1.f / maxes[sy.max_slot];
+  const SgLinear dr = sy.drift;
+  int ecur = -1, di = tl.wdrift[0];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t k = tl.k0 + 256 * j + 4 * lane + e;
+      float v = x[4 * j + e];
+      if (sy.env.kind != 0) v = (float)((double)v * sgd::contour_at_cursor(sy.env, cknots, sy.L, k, ecur));
+      v *= inv_max;
+      if (sy.fade >= 2) v *= fade_at(sy.fade, sy.L, k);
+      if (dr.nk > 1) v = (float)((double)v * sgd::linear_at_cursor(dr, cknots, sy.L, k, di));
+      else if (dr.nk == 1) v = (float)((double)v * cknots[dr.k_off + 1]);
+      x[4 * j + e] = v;
+    }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t k = tl.k0 + 256 * j + 4 * lane + e;
+      if (k < tile_end) out[k] = x[4 * j + e];
+    }
+  return true;
+}
+
 extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize(
     const SgSylTile* __restrict__ stiles, int64_t ntiles, const SgPiece* __restrict__ pieces,
     const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, const float* __restrict__ W,
@@ -985,12 +1043,13 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize(
 #endif
   __shared__ double lk[4][3 * 8];  // per wave: drift intervals (x, y, slope)
   double* lkw = lk[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
-#if SG_FIN_WAVE_TILE
-  // wave w takes tile 4 b + w whole (its quarters in turn): one descriptor chain per 1024 samples
+#if SG_FIN_WAVE_TILE || SG_FIN_DIRECT
+  // wave w takes tile 4 b + w whole: the direct path, else its quarters in turn
   const int64_t t = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (t >= ntiles) return;
   const SgSylTile tl = stiles[t];
-#pragma unroll
+  if (SG_FIN_DIRECT && finalize_tile_direct(tl, pieces, syls, cknots, W, maxes, out_buf, fs)) return;
+#pragma unroll 1
   for (int q = 0; q < 4; ++q) finalize_tile(tl, pieces, syls, cknots, W, maxes, out_buf, fs, lenv, q, lkw);
 #else
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1056,7 +1115,7 @@ void launch_harm_copy(const DevicePlan& D, int64_t c0, int64_t n_ctiles, float* 
 }
 void launch_harm_finalize(const DevicePlan& D, int64_t f0, int64_t n_stiles, float* out, hipStream_t s) {
   if (n_stiles <= 0) return;
-  const int64_t per_block = SG_FIN_WAVE_TILE ? 4 : SG_FIN_TILES;
+  const int64_t per_block = (SG_FIN_WAVE_TILE || SG_FIN_DIRECT) ? 4 : SG_FIN_TILES;
   hipLaunchKernelGGL(sg_harm_finalize, dim3((unsigned)((n_stiles + per_block - 1) / per_block)), dim3(256), 0, s,
                      D.syl_tiles + f0, n_stiles, D.pieces, D.syls,
                      D.cknots, D.W, D.maxes, out, D.fs);
