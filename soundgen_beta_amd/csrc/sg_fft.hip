@@ -873,20 +873,35 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
     const bool lastf = k == S.nf - 1;
     const int bn = lastf ? S.pb : bstart(S.f0 + k + 1);
     const int D = bn - bf;  // samples [bf, bn) are final
-    for (int i = lane; i < D; i += 64) {
-      const int p = bf + i;
-      const int q = p - first;
-      if (p >= S.pa && q >= 0 && q < len) {
-        const float v = (i < Nk ? Af[i] : 0.f) * scale;
-        out[q] = v;
+    if (bf >= S.pa && bf - first >= 0 && bn - first <= len && D <= Nk) {
+      // interior frame (wave-uniform): every final sample is owned, inside the trim and the frame
+      float* __restrict__ o = out + (bf - first);
+      for (int i = lane; i < D; i += 64) {
+        const float v = Af[i] * scale;
+        o[i] = v;
         m = fmaxf(m, v);
+      }
+    } else {
+      for (int i = lane; i < D; i += 64) {
+        const int p = bf + i;
+        const int q = p - first;
+        if (p >= S.pa && q >= 0 && q < len) {
+          const float v = (i < Nk ? Af[i] : 0.f) * scale;
+          out[q] = v;
+          m = fmaxf(m, v);
+        }
       }
     }
     if (!lastf) {
+      const int tail = Nk - D;  // carried samples (pairs beyond it are zero)
 #pragma unroll
       for (int r = 0; r < SG_CARRY_PAIRS; ++r) {
-        const int i0 = 2 * (64 * r + lane) + D;
-        C[r] = make_float2(i0 < Nk ? Af[i0] : 0.f, i0 + 1 < Nk ? Af[i0 + 1] : 0.f);
+        if (128 * r < tail) {  // wave-uniform
+          const int i0 = 2 * (64 * r + lane) + D;
+          C[r] = make_float2(i0 < Nk ? Af[i0] : 0.f, i0 + 1 < Nk ? Af[i0 + 1] : 0.f);
+        } else {
+          C[r] = make_float2(0.f, 0.f);
+        }
       }
     }
     sg_wave_fence();  // the next frame overwrites the slice
