@@ -73,7 +73,8 @@ struct SgWTask {
   int32_t dj0, dj1;    // direct-copy window (fused max)
   int32_t syl;
   int32_t flags;
-  int32_t pad;
+  int32_t Rn;          // rows the recurrence runs: R without the trailing rows whose A and dA are
+                       // all zero (rounded up to 4; they add exact zeros); R keeps the class
 };
 static_assert(sizeof(SgWTask) == 128, "SgWTask layout");
 #ifndef SG_PAIR

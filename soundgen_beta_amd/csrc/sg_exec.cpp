@@ -147,6 +147,19 @@ void finalize_plan(Batch& B) {
     std::fprintf(stderr, "sg plan: sine tasks fp32 %lld (%lld samples, %.3g chain terms), tall %lld (%lld samples, %.3g chain terms, max R %lld; R<256 %lld, <512 %lld, <1024 %lld, <2048 %lld, more %lld)\n",
                  (long long)ntask[0], (long long)samples[0], terms[0], (long long)ntask[1], (long long)samples[1], terms[1],
                  (long long)rmax, (long long)rh[0], (long long)rh[1], (long long)rh[2], (long long)rh[3], (long long)rh[4]);
+    {  // rows above the last nonzero amplitude (A or dA) of each task
+      double rsum[2] = {0, 0}, reff[2] = {0, 0};
+      for (const SgWTask& t : B.tasks) {
+        const int k = t.R > SG_ROWS_F32 ? 1 : 0;
+        int last = 0;
+        for (int r = 0; r < t.R; ++r)
+          if (B.amps[t.a_off + r] != 0.f || (!(t.flags & SG_TASK_CONST) && B.amps[t.d_off + r] != 0.f)) last = r + 1;
+        rsum[k] += (double)t.R * t.len;
+        reff[k] += (double)((last + 3) / 4 * 4) * t.len;
+      }
+      std::fprintf(stderr, "sg plan: row work incl. trailing zero rows: fp32 %.3g -> %.3g, tall %.3g -> %.3g\n", rsum[0],
+                   reff[0], rsum[1], reff[1]);
+    }
     for (int k = 0; k < 2; ++k)
       std::fprintf(stderr, "sg plan: %s tasks <= 64 samples: %lld (%.3g chain terms); len <=64/128/256/512/more: %lld %lld %lld %lld %lld\n",
                    k ? "tall" : "fp32", (long long)nshort[k], sterms[k], (long long)lh[k][0], (long long)lh[k][1],

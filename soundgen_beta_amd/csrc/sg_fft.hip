@@ -1098,7 +1098,10 @@ extern "C" __global__ __launch_bounds__(256) void sg_mix(const SgMixTile* __rest
   const SgMixTile T = tiles[blockIdx.x];
   const SgMix& X = mixes[T.mix];
   float* __restrict__ dst = X.to_fs ? fs : out;
-  constexpr int E = 4;  // samples per thread and chunk
+#ifndef SG_MIX_E
+#define SG_MIX_E 8  // build knob: samples per thread and chunk (8: 2.94 -> 2.75 ms per C5 16k-call launch)
+#endif
+  constexpr int E = SG_MIX_E;  // samples per thread and chunk
   const int64_t kend = T.k0 + SG_MIX_TILE < X.len ? T.k0 + SG_MIX_TILE : X.len;
   // per-tile constants, hoisted out of the sample loops (one scalar-load burst)
   const float base_scale = X.base_kind == SG_BASE_NORM ? 1.f / olamax[X.base_ola] : 1.f;

@@ -203,10 +203,10 @@ __device__ __forceinline__ void run_slots(const SgWTask& T, bool staged, float* 
     }
   }
   if (staged) {
-    clenshaw_any<NS, TWO, Acc>(la, ld, T.R, al, b1, b2, e1, e2);
+    clenshaw_any<NS, TWO, Acc>(la, ld, T.Rn, al, b1, b2, e1, e2);
   } else {  // rare (subharmonic epochs with many rows): 256-row chunks, top first
-    for (int r0 = (T.R - 1) / SG_LDS_ROWS * SG_LDS_ROWS; r0 >= 0; r0 -= SG_LDS_ROWS) {
-      const int n = T.R - r0 < SG_LDS_ROWS ? T.R - r0 : SG_LDS_ROWS;
+    for (int r0 = (T.Rn - 1) / SG_LDS_ROWS * SG_LDS_ROWS; r0 >= 0; r0 -= SG_LDS_ROWS) {
+      const int n = T.Rn - r0 < SG_LDS_ROWS ? T.Rn - r0 : SG_LDS_ROWS;
       stage_rows<TWO>(la, ld, amps + T.a_off, amps + T.d_off, r0, n, lane);
       clenshaw_any<NS, TWO, Acc>(la, ld, n, al, b1, b2, e1, e2);
     }
@@ -231,8 +231,8 @@ template <bool TWO, bool ENV, bool LIN, typename Acc = float>
 __device__ __forceinline__ float run_task(const SgWTask& T, float* __restrict__ la, float* __restrict__ ld,
                                           const float* __restrict__ amps, const SgSyllable* __restrict__ syls,
                                           const double* __restrict__ cknots, float* __restrict__ W, int lane) {
-  const bool staged = T.R <= SG_LDS_ROWS;  // rows stay in LDS for every pass of the task
-  if (staged) stage_rows<TWO>(la, ld, amps + T.a_off, amps + T.d_off, 0, T.R, lane);
+  const bool staged = T.Rn <= SG_LDS_ROWS;  // rows stay in LDS for every pass of the task
+  if (staged) stage_rows<TWO>(la, ld, amps + T.a_off, amps + T.d_off, 0, T.Rn, lane);
   float tmax = 0.f;
   int l0 = 0;
   // passes of 8 / 4 / 2 / 1 slots of 64 samples (8-slot passes on the A chain
@@ -321,14 +321,14 @@ __device__ __forceinline__ void run_pair(const SgWTask& P, const SgWTask& Q, flo
 #ifdef SG_DIAG_NOROWS
   const int R = 0;
 #else
-  const int R = P.R > Q.R ? P.R : Q.R;  // multiples of 16
+  const int R = P.Rn > Q.Rn ? P.Rn : Q.Rn;  // multiples of 16
 #endif
   for (int r = lane; r < R; r += 64) {
-    *reinterpret_cast<float2*>(la + 2 * r) = make_float2(r < P.R ? amps[P.a_off + r] : 0.f, r < Q.R ? amps[Q.a_off + r] : 0.f);
+    *reinterpret_cast<float2*>(la + 2 * r) = make_float2(r < P.Rn ? amps[P.a_off + r] : 0.f, r < Q.Rn ? amps[Q.a_off + r] : 0.f);
     if (TWO)
       *reinterpret_cast<float2*>(ld + 2 * r) =
-          make_float2(r < P.R && !(P.flags & SG_TASK_CONST) ? amps[P.d_off + r] : 0.f,
-                      r < Q.R && !(Q.flags & SG_TASK_CONST) ? amps[Q.d_off + r] : 0.f);
+          make_float2(r < P.Rn && !(P.flags & SG_TASK_CONST) ? amps[P.d_off + r] : 0.f,
+                      r < Q.Rn && !(Q.flags & SG_TASK_CONST) ? amps[Q.d_off + r] : 0.f);
   }
   const bool vp = lane < P.len, vq = lane < Q.len;
   float tp, alp, snp, tq, alq, snq;
@@ -510,10 +510,10 @@ __device__ __forceinline__ void run_pairs_rs(const SgWTask& T, bool staged, floa
     b[p] = d[p] = e[p] = g[p] = f2{0.f, 0.f};
   }
   if (staged) {
-    reinsch_lds<NP, TWO>(la, ld, T.R, u, sg, b, d, e, g);
+    reinsch_lds<NP, TWO>(la, ld, T.Rn, u, sg, b, d, e, g);
   } else {  // more than SG_LDS_ROWS rows: 256-row chunks, top first
-    for (int r0 = (T.R - 1) / SG_LDS_ROWS * SG_LDS_ROWS; r0 >= 0; r0 -= SG_LDS_ROWS) {
-      const int n = T.R - r0 < SG_LDS_ROWS ? T.R - r0 : SG_LDS_ROWS;
+    for (int r0 = (T.Rn - 1) / SG_LDS_ROWS * SG_LDS_ROWS; r0 >= 0; r0 -= SG_LDS_ROWS) {
+      const int n = T.Rn - r0 < SG_LDS_ROWS ? T.Rn - r0 : SG_LDS_ROWS;
       stage_rows<TWO>(la, ld, amps + T.a_off, amps + T.d_off, r0, n, lane);
       reinsch_lds<NP, TWO>(la, ld, n, u, sg, b, d, e, g);
     }
@@ -539,8 +539,8 @@ template <bool TWO, bool ENV>
 __device__ __forceinline__ float run_task_rs(const SgWTask& T, float* __restrict__ la, float* __restrict__ ld,
                                              const float* __restrict__ amps, const SgSyllable* __restrict__ syls,
                                              const double* __restrict__ cknots, float* __restrict__ W, int lane) {
-  const bool staged = T.R <= SG_LDS_ROWS;
-  if (staged) stage_rows<TWO>(la, ld, amps + T.a_off, amps + T.d_off, 0, T.R, lane);
+  const bool staged = T.Rn <= SG_LDS_ROWS;
+  if (staged) stage_rows<TWO>(la, ld, amps + T.a_off, amps + T.d_off, 0, T.Rn, lane);
   float tmax = 0.f;
   int l0 = 0;
 #pragma unroll 1
@@ -561,7 +561,7 @@ template <bool TWO>
 __device__ __forceinline__ void run_pair_rs(const SgWTask& P, const SgWTask& Q, float* __restrict__ la,
                                             float* __restrict__ ld, const float* __restrict__ amps,
                                             float* __restrict__ W, int lane, float& mp, float& mq) {
-  const int R = P.R > Q.R ? P.R : Q.R;
+  const int R = P.Rn > Q.Rn ? P.Rn : Q.Rn;
   const bool vp = lane < P.len, vq = lane < Q.len;
   float tp, up, sgp, snp, tq, uq, sgq, snq;
   rs_setup(P, vp ? lane : 0, TWO, tp, up, sgp, snp);
@@ -589,11 +589,11 @@ __device__ __forceinline__ void run_pair_rs(const SgWTask& P, const SgWTask& Q, 
     for (int r = lane; r < n; r += 64) {
       const int rr = r0 + r;
       *reinterpret_cast<float2*>(la + 2 * r) =
-          make_float2(rr < P.R ? amps[P.a_off + rr] : 0.f, rr < Q.R ? amps[Q.a_off + rr] : 0.f);
+          make_float2(rr < P.Rn ? amps[P.a_off + rr] : 0.f, rr < Q.Rn ? amps[Q.a_off + rr] : 0.f);
       if (TWO)
         *reinterpret_cast<float2*>(ld + 2 * r) =
-            make_float2(rr < P.R && !(P.flags & SG_TASK_CONST) ? amps[P.d_off + rr] : 0.f,
-                        rr < Q.R && !(Q.flags & SG_TASK_CONST) ? amps[Q.d_off + rr] : 0.f);
+            make_float2(rr < P.Rn && !(P.flags & SG_TASK_CONST) ? amps[P.d_off + rr] : 0.f,
+                        rr < Q.Rn && !(Q.flags & SG_TASK_CONST) ? amps[Q.d_off + rr] : 0.f);
     }
 #pragma unroll 1
     for (int r = n - 4; r >= 0; r -= 4) {

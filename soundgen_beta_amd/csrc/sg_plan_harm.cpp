@@ -911,6 +911,7 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
     // sample boundaries of the intervals: jb[i] = first j with xout_j >= knot i+1
     std::vector<int64_t> jb(he.G - 1);
     std::vector<char> cst(he.G - 1);
+    std::vector<int32_t> rn(he.G - 1);
     int64_t ja = 0;
     for (int64_t i = 0; i + 1 < he.G; ++i) {
       int64_t g = he.n;
@@ -927,6 +928,12 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
       bool c = true;
       for (int64_t r = 0; r < ep.R && c; ++r) c = B.amps[ep.da_off + i * ep.R + r] == 0.0f;
       cst[i] = c;
+      // rows the device recurrence needs: up to the last nonzero A (or dA) row
+      int64_t last = ep.R;
+      const float* ar = B.amps.data() + ep.amp_off + i * ep.R;
+      const float* dr = B.amps.data() + ep.da_off + i * ep.R;
+      while (last > 0 && ar[last - 1] == 0.0f && (c || dr[last - 1] == 0.0f)) --last;
+      rn[i] = (int32_t)((last + 3) / 4 * 4);
     }
     int64_t k = 0;
     ja = 0;
@@ -965,6 +972,11 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
         T.xby = (float)ep.xby;
         T.mbase = (int32_t)((double)(he.u0 + j0) - S.t0);
         T.R = ep.R;
+        {  // a span of equal columns: the rows of its intervals (equal A; dA zero)
+          int32_t m = 0;
+          for (int64_t q = i; q < i1; ++q) m = std::max(m, rn[q]);
+          T.Rn = m;
+        }
         T.j0 = (int32_t)j0; T.len = (int32_t)len;
         T.dj0 = ep.dj0; T.dj1 = ep.dj1;
         T.syl = ep.syl;
