@@ -226,18 +226,21 @@ LoessFit smooth_loess(const double* t, const double* v, int64_t n, int64_t len, 
   // (R/smoothContours.R:133-143). predict()'s .C(C_loess_ifit, ..., vval) stops
   // on a NaN vertex value (NAOK = FALSE), so a zero-width fit is that error.
   // Restated, unpinned against R output.
+  LoessFit T;  // the finite fit found here is the floor loop's first fit
   for (int k = 0;; ++k) {
-    LoessFit T;
+    T = LoessFit();
     if (loess_fit(x.data(), y.data(), (int)x.size(), span, T)) break;
     if (k == 200) throw SgError(SG_E_DOMAIN, "loess: no span gives a finite fit");
     span = span + 0.1;
   }
   for (int iter = 0; iter < 200; ++iter) {
-    LoessFit T;
     // a zero-width fit inside the valueFloor loop leaves R comparing a
     // try-error string with valueFloor: not restated
-    if (!loess_fit(x.data(), y.data(), (int)x.size(), span, T))
-      throw SgError(SG_E_UNSUPPORTED, "loess: zero-width fit inside the valueFloor refits");
+    if (iter > 0) {
+      T = LoessFit();
+      if (!loess_fit(x.data(), y.data(), (int)x.size(), span, T))
+        throw SgError(SG_E_UNSUPPORTED, "loess: zero-width fit inside the valueFloor refits");
+    }
     bool below = false;
     if (has_floor)
       for (int64_t k = 0; k < len && !below; ++k) below = T.eval((double)(k + 1)) < vfloor - 1e-6;

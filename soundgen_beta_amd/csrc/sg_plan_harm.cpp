@@ -244,6 +244,8 @@ vec get_rolloff(const vec& pitch, int64_t nH, const vec& rolloff, const vec& rol
   for (double v : rolloffOct) if (v != 0) anyOct = true;
   vec slope(nGC);
   for (int64_t g = 0; g < nGC; ++g) slope[g] = rolloff[g] + rolloffKHz[g] * (pitch[g] - baseline) / 1000;
+  vec lg(nH);  // log2(h), once per call instead of per (gc, harmonic)
+  for (int64_t h = 0; h < nH; ++h) lg[h] = std::log2((double)(h + 1));
   for (int64_t g = 0; g < nGC; ++g) {
     double* col = &r[g * nH];
     for (int64_t h = 0; h < nH; ++h) {
@@ -253,7 +255,7 @@ vec get_rolloff(const vec& pitch, int64_t nH, const vec& rolloff, const vec& rol
         break;
       }
       const double delta = (anyOct && h >= 1) ? rolloffOct[g] * (pitch[g] * hh - baseline) / 1000 : 0.0;
-      col[h] = (slope[g] * std::log2(hh)) + delta;
+      col[h] = (slope[g] * lg[h]) + delta;
     }
   }
   if (rolloffParab != 0) {
@@ -279,11 +281,14 @@ vec get_rolloff(const vec& pitch, int64_t nH, const vec& rolloff, const vec& rol
   }
   for (auto& v : r) v = v == -INFINITY ? 0.0 : std::pow(2.0, v / 10);
   std::vector<int64_t> keep;
-  for (int64_t h = 0; h < nH; ++h) {
-    long double s = 0;
-    for (int64_t g = 0; g < nGC; ++g) s += at(h, g);
-    if ((double)s > 0) keep.push_back(h);
+  // row sums over gc in gc order (the same additions as a per-row loop), read column-wise
+  std::vector<long double> rs((size_t)nH, 0.0L);
+  for (int64_t g = 0; g < nGC; ++g) {
+    const double* col = &r[g * nH];
+    for (int64_t h = 0; h < nH; ++h) rs[h] += col[h];
   }
+  for (int64_t h = 0; h < nH; ++h)
+    if ((double)rs[h] > 0) keep.push_back(h);
   H = (int64_t)keep.size();
   vec o(H * nGC);
   for (int64_t g = 0; g < nGC; ++g)
@@ -357,11 +362,11 @@ static EpochMat fry_per_epoch(const double* roll, int64_t H, int64_t g0, int64_t
   }
   for (auto& v : rn) if (v < throwaway01) v = 0;
   std::vector<int64_t> keep;
-  for (int64_t i = 0; i < nr; ++i) {
-    long double s = 0;
-    for (int64_t g = 0; g < ncol; ++g) s += RN(i, g);
-    if ((double)s > 0) keep.push_back(i);
-  }
+  std::vector<long double> rs((size_t)nr, 0.0L);  // row sums in column order (per row: the same additions)
+  for (int64_t g = 0; g < ncol; ++g)
+    for (int64_t i = 0; i < nr; ++i) rs[i] += RN(i, g);
+  for (int64_t i = 0; i < nr; ++i)
+    if ((double)rs[i] > 0) keep.push_back(i);
   m.D = nSub + 1;
   m.R = keep.empty() ? 0 : keep.back();
   m.A.assign(ncol * std::max<int64_t>(m.R, 1), 0.0);
@@ -698,7 +703,9 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
     for (double v0 : idx) {
       const double v = r_round(v0);
       if (v > (double)nGC) continue;
-      if (std::find(idx2.begin(), idx2.end(), v) == idx2.end()) idx2.push_back(v);
+      // unique(): idx is strictly increasing, so its rounded values are
+      // non-decreasing and a repeat can only equal the last value kept
+      if (idx2.empty() || idx2.back() != v) idx2.push_back(v);
     }
     vec jit(idx2.size());
     for (size_t k = 0; k < idx2.size(); ++k) {
