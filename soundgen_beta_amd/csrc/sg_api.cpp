@@ -96,6 +96,35 @@ struct Checkpoint {
 };
 
 // Plan calls [c0, c1) into B (empty), output slots from offset 0.
+// Bulk-array elements per call over the parts planned so far: a later part
+// reserves its arrays up front (x1.25 of the running mean; reserve it never
+// touches is never faulted in) instead of growing them by doubling, whose
+// relocation copies and fresh-page faults were ~20 % of planning time.
+struct GrowthEstimate {
+  static constexpr int N = 10;
+  std::atomic<int64_t> calls{0};
+  std::atomic<int64_t> elems[N];
+  GrowthEstimate() {
+    for (auto& e : elems) e.store(0);
+  }
+  template <class F>
+  static void each(sg::Batch& B, F&& f) {
+    f(0, B.segs); f(1, B.epochs); f(2, B.knots); f(3, B.amps); f(4, B.tasks);
+    f(5, B.pieces); f(6, B.syl_tiles); f(7, B.fl); f(8, B.cknots); f(9, B.eterms);
+  }
+  void reserve(sg::Batch& B, int64_t n_calls) const {
+    const int64_t c = calls.load();
+    if (c <= 0) return;
+    each(B, [&](int i, auto& v) {
+      v.reserve((size_t)(1.25 * (double)elems[i].load() / (double)c * (double)n_calls) + 256);
+    });
+  }
+  void record(sg::Batch& B, int64_t n_calls) {
+    each(B, [&](int i, auto& v) { elems[i] += (int64_t)v.size(); });
+    calls += n_calls;
+  }
+};
+
 void plan_range(sg::Batch& B, const sg_call_desc* calls, int64_t c0, int64_t c1) {
   const int64_t n = c1 - c0;
   B.call_len.assign(n, 0);
@@ -346,10 +375,14 @@ int sg_plan_batch(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, sg_pl
       std::vector<sg::Batch> parts((size_t)nchunk);
       std::vector<std::exception_ptr> errs((size_t)nchunk);
       std::atomic<int64_t> next{0};
+      GrowthEstimate growth;
       auto work = [&]() {
         for (int64_t k; (k = next.fetch_add(1)) < nchunk;) {
           try {
-            plan_range(parts[k], calls, k * n_calls / nchunk, (k + 1) * n_calls / nchunk);
+            const int64_t c0 = k * n_calls / nchunk, c1 = (k + 1) * n_calls / nchunk;
+            growth.reserve(parts[k], c1 - c0);
+            plan_range(parts[k], calls, c0, c1);
+            growth.record(parts[k], c1 - c0);
           } catch (...) {
             errs[k] = std::current_exception();
           }

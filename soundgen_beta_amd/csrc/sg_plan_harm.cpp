@@ -230,6 +230,27 @@ void clumper(vec& s, const vec& minLen_in) {
 }
 
 // ------------------------------------------------------------- rolloff
+// rowSums() of a column-major nrow x ncol matrix with R's long double
+// accumulator, each row summed in column order; four rows per pass so that a
+// column's reads share cache lines and the accumulators stay in registers.
+static void row_sums(const double* M, int64_t nrow, int64_t ncol, std::vector<long double>& out) {
+  out.assign((size_t)nrow, 0.0L);
+  int64_t i = 0;
+  for (; i + 4 <= nrow; i += 4) {
+    long double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    for (int64_t g = 0; g < ncol; ++g) {
+      const double* c = M + g * nrow + i;
+      s0 += c[0]; s1 += c[1]; s2 += c[2]; s3 += c[3];
+    }
+    out[i] = s0; out[i + 1] = s1; out[i + 2] = s2; out[i + 3] = s3;
+  }
+  for (; i < nrow; ++i) {
+    long double s = 0;
+    for (int64_t g = 0; g < ncol; ++g) s += M[g * nrow + i];
+    out[i] = s;
+  }
+}
+
 // getRolloff(), R/sourceSpectrum.R:71-186 with per-gc vector parameters.
 // Returns H x nGC column-major (kept rows compacted, renumbered 1..H).
 vec get_rolloff(const vec& pitch, int64_t nH, const vec& rolloff, const vec& rolloffOct, double rolloffParab,
@@ -281,12 +302,8 @@ vec get_rolloff(const vec& pitch, int64_t nH, const vec& rolloff, const vec& rol
   }
   for (auto& v : r) v = v == -INFINITY ? 0.0 : std::pow(2.0, v / 10);
   std::vector<int64_t> keep;
-  // row sums over gc in gc order (the same additions as a per-row loop), read column-wise
-  std::vector<long double> rs((size_t)nH, 0.0L);
-  for (int64_t g = 0; g < nGC; ++g) {
-    const double* col = &r[g * nH];
-    for (int64_t h = 0; h < nH; ++h) rs[h] += col[h];
-  }
+  std::vector<long double> rs;
+  row_sums(r.data(), nH, nGC, rs);
   for (int64_t h = 0; h < nH; ++h)
     if ((double)rs[h] > 0) keep.push_back(h);
   H = (int64_t)keep.size();
@@ -362,9 +379,8 @@ static EpochMat fry_per_epoch(const double* roll, int64_t H, int64_t g0, int64_t
   }
   for (auto& v : rn) if (v < throwaway01) v = 0;
   std::vector<int64_t> keep;
-  std::vector<long double> rs((size_t)nr, 0.0L);  // row sums in column order (per row: the same additions)
-  for (int64_t g = 0; g < ncol; ++g)
-    for (int64_t i = 0; i < nr; ++i) rs[i] += RN(i, g);
+  std::vector<long double> rs;
+  row_sums(rn.data(), nr, ncol, rs);
   for (int64_t i = 0; i < nr; ++i)
     if ((double)rs[i] > 0) keep.push_back(i);
   m.D = nSub + 1;
