@@ -318,14 +318,12 @@ def main():
     base = 0
     failed = 0
     first_msg = None
-    for a in range(0, len(mine), args.plan_chunk):
-        p = batch.Plan(mine[a:a + args.plan_chunk], ctx)
+    # chunk k + 1 plans on the host while chunk k uploads (batch.plan_uploaded)
+    for p, a in batch.plan_uploaded(mine, ctx, args.plan_chunk):
         bad = np.nonzero(p.status)[0]
         failed += len(bad)
         if len(bad) and first_msg is None:
             first_msg = p.message(int(bad[0]))
-        p.upload()
-        p.release_host()
         plans.append((p, base, idx[a:a + args.plan_chunk]))
         base += (p.total + 63) // 64 * 64
         if rank == 0:

@@ -112,6 +112,28 @@ def execute_plans(ctx, plans, d_out_ptrs, stream_ptr=None):
                  ctx.ptr)
 
 
+def plan_uploaded(calls, ctx, chunk):
+    """Plan `calls` in chunks of `chunk` and upload each plan, yielding
+    (plan, first call index) in order. Chunk k + 1 is planned on a worker thread
+    while chunk k uploads: both native calls run without the GIL (ctypes), so
+    the host planner's threads overlap the pageable H2D copy of the previous
+    plan. Each yielded plan is uploaded and its host arrays released."""
+    from concurrent.futures import ThreadPoolExecutor
+    starts = list(range(0, len(calls), chunk))
+    if not starts:
+        return
+    with ThreadPoolExecutor(1) as ex:
+        fut = ex.submit(Plan, calls[0:chunk], ctx)
+        for i, a in enumerate(starts):
+            p = fut.result()
+            if i + 1 < len(starts):
+                b = starts[i + 1]
+                fut = ex.submit(Plan, calls[b:b + chunk], ctx)
+            p.upload()
+            p.release_host()
+            yield p, a
+
+
 def synthesize_to_wav(calls, paths, sampling_rates, device=0):
     """soundgen(..., savePath = path) for a batch: synthesize on the GPU, convert
     every call to 16-bit PCM on the GPU (half the bytes cross PCIe), write one

@@ -124,6 +124,21 @@ bool vertex_fit(const double* x, const double* y, int n, int nf, double f, doubl
 double LoessFit::eval(double z) const {
   int p = 0;
   while (split[p]) p = z <= xi[p] ? son_lo[p] : son_hi[p];
+  return hermite(p, z);
+}
+
+double LoessFit::eval_seq(double z, int& p) const {
+  // z non-decreasing over the calls: the leaf found for an earlier z holds every
+  // z up to its upper vertex (the tree sends z <= split to the low son, and that
+  // vertex is the split), or every z when its upper vertex is the outer one (1)
+  if (p < 0 || !(cv1[p] == 1 || z <= vx[cv1[p]])) {
+    p = 0;
+    while (split[p]) p = z <= xi[p] ? son_lo[p] : son_hi[p];
+  }
+  return hermite(p, z);
+}
+
+double LoessFit::hermite(int p, double z) const {
   const int a = cv0[p], b = cv1[p];
   const double v0 = vx[a], v1 = vx[b];
   const double h = (z - v0) / (v1 - v0);
@@ -242,8 +257,10 @@ LoessFit smooth_loess(const double* t, const double* v, int64_t n, int64_t len, 
         throw SgError(SG_E_UNSUPPORTED, "loess: zero-width fit inside the valueFloor refits");
     }
     bool below = false;
-    if (has_floor)
-      for (int64_t k = 0; k < len && !below; ++k) below = T.eval((double)(k + 1)) < vfloor - 1e-6;
+    if (has_floor) {
+      int leaf = -1;
+      for (int64_t k = 0; k < len && !below; ++k) below = T.eval_seq((double)(k + 1), leaf) < vfloor - 1e-6;
+    }
     if (!below) return T;
     span = span / 1.1;  // less smoothing while the contour dips below the floor
   }

@@ -21,6 +21,9 @@ struct LoessFit {
   std::vector<double> xi;
   double xmin = 0, xmax = 0;           // data range (predict gives NA outside)
   double eval(double z) const;         // Hermite interpolation in the leaf cell containing z
+  // eval() for non-decreasing z: *leaf (start at -1) carries the last leaf between calls
+  double eval_seq(double z, int& leaf) const;
+  double hermite(int leaf, double z) const;
 };
 
 // fit; throws SgError for spans R rejects. Returns false when a vertex value

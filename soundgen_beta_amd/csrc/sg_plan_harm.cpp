@@ -45,9 +45,10 @@ bool smooth_contour(const sg_anchors& an, int64_t len, bool thisIsPitch, int met
     if (method != 1) {  // loess, R/smoothContours.R:119-154 (duration_ms = len / sr * 1000)
       const LoessFit T = smooth_loess(t.data(), v.data(), n, len, (double)len / sr * 1000, has_floor, vfloor);
       out.resize(len);
+      int leaf = -1;
       for (int64_t k = 0; k < len; ++k) {
         const double z = (double)(k + 1);
-        out[k] = (z < T.xmin || z > T.xmax) ? NAN : T.eval(z);
+        out[k] = (z < T.xmin || z > T.xmax) ? NAN : T.eval_seq(z, leaf);
       }
     } else {
       out = r_spline(t, v, len);
@@ -373,8 +374,8 @@ static EpochMat fry_per_epoch(const double* roll, int64_t H, int64_t g0, int64_t
   for (int64_t block = 1; block <= H + 1; ++block) {
     const int64_t row_lwr = 1 + (block - 1) * (nSub + 1), row_upr = row_lwr + nSub + 1;
     const double Alin = rn[row_lwr - 1], Blin = rn[row_upr - 1];  // linear index = column 1 (quirk)
-    for (int64_t gg = 1; gg <= nSub; ++gg)
-      for (int64_t g = 0; g < ncol; ++g)
+    for (int64_t g = 0; g < ncol; ++g)  // column-major writes (each element written once)
+      for (int64_t gg = 1; gg <= nSub; ++gg)
         RN(row_lwr + gg - 1, g) = Alin * ml[(gg - 1) * ncol + g] + Blin * ml[(nSub - gg) * ncol + g];
   }
   for (auto& v : rn) if (v < throwaway01) v = 0;
@@ -387,11 +388,10 @@ static EpochMat fry_per_epoch(const double* roll, int64_t H, int64_t g0, int64_t
   m.R = keep.empty() ? 0 : keep.back();
   m.A.assign(ncol * std::max<int64_t>(m.R, 1), 0.0);
   m.mult.assign(std::max<int64_t>(m.R, 1), 0.0);
-  for (int64_t i : keep) {
-    // rank i (0 never survives: row 1 is all zero)
-    for (int64_t g = 0; g < ncol; ++g) m.A[g * m.R + (i - 1)] = RN(i, g);
-    m.mult[i - 1] = rowname_num(gseq[i]);
-  }
+  // rank i (0 never survives: row 1 is all zero)
+  for (int64_t i : keep) m.mult[i - 1] = rowname_num(gseq[i]);
+  for (int64_t g = 0; g < ncol; ++g)
+    for (int64_t i : keep) m.A[g * m.R + (i - 1)] = RN(i, g);
   return m;
 }
 

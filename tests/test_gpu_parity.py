@@ -183,6 +183,35 @@ def test_sharded_batch_byte_equal():
             assert np.array_equal(y.view(np.uint32), whole[i].view(np.uint32)), (r, int(i))
 
 
+def test_plan_uploaded_pipeline_byte_equal():
+    """batch.plan_uploaded (chunk k + 1 planned on a worker thread while chunk k
+    uploads) yields, in order, plans whose outputs equal those of plans built and
+    uploaded one after another."""
+    import os
+    import sys
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from soundgen_beta_amd import batch, native
+    calls = bench.c5_calls(70)
+    ctx = native.default_context(0)
+    sptr = torch.cuda.current_stream().cuda_stream
+    got = list(batch.plan_uploaded(calls, ctx, 32))
+    assert [a for _, a in got] == [0, 32, 64]
+    for p, a in got:
+        ref = batch.Plan(calls[a:a + 32], ctx)
+        assert ref.total == p.total and (ref.lengths == p.lengths).all() and (p.status == 0).all()
+        ref.upload()
+        o1 = torch.zeros(max(p.total, 1), dtype=torch.float32, device="cuda")
+        o2 = torch.zeros_like(o1)
+        p.execute(o1.data_ptr(), sptr)
+        ref.execute(o2.data_ptr(), sptr)
+        torch.cuda.synchronize()
+        assert torch.equal(o1.view(torch.int32), o2.view(torch.int32))
+        ref.close()
+        p.close()
+
+
 def test_execute_plans_equals_per_plan_execute():
     """sg_execute_plans (several uploaded plans as one batch, the harmonic chains of
     later plans overlapping the spectral phases of earlier ones on the context's
