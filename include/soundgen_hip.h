@@ -187,6 +187,8 @@ int sg_plan_upload(sg_ctx* ctx, sg_plan* plan);
 /* After upload: free the plan's host copies of descriptors and inputs (a
  * 65,536-call preset batch holds ~0.7 MB per call on the host). Execution,
  * lengths, offsets, statuses and messages keep working; re-upload does not.
+ * The bulk arrays are returned to the OS on a detached host thread, so the
+ * call returns before their pages are unmapped.
  * No reference counterpart (R holds nothing between calls). */
 int sg_plan_release_host(sg_plan* plan);
 /* Run every kernel of the plan on `stream` (hipStream_t; NULL = the null
