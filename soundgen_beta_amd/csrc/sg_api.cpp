@@ -239,10 +239,7 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
     D.frames[ph].resize(c.fr[ph]); D.frame_geom[ph].resize(c.fr[ph]);
     D.olas[ph].resize(c.ola[ph]); D.mixes[ph].resize(c.mix[ph]);
   }
-  auto put = [](auto& dst, auto& src, int64_t at) {
-    std::copy(src.begin(), src.end(), dst.begin() + at);
-    std::remove_reference_t<decltype(src)>().swap(src);
-  };
+  auto put = [](auto& dst, auto& src, int64_t at) { std::copy(src.begin(), src.end(), dst.begin() + at); };
   auto one = [&](size_t k) {
     sg::Batch& S = parts[k];
     const PartBase& b = base[k];
@@ -308,7 +305,6 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
       put(D.frames[ph], S.frames[ph], b.fr[ph]); put(D.frame_geom[ph], S.frame_geom[ph], b.fr[ph]);
       put(D.olas[ph], S.olas[ph], b.ola[ph]); put(D.mixes[ph], S.mixes[ph], b.mix[ph]);
     }
-    S = sg::Batch();
   };
   std::atomic<size_t> next{0};
   auto work = [&]() {
@@ -318,6 +314,14 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
   for (int t = 1; t < threads; ++t) pool.emplace_back(work);
   work();
   for (auto& t : pool) t.join();
+  // the parts (as large as the merged batch) are unmapped on a detached thread:
+  // freeing them inside the copy loop serialised the merge threads' page faults
+  auto* dead = new std::vector<sg::Batch>(std::move(parts));
+  try {
+    std::thread([dead]() { delete dead; }).detach();
+  } catch (...) {
+    delete dead;
+  }
 }
 }  // namespace
 
