@@ -5,7 +5,7 @@ metric "(whole node)" is quoted on): ONE batch of 65,536 soundgen() calls drawn
 from the 33 presets (R/presets.R:158-399, soundgen_beta_amd/presets.json),
 sylLen x U(0.5, 2) clamped to [20, 5000] ms, pitch anchors x 2^U(-0.5, 0.5),
 44.1 kHz, numpy PCG64 seed 20261015, random draws injected. It fits one
-MI355X (~150 GB of HBM), so N=1 runs all of it; with N ranks the SAME batch is
+MI355X (288 GB of HBM; the arena takes ~40 GB per 16,384 calls), so N=1 runs all of it; with N ranks the SAME batch is
 split by LPT over an analytic per-call cost (soundgen_beta_amd/dist.py), no
 data-path collective: "scaling": "strong".
 --config c2|c3|c4 run the other single-GPU configs (C2 1024 x 1 s tones,
@@ -14,11 +14,12 @@ subharmonics/jitter/shimmer at temperature 0.05).
 
 A "step" = one pass of the hot path over the whole batch: every kernel from
 the envelopes and the sine bank to the final mix, inputs resident in HBM
-(planning and upload happen before the timed region; plan time is reported).
+(planning and upload happen before the timed region; plan time is reported),
+ending with every waveform copied into pinned host memory ("from
+sg_execute entry to waveforms resident in host memory"); each plan chunk's
+copy overlaps the kernels of the chunks after it.
 value = samples of all ranks / max over ranks of the timed wall time.
-value_host_resident adds the device-to-host copy of every waveform into pinned
-host memory inside the timed region ("to waveforms resident in
-host memory"); each plan chunk's copy overlaps the kernels of the chunks after it.
+value_device_resident times the same steps without the copy.
 
 With --gpus N and no WORLD_SIZE in the environment, bench.py starts itself
 under torch.distributed.run with N ranks (one per GPU) before touching the GPU.
@@ -281,7 +282,8 @@ def main():
     ap.add_argument("--calls", type=int, default=0, help="calls in the whole batch (default: the config's)")
     ap.add_argument("--plan-chunk", type=int, default=16384,
                     help="calls per plan (each uploaded, then its host copy freed)")
-    ap.add_argument("--host-steps", type=int, default=2, help="steps timed with the D2H copy (0: skip)")
+    ap.add_argument("--device-steps", type=int, default=5,
+                    help="extra steps timed with the outputs left in HBM (value_device_resident; 0: skip)")
     ap.add_argument("--cpu-budget", type=float, default=16.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", action="store_true",
@@ -340,20 +342,52 @@ def main():
         for p, b, _ in plans:
             p.execute(out.data_ptr() + 4 * b, sptr)
 
+    # the metric's timing: from sg_execute entry to waveforms resident
+    # in host memory. Every plan's outputs are copied into pinned host memory on a
+    # second stream while the following plans compute; plan c of the next step
+    # waits only for the copy of its own region.
+    try:
+        host = torch.empty(max(base, 1), dtype=torch.float32, pin_memory=True)
+        pinned = True
+    except RuntimeError:
+        host = torch.empty(max(base, 1), dtype=torch.float32)
+        pinned = False
+    cstream = torch.cuda.Stream(dev)
+    ends = [b + (p.total + 63) // 64 * 64 for p, b, _ in plans]
+    copied = [None] * len(plans)
+
+    def step_to_host():
+        for i, ((p, b, _), e) in enumerate(zip(plans, ends)):
+            if copied[i] is not None:
+                stream.wait_event(copied[i])  # plan i's region is free again
+            p.execute(out.data_ptr() + 4 * b, sptr)
+            done = torch.cuda.Event()
+            done.record(stream)
+            cstream.wait_event(done)
+            with torch.cuda.stream(cstream):
+                host[b:e].copy_(out[b:e], non_blocking=pinned)
+            copied[i] = torch.cuda.Event()
+            copied[i].record(cstream)
+
+    def timed(fn, k):
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        return time.perf_counter() - t
+
     for _ in range(args.warmup):
-        step()
+        step_to_host()
     torch.cuda.synchronize(dev)
+    dt = timed(step_to_host, args.steps)  # the headline: host-resident
+    # the same steps with the outputs left in HBM (no D2H copy)
+    dt_dev = timed(step, args.device_steps) if args.device_steps > 0 else None
     L = native.lib()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    dt = time.perf_counter() - t0
     # per-kernel HIP events (roofline) over the same number of extra steps, outside the
     # timed region: with profiling on, the harmonic chain and the noise phase run one
     # after the other, so each launch's duration is its own, not shared with a
@@ -368,47 +402,10 @@ def main():
         ms, n = C.c_double(), C.c_int64()
         native.check(L.sg_profile_read_kernel(ctx.ptr, kid, C.byref(ms), C.byref(n)), ctx.ptr)
         prof[name] = (ms.value, n.value)
-
-    # the same steps with every waveform copied to pinned host memory (the timed
-    # region ends with the samples resident on the host). The copy of plan c's
-    # outputs runs on a second stream while the following plans compute; plan c
-    # of the next step waits only for that copy.
-    dt_host = None
-    if args.host_steps > 0:
-        try:
-            host = torch.empty(max(base, 1), dtype=torch.float32, pin_memory=True)
-            pinned = True
-        except RuntimeError:
-            host = torch.empty(max(base, 1), dtype=torch.float32)
-            pinned = False
-        host.copy_(out)
-        cstream = torch.cuda.Stream(dev)
-        ends = [b + (p.total + 63) // 64 * 64 for p, b, _ in plans]
-        if dist:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t1 = time.perf_counter()
-        copied = [None] * len(plans)
-        for _ in range(args.host_steps):
-            for i, ((p, b, _), e) in enumerate(zip(plans, ends)):
-                if copied[i] is not None:
-                    stream.wait_event(copied[i])  # plan i's region is free again
-                p.execute(out.data_ptr() + 4 * b, sptr)
-                done = torch.cuda.Event()
-                done.record(stream)
-                cstream.wait_event(done)
-                with torch.cuda.stream(cstream):
-                    host[b:e].copy_(out[b:e], non_blocking=pinned)
-                copied[i] = torch.cuda.Event()
-                copied[i].record(cstream)
-        torch.cuda.synchronize(dev)
-        if dist:
-            dist.barrier()
-        dt_host = time.perf_counter() - t1
-        del host
+    del host
 
     samples_rank = int(sum(int(p.lengths.sum()) for p, _, _ in plans))  # synthesized samples (padding excluded)
-    vals = [dt, t_plan, float(dt_host or 0.0)]
+    vals = [dt, t_plan, float(dt_dev or 0.0)]
     if dist:
         t = torch.tensor(vals, device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -418,7 +415,7 @@ def main():
         samples_all, failed_all = float(s[0].item()), int(s[1].item())
     else:
         samples_all, failed_all = float(samples_rank), failed
-    dt, t_plan_max, dt_host = vals[0], vals[1], (vals[2] if args.host_steps > 0 else None)
+    dt, t_plan_max, dt_dev = vals[0], vals[1], (vals[2] if args.device_steps > 0 else None)
     value = samples_all * args.steps / dt
 
     gather_ms = None
@@ -466,8 +463,9 @@ def main():
                        "samples": int(samples_all), "sampling_rate": 44100,
                        "parallelism": "dp%d (one batch split by calls, LPT)" % world,
                        "plans_per_rank": len(plans), "failed_calls": failed_all},
-            "value_host_resident": (samples_all * args.host_steps / dt_host) if dt_host else None,
-            "ms_per_step_host_resident": (dt_host / args.host_steps * 1e3) if dt_host else None,
+            "timing": "sg_execute entry to waveforms resident in pinned host memory (SURVEY 8d)",
+            "value_device_resident": (samples_all * args.device_steps / dt_dev) if dt_dev else None,
+            "ms_per_step_device_resident": (dt_dev / args.device_steps * 1e3) if dt_dev else None,
             "plan_s": t_plan_max, "calls_gen_s": t_gen,
             "value_incl_planning": samples_all / (t_plan_max + dt / args.steps),
             "rms_error_vs_oracle": max(rms) if rms else None,

@@ -21,7 +21,7 @@ for v in default ${VARIANTS}; do
     *) export SG_HIP_LIB=$R/soundgen_beta_amd/lib/exp_$v.so ;;
   esac
   cd /tmp
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/pk_${TAG}_$v" -o run -- python "$R/bench.py" --config c5 --calls ${CALLS:-16384} --steps 3 --warmup 1 --host-steps 0 --no-cpu-baseline > "$R/gpurun_out/pk_${TAG}_$v.log" 2>&1 || { tail -20 "$R/gpurun_out/pk_${TAG}_$v.log"; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/pk_${TAG}_$v" -o run -- python "$R/bench.py" --config c5 --calls ${CALLS:-16384} --steps 3 --warmup 1 --device-steps 0 --no-cpu-baseline > "$R/gpurun_out/pk_${TAG}_$v.log" 2>&1 || { tail -20 "$R/gpurun_out/pk_${TAG}_$v.log"; exit 1; }
   cd "$R"
   echo "== $v $(python -c "import json,sys; d=json.load(open(sys.argv[1])); print('%.4g samples/s %.2f ms/step rms %.2g' % (d['value'], d['ms_per_step'], d['rms_error_vs_oracle']))" "$(ls gpurun_out/pk_${TAG}_$v.log)" 2>/dev/null || grep -o '"value": [0-9.e+]*' gpurun_out/pk_${TAG}_$v.log)"
   cut -d, -f1-4 "gpurun_out/pk_${TAG}_$v/run_kernel_stats.csv" | head -9 | tail -8
