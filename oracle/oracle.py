@@ -52,6 +52,8 @@ def lib():
         L.or_glottal_cycles.restype = i64
         L.or_spline.argtypes = [dp, dp, i64, i64, dp]
         L.or_approx.argtypes = [dp, dp, i64, i64, dp]
+        L.or_spline_at.argtypes = [dp, dp, i64, dp, i64, dp]
+        L.or_approx_at.argtypes = [dp, dp, i64, dp, i64, dp]
         L.or_find_zero_crossing.argtypes = [dp, i64, i64]
         L.or_find_zero_crossing.restype = i64
         L.or_clumper.argtypes = [dp, i64, dp, i64]
@@ -219,6 +221,22 @@ def approx(x, y, n):
     x, y = _f64(x), _f64(y)
     out = np.zeros(n)
     _check(lib().or_approx(_abi.dptr(x), _abi.dptr(y), len(x), n, _abi.dptr(out)))
+    return out
+
+
+def spline_at(x, y, u):
+    """splinefun(x, y, method = "fmm")(u)."""
+    x, y, u = _f64(x), _f64(y), _f64(u)
+    out = np.zeros(len(u))
+    lib().or_spline_at(_abi.dptr(x), _abi.dptr(y), len(x), _abi.dptr(u), len(u), _abi.dptr(out))
+    return out
+
+
+def approx_at(x, y, v):
+    """approx(x, y, xout = v)$y (linear, rule = 1: NaN outside [x1, xn])."""
+    x, y, v = _f64(x), _f64(y), _f64(v)
+    out = np.zeros(len(v))
+    lib().or_approx_at(_abi.dptr(x), _abi.dptr(y), len(x), _abi.dptr(v), len(v), _abi.dptr(out))
     return out
 
 

@@ -1513,6 +1513,14 @@ OR_API void or_spline(const double* x, const double* y, int64_t nx, int64_t n, d
 OR_API int or_approx(const double* x, const double* y, int64_t nx, int64_t n, double* out) {
   dv a; int rc = r_approx_n(x, y, nx, n, &a); if (!rc) { memcpy(out, a.v, n * sizeof(double)); dv_free(&a); } return rc;
 }
+/* splinefun(x, y, method = "fmm")(u) (stats splines.c: SplineCoef + SplineEval) */
+OR_API void or_spline_at(const double* x, const double* y, int64_t nx, const double* u, int64_t nu, double* out) {
+  spl_t s = fmm_coef(x, y, nx); spl_eval(&s, u, out, nu); spl_free(&s);
+}
+/* approx(x, y, xout = v)$y, linear, rule = 1 (stats approx.c approx1): NaN outside */
+OR_API void or_approx_at(const double* x, const double* y, int64_t nx, const double* v, int64_t nv, double* out) {
+  for (int64_t l = 0; l < nv; ++l) out[l] = approx1(v[l], x, y, nx);
+}
 OR_API int64_t or_find_zero_crossing(const double* a, int64_t len, int64_t location) { return find_zero_crossing(a, len, location); }
 OR_API void or_clumper(double* s, int64_t n, const double* minLength, int64_t nml) { clumper(s, n, minLength, nml); }
 OR_API int64_t or_cross_fade(const double* a1, int64_t n1, const double* a2, int64_t n2, double sr, double crossLen, double* out) {

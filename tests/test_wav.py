@@ -81,3 +81,20 @@ def test_batch_wav_output_matches_restatement(oracle, tmp_path):
         want = oracle.savewav_pcm(np.asarray(y, np.float64))
         assert np.array_equal(p, want), i
         assert open(paths[i], "rb").read() == _expected_file(want, 44100)
+
+
+@pytest.mark.gpu
+def test_savewav_gpu_vs_r_printed(tmp_path):
+    """The GPU conversion (sg_pcm_stats + sg_pcm_convert) of tuneR's x1 =
+    sine(660, pcm = TRUE, bit = 8, duration = 500) gives the samples R printed for
+    normalize(x1, "16", center = TRUE, level = 1, rescale = TRUE)
+    (tuneRTest.Rout.save:325-326; tests/golden/r_pins.json), the conversion
+    seewave::savewav applies when max(wave) > 1."""
+    import json
+    import math
+    from soundgen_beta_amd import api
+    pins = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "r_pins.json")))
+    s = np.array([math.sin(2 * math.pi * 660 * k / 44100) for k in range(500)])
+    x1 = np.rint(s / np.max(np.abs(s)) * 127 + 127)
+    got = api.savewav(x1, f=44100, filename=str(tmp_path / "x1.wav"))
+    assert list(got[:10]) == pins["tuneR"]["x13_normalize16_rescale"]

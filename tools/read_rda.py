@@ -104,6 +104,13 @@ class _Reader:
         if t == 14:  # REALSXP
             n = self.length()
             return self._attrs(self.f64s(n), has_attr)
+        if t == 15:  # CPLXSXP: n (re, im) pairs
+            n = self.length()
+            f = self.f64s(2 * n)
+            return self._attrs([complex(f[2 * i], f[2 * i + 1]) for i in range(n)], has_attr)
+        if t == 24:  # RAWSXP
+            n = self.length()
+            return self._attrs(list(self.raw(n)), has_attr)
         if t == 16:  # STRSXP
             n = self.length()
             return self._attrs([self.item() for _ in range(n)], has_attr)
