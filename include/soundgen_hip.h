@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SG_ABI_VERSION 1
+#define SG_ABI_VERSION 2
 
 enum {
   SG_OK = 0,
@@ -238,6 +238,17 @@ int sg_plan_kernel_stats(const sg_plan* plan, int64_t* harm_samples,
  * output samples, algorithmic HBM bytes (source/uniforms + envelope columns +
  * output) and nominal flops (5 wl log2 wl per transform). */
 int sg_plan_stft_stats(const sg_plan* plan, int64_t* samples, int64_t* alg_bytes, double* flops);
+/* Precision path of the plan (ABI 2): per call, the number of its bouts whose
+ * formant filter runs in fp64 (source, pre-filter mix and forward STFT; the
+ * planner's conditioning estimate of the fp32 round-off through the envelope
+ * exceeded its threshold, env SG_HP_RHO, default 300; SG_HP=0 never, 2 always);
+ * totals of fp64 filter frames and sine-bank tasks. Any pointer may be NULL.
+ * No reference counterpart: the R path is fp64 throughout. */
+int sg_plan_precision(const sg_plan* plan, int32_t* call_fp64, int64_t* fp64_frames, int64_t* fp64_tasks);
+/* Process-wide policy of the fp64 filter path for later sg_plan_batch calls:
+ * mode 0 never, 1 when the conditioning estimate exceeds rho (default 300),
+ * 2 every filtered bout. SG_E_ARG for an invalid mode or rho. */
+int sg_set_fp64_policy(int32_t mode, double rho);
 
 /* ---- function-level entries mirroring the R API (synchronous) ---------- */
 int sg_generate_harmonics(sg_ctx* ctx, const double* pitch, int64_t len,

@@ -1443,8 +1443,17 @@ OR_API int or_spectral_envelope(int32_t nr, int32_t nc, const sg_formants* F, do
 }
 
 /* Formant filter block of soundgen(), R/soundgen.R:743-807 (wl already set) */
+/* diagnostics (tests only): with capture on, the last formant filter's inputs are kept */
+static int g_cap_on = 0;
+static dv g_cap_sound = {0, 0}, g_cap_env = {0, 0};
+static int64_t g_cap_nc = 0, g_cap_wl = 0;
 static int formant_filter(const double* sound, int64_t L, const double* env, int64_t env_nc, int64_t wl,
                           double overlap, dv* out) {
+  if (g_cap_on) {
+    dv_free(&g_cap_sound); dv_free(&g_cap_env);
+    g_cap_sound = dv_copy(sound, L); g_cap_env = dv_copy(env, env_nc * (wl / 2));
+    g_cap_nc = env_nc; g_cap_wl = wl;
+  }
   dv step = r_seq_by(1, (double)(L - wl > 1 ? L - wl : 1), (double)wl - (overlap * (double)wl / 100));
   int64_t nc = step.n, nr = wl / 2;
   double* zre = (double*)malloc(nr * nc * sizeof(double)); double* zim = (double*)malloc(nr * nc * sizeof(double));
@@ -1460,6 +1469,14 @@ static int formant_filter(const double* sound, int64_t L, const double* env, int
   free(zre); free(zim); dv_free(&step);
   *out = y;
   return 0;
+}
+OR_API void or_debug_capture(int on) { g_cap_on = on; }
+OR_API int64_t or_debug_captured(double* sound, double* env, int64_t* env_nc, int64_t* wl) {
+  if (sound) memcpy(sound, g_cap_sound.v, g_cap_sound.n * sizeof(double));
+  if (env) memcpy(env, g_cap_env.v, g_cap_env.n * sizeof(double));
+  if (env_nc) *env_nc = g_cap_nc;
+  if (wl) *wl = g_cap_wl;
+  return g_cap_sound.n;
 }
 OR_API int or_formant_filter(const double* sound, int64_t L, const double* env, int32_t env_nc, int32_t wl,
                              double overlap, double** out, int64_t* out_len) {

@@ -63,6 +63,13 @@ class Plan:
         return dict(harm_samples=v[0].value, harm_terms=v[1].value, harm_amp_bytes=v[2].value,
                     fft_frames=v[3].value, stft_samples=w[0].value, stft_bytes=w[1].value, stft_flops=w[2].value)
 
+    def precision(self):
+        """Per call: bouts on the fp64 filter path; totals of fp64 frames and tasks."""
+        v = np.zeros(self.n, dtype=np.int32)
+        fr, tk = C.c_int64(), C.c_int64()
+        native.lib().sg_plan_precision(self.ptr, v.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(fr), C.byref(tk))
+        return v, fr.value, tk.value
+
     def device_bytes(self):
         return int(native.lib().sg_plan_device_bytes(self.ptr))
 

@@ -70,15 +70,18 @@ int guarded(sg_ctx* ctx, F&& f) {
 // Rolls a Batch back to a checkpoint when planning one call fails.
 struct Checkpoint {
   size_t segs, epochs, knots, amps, tasks, pieces, syls, syl_tiles, cknots, fl, items;
-  size_t frames[2], olas[2], mixes[2], copies, eterms, ecols, envjobs;
-  int64_t w_total, harm_samples, harm_terms, harm_amp_bytes, fft_frames, fs_total, fe_total;
+  size_t frames[2], olas[2], mixes[2], copies, eterms, ecols, envjobs, frames64;
+  int64_t w_total, harm_samples, harm_terms, harm_amp_bytes, fft_frames, fs_total, fe_total, w64_total, fh_total,
+      hp_bouts;
   explicit Checkpoint(const sg::Batch& B)
       : segs(B.segs.size()), epochs(B.epochs.size()), knots(B.knots.size()), amps(B.amps.size()),
         tasks(B.tasks.size()), pieces(B.pieces.size()), syls(B.syls.size()), syl_tiles(B.syl_tiles.size()),
         cknots(B.cknots.size()), fl(B.fl.size()), items(B.items.size()), copies(B.copies.size()),
         eterms(B.eterms.size()), ecols(B.ecols.size()), envjobs(B.envjobs.size()), w_total(B.w_total),
         harm_samples(B.harm_samples), harm_terms(B.harm_terms), harm_amp_bytes(B.harm_amp_bytes),
-        fft_frames(B.fft_frames), fs_total(B.fs_total), fe_total(B.fe_total) {
+        fft_frames(B.fft_frames), fs_total(B.fs_total), fe_total(B.fe_total), w64_total(B.w64_total),
+        fh_total(B.fh_total), hp_bouts(B.hp_bouts) {
+    frames64 = B.frames64.size();
     for (int p = 0; p < 2; ++p) { frames[p] = B.frames[p].size(); olas[p] = B.olas[p].size(); mixes[p] = B.mixes[p].size(); }
   }
   void restore(sg::Batch& B) const {
@@ -92,6 +95,7 @@ struct Checkpoint {
     B.w_total = w_total; B.harm_samples = harm_samples; B.harm_terms = harm_terms;
     B.harm_amp_bytes = harm_amp_bytes; B.fft_frames = fft_frames; B.fs_total = fs_total;
     B.eterms.resize(eterms); B.ecols.resize(ecols); B.envjobs.resize(envjobs); B.fe_total = fe_total;
+    B.frames64.resize(frames64); B.w64_total = w64_total; B.fh_total = fh_total; B.hp_bouts = hp_bouts;
   }
 };
 
@@ -130,12 +134,14 @@ void plan_range(sg::Batch& B, const sg_call_desc* calls, int64_t c0, int64_t c1)
   B.call_len.assign(n, 0);
   B.call_off.assign(n, 0);
   B.call_status.assign(n, 0);
+  B.call_fp64.assign(n, 0);
   B.call_msg.assign(n, "");
   int64_t off = 0;
   for (int64_t i = 0; i < n; ++i) {
     const sg_call_desc& d = calls[c0 + i];
     Checkpoint cp(B);
     const int first_syl = (int)B.syls.size();
+    const int64_t hp0 = B.hp_bouts;
     try {
       sg::Rng R;
       R.s = &d.random;
@@ -158,6 +164,7 @@ void plan_range(sg::Batch& B, const sg_call_desc* calls, int64_t c0, int64_t c1)
       }
       B.call_off[i] = off;
       B.call_len[i] = L;
+      B.call_fp64[i] = (int32_t)(B.hp_bouts - hp0);
       off += (L + 63) / 64 * 64;  // 256-B aligned call slots
     } catch (const sg::SgError& e) {
       cp.restore(B);
@@ -182,6 +189,7 @@ int plan_threads(int64_t n_calls) {
 // Where one part's arrays land in the merged batch.
 struct PartBase {
   int64_t out, fs, fl, w, amp, knot, ck, task, seg, syl, piece, st, item, copy, call, epoch, fe, term, col, job;
+  int64_t w64, fh, fr64;
   int64_t fr[2], ola[2], mix[2];
 };
 
@@ -222,6 +230,8 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
     c.copy += (int64_t)S.copies.size(); c.call += (int64_t)S.call_len.size(); c.epoch += (int64_t)S.epochs.size();
     c.fe += S.fe_total; c.term += (int64_t)S.eterms.size(); c.col += (int64_t)S.ecols.size();
     c.job += (int64_t)S.envjobs.size();
+    c.w64 += S.w64_total; c.fh += S.fh_total; c.fr64 += (int64_t)S.frames64.size();
+    D.hp_bouts += S.hp_bouts;
     for (int ph = 0; ph < 2; ++ph) {
       c.fr[ph] += (int64_t)S.frames[ph].size(); c.ola[ph] += (int64_t)S.olas[ph].size();
       c.mix[ph] += (int64_t)S.mixes[ph].size();
@@ -230,8 +240,10 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
     D.fft_frames += S.fft_frames;
   }
   D.total_out = c.out; D.fs_total = c.fs; D.w_total = c.w; D.fe_total = c.fe;
+  D.w64_total = c.w64; D.fh_total = c.fh; D.frames64.resize(c.fr64);
   D.eterms.resize(c.term); D.ecols.resize(c.col); D.envjobs.resize(c.job);
   D.call_len.resize(c.call); D.call_off.resize(c.call); D.call_status.resize(c.call); D.call_msg.resize(c.call);
+  D.call_fp64.resize(c.call);
   D.segs.resize(c.seg); D.epochs.resize(c.epoch); D.knots.resize(c.knot); D.amps.resize(c.amp);
   D.tasks.resize(c.task); D.pieces.resize(c.piece); D.syls.resize(c.syl); D.syl_tiles.resize(c.st);
   D.cknots.resize(c.ck); D.fl.resize(c.fl); D.items.resize(c.item); D.copies.resize(c.copy);
@@ -248,17 +260,24 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
       D.call_len[b.call + i] = S.call_len[i];
       D.call_off[b.call + i] = S.call_off[i] + b.out;
       D.call_status[b.call + i] = S.call_status[i];
+      D.call_fp64[b.call + i] = S.call_fp64[i];
       D.call_msg[b.call + i] = std::move(S.call_msg[i]);
     }
     for (auto& e : S.epochs) {
       e.w_off += b.w; e.amp_off += b.amp; e.da_off += b.amp; e.knot_off += b.knot;
       e.seg_off += (int32_t)b.seg; e.syl += (int32_t)b.syl;
     }
-    for (auto& t : S.tasks) { t.w_off += b.w; t.a_off += b.amp; t.d_off += b.amp; t.syl += (int32_t)b.syl; }
-    for (auto& p : S.pieces)
-      for (int q = 0; q < (p.nterms < 0 ? 1 : p.nterms); ++q) p.t[q].src += b.w;
+    for (auto& t : S.tasks) {
+      t.w_off += (t.flags & SG_TASK_HP) ? b.w64 : b.w;
+      t.a_off += b.amp; t.d_off += b.amp; t.syl += (int32_t)b.syl;
+    }
+    for (auto& s : S.syls)  // a syllable's pieces read W, or W64 for an fp64 syllable
+      for (int32_t pi = s.piece0; pi < s.piece0 + s.npiece; ++pi) {
+        SgPiece& p = S.pieces[pi];
+        for (int q = 0; q < (p.nterms < 0 ? 1 : p.nterms); ++q) p.t[q].src += s.hp ? b.w64 : b.w;
+      }
     for (auto& s : S.syls) {
-      s.out_off += s.dst_fs ? b.fs : b.out;
+      s.out_off += s.hp ? b.fh : (s.dst_fs ? b.fs : b.out);
       s.piece0 += (int32_t)b.piece; s.max_slot += (int32_t)b.syl; s.task0 += b.task;
       ck(s.env);
       if (s.drift.nk > 0) s.drift.k_off += b.ck;
@@ -275,12 +294,12 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
       }
       for (auto& g : S.frame_geom[ph]) g = gmap[k][g];
       for (auto& o : S.olas[ph]) {
-        o.fidx += (int32_t)b.fr[ph];
+        if (o.fidx >= 0) o.fidx += (int32_t)b.fr[ph];
         if (!o.fused) o.frames += b.fs;
         o.out += b.fs;
       }
       for (auto& m : S.mixes[ph]) {
-        m.dst += m.to_fs ? b.fs : b.out;
+        m.dst += m.to_fs == 2 ? b.fh : (m.to_fs ? b.fs : b.out);
         if (m.base_kind != SG_BASE_NONE) m.base += b.fs;
         if (m.base_kind == SG_BASE_NORM) m.base_ola += (int32_t)b.ola[1];
         m.item0 += (int32_t)b.item;
@@ -288,8 +307,13 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
         ck(m.mult);
       }
     }
+    for (auto& f : S.frames64) {
+      f.src += b.fh;
+      f.env = f.env < 0 ? f.env - b.fe : f.env + b.fl;
+      f.dst += b.fs;
+    }
     for (auto& it : S.items) {
-      it.raw += b.fs;
+      it.raw += (it.flags & SG_ITEM_F64) ? b.fh : b.fs;
       if (it.flags & SG_ITEM_FILTER_OLA) it.ola += (int32_t)b.ola[1];
       else if (it.ola >= 0) it.ola += (int32_t)b.ola[0];
       ck(it.strength);
@@ -301,6 +325,7 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
     put(D.amps, S.amps, b.amp); put(D.tasks, S.tasks, b.task); put(D.pieces, S.pieces, b.piece);
     put(D.syls, S.syls, b.syl); put(D.syl_tiles, S.syl_tiles, b.st); put(D.cknots, S.cknots, b.ck);
     put(D.fl, S.fl, b.fl); put(D.items, S.items, b.item); put(D.copies, S.copies, b.copy);
+    put(D.frames64, S.frames64, b.fr64);
     for (int ph = 0; ph < 2; ++ph) {
       put(D.frames[ph], S.frames[ph], b.fr[ph]); put(D.frame_geom[ph], S.frame_geom[ph], b.fr[ph]);
       put(D.olas[ph], S.olas[ph], b.ola[ph]); put(D.mixes[ph], S.mixes[ph], b.mix[ph]);
@@ -589,6 +614,19 @@ int sg_plan_stft_stats(const sg_plan* plan, int64_t* samples, int64_t* alg_bytes
   *samples = plan->B.stft_samples;
   *alg_bytes = plan->B.stft_bytes;
   *flops = plan->B.stft_flops;
+  return SG_OK;
+}
+
+int sg_plan_precision(const sg_plan* plan, int32_t* call_fp64, int64_t* fp64_frames, int64_t* fp64_tasks) {
+  if (!plan) return SG_E_ARG;
+  const sg::Batch& B = plan->B;
+  if (call_fp64) std::memcpy(call_fp64, B.call_fp64.data(), B.call_fp64.size() * sizeof(int32_t));
+  if (fp64_frames) *fp64_frames = (int64_t)B.frames64.size();
+  if (fp64_tasks) {
+    int64_t n = 0;
+    for (const SgWTask& t : B.tasks) n += (t.flags & SG_TASK_HP) ? 1 : 0;
+    *fp64_tasks = n;
+  }
   return SG_OK;
 }
 

@@ -58,6 +58,9 @@ constexpr int SG_TASK_ENV = 4;    // the syllable has an amplitude envelope (max
 #endif
 constexpr int SG_ROWS_F32 = SG_ROWS_F32_N;
 constexpr int SG_TASK_LIN = 2;    // phase segment linear (c2 = c3 = c4 = 0): one fp64 FMA per sample
+// fp64 source of an ill-conditioned formant-filter call (planner: filter_conditioning,
+// sg_plan_soundgen.cpp): fp64 angle and recurrence, w_off indexes the fp64 epoch scratch W64
+constexpr int SG_TASK_HP = 8;
 constexpr int SG_TASK_MAX = 1024;  // samples per task (16 slots of 64 lanes)
 struct SgWTask {
   int64_t w_off;       // W offset of epoch sample 0
@@ -163,7 +166,7 @@ struct SgSyllable {
   int32_t ptile0;    // crossfade-piece tiles: per-tile max slots [ptile0, ptile0+nptile)
   int32_t nptile;
   int32_t dst_fs;    // 1: out_off is in the spectral scratch (voiced part of a soundgen() bout)
-  int32_t pad2;
+  int32_t hp;        // 1: fp64 syllable: pieces read W64, out_off indexes the fp64 scratch fh
   SgContour env;     // amplEnvelope (kind 0 = none)
   SgLinear drift;
 };
@@ -245,6 +248,16 @@ struct SgFrame {
   int64_t env;  // fl offset of the nr envelope (FILTER) / filter (NOISE) values
   int64_t dst;  // fs offset of the wl windowed ISTFT outputs
 };
+// A formant-filter frame of an ill-conditioned call (sg_fft_frames64): the fp64
+// sound fh[src .. src + wl) -> hamming -> fp64 DFT / wl -> x env (fp32 envelope
+// area / fl) -> fp64 inverse DFT / 2M -> x hann -> fs[dst .. dst + wl) (fp32, for sg_ola)
+struct SgFrame64 {
+  int64_t src;
+  int64_t env;
+  int64_t dst;
+  int32_t wl;
+  int32_t pad;
+};
 struct SgFrameGroup {  // frames of one workgroup: same geometry and mode
   int32_t geom, mode;
   int32_t f0, nf;
@@ -305,6 +318,7 @@ struct SgNoiseItem {
 };
 constexpr int SG_ITEM_FILTER_OLA = 1;  // ola indexes the filter-phase OLAs (shifted at finalize)
 constexpr int SG_ITEM_ZERO = 2;        // all-zero content (R's rep(0, len)): layout only
+constexpr int SG_ITEM_F64 = 4;         // raw indexes the fp64 scratch fh (voiced part of an fp64 bout)
 // One output range: v = base + sum(noise items), * mult contour, * AM trill.
 constexpr int SG_BASE_NONE = 0;  // zeros
 constexpr int SG_BASE_RAW = 1;   // fs[base + k]
@@ -315,7 +329,7 @@ struct SgMix {
   int64_t base, base_len;
   int32_t base_kind, base_ola;
   int32_t item0, nitems;
-  int32_t to_fs;
+  int32_t to_fs;      // 0: output buffer, 1: fs, 2: fh (fp64 sound of an ill-conditioned filter call)
   int32_t am_lo;      // AM trill: half period of the sigmoid table (0: none)
   int64_t am_tab;     // fl offset of the sigmoid half period
   float am_dep, pad;

@@ -22,7 +22,7 @@ constexpr size_t ALIGN = 256;
 size_t up(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
 struct Layout {
-  size_t tall, tlong, tshort, tallp;
+  size_t tall, tlong, tshort, tallp, thp, fin_tiles_hp, W64, fh, frames64;
   size_t segs, epochs, knots, amps, tasks, pieces, syls, syl_tiles, copy_tiles, ptiles, cknots, W, taskmax, ptilemax, maxes, total;
   size_t geoms, frames, fgroups, olas, olatiles, olasegs, olatilemax, olamax, items, mixes, mixtiles, fl, fs;
   size_t eterms, ecols, envjobs, envtasks, elog2;
@@ -38,6 +38,11 @@ struct Layout {
     tlong = take(B.tasks.size() * sizeof(int32_t));
     tshort = take(B.tasks.size() * sizeof(int32_t));
     tallp = take(B.tasks.size() * sizeof(int32_t));
+    thp = take(B.tasks.size() * sizeof(int32_t));
+    fin_tiles_hp = take(B.fin_tiles_hp.size() * sizeof(SgSylTile));
+    W64 = take((size_t)B.w64_total * sizeof(double));
+    fh = take((size_t)B.fh_total * sizeof(double));
+    frames64 = take(B.frames64.size() * sizeof(SgFrame64));
     pieces = take(B.pieces.size() * sizeof(SgPiece));
     syls = take(B.syls.size() * sizeof(SgSyllable));
     syl_tiles = take(B.fin_tiles.size() * sizeof(SgSylTile));
@@ -81,9 +86,14 @@ static void split_finalize_tiles(Batch& B) {
   int64_t copy_tile = SG_COPY_TILE;
   if (const char* e = std::getenv("SG_COPY_TILE")) copy_tile = std::min<int64_t>(SG_COPY_TILE_MAX, std::max(1024, std::atoi(e)));
   B.fin_tiles.clear();
+  B.fin_tiles_hp.clear();
   B.copy_tiles.clear();
   for (const SgSylTile& t : B.syl_tiles) {
     const SgSyllable& sy = B.syls[t.syl];
+    if (sy.hp) {  // fp64 syllable: sg_harm_finalize_hp
+      B.fin_tiles_hp.push_back(t);
+      continue;
+    }
     const int64_t end = std::min<int64_t>(t.k0 + 1024, sy.L);
     const int pend = sy.piece0 + sy.npiece;
     bool ok = sy.env.kind == 0 && sy.drift.nk == 0;
@@ -165,14 +175,21 @@ void finalize_plan(Batch& B) {
                    k ? "tall" : "fp32", (long long)nshort[k], sterms[k], (long long)lh[k][0], (long long)lh[k][1],
                    (long long)lh[k][2], (long long)lh[k][3], (long long)lh[k][4]);
   }
+  // crossfade-piece tiles: fp32 syllables first, then the fp64 ones (sg_piece_max_hp)
   B.ptiles.clear();
-  for (size_t s = 0; s < B.syls.size(); ++s) {
-    SgSyllable& sy = B.syls[s];
-    sy.ptile0 = (int32_t)B.ptiles.size();
-    for (int32_t p = sy.piece0; p < sy.piece0 + sy.npiece; ++p)
-      if (B.pieces[p].nterms > 0)
-        for (int64_t q0 = 0; q0 < B.pieces[p].len; q0 += 256) B.ptiles.push_back(SgSylTile{(int32_t)s, p, q0});
-    sy.nptile = (int32_t)B.ptiles.size() - sy.ptile0;
+  bool any_hp = false;
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass == 1) B.ptile_hp = (int64_t)B.ptiles.size();
+    for (size_t s = 0; s < B.syls.size(); ++s) {
+      SgSyllable& sy = B.syls[s];
+      if ((sy.hp != 0) != (pass == 1)) continue;
+      any_hp |= sy.hp != 0;
+      sy.ptile0 = (int32_t)B.ptiles.size();
+      for (int32_t p = sy.piece0; p < sy.piece0 + sy.npiece; ++p)
+        if (B.pieces[p].nterms > 0)
+          for (int64_t q0 = 0; q0 < B.pieces[p].len; q0 += 256) B.ptiles.push_back(SgSylTile{(int32_t)s, p, q0});
+      sy.nptile = (int32_t)B.ptiles.size() - sy.ptile0;
+    }
   }
   // slices of whole syllables with about equal sample counts
   B.slices.clear();
@@ -182,6 +199,7 @@ void finalize_plan(Batch& B) {
   for (const SgSyllable& sy : B.syls) total += sy.L;
   int slices = SG_SLICES;
   if (const char* e = std::getenv("SG_SLICES")) slices = std::max(1, std::atoi(e));  // experiment knob
+  if (any_hp) slices = 1;  // the fp64 syllables' tiles are listed after every fp32 one
   const int K = (int)std::min<int64_t>(slices, nsyl);
   int64_t acc = 0, ft = 0, ct = 0;
   int32_t s0 = 0;
@@ -193,8 +211,8 @@ void finalize_plan(Batch& B) {
     c.s0 = s0; c.s1 = s + 1;
     c.t0 = B.syls[s0].task0;
     c.t1 = B.syls[s].task0 + B.syls[s].ntask;
-    c.p0 = B.syls[s0].ptile0;
-    c.p1 = B.syls[s].ptile0 + B.syls[s].nptile;
+    c.p0 = K == 1 ? 0 : B.syls[s0].ptile0;
+    c.p1 = K == 1 ? B.ptile_hp : B.syls[s].ptile0 + B.syls[s].nptile;
     c.f0 = ft;
     while (ft < (int64_t)B.fin_tiles.size() && B.fin_tiles[ft].syl <= s) ++ft;
     c.f1 = ft;
@@ -234,6 +252,11 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   D.tlong = (int32_t*)(a + L.tlong);
   D.tshort = (int32_t*)(a + L.tshort);
   D.tallp = (int32_t*)(a + L.tallp);
+  D.thp = (int32_t*)(a + L.thp);
+  D.fin_tiles_hp = (SgSylTile*)(a + L.fin_tiles_hp);
+  D.W64 = (double*)(a + L.W64);
+  D.fh = (double*)(a + L.fh);
+  D.frames64 = (SgFrame64*)(a + L.frames64);
   D.pieces = (SgPiece*)(a + L.pieces);
   D.syls = (SgSyllable*)(a + L.syls);
   D.syl_tiles = (SgSylTile*)(a + L.syl_tiles);
@@ -276,10 +299,12 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   D.tlong_host.clear();
   D.tshort_host.clear();
   D.tallp_host.clear();
+  D.thp_host.clear();
   for (size_t i = 0; i < B.tasks.size(); ++i) {
     const SgWTask& t = B.tasks[i];
     const bool shrt = t.len <= 64 && !(t.flags & SG_TASK_ENV);
-    if (t.R > SG_ROWS_F32) (SG_TALL_PAIR && shrt ? D.tallp_host : D.tall_host).push_back((int32_t)i);
+    if (t.flags & SG_TASK_HP) D.thp_host.push_back((int32_t)i);
+    else if (t.R > SG_ROWS_F32) (SG_TALL_PAIR && shrt ? D.tallp_host : D.tall_host).push_back((int32_t)i);
     else if (SG_PAIR && t.len <= 64 && !(t.flags & SG_TASK_ENV)) D.tshort_host.push_back((int32_t)i);
     else D.tlong_host.push_back((int32_t)i);
   }
@@ -287,6 +312,9 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   cp(D.tlong, D.tlong_host.data(), D.tlong_host.size() * sizeof(int32_t));
   cp(D.tshort, D.tshort_host.data(), D.tshort_host.size() * sizeof(int32_t));
   cp(D.tallp, D.tallp_host.data(), D.tallp_host.size() * sizeof(int32_t));
+  cp(D.thp, D.thp_host.data(), D.thp_host.size() * sizeof(int32_t));
+  cp(D.fin_tiles_hp, B.fin_tiles_hp.data(), B.fin_tiles_hp.size() * sizeof(SgSylTile));
+  cp(D.frames64, B.frames64.data(), B.frames64.size() * sizeof(SgFrame64));
   cp(D.pieces, B.pieces.data(), B.pieces.size() * sizeof(SgPiece));
   cp(D.syls, B.syls.data(), B.syls.size() * sizeof(SgSyllable));
   cp(D.syl_tiles, B.fin_tiles.data(), B.fin_tiles.size() * sizeof(SgSylTile));
@@ -324,6 +352,10 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
 // maxima, finalize
 static void device_execute_harm(const Batch& B, DevicePlan& D, float* d_out, hipStream_t h,
                                 std::vector<SgProfEvent>* prof) {
+  // fp64 syllables: their sine-bank tasks and crossfade maxima first, so the
+  // slices' per-syllable maxima include them; their finalize after the slices
+  launch_sine_bank_hp(D, (int64_t)D.thp_host.size(), h);
+  launch_piece_max_hp(D, B.ptile_hp, (int64_t)B.ptiles.size() - B.ptile_hp, h);
   for (size_t c = 0; c < B.slices.size(); ++c) {
     const Slice& sl = B.slices[c];
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -358,6 +390,7 @@ static void device_execute_harm(const Batch& B, DevicePlan& D, float* d_out, hip
     launch_harm_copy(D, sl.c0, sl.c1 - sl.c0, d_out, h);
     launch_harm_finalize(D, sl.f0, sl.f1 - sl.f0, d_out, h);
   }
+  launch_harm_finalize_hp(D, (int64_t)B.fin_tiles_hp.size(), h);
 }
 
 // The harmonic source (sine banks -> maxima -> finalize) and the noise phase
@@ -428,6 +461,7 @@ void device_execute_spec(const Batch& B, const DevicePlan& D, float* d_out, hipS
       prof->push_back({SG_PROF_STFT_OLA, e0, e1});
     }
     launch_fft_frames(D, r[1], r[2] - r[1], B.fgroup_lds[ph][1], s);
+    if (ph == 1) launch_fft_frames64(D, (int64_t)B.frames64.size(), B.frames64_wl, s);
     const int64_t t0 = ph == 0 ? 0 : B.olatile_split, t1 = ph == 0 ? B.olatile_split : (int64_t)B.olatiles.size();
     const int64_t o0 = ph == 0 ? 0 : B.ola_split, o1 = ph == 0 ? B.ola_split : (int64_t)B.olas_dev.size();
     launch_ola(D, t0, t1 - t0, s);
@@ -437,7 +471,8 @@ void device_execute_spec(const Batch& B, const DevicePlan& D, float* d_out, hipS
   for (const Batch::Copy& c : B.copies)
     HIPCHK(hipMemcpyAsync(D.fs + c.fs_off, D.fl + c.fl_off, (size_t)c.n * sizeof(float), hipMemcpyDeviceToDevice, s));
   if (join) HIPCHK(hipStreamWaitEvent(s, harm_done, 0));  // the harmonic syllables (fs, out) are final
-  launch_mix(D, 0, B.mixtile_split, d_out, s);
+  launch_mix(D, 0, B.mixtile_hp, d_out, s);
+  launch_mix_hp(D, B.mixtile_hp, B.mixtile_split - B.mixtile_hp, s);
   phase(1);
   launch_mix(D, B.mixtile_split, (int64_t)B.mixtiles.size() - B.mixtile_split, d_out, s);
   HIPCHK(hipGetLastError());

@@ -38,6 +38,12 @@ struct DevicePlan {
   std::vector<int32_t> tshort_host;
   int32_t* tallp = nullptr;          // tall tasks of <= 64 samples, two per wave (sg_sine_bank_tall_pairs)
   std::vector<int32_t> tallp_host;
+  int32_t* thp = nullptr;            // SG_TASK_HP tasks (sg_sine_bank_hp)
+  std::vector<int32_t> thp_host;
+  SgSylTile* fin_tiles_hp = nullptr; // finalize tiles of fp64 syllables (sg_harm_finalize_hp)
+  double* W64 = nullptr;             // fp64 epoch waveforms of SG_TASK_HP tasks
+  double* fh = nullptr;              // fp64 sounds (voiced parts, pre-filter sounds) of fp64 bouts
+  SgFrame64* frames64 = nullptr;     // their filter frames (sg_fft_frames64)
   SgPiece* pieces = nullptr;
   SgSyllable* syls = nullptr;
   SgSylTile* syl_tiles = nullptr;    // general-path finalize tiles (Batch::fin_tiles)
@@ -103,6 +109,12 @@ void launch_syl_max(const DevicePlan& D, int64_t s0, int64_t n_syls, hipStream_t
 void launch_piece_max(const DevicePlan& D, int64_t p0, int64_t n_ptiles, hipStream_t s);
 void launch_harm_finalize(const DevicePlan& D, int64_t f0, int64_t n_stiles, float* out, hipStream_t s);
 void launch_harm_copy(const DevicePlan& D, int64_t c0, int64_t n_ctiles, float* out, hipStream_t s);
+// the fp64 path of ill-conditioned formant-filter calls (SG_TASK_HP, SgSyllable::hp, sg_mix to fh, SgFrame64)
+void launch_sine_bank_hp(const DevicePlan& D, int64_t n, hipStream_t s);
+void launch_piece_max_hp(const DevicePlan& D, int64_t p0, int64_t n_ptiles, hipStream_t s);
+void launch_harm_finalize_hp(const DevicePlan& D, int64_t n_stiles, hipStream_t s);
+void launch_mix_hp(const DevicePlan& D, int64_t t0, int64_t n_tiles, hipStream_t s);
+void launch_fft_frames64(const DevicePlan& D, int64_t n_frames, int max_wl, hipStream_t s);
 // sg_fft.hip
 void launch_fft_frames(const DevicePlan& D, int64_t g0, int64_t n_groups, int lds_bytes, hipStream_t s);
 void launch_stft_ola(const DevicePlan& D, int phase, int64_t s0, int64_t n_segs, int lds_bytes, hipStream_t s);

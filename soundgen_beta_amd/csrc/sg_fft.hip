@@ -18,6 +18,8 @@
 // and writes per-tile maxima for the following normalisation.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "sg_dev.h"
 #ifndef SG_FFT_WPE
 #define SG_FFT_WPE 2  // build knob: waves per SIMD for sg_stft_ola
@@ -1088,16 +1090,135 @@ __device__ __forceinline__ float fade_in_out(int lf, int64_t L, int64_t k) {  //
   return f;
 }
 
-extern "C" __global__ __launch_bounds__(256) void sg_mix(const SgMixTile* __restrict__ tiles,
-                                                         const SgMix* __restrict__ mixes,
-                                                         const SgNoiseItem* __restrict__ items,
-                                                         const float* __restrict__ olamax,
-                                                         const double* __restrict__ cknots,
-                                                         const float* __restrict__ fl, float* __restrict__ fs,
-                                                         float* __restrict__ out) {
+// ------------------------------------------------ fp64 filter frames
+// Frames of an ill-conditioned formant-filter call (SgFrame64; planner:
+// filter_conditioning): seewave's stft x env -> istft for ONE frame per
+// workgroup, in fp64: the wl-point DFT of the hamming-windowed fp64 sound,
+// / wl, x the envelope column, seewave's Hermitian extension to 2M points
+// (Nyquist = Re Y_{M-1}, seewave.r:3474), the 2M-point inverse DFT / 2M, x hann,
+// written as fp32 for the overlap-add (sg_ola; its round-off is relative to
+// the filtered output, ~1e-8 RMS). Stockham autosort, out of place in LDS,
+// radices 4, 2, then odd primes <= 31; an R-point butterfly is a direct sum
+// over a per-frame table of the n-th roots of unity (fp64 sincospi).
+namespace {
+__device__ __forceinline__ double2 cmul64(double2 a, double2 b) {
+  return make_double2(fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x));
+}
+__device__ __forceinline__ double2 root64(const double2* __restrict__ T, int t, bool inv) {
+  const double2 w = T[t];
+  return inv ? make_double2(w.x, -w.y) : w;
+}
+template <int R>
+__device__ void stage64(const double2* __restrict__ src, double2* __restrict__ dst, int n, int Ns,
+                        const double2* __restrict__ T, bool inv) {
+  const int nR = n / R, tstep = n / (Ns * R);
+  for (int j = threadIdx.x; j < nR; j += blockDim.x) {
+    const int jm = j % Ns;
+    double2 v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      v[r] = src[j + r * nR];
+      if (r > 0 && jm > 0) v[r] = cmul64(v[r], root64(T, r * jm * tstep, inv));
+    }
+    double2* y = dst + (j - jm) * R + jm;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      double2 acc = v[0];
+#pragma unroll
+      for (int r = 1; r < R; ++r) {
+        const double2 w = root64(T, ((r * k) % R) * nR, inv);
+        acc.x = fma(v[r].x, w.x, fma(-v[r].y, w.y, acc.x));
+        acc.y = fma(v[r].x, w.y, fma(v[r].y, w.x, acc.y));
+      }
+      y[k * Ns] = acc;
+    }
+  }
+}
+// n-point complex DFT of *a (result in *a, *b is the other buffer), T = roots of unity of n
+__device__ void fft64(double2*& a, double2*& b, int n, const double2* __restrict__ T, bool inv) {
+  int rest = n, Ns = 1;
+  while (rest > 1) {
+    int R = rest % 4 == 0 ? 4 : rest % 2 == 0 ? 2 : 0;
+    if (!R)
+      for (int p : {3, 5, 7, 11, 13, 17, 19, 23, 29, 31})
+        if (rest % p == 0) { R = p; break; }
+    switch (R) {
+#define SG_S64(RR) case RR: stage64<RR>(a, b, n, Ns, T, inv); break;
+      SG_S64(2) SG_S64(3) SG_S64(4) SG_S64(5) SG_S64(7) SG_S64(11) SG_S64(13) SG_S64(17) SG_S64(19) SG_S64(23)
+      SG_S64(29) SG_S64(31)
+#undef SG_S64
+      default: return;  // the planner only sends 31-smooth sizes
+    }
+    __syncthreads();
+    double2* t = a; a = b; b = t;
+    Ns *= R;
+    rest /= R;
+  }
+}
+__device__ void roots64(double2* T, int n) {
+  for (int t = threadIdx.x; t < n; t += blockDim.x) {
+    double sn, cs;
+    sincospi(-2.0 * (double)t / (double)n, &sn, &cs);
+    T[t] = make_double2(cs, sn);
+  }
+  __syncthreads();
+}
+}  // namespace
+
+extern "C" __global__ __launch_bounds__(256) void sg_fft_frames64(const SgFrame64* __restrict__ frames,
+                                                                  const float* __restrict__ fl,
+                                                                  const double* __restrict__ fh,
+                                                                  float* __restrict__ fs) {
+  extern __shared__ double2 lds64[];
+  const SgFrame64 F = frames[blockIdx.x];
+  const int N = F.wl, M = N / 2, N2 = 2 * M;
+  const int cap = N;  // N >= N2
+  double2* a = lds64;
+  double2* b = a + cap;
+  double2* T = b + cap;
+  roots64(T, N);
+  const double* x = fh + F.src;
+  const double wd = (double)(N - 1);
+  for (int n = threadIdx.x; n < N; n += blockDim.x)  // hamming (seewave ftwindow)
+    a[n] = make_double2(x[n] * (0.54 - 0.46 * cospi(2.0 * (double)n / wd)), 0.0);
+  __syncthreads();
+  fft64(a, b, N, T, false);
+  const float* env = fl + F.env;
+  const double invN = 1.0 / (double)N;
+  // Y_k = X_k / N * env_k (k < M) into b, with its Hermitian extension to 2M points
+  for (int k = threadIdx.x; k < M; k += blockDim.x) {
+    const double sc = invN * (double)env[k];
+    const double2 y = make_double2(a[k].x * sc, a[k].y * sc);
+    b[k] = y;
+    if (k > 0) b[N2 - k] = make_double2(y.x, -y.y);
+    if (k == M - 1) b[M] = make_double2(y.x, 0.0);
+  }
+  __syncthreads();
+  if (N2 != N) roots64(T, N2);
+  double2* c = b;
+  double2* d = a;
+  fft64(c, d, N2, T, true);
+  const double invN2 = 1.0 / (double)N2;
+  float* out = fs + F.dst;
+  for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    const double han = 0.5 - 0.5 * cospi(2.0 * (double)i / wd);
+    out[i] = (float)(c[i < N2 ? i : i - N2].x * invN2 * han);
+  }
+}
+
+// HP: the pre-filter sound of an fp64 bout: fp64 sum into fh (X.to_fs == 2), voiced
+// items (SG_ITEM_F64) read from fh, noise items from fs
+template <bool HP>
+__device__ __forceinline__ void mix_body(const SgMixTile* __restrict__ tiles, const SgMix* __restrict__ mixes,
+                                         const SgNoiseItem* __restrict__ items, const float* __restrict__ olamax,
+                                         const double* __restrict__ cknots, const float* __restrict__ fl,
+                                         float* __restrict__ fs, float* __restrict__ out, double* __restrict__ fh) {
+  using V = typename std::conditional<HP, double, float>::type;
   const SgMixTile T = tiles[blockIdx.x];
   const SgMix& X = mixes[T.mix];
-  float* __restrict__ dst = X.to_fs ? fs : out;
+  V* __restrict__ dst;
+  if constexpr (HP) dst = fh;
+  else dst = X.to_fs ? fs : out;
 #ifndef SG_MIX_E
 #define SG_MIX_E 8  // build knob: samples per thread and chunk (8: 2.94 -> 2.75 ms per C5 16k-call launch)
 #endif
@@ -1129,7 +1250,7 @@ extern "C" __global__ __launch_bounds__(256) void sg_mix(const SgMixTile* __rest
 #endif
 #pragma unroll 1
   for (int64_t kc = T.k0; kc < kend; kc += E * 256) {
-    float v[E];
+    V v[E];
     // loads are unconditional (clamped addresses), selects afterwards: a load
     // under a branch is followed by its own vmcnt(0) wait, serialising the chunk
 #pragma unroll
@@ -1137,7 +1258,7 @@ extern "C" __global__ __launch_bounds__(256) void sg_mix(const SgMixTile* __rest
       const int64_t k = kc + e * 256 + threadIdx.x;
       const bool in = has_base && k < kend && k < X.base_len;
       const float x = fs[X.base + (in ? k : 0)];
-      v[e] = in ? x * base_scale : 0.f;
+      v[e] = in ? (V)(x * base_scale) : (V)0;
     }
     // noise items: descriptor once per chunk, then its samples (addVectors)
     for (int i = 0; i < X.nitems; ++i) {
@@ -1147,30 +1268,33 @@ extern "C" __global__ __launch_bounds__(256) void sg_mix(const SgMixTile* __rest
       const float nscale = it.ola >= 0 ? 1.f / olamax[it.ola] : 1.f;
       const bool flat = it.strength.kind == 1;
       const float sflat = flat ? (float)contour_at(it.strength, cknots, it.len, 0) : 1.f;
-      float raw[E];
+      V raw[E];
+      const bool f64 = HP && (it.flags & SG_ITEM_F64);
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const int64_t j = j0 + e * 256;
-        raw[e] = fs[it.raw + (j < 0 ? 0 : (j >= it.len ? it.len - 1 : j))];
+        const int64_t jj = it.raw + (j < 0 ? 0 : (j >= it.len ? it.len - 1 : j));
+        if constexpr (HP) raw[e] = f64 ? fh[jj] : (V)fs[jj];
+        else raw[e] = fs[jj];
       }
       int cur = i < NC ? curs[i][threadIdx.x] : -1;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const int64_t k = kc + e * 256 + threadIdx.x, j = j0 + e * 256;
         if (k >= kend || j < 0 || j >= it.len) continue;
-        float nv = raw[e] * nscale;
-        if (flat) nv *= sflat;
+        V nv = raw[e] * (V)nscale;
+        if (flat) nv *= (V)sflat;
         else if (it.strength.kind != 0) {
 #if SG_MIX_LDS_SPLINE
           if (i < NC && lds_ok(it.strength)) {
             SgContour cl = it.strength;
             cl.k_off = 0;
-            nv = (float)((double)nv * sgd::contour_at_cursor(cl, &cks[i][0], it.len, j, cur));
+            nv = (V)((double)nv * sgd::contour_at_cursor(cl, &cks[i][0], it.len, j, cur));
           } else
 #endif
-            nv = (float)((double)nv * sgd::contour_at_cursor(it.strength, cknots, it.len, j, cur));
+            nv = (V)((double)nv * sgd::contour_at_cursor(it.strength, cknots, it.len, j, cur));
         }
-        nv *= fade_in_out(it.fade, it.len, j);
+        nv *= (V)fade_in_out(it.fade, it.len, j);
         v[e] += nv;
       }
       if (i < NC) curs[i][threadIdx.x] = cur;
@@ -1183,12 +1307,12 @@ extern "C" __global__ __launch_bounds__(256) void sg_mix(const SgMixTile* __rest
         if (lds_ok(X.mult)) {
           SgContour cl = X.mult;
           cl.k_off = 0;
-          v[e] = (float)((double)v[e] * sgd::contour_at_cursor(cl, &cks[NC][0], X.len, k, mcur));
+          v[e] = (V)((double)v[e] * sgd::contour_at_cursor(cl, &cks[NC][0], X.len, k, mcur));
         } else
 #endif
-          v[e] = (float)((double)v[e] * sgd::contour_at_cursor(X.mult, cknots, X.len, k, mcur));
+          v[e] = (V)((double)v[e] * sgd::contour_at_cursor(X.mult, cknots, X.len, k, mcur));
       }
-      if (X.am_lo > 0) v[e] *= 1.f - sigmoid_at(fl + X.am_tab, X.am_lo, k) * X.am_dep / 100.f;
+      if (X.am_lo > 0) v[e] *= (V)(1.f - sigmoid_at(fl + X.am_tab, X.am_lo, k) * X.am_dep / 100.f);
     }
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -1196,6 +1320,25 @@ extern "C" __global__ __launch_bounds__(256) void sg_mix(const SgMixTile* __rest
       if (k < kend) dst[X.dst + k] = v[e];
     }
   }
+}
+
+extern "C" __global__ __launch_bounds__(256) void sg_mix(const SgMixTile* __restrict__ tiles,
+                                                         const SgMix* __restrict__ mixes,
+                                                         const SgNoiseItem* __restrict__ items,
+                                                         const float* __restrict__ olamax,
+                                                         const double* __restrict__ cknots,
+                                                         const float* __restrict__ fl, float* __restrict__ fs,
+                                                         float* __restrict__ out) {
+  mix_body<false>(tiles, mixes, items, olamax, cknots, fl, fs, out, nullptr);
+}
+extern "C" __global__ __launch_bounds__(256) void sg_mix_hp(const SgMixTile* __restrict__ tiles,
+                                                            const SgMix* __restrict__ mixes,
+                                                            const SgNoiseItem* __restrict__ items,
+                                                            const float* __restrict__ olamax,
+                                                            const double* __restrict__ cknots,
+                                                            const float* __restrict__ fl, float* __restrict__ fs,
+                                                            double* __restrict__ fh) {
+  mix_body<true>(tiles, mixes, items, olamax, cknots, fl, fs, nullptr, fh);
 }
 
 // ---------------------------------------------------------------- launchers
@@ -1250,6 +1393,19 @@ void launch_fft_probe(const SgFftGeom* geom, const float* fl, float* data, int M
   hipLaunchKernelGGL(sg_fft_probe, dim3((unsigned)nframes), dim3(64), 2 * M * 8, s, geom, fl,
                      reinterpret_cast<float2*>(data), inverse);
   SG_LAUNCHED("sg_fft_probe");
+}
+void launch_fft_frames64(const DevicePlan& D, int64_t n_frames, int max_wl, hipStream_t s) {
+  if (n_frames <= 0) return;
+  const int lds = 3 * max_wl * (int)sizeof(double2);
+  lds_opt_in(reinterpret_cast<const void*>(&sg_fft_frames64), lds, "sg_fft_frames64");
+  hipLaunchKernelGGL(sg_fft_frames64, dim3((unsigned)n_frames), dim3(256), lds, s, D.frames64, D.fl, D.fh, D.fs);
+  SG_LAUNCHED("sg_fft_frames64");
+}
+void launch_mix_hp(const DevicePlan& D, int64_t t0, int64_t n_tiles, hipStream_t s) {
+  if (n_tiles <= 0) return;
+  hipLaunchKernelGGL(sg_mix_hp, dim3((unsigned)n_tiles), dim3(256), 0, s, D.mixtiles + t0, D.mixes, D.items, D.olamax,
+                     D.cknots, D.fl, D.fs, D.fh);
+  SG_LAUNCHED("sg_mix_hp");
 }
 void launch_ola(const DevicePlan& D, int64_t t0, int64_t n_tiles, hipStream_t s) {
   if (n_tiles <= 0) return;

@@ -178,10 +178,10 @@ __device__ __forceinline__ void sample_setup(const SgWTask& T, int l, float& t, 
 #ifndef SG_ROT
 #define SG_ROT 1  // build knob: linear-phase slots 1..7 by rotation of slot 0 (no per-slot fp64 / v_sin / v_cos)
 #endif
-template <int NS, bool TWO, bool ENV, bool LIN, typename Acc>
+template <int NS, bool TWO, bool ENV, bool LIN, typename Acc, typename WT = float>
 __device__ __forceinline__ void run_slots(const SgWTask& T, bool staged, float* __restrict__ la, float* __restrict__ ld,
                                           const float* __restrict__ amps, const SgSyllable* __restrict__ syls,
-                                          const double* __restrict__ cknots, float* __restrict__ W, int l0, int lane,
+                                          const double* __restrict__ cknots, WT* __restrict__ W, int l0, int lane,
                                           float& tmax, const float (&rc)[8], const float (&rs)[8]) {
   constexpr bool ROT = SG_ROT && LIN && sizeof(Acc) == 4 && NS > 1;
   float t[NS];
@@ -213,9 +213,10 @@ __device__ __forceinline__ void run_slots(const SgWTask& T, bool staged, float* 
   }
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    const float y = (float)((TWO ? fma((Acc)t[s], e1[s], b1[s]) : b1[s]) * sn[s]);
+    const Acc yv = (TWO ? fma((Acc)t[s], e1[s], b1[s]) : b1[s]) * sn[s];
+    const float y = (float)yv;
     const int j = T.j0 + l[s];
-    if (valid[s]) W[T.w_off + j] = y;
+    if (valid[s]) W[T.w_off + j] = (WT)yv;
     // fused max over the samples that land 1:1 in the syllable (branch-free)
     const bool in = valid[s] && j >= T.dj0 && j < T.dj1;
     if (!ENV) {
@@ -227,10 +228,10 @@ __device__ __forceinline__ void run_slots(const SgWTask& T, bool staged, float* 
   }
 }
 
-template <bool TWO, bool ENV, bool LIN, typename Acc = float>
+template <bool TWO, bool ENV, bool LIN, typename Acc = float, typename WT = float>
 __device__ __forceinline__ float run_task(const SgWTask& T, float* __restrict__ la, float* __restrict__ ld,
                                           const float* __restrict__ amps, const SgSyllable* __restrict__ syls,
-                                          const double* __restrict__ cknots, float* __restrict__ W, int lane) {
+                                          const double* __restrict__ cknots, WT* __restrict__ W, int lane) {
   const bool staged = T.Rn <= SG_LDS_ROWS;  // rows stay in LDS for every pass of the task
   if (staged) stage_rows<TWO>(la, ld, amps + T.a_off, amps + T.d_off, 0, T.Rn, lane);
   float tmax = 0.f;
@@ -259,23 +260,25 @@ __device__ __forceinline__ float run_task(const SgWTask& T, float* __restrict__ 
   if constexpr (!F32 && SG_F64_NS_MAX < 4) {
 #pragma unroll 1
     for (; T.len - l0 > 64; l0 += 128)
-      run_slots<2, TWO, ENV, LIN, Acc>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax, rc, rs);
-    if (l0 < T.len) run_slots<1, TWO, ENV, LIN, Acc>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax, rc, rs);
+      run_slots<2, TWO, ENV, LIN, Acc, WT>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax, rc, rs);
+    if (l0 < T.len)
+      run_slots<1, TWO, ENV, LIN, Acc, WT>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax, rc, rs);
     return tmax;
   }
   if (F32 && (!TWO || SG_NS8_TWO) && SG_NS_MAX >= 8) {
 #pragma unroll 1
     for (; T.len - l0 > 448; l0 += 512)
-      run_slots<8, TWO, ENV, LIN, Acc>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax, rc, rs);
+      run_slots<8, TWO, ENV, LIN, Acc, WT>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax, rc, rs);
   }
 #pragma unroll 1
   for (; T.len - l0 > 192; l0 += 256)
-    run_slots<4, TWO, ENV, LIN, Acc>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax, rc, rs);
+    run_slots<4, TWO, ENV, LIN, Acc, WT>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax, rc, rs);
   if (T.len - l0 > 64) {
-    run_slots<2, TWO, ENV, LIN, Acc>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax, rc, rs);
+    run_slots<2, TWO, ENV, LIN, Acc, WT>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax, rc, rs);
     l0 += 128;
   }
-  if (l0 < T.len) run_slots<1, TWO, ENV, LIN, Acc>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax, rc, rs);
+  if (l0 < T.len)
+    run_slots<1, TWO, ENV, LIN, Acc, WT>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax, rc, rs);
   return tmax;
 }
 
@@ -680,6 +683,41 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_tall_pairs(
   }
 }
 
+// ------------------------------------------- fp64 path (SG_TASK_HP tasks)
+// Tasks of an ill-conditioned formant-filter bout (planner: filter_conditioning):
+// fp64 angle (sincospi) and fp64 Clenshaw chains, the epoch waveform kept in
+// fp64 (W64). Amplitudes stay fp32: their rounding scales each harmonic by
+// (1 + 6e-8), an error at the harmonic's own frequency, which the envelope
+// weighs like the harmonic itself (only white round-off is amplified).
+__device__ __forceinline__ float run_one_hp(const SgWTask& T, float* __restrict__ la, float* __restrict__ ld,
+                                            const float* __restrict__ amps, const SgSyllable* __restrict__ syls,
+                                            const double* __restrict__ cknots, double* __restrict__ W, int lane) {
+  const bool c = T.flags & SG_TASK_CONST;
+  if (T.flags & SG_TASK_ENV)
+    return c ? run_task<false, true, false, double, double>(T, la, ld, amps, syls, cknots, W, lane)
+             : run_task<true, true, false, double, double>(T, la, ld, amps, syls, cknots, W, lane);
+  if (T.flags & SG_TASK_LIN)
+    return c ? run_task<false, false, true, double, double>(T, la, ld, amps, syls, cknots, W, lane)
+             : run_task<true, false, true, double, double>(T, la, ld, amps, syls, cknots, W, lane);
+  return c ? run_task<false, false, false, double, double>(T, la, ld, amps, syls, cknots, W, lane)
+           : run_task<true, false, false, double, double>(T, la, ld, amps, syls, cknots, W, lane);
+}
+
+extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_hp(
+    const int32_t* __restrict__ idx, int64_t n, const SgWTask* __restrict__ tasks, const float* __restrict__ amps,
+    const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, double* __restrict__ W64,
+    float* __restrict__ taskmax) {
+  __shared__ __attribute__((aligned(16))) float rows[4][2][SG_LDS_ROWS];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t k = (int64_t)blockIdx.x * 4 + wave;
+  if (k >= n) return;
+  const int64_t ti = idx[k];
+  const SgWTask T = tasks[ti];
+  const float wm = wave_max(run_one_hp(T, rows[wave][0], rows[wave][1], amps, syls, cknots, W64, lane));
+  if (lane == 0) taskmax[ti] = wm;
+}
+
 // per-syllable max over its task slots and crossfade-piece slots
 extern "C" __global__ __launch_bounds__(256) void sg_syl_max(const SgSyllable* __restrict__ syls,
                                                              const float* __restrict__ taskmax,
@@ -697,28 +735,30 @@ extern "C" __global__ __launch_bounds__(256) void sg_syl_max(const SgSyllable* _
 }
 
 namespace {
-__device__ __forceinline__ float piece_value(const SgPiece& p, const float* __restrict__ W, int64_t q) {
+template <typename V>
+__device__ __forceinline__ V piece_value(const SgPiece& p, const V* __restrict__ W, int64_t q) {
   if (p.nterms < 0) return W[p.t[0].src + q];
-  float v = 0.f;
-  const float qf = (float)q;
+  V v = 0;
+  const V qf = (V)q;
   for (int t = 0; t < p.nterms; ++t)
-    v = fmaf(fmaf(qf, fmaf(qf, p.t[t].w2, p.t[t].w1), p.t[t].w0), W[p.t[t].src + q], v);
+    v = vfma(vfma(qf, vfma(qf, (V)p.t[t].w2, (V)p.t[t].w1), (V)p.t[t].w0), W[p.t[t].src + q], v);
   return v;
 }
-}  // namespace
 
 // max over crossfade pieces (multi-term); tiles list (syl, piece, q0)
-extern "C" __global__ __launch_bounds__(256) void sg_piece_max(
-    const SgSylTile* __restrict__ ptiles, const SgPiece* __restrict__ pieces, const SgSyllable* __restrict__ syls,
-    const double* __restrict__ cknots, const float* __restrict__ W, float* __restrict__ ptilemax) {
+template <typename V>
+__device__ __forceinline__ void piece_max_body(const SgSylTile* __restrict__ ptiles, const SgPiece* __restrict__ pieces,
+                                               const SgSyllable* __restrict__ syls, const double* __restrict__ cknots,
+                                               const V* __restrict__ W, float* __restrict__ ptilemax) {
   const SgSylTile tl = ptiles[blockIdx.x];
   const SgPiece& p = pieces[tl.piece];
   const SgSyllable& sy = syls[tl.syl];
   const int64_t q = tl.k0 + threadIdx.x;
   float cand = 0.f;
   if (q < p.len) {
-    cand = piece_value(p, W, q);
-    if (sy.env.kind != 0) cand = (float)((double)cand * contour_at(sy.env, cknots, sy.L, p.start + q));
+    const V v = piece_value(p, W, q);
+    cand = (float)v;
+    if (sy.env.kind != 0) cand = (float)((double)v * contour_at(sy.env, cknots, sy.L, p.start + q));
   }
   __shared__ float red[4];
   const float wm = wave_max(cand);
@@ -728,17 +768,30 @@ extern "C" __global__ __launch_bounds__(256) void sg_piece_max(
     ptilemax[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   }
 }
+}  // namespace
+
+extern "C" __global__ __launch_bounds__(256) void sg_piece_max(
+    const SgSylTile* __restrict__ ptiles, const SgPiece* __restrict__ pieces, const SgSyllable* __restrict__ syls,
+    const double* __restrict__ cknots, const float* __restrict__ W, float* __restrict__ ptilemax) {
+  piece_max_body<float>(ptiles, pieces, syls, cknots, W, ptilemax);
+}
+extern "C" __global__ __launch_bounds__(256) void sg_piece_max_hp(
+    const SgSylTile* __restrict__ ptiles, const SgPiece* __restrict__ pieces, const SgSyllable* __restrict__ syls,
+    const double* __restrict__ cknots, const double* __restrict__ W64, float* __restrict__ ptilemax) {
+  piece_max_body<double>(ptiles, pieces, syls, cknots, W64, ptilemax);
+}
 
 // out[k] = assembled[k] * env[k] / max * fade[k] * drift[k]   (R/source.R:436-467)
 // A tile lying inside one direct piece with a 16-B aligned source and
 // destination moves float4s (4 consecutive samples per thread); otherwise
 // each thread takes samples k0 + 256 e + tid.
-__device__ __forceinline__ float fade_at(int lf, int64_t L, int64_t k) {
-  float f = 1.f;
-  const float by = 1.f / (float)(lf - 1);
-  if (k < lf) f *= (k == lf - 1) ? 1.f : (float)k * by;
+template <typename V = float>
+__device__ __forceinline__ V fade_at(int lf, int64_t L, int64_t k) {
+  V f = 1;
+  const V by = (V)1 / (V)(lf - 1);
+  if (k < lf) f *= (k == lf - 1) ? (V)1 : (V)k * by;
   const int64_t kb = L - 1 - k;
-  if (kb < lf) f *= (kb == lf - 1) ? 1.f : (float)kb * by;
+  if (kb < lf) f *= (kb == lf - 1) ? (V)1 : (V)kb * by;
   return f;
 }
 
@@ -824,10 +877,12 @@ static_assert(!((SG_FIN_WAVE_TILE || SG_FIN_DIRECT) && SG_FIN_LDS_ENV == 1), "LD
 #define SG_FIN_DRIFT_LDS 1  // build knob: drift interval by index from per-wave LDS (x, y, slope) rows
 #endif
 constexpr int SG_FIN_KMAX = 32;  // knots of an LDS-staged envelope
+// V = double: an fp64 syllable (W64 -> fh; out_buf is fh, fs unused)
+template <typename V = float>
 __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece* __restrict__ pieces,
                                               const SgSyllable* __restrict__ syls, const double* __restrict__ cknots,
-                                              const float* __restrict__ W, const float* __restrict__ maxes,
-                                              float* __restrict__ out_buf, float* __restrict__ fs, double* lenv,
+                                              const V* __restrict__ W, const float* __restrict__ maxes,
+                                              V* __restrict__ out_buf, V* __restrict__ fs, double* lenv,
                                               int wv, double* lkw) {
   const SgSyllable& sy = syls[tl.syl];
 #if SG_FIN_LDS_ENV == 1
@@ -850,8 +905,9 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
   }
 #endif
   int ecur = -1;  // a lane's samples increase: the envelope interval is found by stepping
-  float* __restrict__ out = sy.dst_fs ? fs : out_buf;
-  const float inv_max = 1.f / maxes[sy.max_slot];
+  constexpr bool F64 = sizeof(V) == 8;
+  V* __restrict__ out = (!F64 && sy.dst_fs) ? fs : out_buf;
+  const V inv_max = (V)1 / (V)maxes[sy.max_slot];
   const int pend = sy.piece0 + sy.npiece;
   const int64_t tile_end = tl.k0 + 1024 < sy.L ? tl.k0 + 1024 : sy.L;
   // general path: wave w owns samples [k0 + 256 w, +256), lane l takes
@@ -907,37 +963,37 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
 #endif
   }
   int p = pu, di = d0;
-  float res[4];  // every load of the chunk before its stores
+  V res[4];  // every load of the chunk before its stores
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int64_t k = c0 + 64 * e + lane;
-    res[e] = 0.f;
+    res[e] = 0;
     if (k >= c1) break;
-    float x;
+    V x;
     if (one_piece) {
       const SgPiece& pc = pieces[pu];
-      x = pc.nterms == 0 ? 0.f : piece_value(pc, W, k - pc.start);
+      x = pc.nterms == 0 ? (V)0 : piece_value(pc, W, k - pc.start);
     } else {
       while (p + 1 < pend && pieces[p + 1].start <= k) ++p;
       const SgPiece& pc = pieces[p];
-      x = pc.nterms == 0 ? 0.f : piece_value(pc, W, k - pc.start);
+      x = pc.nterms == 0 ? (V)0 : piece_value(pc, W, k - pc.start);
     }
     if (sy.env.kind != 0) {
 #if SG_FIN_LDS_ENV == 1 || SG_FIN_LDS_ENV == 3
       if (envl) {
         SgContour cl = sy.env;
         cl.k_off = 0;
-        x = (float)((double)x * sgd::contour_at_cursor(cl, lenv, sy.L, k, ecur));
+        x = (V)((double)x * sgd::contour_at_cursor(cl, lenv, sy.L, k, ecur));
       } else
-        x = (float)((double)x * sgd::contour_at_cursor(sy.env, cknots, sy.L, k, ecur));
+        x = (V)((double)x * sgd::contour_at_cursor(sy.env, cknots, sy.L, k, ecur));
 #elif SG_FIN_LDS_ENV == 2
-      x = (float)((double)x * sgd::contour_at_cursor(sy.env, cknots, sy.L, k, ecur));
+      x = (V)((double)x * sgd::contour_at_cursor(sy.env, cknots, sy.L, k, ecur));
 #else
-      x = (float)((double)x * contour_at(sy.env, cknots, sy.L, k));
+      x = (V)((double)x * contour_at(sy.env, cknots, sy.L, k));
 #endif
     }
     x *= inv_max;
-    if (sy.fade >= 2) x *= fade_at(sy.fade, sy.L, k);
+    if (sy.fade >= 2) x *= fade_at<V>(sy.fade, sy.L, k);
     if (drift) {
       double dm;
       if (local_knots) {  // linear_at's interval and arithmetic, knots from registers
@@ -958,9 +1014,9 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
       } else {
         dm = sgd::linear_at_cursor(dr, cknots, sy.L, k, di);
       }
-      x = (float)((double)x * dm);
+      x = (V)((double)x * dm);
     } else if (dr.nk == 1) {
-      x = (float)((double)x * cknots[dr.k_off + 1]);
+      x = (V)((double)x * cknots[dr.k_off + 1]);
     }
     res[e] = x;
   }
@@ -1062,6 +1118,19 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize(
 #endif
 }
 
+// fp64 syllables (SgSyllable::hp): W64 -> fh, the general path in fp64
+extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize_hp(
+    const SgSylTile* __restrict__ stiles, int64_t ntiles, const SgPiece* __restrict__ pieces,
+    const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, const double* __restrict__ W64,
+    const float* __restrict__ maxes, double* __restrict__ fh) {
+  __shared__ double lenv[5 * SG_FIN_KMAX];
+  __shared__ double lk[4][3 * 8];
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t t = blockIdx.x;
+  if (t >= ntiles) return;
+  finalize_tile<double>(stiles[t], pieces, syls, cknots, W64, maxes, fh, fh, lenv, wv, lk[wv]);
+}
+
 // ---------------------------------------------------------------- launchers
 #include "sg_exec.h"
 namespace sg {
@@ -1112,6 +1181,24 @@ void launch_harm_copy(const DevicePlan& D, int64_t c0, int64_t n_ctiles, float* 
   hipLaunchKernelGGL(sg_harm_copy, dim3((unsigned)((n_ctiles + 3) / 4)), dim3(256), 0, s, D.copy_tiles + c0, n_ctiles, D.W,
                      D.maxes, out, D.fs);
   SG_LAUNCHED("sg_harm_copy");
+}
+void launch_sine_bank_hp(const DevicePlan& D, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(sg_sine_bank_hp, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, D.thp, n, D.tasks, D.amps, D.syls,
+                     D.cknots, D.W64, D.taskmax);
+  SG_LAUNCHED("sg_sine_bank_hp");
+}
+void launch_piece_max_hp(const DevicePlan& D, int64_t p0, int64_t n_ptiles, hipStream_t s) {
+  if (n_ptiles <= 0) return;
+  hipLaunchKernelGGL(sg_piece_max_hp, dim3((unsigned)n_ptiles), dim3(256), 0, s, D.ptiles + p0, D.pieces, D.syls,
+                     D.cknots, D.W64, D.ptilemax + p0);
+  SG_LAUNCHED("sg_piece_max_hp");
+}
+void launch_harm_finalize_hp(const DevicePlan& D, int64_t n_stiles, hipStream_t s) {
+  if (n_stiles <= 0) return;
+  hipLaunchKernelGGL(sg_harm_finalize_hp, dim3((unsigned)n_stiles), dim3(256), 0, s, D.fin_tiles_hp, n_stiles, D.pieces,
+                     D.syls, D.cknots, D.W64, D.maxes, D.fh);
+  SG_LAUNCHED("sg_harm_finalize_hp");
 }
 void launch_harm_finalize(const DevicePlan& D, int64_t f0, int64_t n_stiles, float* out, hipStream_t s) {
   if (n_stiles <= 0) return;

@@ -58,7 +58,9 @@ struct Batch {
   bulk<SgSylTile> syl_tiles;
   std::vector<SgSylTile> fin_tiles;    // derived (finalize_plan): syl_tiles the fast path does not take
   std::vector<SgCopyTile> copy_tiles;  // derived (finalize_plan): fast-path finalize tiles
-  std::vector<SgSylTile> ptiles;   // tiles over multi-term (crossfade) pieces
+  std::vector<SgSylTile> ptiles;   // tiles over multi-term (crossfade) pieces: [fp32 syllables..., fp64 syllables...]
+  int64_t ptile_hp = 0;            // derived: first ptile of an fp64 syllable
+  std::vector<SgSylTile> fin_tiles_hp;  // derived: finalize tiles of fp64 syllables (sg_harm_finalize_hp)
   std::vector<Slice> slices;
   // ---- spectral part (noise, formant filter, assembly) ----
   bulk<float> fl;                 // host-initialised floats (windows, twiddles, uniforms, envelopes, ...)
@@ -67,6 +69,8 @@ struct Batch {
   std::vector<SgFrame> frames[2];        // [0] noise frames, [1] filter frames
   std::vector<int32_t> frame_geom[2];
   std::vector<SgOla> olas[2];            // [0] noise OLAs, [1] filter OLAs (device: [0] then [1])
+  std::vector<SgFrame64> frames64;       // filter frames of fp64 (ill-conditioned) calls: sg_fft_frames64
+  int32_t frames64_wl = 0;               // derived (finalize_spec): their largest window
   std::vector<SgNoiseItem> items;        // items[].ola indexes the device OLA table
   std::vector<SgMix> mixes[2];           // [0] pre-filter sounds (fs), [1] final output
   struct Copy { int64_t fl_off, fs_off, n; };
@@ -86,8 +90,12 @@ struct Batch {
   std::vector<SgMix> mixes_dev;
   std::vector<SgMixTile> mixtiles;
   int64_t mixtile_split = 0;
+  int64_t mixtile_hp = 0;                // pre-filter tiles [mixtile_hp, mixtile_split) write fh (sg_mix_hp)
   bulk<double> cknots;   // contour / linear knot data
   int64_t w_total = 0;          // epoch-waveform scratch (floats)
+  int64_t w64_total = 0;        // fp64 epoch-waveform scratch W64 (doubles; SG_TASK_HP tasks)
+  int64_t fh_total = 0;         // fp64 sound scratch fh (doubles): voiced parts and sounds of fp64 bouts
+  int64_t hp_bouts = 0;         // bouts whose formant filter runs the fp64 path
   // device spectral envelopes (sg_spec_env): per-column/track terms, per-column
   // factors, jobs; outputs in the envelope area (fe_total floats after fe_base,
   // the end of the uploaded fl floats, fixed at finalize_spec). Until then a
@@ -101,6 +109,7 @@ struct Batch {
   // ---- per call ----
   std::vector<int64_t> call_len, call_off;
   std::vector<int32_t> call_status;
+  std::vector<int32_t> call_fp64;   // bouts of the call on the fp64 filter path
   std::vector<std::string> call_msg;
   int64_t total_out = 0;
   // ---- stats ----
@@ -113,9 +122,20 @@ struct Batch {
 // `out_off` of the output buffer. Returns the syllable length.
 // to_fs: the syllable goes to a fresh spectral-scratch region (*fs_off), the
 // voiced part of a soundgen() bout, instead of the output buffer.
+// A glottal cycle's harmonic spectrum sampled by the planner (formant-filter
+// conditioning, sg_plan_soundgen.cpp): syllable sample, f0, row amplitudes (linear)
+struct HarmProbe {
+  int64_t t;
+  double f0;
+  std::vector<double> amp;
+};
 int64_t plan_harmonics(Batch& B, const double* pitch, int64_t len, const sg_harm_params& P,
                        const sg_anchors& amplAnchors, Rng& R, int64_t out_off, bool dry_run, bool to_fs = false,
-                       int64_t* fs_off = nullptr);
+                       int64_t* fs_off = nullptr, std::vector<HarmProbe>* probes = nullptr);
+// Move syllable s (planned to fs) to the fp64 path: epochs' waveforms to W64,
+// its tasks flagged SG_TASK_HP, output to a fresh fh region; returns that offset.
+int64_t syllable_to_fp64(Batch& B, int s);
+int64_t fh_alloc(Batch& B, int64_t n);
 
 // getSmoothContour() for the lengths/values the planner needs on the host.
 // method: 0 loess (default; 3-10 anchors -> sg_loess), 1 spline. sr is the
@@ -148,8 +168,9 @@ int64_t fl_push(Batch& B, const double* v, int64_t n);
 // (R/soundgen.R:743-806). env: nr x env_nc (column-major) at fl offset env
 // (>= 0) or envelope-area offset -(env + 1) (< 0); returns the
 // filter OLA index (phase 1); *out_len = istft length.
+// hp: the sound is in fh (fp64) and the frames run sg_fft_frames64 (unfused)
 int plan_filter(Batch& B, int64_t sound, int64_t L, int wl, double overlap, int64_t env, int64_t env_nc,
-                int64_t* out_len, int64_t* out_fs);
+                int64_t* out_len, int64_t* out_fs, bool hp = false);
 // generateNoise(), R/source.R:57-138: returns a noise item (off = 0);
 // ok == false when the noise contour is NA (R returns zeros). filterNoise: host
 // nr x fnc matrix; or filt_env < 0: a device envelope job (envelope-area

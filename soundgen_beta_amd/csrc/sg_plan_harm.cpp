@@ -663,7 +663,7 @@ static bool lin_continues(const SgSeg& a, const SgSeg& b) {
 
 int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_harm_params& P,
                        const sg_anchors& amplAnchors, Rng& R, int64_t out_off, bool dry_run, bool to_fs,
-                       int64_t* fs_off) {
+                       int64_t* fs_off, std::vector<HarmProbe>* probes) {
   ProfScope ps(PF_HARM);
   const double sr = P.samplingRate;
   if (len < 2) throw SgError(SG_E_DOMAIN, "generateHarmonics: pitch contour too short");
@@ -815,6 +815,17 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
   for (size_t e = 0; e < mats.size(); ++e) cross_fade(A, HE[e], (int64_t)e, sr, 15);
   const int64_t Lsyl = A.L();
   if (dry_run) return Lsyl;
+  if (probes) {  // up to 4 glottal cycles' spectra (formant-filter conditioning)
+    const int64_t np = std::min<int64_t>(4, nGC);
+    for (int64_t q = 0; q < np; ++q) {
+      const int64_t g = (2 * q + 1) * nGC / (2 * np);
+      HarmProbe hp;
+      hp.t = (int64_t)gc_up[g] - 1;
+      hp.f0 = ppg[g];
+      hp.amp.assign(roll.begin() + g * H, roll.begin() + (g + 1) * H);
+      probes->push_back(std::move(hp));
+    }
+  }
   if (to_fs) {
     out_off = fs_alloc(B, Lsyl);
     if (fs_off) *fs_off = out_off;
@@ -1014,6 +1025,47 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
   }
   B.syls.back().ntask = (int32_t)((int64_t)B.tasks.size() - B.syls.back().task0);
   return Lsyl;
+}
+
+int64_t fh_alloc(Batch& B, int64_t n) {
+  const int64_t o = B.fh_total;
+  B.fh_total += (n + 31) / 32 * 32;  // 256-B aligned regions
+  return o;
+}
+
+// The syllable's epoch waveforms move from W to a fresh W64 range (same relative
+// layout; its epochs are consecutive in W), its tasks take the fp64 class and
+// its output goes to fh. W keeps the now unused floats (scratch only).
+int64_t syllable_to_fp64(Batch& B, int s) {
+  SgSyllable& sy = B.syls[s];
+  int64_t wlo = INT64_MAX, whi = 0;
+  for (int64_t t = sy.task0; t < sy.task0 + sy.ntask; ++t) {
+    const SgWTask& T = B.tasks[t];
+    wlo = std::min<int64_t>(wlo, T.w_off + T.j0);
+    whi = std::max<int64_t>(whi, T.w_off + T.j0 + T.len);
+  }
+  for (int32_t p = sy.piece0; p < sy.piece0 + sy.npiece; ++p) {
+    const SgPiece& pc = B.pieces[p];
+    for (int q = 0; q < (pc.nterms < 0 ? 1 : pc.nterms); ++q) {
+      wlo = std::min<int64_t>(wlo, pc.t[q].src);
+      whi = std::max<int64_t>(whi, pc.t[q].src + pc.len);
+    }
+  }
+  if (wlo > whi) wlo = whi = 0;
+  const int64_t base = B.w64_total - wlo;
+  B.w64_total += (whi - wlo + 31) / 32 * 32;
+  for (int64_t t = sy.task0; t < sy.task0 + sy.ntask; ++t) {
+    SgWTask& T = B.tasks[t];
+    T.w_off += base;
+    T.flags |= SG_TASK_HP;
+  }
+  for (int32_t p = sy.piece0; p < sy.piece0 + sy.npiece; ++p) {
+    SgPiece& pc = B.pieces[p];
+    for (int q = 0; q < (pc.nterms < 0 ? 1 : pc.nterms); ++q) pc.t[q].src += base;
+  }
+  sy.hp = 1;
+  sy.out_off = fh_alloc(B, sy.L);
+  return sy.out_off;
 }
 
 // drift-knot interval of sample k: largest i in [0, nk - 2] with x[i] <= u(k),

@@ -7,7 +7,9 @@
 // per-sample work is emitted as device descriptors (syllables, noise frames,
 // filter frames, OLAs, mixes) executed by sg_exec.cpp.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "sg_plan.h"
@@ -240,6 +242,95 @@ SgNoiseItem raw_item(int64_t fs_off, int64_t len, int64_t off) {
   return it;
 }
 
+// ---- conditioning of the formant filter in fp32 ---------------------------
+// The filter output's fp32 round-off is white source noise (the sine bank's and
+// the forward STFT's, relative to the local source level) passed through the
+// envelope, against the source's own harmonics passed through it. Per sampled
+// glottal cycle, with its harmonic amplitudes a_h at bins k_h and the envelope
+// column of the frame over it:
+//   rho = rms_k env(k) / sqrt(sum_h a_h^2 env(k_h)^2 / sum_h a_h^2)
+// Measured on C5's presets (tools/precision_study.py): the fp32 error of the
+// normalised output is ~7e-9 rho; Misc$Cow reaches rho ~1e3-2e3 (1-3e-5 RMS on
+// the GPU), every other preset stays below ~250. Bouts above SG_HP_RHO run
+// the fp64 source and forward transform (DESIGN.md §5 "fp64 path").
+double env_db_at(const Batch& B, const SgEnvJob& J, int64_t c, int64_t k) {
+  const SgEnvTerm* tm = B.eterms.data() + J.term0 + c * J.ntr;
+  const SgEnvCol& C = B.ecols[J.col0 + c];
+  const double lk = std::log2((double)k);
+  double acc = 0;
+  for (int32_t t = 0; t < J.ntr; ++t) {
+    const SgEnvTerm& e = tm[t];
+    if (k < e.klo || k > e.khi) continue;
+    const double d = e.A * lk - e.Rr * (double)k - e.Lm;
+    if (d > -SG_ENV_CUT) acc += e.amp * std::exp2(d);
+  }
+  return (acc + C.lip * lk) * C.boost + J.slope * lk;
+}
+
+struct ProbeAt {
+  int64_t pos;  // sample of the bout's pre-filter sound
+  const HarmProbe* p;
+};
+
+double filter_conditioning(const Batch& B, const SgEnvJob& J, const std::vector<ProbeAt>& probes, double hop, int wl,
+                           double sr) {
+  double worst = 0;
+  const int64_t nr = J.nr;
+  const int64_t st = std::max<int64_t>(1, nr / 256);
+  for (const ProbeAt& pa : probes) {
+    int64_t c = 0;
+    if (J.nc > 1) {
+      c = (int64_t)std::llround(((double)pa.pos - wl / 2.0) / hop);
+      c = std::min<int64_t>(std::max<int64_t>(c, 0), J.nc - 1);
+    }
+    double n2 = 0;
+    int64_t nk = 0;
+    for (int64_t k = 1; k <= nr; k += st, ++nk) n2 += std::exp2(env_db_at(B, J, c, k) / 5);  // env^2
+    double s2 = 0, a2 = 0;
+    const HarmProbe& hp = *pa.p;
+    for (size_t h = 0; h < hp.amp.size(); ++h) {
+      const double a = hp.amp[h];
+      if (!(a > 0)) continue;
+      const int64_t k = (int64_t)std::llround((double)(h + 1) * hp.f0 * wl / sr) + 1;
+      if (k > nr) break;
+      s2 += a * a * std::exp2(env_db_at(B, J, c, k) / 5);
+      a2 += a * a;
+    }
+    if (a2 <= 0 || s2 <= 0 || nk == 0) continue;
+    worst = std::max(worst, std::sqrt(n2 / (double)nk) / std::sqrt(s2 / a2));
+  }
+  return worst;
+}
+
+bool smooth31(int64_t n) {
+  for (int p : {2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31})
+    while (n > 1 && n % p == 0) n /= p;
+  return n == 1;
+}
+
+// 0: never, 1: above the threshold (default), 2: every filtered bout (tests);
+// defaults from SG_HP / SG_HP_RHO, changed by sg_set_fp64_policy
+std::atomic<int> g_hp_mode{-1};
+std::atomic<double> g_hp_rho{-1.0};
+int hp_mode() {
+  int m = g_hp_mode.load();
+  if (m < 0) {
+    const char* e = std::getenv("SG_HP");
+    m = e ? std::atoi(e) : 1;
+    g_hp_mode.store(m);
+  }
+  return m;
+}
+double hp_rho() {
+  double r = g_hp_rho.load();
+  if (r < 0) {
+    const char* e = std::getenv("SG_HP_RHO");
+    r = e ? std::atof(e) : 300.0;
+    g_hp_rho.store(r);
+  }
+  return r;
+}
+
 }  // namespace
 
 int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t out_off, int first_syl) {
@@ -351,6 +442,9 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
     Layout voiced;
     std::vector<SgNoiseItem> noises;
     std::vector<double> noiseIp;
+    std::vector<HarmProbe> probes;   // spectra of sampled glottal cycles (filter conditioning)
+    std::vector<int64_t> probe_pos;  // their bout samples
+    std::vector<int> bout_syls;      // syllables planned to fs in this bout
     sg_harm_params HPs = HP;
     for (int64_t s = 0; s < nS; ++s) {
       Anc pA = pitchA, aA = amplA;
@@ -392,7 +486,11 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
         sylLen = (int64_t)r_round(dur * sr / 1000);  // zeros: no item
       } else {
         int64_t fs_off = 0;
-        sylLen = plan_harmonics(B, pc.data(), (int64_t)pc.size(), HPs, aA.view(), R, 0, false, true, &fs_off);
+        const size_t np0 = probes.size();
+        sylLen = plan_harmonics(B, pc.data(), (int64_t)pc.size(), HPs, aA.view(), R, 0, false, true, &fs_off,
+                                &probes);
+        for (size_t q = np0; q < probes.size(); ++q) probe_pos.push_back(voiced.len + probes[q].t);
+        bout_syls.push_back((int)B.syls.size() - 1);
         SgNoiseItem it = raw_item(fs_off, sylLen, voiced.len);
         voiced.items.push_back(it);
       }
@@ -439,13 +537,59 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
     if (!postNoise)
       for (size_t s = 0; s < noises.size(); ++s) sound.add(noises[s], noiseIp[s]);
     const int64_t Ls = sound.len;
-    const int64_t sound_fs = fs_alloc(B, std::max<int64_t>(Ls, 1));
+    int32_t ncontent = 0;
+    for (const auto& it : sound.items)
+      if (!(it.flags & SG_ITEM_ZERO) && it.len > 0) ++ncontent;
+    // the formant filter's envelope (R/soundgen.R:762-775; no draw between here
+    // and there in R) and, from it, the bout's precision path
+    int wl = 0;
+    int64_t filt_env = 0, nInt = 1;
+    bool hp = false;
+    if (ncontent > 0) {
+      const double fl2 = std::floor((double)Ls / 2);
+      if (fl2 < wlp) wlp = fl2;  // persists into later bouts and their noise
+      wl = (int)wlp;
+      const vec step = r_seq_by(1, (double)std::max<int64_t>(1, Ls - wl), (double)wl - A.overlap * wl / 100);
+      const int64_t nc = (int64_t)step.size();
+      bool moving = formants_moving(Fm);
+      bool mouthMoves = false;
+      for (double v : mouthA.v) if (v != .5) mouthMoves = true;
+      if (mouthA.n() > 0 && mouthMoves) moving = true;
+      nInt = moving ? nc : 1;
+      filt_env = plan_envelope(B, R, (double)wl / 2, nInt, &Fm, A.formantDep, A.rolloffLip, mouthA.view(), 0, 0,
+                               A.vocalTract, T, A.tempEffects[1], A.tempEffects[2], A.formantDepStoch, 1, sr, 35400);
+      const int mode = hp_mode();
+      const int64_t nr2 = 2 * (wl / 2);
+      if (mode > 0 && !bout_syls.empty() && wl <= 3072 && smooth31(wl) && smooth31(nr2)) {
+        if (mode == 2) {
+          hp = true;
+        } else {
+          std::vector<ProbeAt> pa;
+          for (size_t q = 0; q < probes.size(); ++q) pa.push_back(ProbeAt{probe_pos[q], &probes[q]});
+          hp = filter_conditioning(B, B.envjobs.back(), pa, (double)wl - A.overlap * wl / 100, wl, sr) > hp_rho();
+        }
+      }
+    }
+    if (hp) {  // voiced syllables to the fp64 path; their items read fh
+      ++B.hp_bouts;
+      for (int si : bout_syls) {
+        const int64_t old_off = B.syls[si].out_off;
+        const int64_t fh_off = syllable_to_fp64(B, si);
+        for (auto& it : sound.items)
+          if (it.ola < 0 && !(it.flags & SG_ITEM_F64) && it.raw == old_off) {
+            it.raw = fh_off;
+            it.flags |= SG_ITEM_F64;
+            break;
+          }
+      }
+    }
+    const int64_t sound_fs = hp ? fh_alloc(B, std::max<int64_t>(Ls, 1)) : fs_alloc(B, std::max<int64_t>(Ls, 1));
     SgMix pre{};
     pre.dst = sound_fs;
     pre.len = Ls;
-    pre.to_fs = 1;
+    pre.to_fs = hp ? 2 : 1;
     pre.base_kind = SG_BASE_NONE;
-    const int32_t ncontent = emit(sound, pre.item0);
+    ncontent = emit(sound, pre.item0);
     pre.nitems = ncontent;
     pre.mult.kind = 0;
     {  // amplAnchorsGlobal (R/soundgen.R:715-733)
@@ -465,21 +609,8 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
       post.items.push_back(raw_item(sound_fs, Ls, 0));
       post.len = Ls;
     } else {
-      const double fl2 = std::floor((double)Ls / 2);
-      if (fl2 < wlp) wlp = fl2;  // persists into later bouts and their noise
-      const int wl = (int)wlp;
-      const vec step = r_seq_by(1, (double)std::max<int64_t>(1, Ls - wl), (double)wl - A.overlap * wl / 100);
-      const int64_t nc = (int64_t)step.size();
-      bool moving = formants_moving(Fm);
-      bool mouthMoves = false;
-      for (double v : mouthA.v) if (v != .5) mouthMoves = true;
-      if (mouthA.n() > 0 && mouthMoves) moving = true;
-      const int64_t nInt = moving ? nc : 1;
-      const int64_t env = plan_envelope(B, R, (double)wl / 2, nInt, &Fm, A.formantDep, A.rolloffLip, mouthA.view(),
-                                        0, 0, A.vocalTract, T, A.tempEffects[1], A.tempEffects[2],
-                                        A.formantDepStoch, 1, sr, 35400);
       int64_t filt_fs = 0, Lf = 0;
-      const int ola = plan_filter(B, sound_fs, Ls, wl, A.overlap, env, nInt, &Lf, &filt_fs);
+      const int ola = plan_filter(B, sound_fs, Ls, wl, A.overlap, filt_env, nInt, &Lf, &filt_fs, hp);
       SgNoiseItem fi = raw_item(filt_fs, Lf, 0);  // soundFiltered / max(soundFiltered)
       fi.ola = ola;
       fi.flags = SG_ITEM_FILTER_OLA;
@@ -541,6 +672,13 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
 void restore_soundgen_tail(Batch&, int) {}
 
 }  // namespace sg
+
+extern "C" int sg_set_fp64_policy(int32_t mode, double rho) {
+  if (mode < 0 || mode > 2 || !(rho >= 0)) return SG_E_ARG;
+  sg::g_hp_mode.store(mode);
+  sg::g_hp_rho.store(rho);
+  return SG_OK;
+}
 
 extern "C" int sg_permitted_value(int32_t i, const char** name, double* def_low_high) {
   if (i < 0 || i >= sg::kNPV) return SG_E_ARG;

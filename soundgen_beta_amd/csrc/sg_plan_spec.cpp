@@ -257,10 +257,11 @@ static bool fusable(const SgFftGeom& g, double hop) {
 }
 
 static int push_ola(Batch& B, int phase, int64_t frames, int64_t nframes, int wl, const IstftGeom& ig, int64_t first,
-                    int64_t len, int64_t out, bool fused) {
+                    int64_t len, int64_t out, bool fused, bool f64 = false) {
   if (fused && ig.xlen >= (int64_t)1 << 31) throw SgError(SG_E_UNSUPPORTED, "istft: output longer than 2^31 samples");
   SgOla o{};
-  o.fidx = (int32_t)((int64_t)B.frames[phase].size() - nframes);
+  // fp64 frames (B.frames64) have no SgFrame: fidx -1 (unfused, sg_ola reads the frame scratch)
+  o.fidx = f64 ? -1 : (int32_t)((int64_t)B.frames[phase].size() - nframes);
   o.fused = fused ? 1 : 0;
   o.frames = frames;
   o.out = out;
@@ -277,7 +278,7 @@ static int push_ola(Batch& B, int phase, int64_t frames, int64_t nframes, int wl
 }
 
 int plan_filter(Batch& B, int64_t sound, int64_t L, int wl, double overlap, int64_t env, int64_t env_nc,
-                int64_t* out_len, int64_t* out_fs) {
+                int64_t* out_len, int64_t* out_fs, bool hp) {
   ProfScope ps(PF_FILTER);
   const int gi = geometry(B, wl);
   const int64_t nr = wl / 2;
@@ -288,8 +289,25 @@ int plan_filter(Batch& B, int64_t sound, int64_t L, int wl, double overlap, int6
   if (env_nc != 1 && env_nc != nc) throw SgError(SG_E_ARG, "formant filter: envelope columns != frames");
   for (double x0 : step)
     if ((int64_t)x0 - 1 + wl > L) throw SgError(SG_E_DOMAIN, "stft: frame beyond the sound");
-  const bool fused = fusable(B.geoms[gi], (double)wl * (100 - overlap) / 100);
+  const bool fused = !hp && fusable(B.geoms[gi], (double)wl * (100 - overlap) / 100);
   const int64_t fr = fused ? 0 : fs_alloc(B, nc * wl);  // frame scratch only for the unfused path
+  if (hp) {  // fp64 forward transforms (sg_fft_frames64), then the fp32 overlap-add (sg_ola)
+    for (int64_t c = 0; c < nc; ++c) {
+      SgFrame64 f{};
+      f.src = sound + (int64_t)step[c] - 1;
+      const int64_t col = env_nc == 1 ? 0 : c * nr;
+      f.env = env < 0 ? env - col : env + col;
+      f.dst = fr + c * wl;
+      f.wl = wl;
+      B.frames64.push_back(f);
+    }
+    const IstftGeom ig = istft_geom(wl, nc, overlap);
+    const int64_t out = fs_alloc(B, ig.xlen);
+    B.fft_frames += nc;
+    *out_len = ig.xlen;
+    *out_fs = out;
+    return push_ola(B, 1, fr, nc, wl, ig, 0, ig.xlen, out, false, true);
+  }
   for (int64_t c = 0; c < nc; ++c) {
     SgFrame f{};
     f.src = sound + (int64_t)step[c] - 1;  // wave[x:(x + wl - 1)], x truncated
@@ -637,6 +655,11 @@ void finalize_spec(Batch& B) {
   for (int ph = 0; ph < 2; ++ph)
     for (SgFrame& f : B.frames[ph])
       if (f.env < 0) f.env = B.fe_base + (-f.env - 1);
+  B.frames64_wl = 0;
+  for (SgFrame64& f : B.frames64) {
+    if (f.env < 0) f.env = B.fe_base + (-f.env - 1);
+    B.frames64_wl = std::max(B.frames64_wl, f.wl);
+  }
   int32_t maxnr = 0;
   for (const SgEnvJob& j : B.envjobs) {
     maxnr = std::max(maxnr, j.nr);
@@ -700,7 +723,7 @@ void finalize_spec(Batch& B) {
     const int32_t base = ph == 0 ? 0 : (int32_t)B.frames[0].size();
     for (const SgOla& o0 : B.olas[ph]) {
       SgOla o = o0;
-      o.fidx = base + (int32_t)pos[ph][o0.fidx];
+      if (o0.fidx >= 0) o.fidx = base + (int32_t)pos[ph][o0.fidx];
       const int32_t oi = (int32_t)B.olas_dev.size();
       if (!o.fused) {
         o.tile0 = (int32_t)B.olatiles.size();
@@ -865,9 +888,13 @@ void finalize_spec(Batch& B) {
   // mixes: [pre-filter..., final...]
   B.mixes_dev.clear();
   B.mixtiles.clear();
-  for (int ph = 0; ph < 2; ++ph) {
-    if (ph == 1) B.mixtile_split = (int64_t)B.mixtiles.size();
+  // mixes: [pre-filter fp32..., pre-filter fp64 (to fh)..., final...]
+  for (int pass = 0; pass < 3; ++pass) {
+    const int ph = pass == 2 ? 1 : 0;
+    if (pass == 1) B.mixtile_hp = (int64_t)B.mixtiles.size();
+    if (pass == 2) B.mixtile_split = (int64_t)B.mixtiles.size();
     for (const SgMix& m0 : B.mixes[ph]) {
+      if (ph == 0 && (m0.to_fs == 2) != (pass == 1)) continue;
       const int32_t mi = (int32_t)B.mixes_dev.size();
       for (int64_t k0 = 0; k0 < m0.len; k0 += SG_MIX_TILE) B.mixtiles.push_back(SgMixTile{mi, 0, k0});
       SgMix m = m0;

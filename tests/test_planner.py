@@ -136,3 +136,45 @@ def test_fast_zero_crossing_search_equals_exact(tmp_path):
         subprocess.run([sys.executable, "-c", code, f], check=True, env=env, timeout=600)
         outs.append(np.load(f))
     assert np.array_equal(outs[0], outs[1])
+
+
+def _bench():
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    return bench
+
+
+def test_precision_path_flags_ill_conditioned_presets():
+    """The planner's conditioning estimate (filter_conditioning,
+    sg_plan_soundgen.cpp) sends Misc$Cow's bouts (fp32 round-off through its
+    envelope reached 1-3e-5 RMS) to the fp64 filter path and no other preset of
+    the C5 sample; lengths and offsets do not depend on the path."""
+    import os
+    bench = _bench()
+    calls = bench.c5_calls(400)
+    plan = batch.Plan(calls, None)
+    assert (plan.status == 0).all()
+    hp, frames, tasks = plan.precision()
+    presets = np.array([c["preset"] for c in calls])
+    assert hp[presets == "Misc$Cow"].min() >= 1
+    flagged = set(presets[hp > 0])
+    assert flagged <= {"Misc$Cow", "M1$Sigh", "Misc$Elephant"}, flagged
+    assert frames > 0 and tasks > 0
+    from soundgen_beta_amd import native
+    L = native.lib()
+    assert L.sg_set_fp64_policy(0, 300.0) == 0
+    try:
+        p0 = batch.Plan(calls, None)
+        h0, f0, t0 = p0.precision()
+        assert h0.sum() == 0 and f0 == 0 and t0 == 0
+        assert np.array_equal(p0.lengths, plan.lengths) and np.array_equal(p0.offsets, plan.offsets)
+        assert L.sg_set_fp64_policy(2, 300.0) == 0
+        p2 = batch.Plan(calls, None)
+        h2, f2, t2 = p2.precision()
+        assert (h2 >= hp).all() and f2 >= frames and t2 > tasks
+        assert np.array_equal(p2.lengths, plan.lengths) and np.array_equal(p2.offsets, plan.offsets)
+        assert L.sg_set_fp64_policy(3, 300.0) != 0
+    finally:
+        L.sg_set_fp64_policy(1, 300.0)
