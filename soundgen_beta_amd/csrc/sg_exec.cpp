@@ -22,7 +22,7 @@ constexpr size_t ALIGN = 256;
 size_t up(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
 struct Layout {
-  size_t tall, tlong, tshort, tallp, thp, fin_tiles_hp, W64, fh, frames64;
+  size_t tall, tlong, tshort, tallp, thp, fin_tiles_hp, W64, fh, frames64, fgroups64;
   size_t segs, epochs, knots, amps, tasks, pieces, syls, syl_tiles, copy_tiles, ptiles, cknots, W, taskmax, ptilemax, maxes, total;
   size_t geoms, frames, fgroups, olas, olatiles, olasegs, olatilemax, olamax, items, mixes, mixtiles, fl, fs;
   size_t eterms, ecols, envjobs, envtasks, elog2;
@@ -43,6 +43,7 @@ struct Layout {
     W64 = take((size_t)B.w64_total * sizeof(double));
     fh = take((size_t)B.fh_total * sizeof(double));
     frames64 = take(B.frames64.size() * sizeof(SgFrame64));
+    fgroups64 = take(B.fgroups64.size() * sizeof(SgFrameGroup));
     pieces = take(B.pieces.size() * sizeof(SgPiece));
     syls = take(B.syls.size() * sizeof(SgSyllable));
     syl_tiles = take(B.fin_tiles.size() * sizeof(SgSylTile));
@@ -257,6 +258,7 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   D.W64 = (double*)(a + L.W64);
   D.fh = (double*)(a + L.fh);
   D.frames64 = (SgFrame64*)(a + L.frames64);
+  D.fgroups64 = (SgFrameGroup*)(a + L.fgroups64);
   D.pieces = (SgPiece*)(a + L.pieces);
   D.syls = (SgSyllable*)(a + L.syls);
   D.syl_tiles = (SgSylTile*)(a + L.syl_tiles);
@@ -315,6 +317,7 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   cp(D.thp, D.thp_host.data(), D.thp_host.size() * sizeof(int32_t));
   cp(D.fin_tiles_hp, B.fin_tiles_hp.data(), B.fin_tiles_hp.size() * sizeof(SgSylTile));
   cp(D.frames64, B.frames64.data(), B.frames64.size() * sizeof(SgFrame64));
+  cp(D.fgroups64, B.fgroups64.data(), B.fgroups64.size() * sizeof(SgFrameGroup));
   cp(D.pieces, B.pieces.data(), B.pieces.size() * sizeof(SgPiece));
   cp(D.syls, B.syls.data(), B.syls.size() * sizeof(SgSyllable));
   cp(D.syl_tiles, B.fin_tiles.data(), B.fin_tiles.size() * sizeof(SgSylTile));
@@ -461,7 +464,7 @@ void device_execute_spec(const Batch& B, const DevicePlan& D, float* d_out, hipS
       prof->push_back({SG_PROF_STFT_OLA, e0, e1});
     }
     launch_fft_frames(D, r[1], r[2] - r[1], B.fgroup_lds[ph][1], s);
-    if (ph == 1) launch_fft_frames64(D, (int64_t)B.frames64.size(), B.frames64_wl, s);
+    if (ph == 1) launch_fft_frames64(D, (int64_t)B.fgroups64.size(), B.fgroup64_lds, s);
     const int64_t t0 = ph == 0 ? 0 : B.olatile_split, t1 = ph == 0 ? B.olatile_split : (int64_t)B.olatiles.size();
     const int64_t o0 = ph == 0 ? 0 : B.ola_split, o1 = ph == 0 ? B.ola_split : (int64_t)B.olas_dev.size();
     launch_ola(D, t0, t1 - t0, s);

@@ -44,6 +44,7 @@ struct DevicePlan {
   double* W64 = nullptr;             // fp64 epoch waveforms of SG_TASK_HP tasks
   double* fh = nullptr;              // fp64 sounds (voiced parts, pre-filter sounds) of fp64 bouts
   SgFrame64* frames64 = nullptr;     // their filter frames (sg_fft_frames64)
+  SgFrameGroup* fgroups64 = nullptr; // their workgroups: geom = window length, frames [f0, f0 + nf)
   SgPiece* pieces = nullptr;
   SgSyllable* syls = nullptr;
   SgSylTile* syl_tiles = nullptr;    // general-path finalize tiles (Batch::fin_tiles)
@@ -114,7 +115,7 @@ void launch_sine_bank_hp(const DevicePlan& D, int64_t n, hipStream_t s);
 void launch_piece_max_hp(const DevicePlan& D, int64_t p0, int64_t n_ptiles, hipStream_t s);
 void launch_harm_finalize_hp(const DevicePlan& D, int64_t n_stiles, hipStream_t s);
 void launch_mix_hp(const DevicePlan& D, int64_t t0, int64_t n_tiles, hipStream_t s);
-void launch_fft_frames64(const DevicePlan& D, int64_t n_frames, int max_wl, hipStream_t s);
+void launch_fft_frames64(const DevicePlan& D, int64_t n_groups, int lds_bytes, hipStream_t s);
 // sg_fft.hip
 void launch_fft_frames(const DevicePlan& D, int64_t g0, int64_t n_groups, int lds_bytes, hipStream_t s);
 void launch_stft_ola(const DevicePlan& D, int phase, int64_t s0, int64_t n_segs, int lds_bytes, hipStream_t s);

@@ -70,7 +70,8 @@ struct Batch {
   std::vector<int32_t> frame_geom[2];
   std::vector<SgOla> olas[2];            // [0] noise OLAs, [1] filter OLAs (device: [0] then [1])
   std::vector<SgFrame64> frames64;       // filter frames of fp64 (ill-conditioned) calls: sg_fft_frames64
-  int32_t frames64_wl = 0;               // derived (finalize_spec): their largest window
+  std::vector<SgFrameGroup> fgroups64;   // derived (finalize_spec): sg_fft_frames64 workgroups (geom = wl)
+  int32_t fgroup64_lds = 0;              // derived: their largest dynamic LDS
   std::vector<SgNoiseItem> items;        // items[].ola indexes the device OLA table
   std::vector<SgMix> mixes[2];           // [0] pre-filter sounds (fs), [1] final output
   struct Copy { int64_t fl_off, fs_off, n; };

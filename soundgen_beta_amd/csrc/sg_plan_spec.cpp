@@ -655,10 +655,22 @@ void finalize_spec(Batch& B) {
   for (int ph = 0; ph < 2; ++ph)
     for (SgFrame& f : B.frames[ph])
       if (f.env < 0) f.env = B.fe_base + (-f.env - 1);
-  B.frames64_wl = 0;
-  for (SgFrame64& f : B.frames64) {
+  // fp64 frames: by window length, up to 4 per workgroup as LDS allows (16 N for
+  // the W_N table, 32 M per frame)
+  for (SgFrame64& f : B.frames64)
     if (f.env < 0) f.env = B.fe_base + (-f.env - 1);
-    B.frames64_wl = std::max(B.frames64_wl, f.wl);
+  std::stable_sort(B.frames64.begin(), B.frames64.end(),
+                   [](const SgFrame64& x, const SgFrame64& y) { return x.wl < y.wl; });
+  B.fgroups64.clear();
+  B.fgroup64_lds = 0;
+  for (size_t i = 0; i < B.frames64.size();) {
+    const int N = B.frames64[i].wl, M = N / 2;
+    const int fpb = std::max(1, std::min(4, (160 * 1024 - 16 * N) / (32 * M)));
+    size_t j = i;
+    while (j < B.frames64.size() && B.frames64[j].wl == N && (int)(j - i) < fpb) ++j;
+    B.fgroups64.push_back(SgFrameGroup{N, SG_FRAME_FILTER, (int32_t)i, (int32_t)(j - i)});
+    B.fgroup64_lds = std::max(B.fgroup64_lds, 16 * N + 32 * M * (int)(j - i));
+    i = j;
   }
   int32_t maxnr = 0;
   for (const SgEnvJob& j : B.envjobs) {
