@@ -282,6 +282,8 @@ def main():
     ap.add_argument("--calls", type=int, default=0, help="calls in the whole batch (default: the config's)")
     ap.add_argument("--plan-chunk", type=int, default=16384,
                     help="calls per plan (each uploaded, then its host copy freed)")
+    ap.add_argument("--no-d2h", action="store_true",
+                    help="profiling runs only: the timed steps leave the outputs in HBM (no copy kernels beside them)")
     ap.add_argument("--device-steps", type=int, default=5,
                     help="extra steps timed with the outputs left in HBM (value_device_resident; 0: skip)")
     ap.add_argument("--cpu-budget", type=float, default=16.0)
@@ -381,10 +383,11 @@ def main():
             dist.barrier()
         return time.perf_counter() - t
 
+    main_step = step if args.no_d2h else step_to_host
     for _ in range(args.warmup):
-        step_to_host()
+        main_step()
     torch.cuda.synchronize(dev)
-    dt = timed(step_to_host, args.steps)  # the headline: host-resident
+    dt = timed(main_step, args.steps)  # the headline: host-resident
     # the same steps with the outputs left in HBM (no D2H copy)
     dt_dev = timed(step, args.device_steps) if args.device_steps > 0 else None
     L = native.lib()
@@ -463,7 +466,8 @@ def main():
                        "samples": int(samples_all), "sampling_rate": 44100,
                        "parallelism": "dp%d (one batch split by calls, LPT)" % world,
                        "plans_per_rank": len(plans), "failed_calls": failed_all},
-            "timing": "sg_execute entry to waveforms resident in pinned host memory (SURVEY 8d)",
+            "timing": ("outputs left in HBM (--no-d2h profiling run)" if args.no_d2h else
+                       "sg_execute entry to waveforms resident in pinned host memory (SURVEY 8d)"),
             "value_device_resident": (samples_all * args.device_steps / dt_dev) if dt_dev else None,
             "ms_per_step_device_resident": (dt_dev / args.device_steps * 1e3) if dt_dev else None,
             "plan_s": t_plan_max, "calls_gen_s": t_gen,

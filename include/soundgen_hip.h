@@ -245,6 +245,10 @@ int sg_plan_stft_stats(const sg_plan* plan, int64_t* samples, int64_t* alg_bytes
  * totals of fp64 filter frames and sine-bank tasks. Any pointer may be NULL.
  * No reference counterpart: the R path is fp64 throughout. */
 int sg_plan_precision(const sg_plan* plan, int32_t* call_fp64, int64_t* fp64_frames, int64_t* fp64_tasks);
+/* Per-call device work the plan emits (ABI 2): sine-bank (sample, row) terms and
+ * nominal FFT flops (5 wl log2 wl per transform), for load balancing across
+ * GPUs (soundgen_beta_amd/dist.py). Either pointer may be NULL. */
+int sg_plan_call_work(const sg_plan* plan, double* rows, double* fft_flops);
 /* Process-wide policy of the fp64 filter path for later sg_plan_batch calls:
  * mode 0 never, 1 when the conditioning estimate exceeds rho (default 300),
  * 2 every filtered bout. SG_E_ARG for an invalid mode or rho. */

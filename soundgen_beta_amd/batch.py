@@ -70,6 +70,13 @@ class Plan:
         native.lib().sg_plan_precision(self.ptr, v.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(fr), C.byref(tk))
         return v, fr.value, tk.value
 
+    def call_work(self):
+        """Per call: sine-bank (sample, row) terms and nominal FFT flops."""
+        rows, flops = np.zeros(self.n), np.zeros(self.n)
+        dp = C.POINTER(C.c_double)
+        native.lib().sg_plan_call_work(self.ptr, rows.ctypes.data_as(dp), flops.ctypes.data_as(dp))
+        return rows, flops
+
     def device_bytes(self):
         return int(native.lib().sg_plan_device_bytes(self.ptr))
 
@@ -141,10 +148,11 @@ def plan_uploaded(calls, ctx, chunk):
             yield p, a
 
 
-def synthesize_to_wav(calls, paths, sampling_rates, device=0):
+def synthesize_to_wav(calls, paths, sampling_rates, device=0, return_float=False):
     """soundgen(..., savePath = path) for a batch: synthesize on the GPU, convert
     every call to 16-bit PCM on the GPU (half the bytes cross PCIe), write one
-    WAV file per call (R/soundgen.R:854-856). Returns the int16 arrays."""
+    WAV file per call (R/soundgen.R:854-856). Returns the int16 arrays; with
+    return_float also the fp32 waveforms of the same execute: (pcm, waves)."""
     import torch
     from . import api
     ctx = native.default_context(device)
@@ -158,16 +166,39 @@ def synthesize_to_wav(calls, paths, sampling_rates, device=0):
     plan.pcm16(out.data_ptr(), pcm.data_ptr(), sptr)
     torch.cuda.synchronize(device)
     host = pcm.cpu().numpy()
-    res = []
+    hostf = out.cpu().numpy() if return_float else None
+    res, waves = [], []
     for i in range(plan.n):
         if plan.status[i] != 0:
-            res.append(native.SoundgenError(int(plan.status[i]), plan.message(i)))
+            err = native.SoundgenError(int(plan.status[i]), plan.message(i))
+            res.append(err)
+            waves.append(err)
             continue
         y = host[plan.offsets[i]:plan.offsets[i] + plan.lengths[i]].copy()
         api.write_wav(paths[i], y, sampling_rates[i] if hasattr(sampling_rates, "__len__") else sampling_rates)
         res.append(y)
+        if return_float:
+            waves.append(hostf[plan.offsets[i]:plan.offsets[i] + plan.lengths[i]].copy())
     plan.close()
-    return res
+    return (res, waves) if return_float else res
+
+
+def synthesize_packed(calls, device=0):
+    """Plan + run a batch on one GPU and keep the outputs packed in HBM: returns
+    (float32 device tensor, offsets, lengths), call i at offsets[i] with
+    lengths[i] samples, -1 for a call the planner refused (dist.gather_packed
+    sends this buffer as is)."""
+    import torch
+    ctx = native.default_context(device)
+    plan = Plan(calls, ctx)
+    plan.upload()
+    out = torch.empty(max(plan.total, 1), dtype=torch.float32, device="cuda:%d" % device)
+    plan.execute(out.data_ptr(), torch.cuda.current_stream(device).cuda_stream)
+    torch.cuda.synchronize(device)
+    lens = np.where(plan.status == 0, plan.lengths, -1).astype(np.int64)
+    offs = plan.offsets.astype(np.int64).copy()
+    plan.close()
+    return out[:plan.total], offs, lens
 
 
 def synthesize(calls, device=0):

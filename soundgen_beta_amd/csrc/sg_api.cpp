@@ -73,6 +73,7 @@ struct Checkpoint {
   size_t frames[2], olas[2], mixes[2], copies, eterms, ecols, envjobs, frames64;
   int64_t w_total, harm_samples, harm_terms, harm_amp_bytes, fft_frames, fs_total, fe_total, w64_total, fh_total,
       hp_bouts;
+  double fft_flops;
   explicit Checkpoint(const sg::Batch& B)
       : segs(B.segs.size()), epochs(B.epochs.size()), knots(B.knots.size()), amps(B.amps.size()),
         tasks(B.tasks.size()), pieces(B.pieces.size()), syls(B.syls.size()), syl_tiles(B.syl_tiles.size()),
@@ -80,7 +81,7 @@ struct Checkpoint {
         eterms(B.eterms.size()), ecols(B.ecols.size()), envjobs(B.envjobs.size()), w_total(B.w_total),
         harm_samples(B.harm_samples), harm_terms(B.harm_terms), harm_amp_bytes(B.harm_amp_bytes),
         fft_frames(B.fft_frames), fs_total(B.fs_total), fe_total(B.fe_total), w64_total(B.w64_total),
-        fh_total(B.fh_total), hp_bouts(B.hp_bouts) {
+        fh_total(B.fh_total), hp_bouts(B.hp_bouts), fft_flops(B.fft_flops) {
     frames64 = B.frames64.size();
     for (int p = 0; p < 2; ++p) { frames[p] = B.frames[p].size(); olas[p] = B.olas[p].size(); mixes[p] = B.mixes[p].size(); }
   }
@@ -96,6 +97,7 @@ struct Checkpoint {
     B.harm_amp_bytes = harm_amp_bytes; B.fft_frames = fft_frames; B.fs_total = fs_total;
     B.eterms.resize(eterms); B.ecols.resize(ecols); B.envjobs.resize(envjobs); B.fe_total = fe_total;
     B.frames64.resize(frames64); B.w64_total = w64_total; B.fh_total = fh_total; B.hp_bouts = hp_bouts;
+    B.fft_flops = fft_flops;
   }
 };
 
@@ -135,13 +137,16 @@ void plan_range(sg::Batch& B, const sg_call_desc* calls, int64_t c0, int64_t c1)
   B.call_off.assign(n, 0);
   B.call_status.assign(n, 0);
   B.call_fp64.assign(n, 0);
+  B.call_rows.assign(n, 0.0);
+  B.call_flops.assign(n, 0.0);
   B.call_msg.assign(n, "");
   int64_t off = 0;
   for (int64_t i = 0; i < n; ++i) {
     const sg_call_desc& d = calls[c0 + i];
     Checkpoint cp(B);
     const int first_syl = (int)B.syls.size();
-    const int64_t hp0 = B.hp_bouts;
+    const int64_t hp0 = B.hp_bouts, rows0 = B.harm_terms;
+    const double fl0 = B.fft_flops;
     try {
       sg::Rng R;
       R.s = &d.random;
@@ -165,6 +170,8 @@ void plan_range(sg::Batch& B, const sg_call_desc* calls, int64_t c0, int64_t c1)
       B.call_off[i] = off;
       B.call_len[i] = L;
       B.call_fp64[i] = (int32_t)(B.hp_bouts - hp0);
+      B.call_rows[i] = (double)(B.harm_terms - rows0);
+      B.call_flops[i] = B.fft_flops - fl0;
       off += (L + 63) / 64 * 64;  // 256-B aligned call slots
     } catch (const sg::SgError& e) {
       cp.restore(B);
@@ -238,12 +245,13 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
     }
     D.harm_samples += S.harm_samples; D.harm_terms += S.harm_terms; D.harm_amp_bytes += S.harm_amp_bytes;
     D.fft_frames += S.fft_frames;
+    D.fft_flops += S.fft_flops;
   }
   D.total_out = c.out; D.fs_total = c.fs; D.w_total = c.w; D.fe_total = c.fe;
   D.w64_total = c.w64; D.fh_total = c.fh; D.frames64.resize(c.fr64);
   D.eterms.resize(c.term); D.ecols.resize(c.col); D.envjobs.resize(c.job);
   D.call_len.resize(c.call); D.call_off.resize(c.call); D.call_status.resize(c.call); D.call_msg.resize(c.call);
-  D.call_fp64.resize(c.call);
+  D.call_fp64.resize(c.call); D.call_rows.resize(c.call); D.call_flops.resize(c.call);
   D.segs.resize(c.seg); D.epochs.resize(c.epoch); D.knots.resize(c.knot); D.amps.resize(c.amp);
   D.tasks.resize(c.task); D.pieces.resize(c.piece); D.syls.resize(c.syl); D.syl_tiles.resize(c.st);
   D.cknots.resize(c.ck); D.fl.resize(c.fl); D.items.resize(c.item); D.copies.resize(c.copy);
@@ -261,6 +269,8 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
       D.call_off[b.call + i] = S.call_off[i] + b.out;
       D.call_status[b.call + i] = S.call_status[i];
       D.call_fp64[b.call + i] = S.call_fp64[i];
+      D.call_rows[b.call + i] = S.call_rows[i];
+      D.call_flops[b.call + i] = S.call_flops[i];
       D.call_msg[b.call + i] = std::move(S.call_msg[i]);
     }
     for (auto& e : S.epochs) {
@@ -627,6 +637,14 @@ int sg_plan_precision(const sg_plan* plan, int32_t* call_fp64, int64_t* fp64_fra
     for (const SgWTask& t : B.tasks) n += (t.flags & SG_TASK_HP) ? 1 : 0;
     *fp64_tasks = n;
   }
+  return SG_OK;
+}
+
+int sg_plan_call_work(const sg_plan* plan, double* rows, double* fft_flops) {
+  if (!plan) return SG_E_ARG;
+  const sg::Batch& B = plan->B;
+  if (rows) std::memcpy(rows, B.call_rows.data(), B.call_rows.size() * sizeof(double));
+  if (fft_flops) std::memcpy(fft_flops, B.call_flops.data(), B.call_flops.size() * sizeof(double));
   return SG_OK;
 }
 

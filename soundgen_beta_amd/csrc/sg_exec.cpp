@@ -22,7 +22,8 @@ constexpr size_t ALIGN = 256;
 size_t up(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
 struct Layout {
-  size_t tall, tlong, tshort, tallp, thp, fin_tiles_hp, W64, fh, frames64, fgroups64;
+  size_t tall, tlong, tshort, tallp, thp, fin_tiles_hp, W64, fh, frames64, frames64_tab, roots64, roots64_wl,
+      roots64_off;
   size_t segs, epochs, knots, amps, tasks, pieces, syls, syl_tiles, copy_tiles, ptiles, cknots, W, taskmax, ptilemax, maxes, total;
   size_t geoms, frames, fgroups, olas, olatiles, olasegs, olatilemax, olamax, items, mixes, mixtiles, fl, fs;
   size_t eterms, ecols, envjobs, envtasks, elog2;
@@ -43,7 +44,10 @@ struct Layout {
     W64 = take((size_t)B.w64_total * sizeof(double));
     fh = take((size_t)B.fh_total * sizeof(double));
     frames64 = take(B.frames64.size() * sizeof(SgFrame64));
-    fgroups64 = take(B.fgroups64.size() * sizeof(SgFrameGroup));
+    frames64_tab = take(B.frames64_tab.size() * sizeof(int64_t));
+    roots64 = take((size_t)B.roots64_total * 2 * sizeof(double));
+    roots64_wl = take(B.roots64_wl.size() * sizeof(int32_t));
+    roots64_off = take(B.roots64_off.size() * sizeof(int64_t));
     pieces = take(B.pieces.size() * sizeof(SgPiece));
     syls = take(B.syls.size() * sizeof(SgSyllable));
     syl_tiles = take(B.fin_tiles.size() * sizeof(SgSylTile));
@@ -143,6 +147,18 @@ void finalize_plan(Batch& B) {
     std::map<int, int64_t> rh;
     int64_t nshort[2] = {0, 0}, lh[2][5] = {{0}};
     double sterms[2] = {0, 0};
+    {  // fp64 (SG_TASK_HP) tasks
+      int64_t nh = 0, sh = 0, lh64 = 0;
+      double th = 0, rn = 0;
+      for (const SgWTask& t : B.tasks)
+        if (t.flags & SG_TASK_HP) {
+          ++nh; sh += t.len; lh64 += t.len <= 64;
+          th += (double)t.Rn * t.len * ((t.flags & SG_TASK_CONST) ? 1 : 2);
+          rn += t.Rn;
+        }
+      std::fprintf(stderr, "sg plan: fp64 tasks %lld (%lld samples, %lld of <= 64 samples, %.3g chain terms, mean Rn %.1f)\n",
+                   (long long)nh, (long long)sh, (long long)lh64, th, nh ? rn / nh : 0.0);
+    }
     for (const SgWTask& t : B.tasks) {
       const int k = t.R > SG_ROWS_F32 ? 1 : 0;
       terms[k] += (double)t.R * t.len * ((t.flags & SG_TASK_CONST) ? 1 : 2);
@@ -258,7 +274,10 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   D.W64 = (double*)(a + L.W64);
   D.fh = (double*)(a + L.fh);
   D.frames64 = (SgFrame64*)(a + L.frames64);
-  D.fgroups64 = (SgFrameGroup*)(a + L.fgroups64);
+  D.frames64_tab = (int64_t*)(a + L.frames64_tab);
+  D.roots64 = (double*)(a + L.roots64);
+  D.roots64_wl = (int32_t*)(a + L.roots64_wl);
+  D.roots64_off = (int64_t*)(a + L.roots64_off);
   D.pieces = (SgPiece*)(a + L.pieces);
   D.syls = (SgSyllable*)(a + L.syls);
   D.syl_tiles = (SgSylTile*)(a + L.syl_tiles);
@@ -317,7 +336,9 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   cp(D.thp, D.thp_host.data(), D.thp_host.size() * sizeof(int32_t));
   cp(D.fin_tiles_hp, B.fin_tiles_hp.data(), B.fin_tiles_hp.size() * sizeof(SgSylTile));
   cp(D.frames64, B.frames64.data(), B.frames64.size() * sizeof(SgFrame64));
-  cp(D.fgroups64, B.fgroups64.data(), B.fgroups64.size() * sizeof(SgFrameGroup));
+  cp(D.frames64_tab, B.frames64_tab.data(), B.frames64_tab.size() * sizeof(int64_t));
+  cp(D.roots64_wl, B.roots64_wl.data(), B.roots64_wl.size() * sizeof(int32_t));
+  cp(D.roots64_off, B.roots64_off.data(), B.roots64_off.size() * sizeof(int64_t));
   cp(D.pieces, B.pieces.data(), B.pieces.size() * sizeof(SgPiece));
   cp(D.syls, B.syls.data(), B.syls.size() * sizeof(SgSyllable));
   cp(D.syl_tiles, B.fin_tiles.data(), B.fin_tiles.size() * sizeof(SgSylTile));
@@ -464,7 +485,7 @@ void device_execute_spec(const Batch& B, const DevicePlan& D, float* d_out, hipS
       prof->push_back({SG_PROF_STFT_OLA, e0, e1});
     }
     launch_fft_frames(D, r[1], r[2] - r[1], B.fgroup_lds[ph][1], s);
-    if (ph == 1) launch_fft_frames64(D, (int64_t)B.fgroups64.size(), B.fgroup64_lds, s);
+    if (ph == 1) launch_fft_frames64(D, B, s);
     const int64_t t0 = ph == 0 ? 0 : B.olatile_split, t1 = ph == 0 ? B.olatile_split : (int64_t)B.olatiles.size();
     const int64_t o0 = ph == 0 ? 0 : B.ola_split, o1 = ph == 0 ? B.ola_split : (int64_t)B.olas_dev.size();
     launch_ola(D, t0, t1 - t0, s);

@@ -44,7 +44,10 @@ struct DevicePlan {
   double* W64 = nullptr;             // fp64 epoch waveforms of SG_TASK_HP tasks
   double* fh = nullptr;              // fp64 sounds (voiced parts, pre-filter sounds) of fp64 bouts
   SgFrame64* frames64 = nullptr;     // their filter frames (sg_fft_frames64)
-  SgFrameGroup* fgroups64 = nullptr; // their workgroups: geom = window length, frames [f0, f0 + nf)
+  int64_t* frames64_tab = nullptr;   // per frame: offset of its root table in roots64
+  double* roots64 = nullptr;         // W_N^t tables (double2), one per window length (sg_roots64)
+  int32_t* roots64_wl = nullptr;
+  int64_t* roots64_off = nullptr;
   SgPiece* pieces = nullptr;
   SgSyllable* syls = nullptr;
   SgSylTile* syl_tiles = nullptr;    // general-path finalize tiles (Batch::fin_tiles)
@@ -115,7 +118,7 @@ void launch_sine_bank_hp(const DevicePlan& D, int64_t n, hipStream_t s);
 void launch_piece_max_hp(const DevicePlan& D, int64_t p0, int64_t n_ptiles, hipStream_t s);
 void launch_harm_finalize_hp(const DevicePlan& D, int64_t n_stiles, hipStream_t s);
 void launch_mix_hp(const DevicePlan& D, int64_t t0, int64_t n_tiles, hipStream_t s);
-void launch_fft_frames64(const DevicePlan& D, int64_t n_groups, int lds_bytes, hipStream_t s);
+void launch_fft_frames64(const DevicePlan& D, const Batch& B, hipStream_t s);
 // sg_fft.hip
 void launch_fft_frames(const DevicePlan& D, int64_t g0, int64_t n_groups, int lds_bytes, hipStream_t s);
 void launch_stft_ola(const DevicePlan& D, int phase, int64_t s0, int64_t n_segs, int lds_bytes, hipStream_t s);

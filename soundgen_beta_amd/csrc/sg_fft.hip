@@ -1092,8 +1092,8 @@ __device__ __forceinline__ float fade_in_out(int lf, int64_t L, int64_t k) {  //
 
 // ------------------------------------------------ fp64 filter frames
 // Frames of an ill-conditioned formant-filter call (SgFrame64; planner:
-// filter_conditioning): seewave's stft x env -> istft in fp64, nf frames of one
-// even window length N = 2M per workgroup (SgFrameGroup: geom = N):
+// filter_conditioning): seewave's stft x env -> istft in fp64, one frame of an
+// even window length N = 2M per 256-thread workgroup (M <= 2048):
 //   forward: the M-point complex DFT of z_n = x_2n + i x_2n+1 (x = hamming x
 //            fp64 sound), untangled to X_k = E_k + W_N^k O_k;  Y_k = X_k / N env_k
 //   inverse: seewave's Hermitian extension X' (X'_M = Re Y_{M-1}, seewave.r:3474)
@@ -1101,100 +1101,97 @@ __device__ __forceinline__ float fade_in_out(int lf, int64_t L, int64_t k) {  //
 //            M-point inverse DFT gives x_2n + i x_2n+1; / N x hann, stored fp32 for
 //            the overlap-add (sg_ola; that round-off is relative to the filtered
 //            output, ~1e-8 RMS)
-// Stockham autosort, out of place in LDS. Per stage of radix R: (a) every input
-// times its twiddle, in place; (b) odd R: one work item per (butterfly, output
-// pair k, R - k) from the symmetric sums x_m +- x_{R-m} (all threads busy for
-// R = 19, 29); R = 2, 4: one item per butterfly. Roots from one table W_N^t
-// (fp64 sincospi) shared by the workgroup's frames.
+// Stockham autosort, out of place between two M-point LDS buffers (35 KB for
+// wl = 2204: 4 workgroups per CU). Per stage of radix R: (a) every input times
+// its twiddle, in place; (b) odd R: one work item per (butterfly, output pair k,
+// R - k) from the symmetric sums x_m +- x_{R-m} (all threads busy for R = 19,
+// 29), R = 2, 4: one item per butterfly. Roots of unity W_N^t from an fp64 table
+// in global memory, one per window length (sg_roots64), L2-resident.
+constexpr int SG_F64_THREADS = 256;
 namespace {
 __device__ __forceinline__ double2 cmul64(double2 a, double2 b) {
   return make_double2(fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x));
 }
-// one radix-R stage over nf frames of M points (src -> dst); TN = W_N^t, t < N = 2M
+__device__ __forceinline__ double2 conj_if(double2 w, bool c) { return c ? make_double2(w.x, -w.y) : w; }
+// one radix-R stage of an M-point frame, src -> dst; TN = W_N^t, t < N = 2M; rt = W_R^t
 template <int R>
-__device__ void stage64(double2* __restrict__ src, double2* __restrict__ dst, int M, int nf, int Ns,
-                        const double2* __restrict__ TN, bool inv) {
+__device__ void stage64(double2* __restrict__ src, double2* __restrict__ dst, int M, int Ns,
+                        const double2* __restrict__ TN, const double2* __restrict__ rt, bool inv) {
   const int nR = M / R, tstep2 = 2 * (M / (Ns * R));  // W_{Ns R}^e = W_N^(2 e M / (Ns R))
-  if (Ns > 1) {  // (a) twiddles, in place: input j + r nR of butterfly j times W_{Ns R}^(r (j mod Ns))
-    for (int i = threadIdx.x; i < nf * M; i += blockDim.x) {
-      const int f = i / M, q = i - f * M;
+  if (Ns > 1) {  // (a) input j + r nR of butterfly j times W_{Ns R}^(r (j mod Ns)), in place
+    for (int q = threadIdx.x; q < M; q += SG_F64_THREADS) {
       const int r = q / nR, jm = (q - r * nR) % Ns;
-      if (r == 0 || jm == 0) continue;
-      double2 w = TN[r * jm * tstep2];
-      if (inv) w.y = -w.y;
-      src[i] = cmul64(src[i], w);
+      if (r != 0 && jm != 0) src[q] = cmul64(src[q], conj_if(TN[r * jm * tstep2], inv));
     }
     __syncthreads();
   }
-  const int NT = M / R * 2;  // W_R^t = W_N^(t * 2M / R)
   if constexpr (R == 2 || R == 4) {
-    for (int i = threadIdx.x; i < nf * nR; i += blockDim.x) {
-      const int f = i / nR, j = i - f * nR, jm = j % Ns;
-      const double2* x = src + f * M + j;
-      double2* y = dst + f * M + (j - jm) * R + jm;
+    for (int j = threadIdx.x; j < nR; j += SG_F64_THREADS) {
+      const int jm = j % Ns;
+      const double2* x = src + j;
+      double2* y = dst + (j - jm) * R + jm;
       if constexpr (R == 2) {
-        const double2 a = x[0], b = x[nR];
-        y[0] = make_double2(a.x + b.x, a.y + b.y);
-        y[Ns] = make_double2(a.x - b.x, a.y - b.y);
+        const double2 u = x[0], v = x[nR];
+        y[0] = make_double2(u.x + v.x, u.y + v.y);
+        y[Ns] = make_double2(u.x - v.x, u.y - v.y);
       } else {
         const double2 a = x[0], b = x[nR], c = x[2 * nR], d = x[3 * nR];
         const double2 s0 = make_double2(a.x + c.x, a.y + c.y), d0 = make_double2(a.x - c.x, a.y - c.y);
         const double2 s1 = make_double2(b.x + d.x, b.y + d.y), d1 = make_double2(b.x - d.x, b.y - d.y);
         // forward: y1 = d0 - i d1, y3 = d0 + i d1 (inverse: swapped)
-        const double2 m1 = inv ? make_double2(d0.x - d1.y, d0.y + d1.x) : make_double2(d0.x + d1.y, d0.y - d1.x);
-        const double2 m3 = inv ? make_double2(d0.x + d1.y, d0.y - d1.x) : make_double2(d0.x - d1.y, d0.y + d1.x);
+        const double2 mm = make_double2(d0.x + d1.y, d0.y - d1.x), mp = make_double2(d0.x - d1.y, d0.y + d1.x);
         y[0] = make_double2(s0.x + s1.x, s0.y + s1.y);
-        y[Ns] = m1;
+        y[Ns] = inv ? mp : mm;
         y[2 * Ns] = make_double2(s0.x - s1.x, s0.y - s1.y);
-        y[3 * Ns] = m3;
+        y[3 * Ns] = inv ? mm : mp;
       }
     }
   } else {
+    // y_k = x_0 + sum_m A_m c_mk -/+ i sum_m B_m s_mk (forward -, inverse +), y_{R-k} the
+    // other sign; A_m = x_m + x_{R-m}, B_m = x_m - x_{R-m}; item k = 0: y_0 = x_0 + sum A_m
     constexpr int H = (R - 1) / 2;
-    // y_k = x_0 + sum_m A_m c_mk -/+ i sum_m B_m s_mk,  y_{R-k}: the other sign,
-    // A_m = x_m + x_{R-m}, B_m = x_m - x_{R-m}, c_mk = cos(2 pi m k / R), s_mk = sin(.)
-    for (int i = threadIdx.x; i < nf * nR * (H + 1); i += blockDim.x) {
-      const int k = i % (H + 1), b = i / (H + 1);
-      const int f = b / nR, j = b - f * nR, jm = j % Ns;
-      const double2* x = src + f * M + j;
-      double2* y = dst + f * M + (j - jm) * R + jm;
+    for (int i = threadIdx.x; i < nR * (H + 1); i += SG_F64_THREADS) {
+      const int k = i % (H + 1), j = i / (H + 1), jm = j % Ns;
+      const double2* x = src + j;
+      double2* y = dst + (j - jm) * R + jm;
       const double2 x0 = x[0];
-      if (k == 0) {
-        double2 acc = x0;
-#pragma unroll
-        for (int r = 1; r < R; ++r) { acc.x += x[r * nR].x; acc.y += x[r * nR].y; }
-        y[0] = acc;
-        continue;
-      }
       double2 P = make_double2(0.0, 0.0), Q = make_double2(0.0, 0.0);
-#pragma unroll
+#pragma unroll 1
       for (int m = 1; m <= H; ++m) {
         const double2 u = x[m * nR], v = x[(R - m) * nR];
-        const double2 w = TN[((m * k) % R) * NT];  // (cos, -sin) of 2 pi m k / R
+        const double2 w = k == 0 ? make_double2(1.0, 0.0) : rt[(m * k) % R];  // (cos, -sin) of 2 pi m k / R
         P.x = fma(u.x + v.x, w.x, P.x);
         P.y = fma(u.y + v.y, w.x, P.y);
         Q.x = fma(u.x - v.x, -w.y, Q.x);
         Q.y = fma(u.y - v.y, -w.y, Q.y);
       }
-      // forward (e^-i): y_k = x0 + P - i Q, y_{R-k} = x0 + P + i Q; inverse: the signs swap
       const double2 ya = make_double2(x0.x + P.x + Q.y, x0.y + P.y - Q.x);
       const double2 yb = make_double2(x0.x + P.x - Q.y, x0.y + P.y + Q.x);
-      y[k * Ns] = inv ? yb : ya;
-      y[(R - k) * Ns] = inv ? ya : yb;
+      if (k == 0) {
+        y[0] = ya;
+      } else {
+        y[k * Ns] = inv ? yb : ya;
+        y[(R - k) * Ns] = inv ? ya : yb;
+      }
     }
   }
   __syncthreads();
 }
-// M-point complex DFT of nf frames in *a (result in *a; *b is scratch)
-__device__ void fft64(double2*& a, double2*& b, int M, int nf, const double2* __restrict__ TN, bool inv) {
+// M-point complex DFT of *a (result in *a, *b scratch); TN: W_N^t (t < 2M), global; rt: LDS (32)
+__device__ void fft64(double2*& a, double2*& b, int M, const double2* __restrict__ TN,
+                                   double2* __restrict__ rt, bool inv) {
   int rest = M, Ns = 1;
   while (rest > 1) {
     int R = rest % 4 == 0 ? 4 : rest % 2 == 0 ? 2 : 0;
     if (!R)
       for (int p : {3, 5, 7, 11, 13, 17, 19, 23, 29, 31})
         if (rest % p == 0) { R = p; break; }
+    if (R > 4) {  // W_R^t = W_N^(t 2M / R), t < R
+      if (threadIdx.x < R) rt[threadIdx.x] = TN[threadIdx.x * (2 * M / R)];
+      __syncthreads();
+    }
     switch (R) {
-#define SG_S64(RR) case RR: stage64<RR>(a, b, M, nf, Ns, TN, inv); break;
+#define SG_S64(RR) case RR: stage64<RR>(a, b, M, Ns, TN, rt, inv); break;
       SG_S64(2) SG_S64(3) SG_S64(4) SG_S64(5) SG_S64(7) SG_S64(11) SG_S64(13) SG_S64(17) SG_S64(19) SG_S64(23)
       SG_S64(29) SG_S64(31)
 #undef SG_S64
@@ -1207,67 +1204,68 @@ __device__ void fft64(double2*& a, double2*& b, int M, int nf, const double2* __
 }
 }  // namespace
 
-extern "C" __global__ __launch_bounds__(256) void sg_fft_frames64(const SgFrameGroup* __restrict__ groups,
-                                                                  const SgFrame64* __restrict__ frames,
-                                                                  const float* __restrict__ fl,
-                                                                  const double* __restrict__ fh,
-                                                                  float* __restrict__ fs) {
-  extern __shared__ double2 lds64[];
-  const SgFrameGroup G = groups[blockIdx.x];
-  const int N = G.geom, M = N / 2, nf = G.nf;
-  double2* TN = lds64;          // W_N^t, t < N
-  double2* a = TN + N;          // nf frames of M points
-  double2* b = a + nf * M;      // nf frames of M points
-  const double wd = (double)(N - 1);
-  for (int t = threadIdx.x; t < N; t += blockDim.x) {
+// W_N^t = exp(-2 pi i t / N), t < N, for every window length of the plan's fp64 frames
+extern "C" __global__ __launch_bounds__(256) void sg_roots64(const int32_t* __restrict__ wls,
+                                                             const int64_t* __restrict__ offs,
+                                                             double2* __restrict__ tabs) {
+  const int N = wls[blockIdx.y];
+  double2* T = tabs + offs[blockIdx.y];
+  for (int t = blockIdx.x * 256 + threadIdx.x; t < N; t += gridDim.x * 256) {
     double sn, cs;
     sincospi(-2.0 * (double)t / (double)N, &sn, &cs);
-    TN[t] = make_double2(cs, sn);
+    T[t] = make_double2(cs, sn);
   }
-  for (int i = threadIdx.x; i < nf * M; i += blockDim.x) {  // hamming (seewave ftwindow), packed pairs
-    const int f = i / M, n = i - f * M;
-    const double* x = fh + frames[G.f0 + f].src + 2 * n;
+}
+
+extern "C" __global__ __launch_bounds__(SG_F64_THREADS) void sg_fft_frames64(
+    const SgFrame64* __restrict__ frames, const int64_t* __restrict__ frame_tab, const double2* __restrict__ tabs,
+    const float* __restrict__ fl, const double* __restrict__ fh, float* __restrict__ fs) {
+  extern __shared__ double2 lds64[];
+  const SgFrame64 F = frames[blockIdx.x];
+  const int N = F.wl, M = N / 2;
+  const double2* __restrict__ TN = tabs + frame_tab[blockIdx.x];
+  double2* a = lds64;        // M points
+  double2* b = a + M;        // M points
+  double2* rt = b + M;       // radix roots (<= 31)
+  const double wd = (double)(N - 1);
+  const double* x = fh + F.src;
+  for (int n = threadIdx.x; n < M; n += SG_F64_THREADS) {  // hamming (seewave ftwindow), packed pairs
     const double h0 = 0.54 - 0.46 * cospi(2.0 * (double)(2 * n) / wd);
     const double h1 = 0.54 - 0.46 * cospi(2.0 * (double)(2 * n + 1) / wd);
-    a[i] = make_double2(x[0] * h0, x[1] * h1);
+    a[n] = make_double2(x[2 * n] * h0, x[2 * n + 1] * h1);
   }
   __syncthreads();
-  fft64(a, b, M, nf, TN, false);
-  // untangle, / N, x env (Y_k, k < M), Hermitian extension, pack for the inverse (into b)
+  fft64(a, b, M, TN, rt, false);
+  // untangle, / N, x env (Y_k, k < M), Hermitian extension, pack for the inverse (a -> b)
   const double invN = 1.0 / (double)N;
-  for (int i = threadIdx.x; i < nf * M; i += blockDim.x) {
-    const int f = i / M, k = i - f * M;
-    const double2* z = a + f * M;
-    const float* env = fl + frames[G.f0 + f].env;
-    auto Yat = [&](int kk) -> double2 {  // Y_kk, 0 <= kk < M
-      const double2 p = z[kk], q = z[kk == 0 ? 0 : M - kk];
-      const double2 e = make_double2(0.5 * (p.x + q.x), 0.5 * (p.y - q.y));
-      const double2 o = make_double2(0.5 * (p.y + q.y), -0.5 * (p.x - q.x));
-      const double2 x = make_double2(e.x + (o.x * TN[kk].x - o.y * TN[kk].y), e.y + (o.x * TN[kk].y + o.y * TN[kk].x));
-      const double sc = invN * (double)env[kk];
-      return make_double2(x.x * sc, x.y * sc);
-    };
+  const float* env = fl + F.env;
+  auto Yat = [&](int kk) -> double2 {  // Y_kk, 0 <= kk < M
+    const double2 p = a[kk], q = a[kk == 0 ? 0 : M - kk], w = TN[kk];
+    const double2 e = make_double2(0.5 * (p.x + q.x), 0.5 * (p.y - q.y));
+    const double2 o = make_double2(0.5 * (p.y + q.y), -0.5 * (p.x - q.x));
+    const double2 xk = make_double2(e.x + (o.x * w.x - o.y * w.y), e.y + (o.x * w.y + o.y * w.x));
+    const double sc = invN * (double)env[kk];
+    return make_double2(xk.x * sc, xk.y * sc);
+  };
+  for (int k = threadIdx.x; k < M; k += SG_F64_THREADS) {
     const double2 yk = Yat(k);
-    // X'_{k+M}: Re Y_{M-1} for k = 0, else conj(Y_{M-k})
-    double2 yh;
+    double2 yh;  // X'_{k+M}: Re Y_{M-1} for k = 0, else conj(Y_{M-k})
     if (k == 0) { const double2 t = Yat(M - 1); yh = make_double2(t.x, 0.0); }
     else { const double2 t = Yat(M - k); yh = make_double2(t.x, -t.y); }
-    const double2 s = make_double2(yk.x + yh.x, yk.y + yh.y), d = make_double2(yk.x - yh.x, yk.y - yh.y);
-    const double2 wc = make_double2(TN[k].x, -TN[k].y);  // W_N^-k
-    const double2 t = cmul64(d, wc);                       // i * t added below
-    b[i] = make_double2(s.x - t.y, s.y + t.x);
+    const double2 sm = make_double2(yk.x + yh.x, yk.y + yh.y), df = make_double2(yk.x - yh.x, yk.y - yh.y);
+    const double2 t = cmul64(df, conj_if(TN[k], true));  // W_N^-k (X'_k - X'_{k+M})
+    b[k] = make_double2(sm.x - t.y, sm.y + t.x);
   }
   __syncthreads();
   double2* c = b;
   double2* d = a;
-  fft64(c, d, M, nf, TN, true);
-  for (int i = threadIdx.x; i < nf * M; i += blockDim.x) {
-    const int f = i / M, n = i - f * M;
-    float* out = fs + frames[G.f0 + f].dst + 2 * n;
+  fft64(c, d, M, TN, rt, true);
+  float* out = fs + F.dst;
+  for (int n = threadIdx.x; n < M; n += SG_F64_THREADS) {
     const double h0 = 0.5 - 0.5 * cospi(2.0 * (double)(2 * n) / wd);
     const double h1 = 0.5 - 0.5 * cospi(2.0 * (double)(2 * n + 1) / wd);
-    out[0] = (float)(c[i].x * invN * h0);
-    out[1] = (float)(c[i].y * invN * h1);
+    out[2 * n] = (float)(c[n].x * invN * h0);
+    out[2 * n + 1] = (float)(c[n].y * invN * h1);
   }
 }
 
@@ -1459,11 +1457,16 @@ void launch_fft_probe(const SgFftGeom* geom, const float* fl, float* data, int M
                      reinterpret_cast<float2*>(data), inverse);
   SG_LAUNCHED("sg_fft_probe");
 }
-void launch_fft_frames64(const DevicePlan& D, int64_t n_groups, int lds_bytes, hipStream_t s) {
-  if (n_groups <= 0) return;
-  lds_opt_in(reinterpret_cast<const void*>(&sg_fft_frames64), lds_bytes, "sg_fft_frames64");
-  hipLaunchKernelGGL(sg_fft_frames64, dim3((unsigned)n_groups), dim3(256), lds_bytes, s, D.fgroups64, D.frames64,
-                     D.fl, D.fh, D.fs);
+void launch_fft_frames64(const DevicePlan& D, const Batch& B, hipStream_t s) {
+  const int64_t n = (int64_t)B.frames64.size();
+  if (n <= 0) return;
+  hipLaunchKernelGGL(sg_roots64, dim3(16, (unsigned)B.roots64_wl.size()), dim3(256), 0, s, D.roots64_wl, D.roots64_off,
+                     reinterpret_cast<double2*>(D.roots64));
+  SG_LAUNCHED("sg_roots64");
+  const int lds = (B.frames64_maxwl + 32) * (int)sizeof(double2);  // two M-point buffers + radix roots
+  lds_opt_in(reinterpret_cast<const void*>(&sg_fft_frames64), lds, "sg_fft_frames64");
+  hipLaunchKernelGGL(sg_fft_frames64, dim3((unsigned)n), dim3(SG_F64_THREADS), lds, s, D.frames64, D.frames64_tab,
+                     reinterpret_cast<const double2*>(D.roots64), D.fl, D.fh, D.fs);
   SG_LAUNCHED("sg_fft_frames64");
 }
 void launch_mix_hp(const DevicePlan& D, int64_t t0, int64_t n_tiles, hipStream_t s) {

@@ -70,8 +70,12 @@ struct Batch {
   std::vector<int32_t> frame_geom[2];
   std::vector<SgOla> olas[2];            // [0] noise OLAs, [1] filter OLAs (device: [0] then [1])
   std::vector<SgFrame64> frames64;       // filter frames of fp64 (ill-conditioned) calls: sg_fft_frames64
-  std::vector<SgFrameGroup> fgroups64;   // derived (finalize_spec): sg_fft_frames64 workgroups (geom = wl)
-  int32_t fgroup64_lds = 0;              // derived: their largest dynamic LDS
+  // derived (finalize_spec): the window lengths of the fp64 frames, their root tables
+  // W_N^t (offsets in double2 units), each frame's table offset, the largest window
+  std::vector<int32_t> roots64_wl;
+  std::vector<int64_t> roots64_off, frames64_tab;
+  int64_t roots64_total = 0;
+  int32_t frames64_maxwl = 0;
   std::vector<SgNoiseItem> items;        // items[].ola indexes the device OLA table
   std::vector<SgMix> mixes[2];           // [0] pre-filter sounds (fs), [1] final output
   struct Copy { int64_t fl_off, fs_off, n; };
@@ -115,6 +119,8 @@ struct Batch {
   int64_t total_out = 0;
   // ---- stats ----
   int64_t harm_samples = 0, harm_terms = 0, harm_amp_bytes = 0, fft_frames = 0;
+  double fft_flops = 0;                      // nominal 5 wl log2 wl per transform, every frame path
+  std::vector<double> call_rows, call_flops;  // per call: sine-bank (sample, row) terms, FFT flops
   int64_t stft_bytes = 0, stft_samples = 0;  // sg_stft_ola: algorithmic bytes, trimmed output samples
   double stft_flops = 0;                     // sg_stft_ola: nominal 5 wl log2 wl per transform
 };

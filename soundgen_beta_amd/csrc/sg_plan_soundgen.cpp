@@ -559,9 +559,8 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
       filt_env = plan_envelope(B, R, (double)wl / 2, nInt, &Fm, A.formantDep, A.rolloffLip, mouthA.view(), 0, 0,
                                A.vocalTract, T, A.tempEffects[1], A.tempEffects[2], A.formantDepStoch, 1, sr, 35400);
       const int mode = hp_mode();
-      // the fp64 frame kernel takes even windows with a 31-smooth half (M); one frame of
-      // 2204 points needs 53 KB of LDS (W_N table + two M-point buffers)
-      if (mode > 0 && !bout_syls.empty() && wl % 2 == 0 && wl <= 4096 && smooth31(wl / 2)) {
+      // the fp64 frame kernel takes even windows with a 31-smooth half M <= 2048
+      if (mode > 0 && !bout_syls.empty() && wl % 2 == 0 && wl <= 4096 && smooth31(wl / 2)) {  // M <= 2048
         if (mode == 2) {
           hp = true;
         } else {

@@ -304,6 +304,7 @@ int plan_filter(Batch& B, int64_t sound, int64_t L, int wl, double overlap, int6
     const IstftGeom ig = istft_geom(wl, nc, overlap);
     const int64_t out = fs_alloc(B, ig.xlen);
     B.fft_frames += nc;
+    B.fft_flops += 2 * 5.0 * wl * std::log2((double)wl) * (double)nc;
     *out_len = ig.xlen;
     *out_fs = out;
     return push_ola(B, 1, fr, nc, wl, ig, 0, ig.xlen, out, false, true);
@@ -320,6 +321,7 @@ int plan_filter(Batch& B, int64_t sound, int64_t L, int wl, double overlap, int6
   const IstftGeom ig = istft_geom(wl, nc, overlap);
   const int64_t out = fs_alloc(B, ig.xlen);
   B.fft_frames += nc;
+  B.fft_flops += 2 * 5.0 * wl * std::log2((double)wl) * (double)nc;
   *out_len = ig.xlen;
   *out_fs = out;
   return push_ola(B, 1, fr, nc, wl, ig, 0, ig.xlen, out, fused);
@@ -387,6 +389,7 @@ bool plan_noise(Batch& B, Rng& R, int64_t len, const sg_anchors& noiseAnchors, d
   const int64_t raw = fs_alloc(B, len);
   const int ola = push_ola(B, 0, fr, nc, wl, ig, first, len, raw, fused);
   B.fft_frames += nc;
+  B.fft_flops += 1 * 5.0 * wl * std::log2((double)wl) * (double)nc;
   item->raw = raw;
   item->len = len;
   item->off = 0;
@@ -655,22 +658,23 @@ void finalize_spec(Batch& B) {
   for (int ph = 0; ph < 2; ++ph)
     for (SgFrame& f : B.frames[ph])
       if (f.env < 0) f.env = B.fe_base + (-f.env - 1);
-  // fp64 frames: by window length, up to 4 per workgroup as LDS allows (16 N for
-  // the W_N table, 32 M per frame)
-  for (SgFrame64& f : B.frames64)
+  // fp64 frames: one root table W_N^t per window length (sg_roots64)
+  B.roots64_wl.clear();
+  B.roots64_off.clear();
+  B.frames64_tab.clear();
+  B.roots64_total = 0;
+  B.frames64_maxwl = 0;
+  for (SgFrame64& f : B.frames64) {
     if (f.env < 0) f.env = B.fe_base + (-f.env - 1);
-  std::stable_sort(B.frames64.begin(), B.frames64.end(),
-                   [](const SgFrame64& x, const SgFrame64& y) { return x.wl < y.wl; });
-  B.fgroups64.clear();
-  B.fgroup64_lds = 0;
-  for (size_t i = 0; i < B.frames64.size();) {
-    const int N = B.frames64[i].wl, M = N / 2;
-    const int fpb = std::max(1, std::min(4, (160 * 1024 - 16 * N) / (32 * M)));
-    size_t j = i;
-    while (j < B.frames64.size() && B.frames64[j].wl == N && (int)(j - i) < fpb) ++j;
-    B.fgroups64.push_back(SgFrameGroup{N, SG_FRAME_FILTER, (int32_t)i, (int32_t)(j - i)});
-    B.fgroup64_lds = std::max(B.fgroup64_lds, 16 * N + 32 * M * (int)(j - i));
-    i = j;
+    size_t w = 0;
+    while (w < B.roots64_wl.size() && B.roots64_wl[w] != f.wl) ++w;
+    if (w == B.roots64_wl.size()) {
+      B.roots64_wl.push_back(f.wl);
+      B.roots64_off.push_back(B.roots64_total);
+      B.roots64_total += f.wl;
+    }
+    B.frames64_tab.push_back(B.roots64_off[w]);
+    B.frames64_maxwl = std::max(B.frames64_maxwl, f.wl);
   }
   int32_t maxnr = 0;
   for (const SgEnvJob& j : B.envjobs) {

@@ -202,8 +202,10 @@ def morphFormants(f1, f2, nMorphs=5):
 
 def morphList(l1, l2, nMorphs=5):
     """R/utilities_morph.R:254-285: equal formant counts (a silent copy of the other
-    list's next formant; R names it after the other list's LAST formant, so names
-    can repeat), then morph formant by formant, by position."""
+    list's next formant), then morph formant by formant, by position. Naming
+    follows R's two loops: padding l2 takes l1's LAST name (names can repeat,
+    :256-260); padding l1 takes l2's name at the new position (names(l1) is
+    indexed after l1 grew, :261-265)."""
     a = [(k, copy.deepcopy(v)) for k, v in l1.items()]
     b = [(k, copy.deepcopy(v)) for k, v in l2.items()]
     while len(a) > len(b):
@@ -213,7 +215,7 @@ def morphList(l1, l2, nMorphs=5):
     while len(b) > len(a):
         f = copy.deepcopy(b[len(a)][1])
         f["amp"] = 0.0
-        a.append((b[-1][0], f))
+        a.append((b[len(a)][0], f))
     out = [[(k, copy.deepcopy(v)) for k, v in a] for _ in range(nMorphs)]
     for fi in range(len(a)):
         temp = morphFormants(a[fi][1], b[fi][1], nMorphs)
@@ -327,17 +329,30 @@ def morph(formula1, formula2, nMorphs, playMorphs=False, savePath=None, sampling
           uniforms=None, device=0):
     """morph(formula1, formula2, nMorphs, playMorphs, savePath, samplingRate),
     R/morph.R:30-209. Returns {"formulas": [...], "sounds": [...]}; the nMorphs
-    soundgen() calls run as one GPU batch (random draws injected per call)."""
+    soundgen() calls run as one GPU batch.
+    Random draws: R's loop (R/morph.R:200-201) runs the morphs on ONE continuous
+    RNG stream, morph h using the draws left by morph h-1. Pass normals/uniforms
+    as a list of nMorphs arrays (each morph's own draws, e.g. R's stream split at
+    the morph boundaries) to reproduce that; a single array is read from its start
+    by every morph (all morphs share one perturbation; parity with R's sequence
+    unpinned then)."""
     if playMorphs:
         raise NotImplementedError("playMorphs: audio playback is outside the synthesis path")
     formulas = morph_formulas(formula1, formula2, nMorphs)
-    calls = [{"kind": "soundgen", "args": _soundgen_args(f), "normals": normals, "uniforms": uniforms}
-             for f in formulas]
+
+    def per(v, h):
+        return v[h] if isinstance(v, (list, tuple)) else v
+    for v in (normals, uniforms):
+        if isinstance(v, (list, tuple)) and len(v) != nMorphs:
+            raise ValueError("per-morph draws: %d arrays for %d morphs" % (len(v), nMorphs))
+    calls = [{"kind": "soundgen", "args": _soundgen_args(f), "normals": per(normals, h), "uniforms": per(uniforms, h)}
+             for h, f in enumerate(formulas)]
     from . import batch
-    if savePath is not None:
+    if savePath is not None:  # one plan and one execute: the 16-bit files and the fp32 sounds
         paths = ["%smorph_%d.wav" % (savePath, h + 1) for h in range(nMorphs)]  # paste0(savePath, 'morph_', h, '.wav')
-        batch.synthesize_to_wav(calls, paths, samplingRate, device)
-    sounds = batch.synthesize(calls, device)
+        _, sounds = batch.synthesize_to_wav(calls, paths, samplingRate, device, return_float=True)
+    else:
+        sounds = batch.synthesize(calls, device)
     for s in sounds:
         if isinstance(s, Exception):
             raise s

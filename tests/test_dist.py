@@ -1,7 +1,10 @@
-"""Sharded batch path (soundgen_beta_amd/dist.py) on CPU: LPT assignment and
-the gather to rank 0 over torch.distributed gloo, world size 2. The per-rank
-synthesizer is the oracle here (test infrastructure); on the GPU box it is
-batch.synthesize, exchanged over RCCL."""
+"""Sharded batch path (soundgen_beta_amd/dist.py) on CPU, torch.distributed gloo
+at world size 2: LPT assignment, the packed exchange step (all_gather of the
+packed lengths, then one point-to-point send per peer of its packed buffer and
+(offset, length) table), and every rank running the REAL host planner on its
+shard. The per-rank synthesizer is the oracle here (test infrastructure); on
+the GPU box it is batch.synthesize_packed and the packed HBM buffer goes over
+RCCL."""
 import os
 import socket
 
@@ -22,6 +25,7 @@ def _calls():
                                                    pitchAnchors=None,
                                                    noiseAnchors={"time": [0, 150], "value": [-20, -20]}),
                   "uniforms": np.random.default_rng(5).uniform(size=400 * 40)})
+    calls.append({"kind": "harmonics", "pitch": np.full(1, 150.0), "params": dict(samplingRate=16000)})  # refused
     return calls
 
 
@@ -29,11 +33,21 @@ def _oracle_synth(calls):
     from oracle import oracle as O
     out = []
     for c in calls:
-        if c["kind"] == "harmonics":
-            out.append(O.generate_harmonics(c["pitch"], **c["params"]))
-        else:
-            out.append(O.soundgen(uniforms=c.get("uniforms"), **c["args"]))
+        try:
+            if c["kind"] == "harmonics":
+                out.append(O.generate_harmonics(c["pitch"], **c["params"]))
+            else:
+                out.append(O.soundgen(uniforms=c.get("uniforms"), **c["args"]))
+        except Exception as e:  # noqa: BLE001 -- a refused call travels as a failed slot
+            out.append(e)
     return out
+
+
+def _bench():
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    return bench
 
 
 def test_lpt_assignment_balanced_and_deterministic():
@@ -43,7 +57,17 @@ def test_lpt_assignment_balanced_and_deterministic():
     loads = [sum(c for c, r in zip(costs, a) if r == k) for k in range(3)]
     assert max(loads) - min(loads) <= max(costs)
     assert set(a) == {0, 1, 2}
-    assert sgd.call_cost(_calls()[0]) > 0 and sgd.call_cost(_calls()[-1]) > 0
+    assert sgd.call_cost(_calls()[0]) > 0 and sgd.call_cost(_calls()[-2]) > 0
+
+
+def test_cost_rows_follow_get_rolloff(oracle):
+    """harmonic_rows() counts the rows getRolloff keeps (the oracle's, no cap)."""
+    for f0, kw in ((100.0, dict(rolloff=-12, rolloffOct=-12, rolloffKHz=-6)),
+                   (71.0, dict(rolloff=-24, rolloffOct=0, rolloffKHz=-10)),
+                   (400.0, dict(rolloff=-6, rolloffOct=-2, rolloffKHz=-6))):
+        nH = int(np.ceil((44100 / 2 - f0) / f0))
+        A = oracle.get_rolloff([f0], nHarmonics=nH, samplingRate=44100, rolloffParab=0, **kw)
+        assert sgd.harmonic_rows(f0, 44100, **kw) == A.shape[0], (f0, kw)
 
 
 def _worker(rank, world, port, q):
@@ -52,8 +76,16 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         res = sgd.synthesize_sharded(_calls(), rank, world, synth=_oracle_synth, comm_device="cpu")
+        # the real host planner on this rank's shard of 96 C5 calls (CPU planning)
+        from soundgen_beta_amd import batch
+        calls = _bench().c5_calls(96)
+        idx, mine, owner = sgd.shard(calls, rank, world)
+        p = batch.Plan(mine, None)
+        mine_plan = (idx.tolist(), p.lengths.tolist(), p.offsets.tolist(), p.status.tolist(), int(p.total))
+        plans = [None] * world
+        dist.all_gather_object(plans, mine_plan)
         if rank == 0:
-            q.put([np.asarray(y, np.float64) for y in res])
+            q.put(([np.asarray(y, np.float64) if not isinstance(y, Exception) else None for y in res], plans))
     finally:
         dist.destroy_process_group()
 
@@ -67,7 +99,7 @@ def _free_port():
 
 
 @pytest.mark.timeout(300)
-def test_gloo_world2_gather_matches_single_process():
+def test_gloo_world2_gather_and_sharded_planning():
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -75,14 +107,33 @@ def test_gloo_world2_gather_matches_single_process():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    got = q.get(timeout=240)
+    got, plans = q.get(timeout=240)
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
+    # the gathered batch equals the single-process one, the refused call stays refused
     want = _oracle_synth(_calls())
     assert len(got) == len(want)
     owner = sgd.lpt_assign([sgd.call_cost(c) for c in _calls()], 2)
     assert set(owner) == {0, 1}  # both ranks did work
     for g, w in zip(got, want):
+        if isinstance(w, Exception):
+            assert g is None
+            continue
         assert len(g) == len(w)
         np.testing.assert_allclose(g, np.asarray(w, np.float32), rtol=0, atol=1e-6)
+    # per-rank planning: the union of the shards is the whole-batch plan (lengths, status),
+    # each shard's offsets are its own 256-B aligned packing
+    from soundgen_beta_amd import batch
+    whole = batch.Plan(_bench().c5_calls(96), None)
+    seen = np.zeros(whole.n, dtype=bool)
+    for idx, lens, offs, status, total in plans:
+        idx = np.asarray(idx)
+        assert not seen[idx].any()
+        seen[idx] = True
+        assert np.array_equal(np.asarray(lens), whole.lengths[idx])
+        assert np.array_equal(np.asarray(status), whole.status[idx])
+        slot = (np.asarray(lens) + 63) // 64 * 64
+        assert np.array_equal(np.asarray(offs), np.concatenate([[0], np.cumsum(slot)[:-1]]))
+        assert total == int(slot.sum())
+    assert seen.all()

@@ -43,6 +43,21 @@ def test_morphList_equalises_formant_counts_with_silent_copies():
     assert out[2]["f1"]["freq"] == [400.0, 400.0] and out[0]["f1"]["freq"] == [700.0, 700.0]
 
 
+def test_morphList_l2_longer_names_by_position():
+    """R/utilities_morph.R:261-265: when l2 is longer, l1 grows and the new slot is
+    named names(l2)[length(l1)] AFTER the append, i.e. l2's name at that position."""
+    l1 = {"f1": {"time": 0, "freq": 700, "amp": 30, "width": 80}}
+    l2 = {"f1": {"time": 0, "freq": 400, "amp": 40, "width": 120},
+          "f2": {"time": 0, "freq": 1100, "amp": 30, "width": 120},
+          "f3": {"time": 0, "freq": 2500, "amp": 20, "width": 150}}
+    out = M.morphList(l1, l2, 3)
+    assert list(out[0]) == ["f1", "f2", "f3"]
+    assert out[0]["f2"]["amp"] == [0.0, 0.0] and out[2]["f2"]["amp"] == [30.0, 30.0]
+    # an empty l1 becomes l2's formants silenced, named f1, f2, f3 (formants$f1 exists)
+    out = M.morphList({}, l2, 2)
+    assert list(out[0]) == ["f1", "f2", "f3"] and out[0]["f1"]["amp"] == [0.0, 0.0]
+
+
 def test_morph_formulas_roxygen_example():
     """morph(formula1 = list(repeatBout = 2), formula2 = presets$Misc$Dog_bark, nMorphs = 5):
     non-default pars of either side are morphed; scalars by seq(), pitch in log Hz."""
@@ -73,3 +88,9 @@ def test_morph_batch_equals_single_calls(tmp_path):
         assert len(ref) == len(y) and np.array_equal(np.float32(ref), np.float32(y))
     for h in range(5):
         assert (tmp_path / ("morph_%d.wav" % (h + 1))).stat().st_size == 80 + 2 * len(m["sounds"][h])
+    # per-morph draws (R's one stream split at the morph boundaries): morph h reads its own arrays
+    Zs = [Z[h * 1000:] for h in range(5)]
+    m2 = M.morph({"repeatBout": 2}, presets.args("Misc", "Dog_bark"), 5, samplingRate=16000, normals=Zs, uniforms=U)
+    for h, (f, y) in enumerate(zip(m2["formulas"], m2["sounds"])):
+        ref = api.soundgen(normals=Zs[h], uniforms=U, **M._soundgen_args(f))
+        assert len(ref) == len(y) and np.array_equal(np.float32(ref), np.float32(y))

@@ -7,5 +7,5 @@ shift || true
 mkdir -p "$R/gpurun_out"
 cd /tmp
 export TMPDIR=/tmp
-timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/${TAG}_ks" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --device-steps 0 --no-cpu-baseline "$@" > "$R/gpurun_out/${TAG}_ks.log" 2>&1 || { tail -20 "$R/gpurun_out/${TAG}_ks.log"; exit 1; }
+timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/${TAG}_ks" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --device-steps 0 --no-d2h --no-cpu-baseline "$@" > "$R/gpurun_out/${TAG}_ks.log" 2>&1 || { tail -20 "$R/gpurun_out/${TAG}_ks.log"; exit 1; }
 cut -d, -f1-5 "$R/gpurun_out/${TAG}_ks/run_kernel_stats.csv" | grep -v "at::native" | head -24
