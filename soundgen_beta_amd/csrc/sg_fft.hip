@@ -1186,7 +1186,7 @@ __device__ void fft64(double2*& a, double2*& b, int M, const double2* __restrict
     if (!R)
       for (int p : {3, 5, 7, 11, 13, 17, 19, 23, 29, 31})
         if (rest % p == 0) { R = p; break; }
-    if (R > 4) {  // W_R^t = W_N^(t 2M / R), t < R
+    if (R != 2 && R != 4) {  // odd radix: W_R^t = W_N^(t 2M / R), t < R
       if (threadIdx.x < R) rt[threadIdx.x] = TN[threadIdx.x * (2 * M / R)];
       __syncthreads();
     }
