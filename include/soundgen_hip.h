@@ -249,6 +249,10 @@ int sg_plan_precision(const sg_plan* plan, int32_t* call_fp64, int64_t* fp64_fra
  * nominal FFT flops (5 wl log2 wl per transform), for load balancing across
  * GPUs (soundgen_beta_amd/dist.py). Either pointer may be NULL. */
 int sg_plan_call_work(const sg_plan* plan, double* rows, double* fft_flops);
+/* compareSounds' 'dtw' method (R/matchPars.R:372-376): dtw::dtw(x, y,
+ * distance.only = TRUE)$normalizedDistance with the dtw package defaults
+ * (|x_i - y_j|, symmetric2, / (n + m)). Host only (ABI 2). */
+int sg_dtw_symmetric2(const double* x, int64_t n, const double* y, int64_t m, double* out);
 /* Process-wide policy of the fp64 filter path for later sg_plan_batch calls:
  * mode 0 never, 1 when the conditioning estimate exceeds rho (default 300),
  * 2 every filtered bout. SG_E_ARG for an invalid mode or rho. */

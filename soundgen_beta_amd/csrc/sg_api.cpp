@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <chrono>
 #include <cstring>
@@ -637,6 +638,32 @@ int sg_plan_precision(const sg_plan* plan, int32_t* call_fp64, int64_t* fp64_fra
     for (const SgWTask& t : B.tasks) n += (t.flags & SG_TASK_HP) ? 1 : 0;
     *fp64_tasks = n;
   }
+  return SG_OK;
+}
+
+// dtw::dtw(x, y, distance.only = TRUE)$normalizedDistance with the package defaults:
+// local distance |x_i - y_j| (Euclidean, 1-D), step pattern symmetric2
+//   g(i, j) = min(g(i-1, j-1) + 2 d(i, j), g(i-1, j) + d(i, j), g(i, j-1) + d(i, j)),
+// g(1, 1) = d(1, 1), normalised by n + m. Host code (compareSounds, R/matchPars.R:372-376).
+int sg_dtw_symmetric2(const double* x, int64_t n, const double* y, int64_t m, double* out) {
+  if (!x || !y || !out || n < 1 || m < 1) return SG_E_ARG;
+  std::vector<double> prev((size_t)m), cur((size_t)m);
+  for (int64_t i = 0; i < n; ++i) {
+    for (int64_t j = 0; j < m; ++j) {
+      const double d = std::fabs(x[i] - y[j]);
+      double g;
+      if (i == 0 && j == 0) g = d;
+      else {
+        g = INFINITY;
+        if (i > 0 && j > 0) g = std::min(g, prev[j - 1] + 2 * d);
+        if (i > 0) g = std::min(g, prev[j] + d);
+        if (j > 0) g = std::min(g, cur[j - 1] + d);
+      }
+      cur[j] = g;
+    }
+    std::swap(prev, cur);
+  }
+  *out = prev[m - 1] / (double)(n + m);
   return SG_OK;
 }
 

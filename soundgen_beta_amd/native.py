@@ -75,6 +75,7 @@ def lib():
     L.sg_plan_precision.argtypes = [vp, C.POINTER(C.c_int32), i64p, i64p]
     L.sg_set_fp64_policy.argtypes = [C.c_int32, C.c_double]
     L.sg_plan_call_work.argtypes = [vp, dp, dp]
+    L.sg_dtw_symmetric2.argtypes = [dp, i64, dp, i64, dp]
     L.sg_rrng_create.argtypes = [C.c_int32, C.POINTER(vp)]
     L.sg_rrng_destroy.argtypes = [vp]
     L.sg_rrng_set_seed.argtypes = [vp, C.c_int32]
