@@ -599,6 +599,9 @@ int64_t plan_envelope(Batch& B, Rng& R, double nrd, int64_t nc, const sg_formant
     // (terms emitted for sg_spec_env; the log-density max over the integer bins is
     // at floor or ceil of the mode (shape - 1) / rate, or at bin 1 for shape <= 1)
     const double L2E = 1.4426950408889634;  // 1 / ln 2
+    // sg_spec_env holds two tracks per lane: more than 128 refuses THIS call (inside
+    // plan_range's per-call try), not the whole batch at finalize_spec
+    if (fu.size() > 2 * 64) throw SgError(SG_E_UNSUPPORTED, "spectral envelope: more than 128 formant tracks");
     job.ntr = (int32_t)fu.size();
     B.eterms.resize(B.eterms.size() + (size_t)(nc * job.ntr));
     SgEnvTerm* tm = &B.eterms[job.term0];
@@ -679,7 +682,7 @@ void finalize_spec(Batch& B) {
   int32_t maxnr = 0;
   for (const SgEnvJob& j : B.envjobs) {
     maxnr = std::max(maxnr, j.nr);
-    if (j.ntr > 2 * 64) throw SgError(SG_E_UNSUPPORTED, "spectral envelope: more than 128 formant tracks");
+    if (j.ntr > 2 * 64) throw SgError(SG_E_DEVICE, "spectral envelope: more than 128 formant tracks (planner check)");
   }
   B.elog2.resize((size_t)maxnr + 64);  // log2(k) for k = 1.. (padded to whole 64-bin chunks)
   for (size_t k = 0; k < B.elog2.size(); ++k) B.elog2[k] = std::log2((double)(k + 1));
