@@ -255,6 +255,13 @@ def roofline(st, prof, steps, config):
     r = {"bound": "hbm", "kernel": kern, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "alg_bytes_per_launch": alg,
          "avg_launch_ms": ms, "launches_timed": n}
+    if kern == "sg_stft_ola":
+        # the fused STFT/ISTFT/OLA runs once per spectral phase of a plan: the noise
+        # phase as sg_stft_ola_noise, the formant-filter phase as sg_stft_ola; bytes,
+        # flops and event time are their sum over both launches, per launch
+        r["kernel"] = "sg_stft_ola + sg_stft_ola_noise"
+        r["rocprof_check"] = ("avg_launch_ms = (TotalDurationNs of sg_stft_ola + sg_stft_ola_noise) / "
+                              "(their Calls) in the kernel-stats summary")
     if src:
         r["traffic_source"] = src
     r.update(extra)

@@ -461,6 +461,7 @@ int sg_plan_batch(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, sg_pl
                    B.pieces.size() * sizeof(SgPiece) * 1e-6, B.syl_tiles.size() * sizeof(SgSylTile) * 1e-6,
                    B.fs_total * 4e-6, B.w_total * 4e-6);
     }
+    sg::scratch_trim();
     *out = P.release();
     return SG_OK;
   });

@@ -16,6 +16,7 @@ namespace sg {
 // Allocator whose resize() leaves new elements default-initialised (no zero
 // fill): the planner's bulk arrays are always written after they grow, and the
 // merged batch is filled by parallel copies (first touch on the copying thread).
+// Blocks of SG_BULK_HUGE and up come from bulk_alloc (huge pages, sg_rmath.h).
 template <class T>
 struct NoInitAlloc : std::allocator<T> {
   template <class U>
@@ -23,6 +24,14 @@ struct NoInitAlloc : std::allocator<T> {
   NoInitAlloc() = default;
   template <class U>
   NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+  T* allocate(size_t n) {
+    if (n * sizeof(T) < SG_BULK_HUGE) return std::allocator<T>::allocate(n);
+    return static_cast<T*>(bulk_alloc(n * sizeof(T)));
+  }
+  void deallocate(T* p, size_t n) noexcept {
+    if (n * sizeof(T) < SG_BULK_HUGE) std::allocator<T>::deallocate(p, n);
+    else bulk_free(p, n * sizeof(T));
+  }
   template <class U, class... A>
   void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
   template <class U>

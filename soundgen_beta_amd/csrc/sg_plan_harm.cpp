@@ -893,12 +893,18 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
     // [G][R] amplitudes then [G-1][R] column differences, 64-B aligned rows
     d.amp_off = (int64_t)B.amps.size();
     d.da_off = d.amp_off + (int64_t)d.G * d.R;
-    B.amps.resize(B.amps.size() + (size_t)(2 * d.G - 1) * d.R, 0.0f);
-    for (int64_t g = 0; g < he.G; ++g)
-      for (int64_t r = 0; r < m.R; ++r) B.amps[d.amp_off + g * d.R + r] = (float)m.A[g * m.R + r];
-    for (int64_t g = 0; g + 1 < he.G; ++g)
-      for (int64_t r = 0; r < m.R; ++r)
-        B.amps[d.da_off + g * d.R + r] = B.amps[d.amp_off + (g + 1) * d.R + r] - B.amps[d.amp_off + g * d.R + r];
+    B.amps.resize(B.amps.size() + (size_t)(2 * d.G - 1) * d.R);  // every element written below
+    {
+      float* a = B.amps.data() + d.amp_off;
+      float* da = B.amps.data() + d.da_off;
+      for (int64_t g = 0; g < he.G; ++g) {
+        float* row = a + g * d.R;
+        for (int64_t r = 0; r < m.R; ++r) row[r] = (float)m.A[g * m.R + r];
+        std::fill(row + m.R, row + d.R, 0.0f);
+      }
+      for (int64_t g = 0; g + 1 < he.G; ++g)
+        for (int64_t r = 0; r < d.R; ++r) da[g * d.R + r] = a[(g + 1) * d.R + r] - a[g * d.R + r];
+    }
     d.syl = syl_idx;
     d.dj0 = d.dj1 = 0;
     d.dk0 = 0;

@@ -363,8 +363,10 @@ bool plan_noise(Batch& B, Rng& R, int64_t len, const sg_anchors& noiseAnchors, d
   // keeps as.integer(nr) rows of them)
   const int64_t ndraw = (int64_t)((double)wl / 2 * (double)nc);
   const int64_t u_off = (int64_t)B.fl.size();
-  B.fl.resize((size_t)(u_off + (nr * nc + 3) / 4 * 4), 0.f);
-  R.unif_f32(std::min<int64_t>(ndraw, nr * nc), B.fl.data() + u_off);
+  const int64_t nu = std::min<int64_t>(ndraw, nr * nc);
+  B.fl.resize((size_t)(u_off + (nr * nc + 3) / 4 * 4));  // the draws, then zeros to the 16-B pad
+  R.unif_f32(nu, B.fl.data() + u_off);
+  std::fill(B.fl.begin() + u_off + nu, B.fl.end(), 0.f);
   if (ndraw > nr * nc) R.unif_f32(ndraw - nr * nc, nullptr);
   const bool fused = fusable(B.geoms[gi], (double)wl * (100 - overlap) / 100);
   const int64_t fr = fused ? 0 : fs_alloc(B, nc * wl);

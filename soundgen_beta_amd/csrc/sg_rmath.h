@@ -13,7 +13,37 @@
 
 namespace sg {
 
-using vec = std::vector<double>;
+// Planner scratch memory. A call's temporaries (rolloff matrices, epoch
+// amplitudes, contours: tens of KB to MB each) come from a per-thread pool of
+// power-of-two blocks that outlives the call, so the next call reuses pages
+// already faulted in instead of mapping, zeroing and unmapping fresh ones
+// (sg_scratch.cpp). Small blocks go straight to malloc.
+void* scratch_alloc(size_t bytes);
+void scratch_free(void* p, size_t bytes) noexcept;
+void scratch_trim() noexcept;  // return the calling thread's pool to the system
+
+// Bulk blocks of 8 MB and up are 2 MB-aligned and marked for transparent huge
+// pages: a plan's host arrays run to GBs, and faulting them in 4 KB pages (on
+// the planning threads, then again in the merge) cost more than writing them.
+void* bulk_alloc(size_t bytes);
+void bulk_free(void* p, size_t bytes) noexcept;
+constexpr size_t SG_BULK_HUGE = size_t(8) << 20;
+
+template <class T>
+struct ScratchAlloc {
+  using value_type = T;
+  ScratchAlloc() = default;
+  template <class U>
+  ScratchAlloc(const ScratchAlloc<U>&) noexcept {}
+  T* allocate(size_t n) { return static_cast<T*>(scratch_alloc(n * sizeof(T))); }
+  void deallocate(T* p, size_t n) noexcept { scratch_free(p, n * sizeof(T)); }
+  template <class U>
+  bool operator==(const ScratchAlloc<U>&) const noexcept { return true; }
+  template <class U>
+  bool operator!=(const ScratchAlloc<U>&) const noexcept { return false; }
+};
+
+using vec = std::vector<double, ScratchAlloc<double>>;
 
 struct SgError : std::runtime_error {
   int code;

@@ -202,6 +202,8 @@ class Holder:
     def __init__(self):
         self.keep = []
         self._fmemo = {}  # formants converted once per object (a batch shares preset formant lists)
+        self._amemo = {}  # anchors by value: one pair of buffers per distinct anchor set
+        self._rmemo = {}  # injected draw arrays by identity (a batch often shares one stream)
 
     def formants_of(self, x):
         """sg_formants of an R formants argument (vowel string, formant lists or NA);
@@ -218,13 +220,17 @@ class Holder:
         return a
 
     def anchors(self, an):
-        s = _abi.sg_anchors()
         if an is None:
+            s = _abi.sg_anchors()
             s.n = 0
             return s
-        t, v = self.arr(an[0]), self.arr(an[1])
-        s.n = len(t)
-        s.time, s.value = _abi.dptr(t), _abi.dptr(v)
+        key = (tuple(an[0]), tuple(an[1]))
+        hit = self._amemo.get(key)
+        if hit is None:
+            t, v = self.arr(an[0]), self.arr(an[1])
+            hit = self._amemo[key] = (len(t), _abi.dptr(t), _abi.dptr(v))
+        s = _abi.sg_anchors()
+        s.n, s.time, s.value = hit
         return s
 
     def formants(self, fl):
@@ -247,12 +253,17 @@ class Holder:
         with standard_normal(), random() and gamma(shape, scale), e.g. a
         numpy Generator) bound to the norm/unif/gamma callbacks."""
         r = _abi.sg_random()
+
+        def buf(x):
+            hit = self._rmemo.get(id(x))
+            if hit is None or hit[0] is not x:
+                a = self.arr(x)
+                hit = self._rmemo[id(x)] = (x, _abi.dptr(a), len(a))
+            return hit[1], hit[2]
         if normals is not None:
-            n = self.arr(normals)
-            r.normals, r.n_normals = _abi.dptr(n), len(n)
+            r.normals, r.n_normals = buf(normals)
         if uniforms is not None:
-            u = self.arr(uniforms)
-            r.uniforms, r.n_uniforms = _abi.dptr(u), len(u)
+            r.uniforms, r.n_uniforms = buf(uniforms)
         if rng is not None and hasattr(rng, "bind"):  # RRng: native callbacks into the library
             rng.bind(r)
             self.keep.append(rng)

@@ -17,7 +17,7 @@ def test_loess_cursor_equals_tree_walk(tmp_path):
     exe = str(tmp_path / "loess_cursor")
     cmd = ["g++", "-O2", "-std=c++17", "-I" + CSRC, "-I" + os.path.join(HERE, "..", "include"),
            "-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__", os.path.join(HERE, "cpp", "loess_cursor.cpp"),
-           os.path.join(CSRC, "sg_loess.cpp"), os.path.join(CSRC, "sg_rrng.cpp"), "-o", exe]
+           os.path.join(CSRC, "sg_loess.cpp"), os.path.join(CSRC, "sg_rrng.cpp"), os.path.join(CSRC, "sg_scratch.cpp"), "-o", exe]
     subprocess.run(cmd, check=True, timeout=300)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr

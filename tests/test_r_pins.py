@@ -93,7 +93,7 @@ def test_planner_rmath_vs_r(tmp_path):
     compiled with g++) against R's values."""
     exe = str(tmp_path / "rmath_pins")
     subprocess.run(["g++", "-O2", "-std=c++17", "-I" + CSRC, "-I" + os.path.join(HERE, "..", "include"),
-                    os.path.join(HERE, "cpp", "rmath_pins.cpp"), "-o", exe], check=True, timeout=300)
+                    os.path.join(HERE, "cpp", "rmath_pins.cpp"), os.path.join(CSRC, "sg_scratch.cpp"), "-o", exe], check=True, timeout=300)
     lines, keys = [], []
     for name in SPLINE + LINEAR:
         c = SIG[name]
