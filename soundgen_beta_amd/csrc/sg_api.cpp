@@ -103,21 +103,30 @@ struct Checkpoint {
 };
 
 // Plan calls [c0, c1) into B (empty), output slots from offset 0.
-// Bulk-array elements per call over the parts planned so far: a later part
-// reserves its arrays up front (x1.25 of the running mean; reserve it never
-// touches is never faulted in) instead of growing them by doubling, whose
-// relocation copies and fresh-page faults were ~20 % of planning time.
+// Bulk-array elements per call over the calls planned so far in this process
+// (g_growth): a part reserves its arrays up front (x1.25 of the running mean;
+// reserve it never touches is never faulted in) instead of growing them by
+// doubling, whose relocation copies and fresh-page faults were ~20 % of
+// planning time. Only the first parts planned in a process grow.
 struct GrowthEstimate {
-  static constexpr int N = 10;
+  static constexpr int N = 16;
   std::atomic<int64_t> calls{0};
   std::atomic<int64_t> elems[N];
   GrowthEstimate() {
     for (auto& e : elems) e.store(0);
   }
+  // one sample per part: keep the estimate a running mean over recent plans
+  void decay() {
+    if (calls.load() < (int64_t(1) << 20)) return;
+    calls = calls.load() / 2;
+    for (auto& e : elems) e = e.load() / 2;
+  }
   template <class F>
   static void each(sg::Batch& B, F&& f) {
     f(0, B.segs); f(1, B.epochs); f(2, B.knots); f(3, B.amps); f(4, B.tasks);
     f(5, B.pieces); f(6, B.syl_tiles); f(7, B.fl); f(8, B.cknots); f(9, B.eterms);
+    f(10, B.frames[0]); f(11, B.frames[1]); f(12, B.frame_geom[0]); f(13, B.frame_geom[1]); f(14, B.syls);
+    f(15, B.ecols);
   }
   void reserve(sg::Batch& B, int64_t n_calls) const {
     const int64_t c = calls.load();
@@ -131,6 +140,8 @@ struct GrowthEstimate {
     calls += n_calls;
   }
 };
+
+GrowthEstimate g_growth;
 
 void plan_range(sg::Batch& B, const sg_call_desc* calls, int64_t c0, int64_t c1) {
   const int64_t n = c1 - c0;
@@ -250,12 +261,19 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
   }
   D.total_out = c.out; D.fs_total = c.fs; D.w_total = c.w; D.fe_total = c.fe;
   D.w64_total = c.w64; D.fh_total = c.fh; D.frames64.resize(c.fr64);
-  D.eterms.resize(c.term); D.ecols.resize(c.col); D.envjobs.resize(c.job);
+  D.ecols.resize(c.col); D.envjobs.resize(c.job);
   D.call_len.resize(c.call); D.call_off.resize(c.call); D.call_status.resize(c.call); D.call_msg.resize(c.call);
   D.call_fp64.resize(c.call); D.call_rows.resize(c.call); D.call_flops.resize(c.call);
-  D.segs.resize(c.seg); D.epochs.resize(c.epoch); D.knots.resize(c.knot); D.amps.resize(c.amp);
-  D.tasks.resize(c.task); D.pieces.resize(c.piece); D.syls.resize(c.syl); D.syl_tiles.resize(c.st);
-  D.cknots.resize(c.ck); D.fl.resize(c.fl); D.items.resize(c.item); D.copies.resize(c.copy);
+  D.epochs.resize(c.epoch); D.knots.resize(c.knot); D.pieces.resize(c.piece); D.syls.resize(c.syl); D.syl_tiles.resize(c.st);
+  D.cknots.resize(c.ck); D.items.resize(c.item);
+  // the largest arrays stay in the parts' blocks (moved below, not copied)
+  auto blocks = [&](auto& x, int64_t n) {
+    x.blocks.resize(np);
+    x.base.resize(np);
+    x.n = n;
+  };
+  blocks(D.segs_x, c.seg); blocks(D.amps_x, c.amp); blocks(D.tasks_x, c.task); blocks(D.fl_x, c.fl);
+  blocks(D.eterms_x, c.term); D.copies.resize(c.copy);
   for (int ph = 0; ph < 2; ++ph) {
     D.frames[ph].resize(c.fr[ph]); D.frame_geom[ph].resize(c.fr[ph]);
     D.olas[ph].resize(c.ola[ph]); D.mixes[ph].resize(c.mix[ph]);
@@ -331,11 +349,16 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
     }
     for (auto& x : S.copies) { x.fl_off += b.fl; x.fs_off += b.fs; }
     for (auto& j : S.envjobs) { j.out += b.fe; j.term0 += b.term; j.col0 += b.col; }
-    put(D.eterms, S.eterms, b.term); put(D.ecols, S.ecols, b.col); put(D.envjobs, S.envjobs, b.job);
-    put(D.segs, S.segs, b.seg); put(D.epochs, S.epochs, b.epoch); put(D.knots, S.knots, b.knot);
-    put(D.amps, S.amps, b.amp); put(D.tasks, S.tasks, b.task); put(D.pieces, S.pieces, b.piece);
+    auto move = [&](auto& x, auto& v, int64_t at) {
+      x.blocks[k] = std::move(v);
+      x.base[k] = at;
+    };
+    move(D.eterms_x, S.eterms, b.term); move(D.segs_x, S.segs, b.seg); move(D.amps_x, S.amps, b.amp);
+    move(D.tasks_x, S.tasks, b.task); move(D.fl_x, S.fl, b.fl);
+    put(D.ecols, S.ecols, b.col); put(D.envjobs, S.envjobs, b.job);
+    put(D.epochs, S.epochs, b.epoch); put(D.knots, S.knots, b.knot); put(D.pieces, S.pieces, b.piece);
     put(D.syls, S.syls, b.syl); put(D.syl_tiles, S.syl_tiles, b.st); put(D.cknots, S.cknots, b.ck);
-    put(D.fl, S.fl, b.fl); put(D.items, S.items, b.item); put(D.copies, S.copies, b.copy);
+    put(D.items, S.items, b.item); put(D.copies, S.copies, b.copy);
     put(D.frames64, S.frames64, b.fr64);
     for (int ph = 0; ph < 2; ++ph) {
       put(D.frames[ph], S.frames[ph], b.fr[ph]); put(D.frame_geom[ph], S.frame_geom[ph], b.fr[ph]);
@@ -408,30 +431,36 @@ int sg_plan_batch(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, sg_pl
     for (int64_t c = 0; c < n_calls && !callbacks; ++c)
       callbacks = calls[c].random.norm_cb || calls[c].random.unif_cb || calls[c].random.gamma_cb;
     const int threads = callbacks ? 1 : plan_threads(n_calls);
+    g_growth.decay();
     if (threads <= 1) {
+      g_growth.reserve(B, n_calls);
       plan_range(B, calls, 0, n_calls);
+      g_growth.record(B, n_calls);
     } else {
       const int64_t nchunk = std::min<int64_t>(n_calls, (int64_t)threads * 8);
       std::vector<sg::Batch> parts((size_t)nchunk);
       std::vector<std::exception_ptr> errs((size_t)nchunk);
       std::atomic<int64_t> next{0};
-      GrowthEstimate growth;
       auto work = [&]() {
         for (int64_t k; (k = next.fetch_add(1)) < nchunk;) {
           try {
             const int64_t c0 = k * n_calls / nchunk, c1 = (k + 1) * n_calls / nchunk;
-            growth.reserve(parts[k], c1 - c0);
+            g_growth.reserve(parts[k], c1 - c0);
             plan_range(parts[k], calls, c0, c1);
-            growth.record(parts[k], c1 - c0);
+            g_growth.record(parts[k], c1 - c0);
           } catch (...) {
             errs[k] = std::current_exception();
           }
         }
       };
+      const auto tp = std::chrono::steady_clock::now();
       std::vector<std::thread> pool;
       for (int t = 1; t < threads; ++t) pool.emplace_back(work);
       work();
       for (auto& t : pool) t.join();
+      if (sg::g_prof_on)
+        std::fprintf(stderr, "sg_plan_prof parts (%lld on %d threads) %.3f s\n", (long long)nchunk, threads,
+                     std::chrono::duration<double>(std::chrono::steady_clock::now() - tp).count());
       for (auto& e : errs)
         if (e) std::rethrow_exception(e);
       const auto tm = std::chrono::steady_clock::now();
@@ -455,8 +484,9 @@ int sg_plan_batch(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, sg_pl
         std::fprintf(stderr, "sg_plan_prof %-14s %.3f s\n", names[i], sg::g_prof_ns[i].exchange(0) * 1e-9);
       std::fprintf(stderr, "sg_plan_prof host MB: fl %.1f amps %.1f knots %.1f cknots %.1f tasks %.1f segs %.1f "
                    "frames %.1f pieces %.1f syl_tiles %.1f; scratch MB: fs %.1f w %.1f\n",
-                   B.fl.size() * 4e-6, B.amps.size() * 4e-6, B.knots.size() * 8e-6, B.cknots.size() * 8e-6,
-                   B.tasks.size() * sizeof(SgWTask) * 1e-6, B.segs.size() * sizeof(SgSeg) * 1e-6,
+                   bulk_size(B.fl_x, B.fl) * 4e-6, bulk_size(B.amps_x, B.amps) * 4e-6, B.knots.size() * 8e-6,
+                   B.cknots.size() * 8e-6, bulk_size(B.tasks_x, B.tasks) * sizeof(SgWTask) * 1e-6,
+                   bulk_size(B.segs_x, B.segs) * sizeof(SgSeg) * 1e-6,
                    (B.frames[0].size() + B.frames[1].size()) * sizeof(SgFrame) * 1e-6,
                    B.pieces.size() * sizeof(SgPiece) * 1e-6, B.syl_tiles.size() * sizeof(SgSylTile) * 1e-6,
                    B.fs_total * 4e-6, B.w_total * 4e-6);
@@ -516,9 +546,16 @@ int sg_plan_release_host(sg_plan* plan) {
     decltype(B.eterms) eterms;
     decltype(B.cknots) cknots;
     decltype(B.knots) knots;
+    decltype(B.amps_x) amps_x;
+    decltype(B.fl_x) fl_x;
+    decltype(B.tasks_x) tasks_x;
+    decltype(B.segs_x) segs_x;
+    decltype(B.eterms_x) eterms_x;
   };
-  auto* bulk = new Bulk{std::move(B.amps), std::move(B.fl),     std::move(B.tasks), std::move(B.segs),
-                        std::move(B.eterms), std::move(B.cknots), std::move(B.knots)};
+  auto* bulk = new Bulk{std::move(B.amps),   std::move(B.fl),     std::move(B.tasks), std::move(B.segs),
+                        std::move(B.eterms), std::move(B.cknots), std::move(B.knots), std::move(B.amps_x),
+                        std::move(B.fl_x),   std::move(B.tasks_x), std::move(B.segs_x), std::move(B.eterms_x)};
+  B.amps_x = {}; B.fl_x = {}; B.tasks_x = {}; B.segs_x = {}; B.eterms_x = {};
   try {
     std::thread([bulk]() { delete bulk; }).detach();
   } catch (...) {
@@ -636,7 +673,9 @@ int sg_plan_precision(const sg_plan* plan, int32_t* call_fp64, int64_t* fp64_fra
   if (fp64_frames) *fp64_frames = (int64_t)B.frames64.size();
   if (fp64_tasks) {
     int64_t n = 0;
-    for (const SgWTask& t : B.tasks) n += (t.flags & SG_TASK_HP) ? 1 : 0;
+    sg::bulk_each(B.tasks_x, B.tasks, [&](int64_t, const SgWTask* p, int64_t k) {
+      for (int64_t i = 0; i < k; ++i) n += (p[i].flags & SG_TASK_HP) ? 1 : 0;
+    });
     *fp64_tasks = n;
   }
   return SG_OK;

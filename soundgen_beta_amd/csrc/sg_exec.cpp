@@ -30,16 +30,17 @@ struct Layout {
   explicit Layout(const Batch& B) {
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o += up(bytes > 0 ? bytes : 1); return r; };
-    segs = take(B.segs.size() * sizeof(SgSeg));
+    const size_t ntask = (size_t)bulk_size(B.tasks_x, B.tasks);
+    segs = take((size_t)bulk_size(B.segs_x, B.segs) * sizeof(SgSeg));
     epochs = take(B.epochs.size() * sizeof(SgEpoch));
     knots = take(B.knots.size() * sizeof(double));
-    amps = take(B.amps.size() * sizeof(float) + 64 * sizeof(float));
-    tasks = take(B.tasks.size() * sizeof(SgWTask));
-    tall = take(B.tasks.size() * sizeof(int32_t));
-    tlong = take(B.tasks.size() * sizeof(int32_t));
-    tshort = take(B.tasks.size() * sizeof(int32_t));
-    tallp = take(B.tasks.size() * sizeof(int32_t));
-    thp = take(B.tasks.size() * sizeof(int32_t));
+    amps = take((size_t)bulk_size(B.amps_x, B.amps) * sizeof(float) + 64 * sizeof(float));
+    tasks = take(ntask * sizeof(SgWTask));
+    tall = take(ntask * sizeof(int32_t));
+    tlong = take(ntask * sizeof(int32_t));
+    tshort = take(ntask * sizeof(int32_t));
+    tallp = take(ntask * sizeof(int32_t));
+    thp = take(ntask * sizeof(int32_t));
     fin_tiles_hp = take(B.fin_tiles_hp.size() * sizeof(SgSylTile));
     W64 = take((size_t)B.w64_total * sizeof(double));
     fh = take((size_t)B.fh_total * sizeof(double));
@@ -55,7 +56,7 @@ struct Layout {
     ptiles = take(B.ptiles.size() * sizeof(SgSylTile));
     cknots = take(B.cknots.size() * sizeof(double));
     W = take((size_t)B.w_total * sizeof(float));
-    taskmax = take(B.tasks.size() * sizeof(float));
+    taskmax = take(ntask * sizeof(float));
     ptilemax = take(B.ptiles.size() * sizeof(float));
     maxes = take(B.syls.size() * sizeof(float));
     geoms = take(B.geoms.size() * sizeof(SgFftGeom));
@@ -69,13 +70,13 @@ struct Layout {
     items = take(B.items.size() * sizeof(SgNoiseItem));
     mixes = take(B.mixes_dev.size() * sizeof(SgMix));
     mixtiles = take(B.mixtiles.size() * sizeof(SgMixTile));
-    eterms = take(B.eterms.size() * sizeof(SgEnvTerm));
+    eterms = take((size_t)bulk_size(B.eterms_x, B.eterms) * sizeof(SgEnvTerm));
     ecols = take(B.ecols.size() * sizeof(SgEnvCol));
     envjobs = take(B.envjobs.size() * sizeof(SgEnvJob));
     envtasks = take(B.envtasks.size() * sizeof(SgEnvTask));
     elog2 = take(B.elog2.size() * sizeof(double));
     // uploaded floats, then the device-computed envelopes from fe_base on
-    fl = take((size_t)std::max<int64_t>((int64_t)B.fl.size(), B.fe_base + B.fe_total) * sizeof(float));
+    fl = take((size_t)std::max<int64_t>(bulk_size(B.fl_x, B.fl), B.fe_base + B.fe_total) * sizeof(float));
     fs = take((size_t)B.fs_total * sizeof(float) + 256);
     total = o;
   }
@@ -140,7 +141,20 @@ void finalize_plan(Batch& B) {
   split_finalize_tiles(B);
   if (std::getenv("SG_DEBUG_PLAN")) {
     std::fprintf(stderr, "sg plan: %zu sine tasks, %zu syllables, %zu copy tiles, %zu general finalize tiles\n",
-                 B.tasks.size(), B.syls.size(), B.copy_tiles.size(), B.fin_tiles.size());
+                 (size_t)bulk_size(B.tasks_x, B.tasks), B.syls.size(), B.copy_tiles.size(), B.fin_tiles.size());
+    {  // amplitude blocks of subharmonic (vocal-fry) epochs vs plain ones
+      double fry = 0, plain = 0;
+      int64_t nfry = 0;
+      for (const SgEpoch& e : B.epochs) {
+        const double b = (double)(2 * e.G - 1) * e.R * 4;
+        if (e.invD < 1) { fry += b; ++nfry; } else plain += b;
+      }
+      std::fprintf(stderr, "sg plan: amplitude bytes: plain epochs %.3g, subharmonic epochs %.3g (%lld of %zu)\n", plain,
+                   fry, (long long)nfry, B.epochs.size());
+    }
+    std::vector<SgWTask> tasks;  // the merged task list (debug statistics only)
+    bulk_each(B.tasks_x, B.tasks, [&](int64_t, const SgWTask* p, int64_t n) { tasks.insert(tasks.end(), p, p + n); });
+    auto amp = [&](int64_t i) { return bulk_at(B.amps_x, B.amps, i); };
     // sine-bank work: (sample, row) terms of the fp32 and the tall tasks, rows histogram of the tall ones
     double terms[2] = {0, 0};
     int64_t ntask[2] = {0, 0}, rmax = 0, samples[2] = {0, 0};
@@ -150,7 +164,7 @@ void finalize_plan(Batch& B) {
     {  // fp64 (SG_TASK_HP) tasks
       int64_t nh = 0, sh = 0, lh64 = 0;
       double th = 0, rn = 0;
-      for (const SgWTask& t : B.tasks)
+      for (const SgWTask& t : tasks)
         if (t.flags & SG_TASK_HP) {
           ++nh; sh += t.len; lh64 += t.len <= 64;
           th += (double)t.Rn * t.len * ((t.flags & SG_TASK_CONST) ? 1 : 2);
@@ -159,7 +173,7 @@ void finalize_plan(Batch& B) {
       std::fprintf(stderr, "sg plan: fp64 tasks %lld (%lld samples, %lld of <= 64 samples, %.3g chain terms, mean Rn %.1f)\n",
                    (long long)nh, (long long)sh, (long long)lh64, th, nh ? rn / nh : 0.0);
     }
-    for (const SgWTask& t : B.tasks) {
+    for (const SgWTask& t : tasks) {
       const int k = t.R > SG_ROWS_F32 ? 1 : 0;
       terms[k] += (double)t.R * t.len * ((t.flags & SG_TASK_CONST) ? 1 : 2);
       ++ntask[k];
@@ -176,11 +190,11 @@ void finalize_plan(Batch& B) {
                  (long long)rmax, (long long)rh[0], (long long)rh[1], (long long)rh[2], (long long)rh[3], (long long)rh[4]);
     {  // rows above the last nonzero amplitude (A or dA) of each task
       double rsum[2] = {0, 0}, reff[2] = {0, 0};
-      for (const SgWTask& t : B.tasks) {
+      for (const SgWTask& t : tasks) {
         const int k = t.R > SG_ROWS_F32 ? 1 : 0;
         int last = 0;
         for (int r = 0; r < t.R; ++r)
-          if (B.amps[t.a_off + r] != 0.f || (!(t.flags & SG_TASK_CONST) && B.amps[t.d_off + r] != 0.f)) last = r + 1;
+          if (amp(t.a_off + r) != 0.f || (!(t.flags & SG_TASK_CONST) && amp(t.d_off + r) != 0.f)) last = r + 1;
         rsum[k] += (double)t.R * t.len;
         reff[k] += (double)((last + 3) / 4 * 4) * t.len;
       }
@@ -309,11 +323,11 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   auto cp = [&](void* dst, const void* src, size_t bytes) {
     if (bytes) HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
   };
-  cp(D.segs, B.segs.data(), B.segs.size() * sizeof(SgSeg));
+  bulk_each(B.segs_x, B.segs, [&](int64_t o, const SgSeg* p, int64_t n) { cp(D.segs + o, p, n * sizeof(SgSeg)); });
   cp(D.epochs, B.epochs.data(), B.epochs.size() * sizeof(SgEpoch));
   cp(D.knots, B.knots.data(), B.knots.size() * sizeof(double));
-  cp(D.amps, B.amps.data(), B.amps.size() * sizeof(float));
-  cp(D.tasks, B.tasks.data(), B.tasks.size() * sizeof(SgWTask));
+  bulk_each(B.amps_x, B.amps, [&](int64_t o, const float* p, int64_t n) { cp(D.amps + o, p, n * sizeof(float)); });
+  bulk_each(B.tasks_x, B.tasks, [&](int64_t o, const SgWTask* p, int64_t n) { cp(D.tasks + o, p, n * sizeof(SgWTask)); });
   // task classes (each task's class depends on the task alone): tall (sg_sine_bank_tall),
   // short fp32 (two per wave, sg_sine_bank_pairs), other fp32 (sg_sine_bank)
   D.tall_host.clear();
@@ -321,14 +335,17 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   D.tshort_host.clear();
   D.tallp_host.clear();
   D.thp_host.clear();
-  for (size_t i = 0; i < B.tasks.size(); ++i) {
-    const SgWTask& t = B.tasks[i];
-    const bool shrt = t.len <= 64 && !(t.flags & SG_TASK_ENV);
-    if (t.flags & SG_TASK_HP) D.thp_host.push_back((int32_t)i);
-    else if (t.R > SG_ROWS_F32) (SG_TALL_PAIR && shrt ? D.tallp_host : D.tall_host).push_back((int32_t)i);
-    else if (SG_PAIR && t.len <= 64 && !(t.flags & SG_TASK_ENV)) D.tshort_host.push_back((int32_t)i);
-    else D.tlong_host.push_back((int32_t)i);
-  }
+  bulk_each(B.tasks_x, B.tasks, [&](int64_t o, const SgWTask* p, int64_t n) {
+    for (int64_t k = 0; k < n; ++k) {
+      const SgWTask& t = p[k];
+      const int32_t i = (int32_t)(o + k);
+      const bool shrt = t.len <= 64 && !(t.flags & SG_TASK_ENV);
+      if (t.flags & SG_TASK_HP) D.thp_host.push_back(i);
+      else if (t.R > SG_ROWS_F32) (SG_TALL_PAIR && shrt ? D.tallp_host : D.tall_host).push_back(i);
+      else if (SG_PAIR && t.len <= 64 && !(t.flags & SG_TASK_ENV)) D.tshort_host.push_back(i);
+      else D.tlong_host.push_back(i);
+    }
+  });
   cp(D.tall, D.tall_host.data(), D.tall_host.size() * sizeof(int32_t));
   cp(D.tlong, D.tlong_host.data(), D.tlong_host.size() * sizeof(int32_t));
   cp(D.tshort, D.tshort_host.data(), D.tshort_host.size() * sizeof(int32_t));
@@ -355,8 +372,9 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   cp(D.items, B.items.data(), B.items.size() * sizeof(SgNoiseItem));
   cp(D.mixes, B.mixes_dev.data(), B.mixes_dev.size() * sizeof(SgMix));
   cp(D.mixtiles, B.mixtiles.data(), B.mixtiles.size() * sizeof(SgMixTile));
-  cp(D.fl, B.fl.data(), B.fl.size() * sizeof(float));
-  cp(D.eterms, B.eterms.data(), B.eterms.size() * sizeof(SgEnvTerm));
+  bulk_each(B.fl_x, B.fl, [&](int64_t o, const float* p, int64_t n) { cp(D.fl + o, p, n * sizeof(float)); });
+  bulk_each(B.eterms_x, B.eterms,
+            [&](int64_t o, const SgEnvTerm* p, int64_t n) { cp(D.eterms + o, p, n * sizeof(SgEnvTerm)); });
   cp(D.ecols, B.ecols.data(), B.ecols.size() * sizeof(SgEnvCol));
   cp(D.envjobs, B.envjobs.data(), B.envjobs.size() * sizeof(SgEnvJob));
   cp(D.envtasks, B.envtasks.data(), B.envtasks.size() * sizeof(SgEnvTask));

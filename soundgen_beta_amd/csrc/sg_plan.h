@@ -40,6 +40,38 @@ struct NoInitAlloc : std::allocator<T> {
 template <class T>
 using bulk = std::vector<T, NoInitAlloc<T>>;
 
+// The largest bulk arrays of a merged batch stay in the planning parts' blocks
+// (merge_parts moves them, no copy): blocks[i] holds elements [base[i],
+// base[i] + blocks[i].size()) of the logical array, which continues with the
+// Batch's own vector from n on. A batch planned in one piece has no blocks.
+template <class T>
+struct Blocks {
+  std::vector<bulk<T>> blocks;
+  std::vector<int64_t> base;
+  int64_t n = 0;
+};
+template <class T>
+inline int64_t bulk_size(const Blocks<T>& x, const bulk<T>& v) {
+  return x.n + (int64_t)v.size();
+}
+// f(first element index, pointer, count) for every block, then the vector
+template <class T, class F>
+inline void bulk_each(const Blocks<T>& x, const bulk<T>& v, F&& f) {
+  for (size_t i = 0; i < x.blocks.size(); ++i)
+    if (!x.blocks[i].empty()) f(x.base[i], x.blocks[i].data(), (int64_t)x.blocks[i].size());
+  if (!v.empty()) f(x.n, v.data(), (int64_t)v.size());
+}
+template <class T>
+inline const T& bulk_at(const Blocks<T>& x, const bulk<T>& v, int64_t i) {  // debugging paths only
+  if (i >= x.n) return v[(size_t)(i - x.n)];
+  size_t lo = 0, hi = x.base.size() - 1;
+  while (lo < hi) {
+    const size_t m = (lo + hi + 1) / 2;
+    if (x.base[m] <= i) lo = m; else hi = m - 1;
+  }
+  return x.blocks[lo][(size_t)(i - x.base[lo])];
+}
+
 struct DeviceArrays;  // sg_api.cpp
 
 // FFT/OLA job of the noise source or the formant filter (seewave istft/stft)
@@ -115,6 +147,11 @@ struct Batch {
   // the end of the uploaded fl floats, fixed at finalize_spec). Until then a
   // frame's env < 0 encodes envelope-area offset -(env + 1).
   bulk<SgEnvTerm> eterms;
+  // merged batch: the parts' blocks ahead of segs, amps, tasks, fl, eterms (Blocks)
+  Blocks<SgSeg> segs_x;
+  Blocks<float> amps_x, fl_x;
+  Blocks<SgWTask> tasks_x;
+  Blocks<SgEnvTerm> eterms_x;
   std::vector<SgEnvCol> ecols;
   std::vector<SgEnvJob> envjobs;
   int64_t fe_total = 0, fe_base = 0;

@@ -30,9 +30,9 @@ int64_t fs_alloc(Batch& B, int64_t n) {
 }
 
 int64_t fl_push(Batch& B, const double* v, int64_t n) {
-  const int64_t o = (int64_t)B.fl.size();
-  B.fl.resize((size_t)(o + (n + 3) / 4 * 4));  // 16-B aligned blocks
-  float* d = B.fl.data() + o;
+  const int64_t o = bulk_size(B.fl_x, B.fl);
+  B.fl.resize(B.fl.size() + (size_t)((n + 3) / 4 * 4));  // 16-B aligned blocks
+  float* d = B.fl.data() + (o - B.fl_x.n);
   for (int64_t i = 0; i < n; ++i) d[i] = (float)v[i];
   for (int64_t i = n; i < (n + 3) / 4 * 4; ++i) d[i] = 0.f;
   return o;
@@ -362,11 +362,11 @@ bool plan_noise(Batch& B, Rng& R, int64_t len, const sg_anchors& noiseAnchors, d
   // (nr = wl / 2 is x.5 for an odd wl: floor(nr * nc) draws, matrix(nrow = nr)
   // keeps as.integer(nr) rows of them)
   const int64_t ndraw = (int64_t)((double)wl / 2 * (double)nc);
-  const int64_t u_off = (int64_t)B.fl.size();
+  const int64_t u_off = bulk_size(B.fl_x, B.fl), u_loc = (int64_t)B.fl.size();
   const int64_t nu = std::min<int64_t>(ndraw, nr * nc);
-  B.fl.resize((size_t)(u_off + (nr * nc + 3) / 4 * 4));  // the draws, then zeros to the 16-B pad
-  R.unif_f32(nu, B.fl.data() + u_off);
-  std::fill(B.fl.begin() + u_off + nu, B.fl.end(), 0.f);
+  B.fl.resize((size_t)(u_loc + (nr * nc + 3) / 4 * 4));  // the draws, then zeros to the 16-B pad
+  R.unif_f32(nu, B.fl.data() + u_loc);
+  std::fill(B.fl.begin() + u_loc + nu, B.fl.end(), 0.f);
   if (ndraw > nr * nc) R.unif_f32(ndraw - nr * nc, nullptr);
   const bool fused = fusable(B.geoms[gi], (double)wl * (100 - overlap) / 100);
   const int64_t fr = fused ? 0 : fs_alloc(B, nc * wl);
@@ -659,7 +659,7 @@ int64_t plan_envelope(Batch& B, Rng& R, double nrd, int64_t nc, const sg_formant
 void finalize_spec(Batch& B) {
   // envelope area after the uploaded floats: decode frame envelope offsets;
   // sg_spec_env wave tasks of SG_ENV_COLS columns
-  B.fe_base = ((int64_t)B.fl.size() + 63) / 64 * 64;
+  B.fe_base = (bulk_size(B.fl_x, B.fl) + 63) / 64 * 64;
   for (int ph = 0; ph < 2; ++ph)
     for (SgFrame& f : B.frames[ph])
       if (f.env < 0) f.env = B.fe_base + (-f.env - 1);

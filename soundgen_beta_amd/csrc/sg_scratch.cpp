@@ -100,7 +100,8 @@ void* bulk_alloc(size_t bytes) {
   const size_t sz = (bytes + HUGE - 1) / HUGE * HUGE;
   void* q = std::aligned_alloc(HUGE, sz);
   if (!q) throw std::bad_alloc();
-  (void)madvise(q, sz, MADV_HUGEPAGE);  // advisory: 4 KB pages when THP is off
+  static const bool no_thp = std::getenv("SG_NO_THP") != nullptr;  // experiment knob
+  if (!no_thp) (void)madvise(q, sz, MADV_HUGEPAGE);  // advisory: 4 KB pages when THP is off
   return q;
 }
 

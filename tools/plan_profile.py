@@ -18,6 +18,9 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+# llvm's addr2line reads the DWARF 5 line tables clang emits (binutils' may not)
+_SYMB = "/opt/rocm/lib/llvm/bin/llvm-symbolizer"
+ADDR2LINE = [_SYMB, "--output-style=GNU"] if os.path.exists(_SYMB) else ["addr2line"]
 
 
 def _maps():
@@ -45,7 +48,7 @@ def _locate(maps, pc):
 def _symbolize(path, offs):
     """{offset: [(function, file:line), ...] innermost first}"""
     out, cur, addr = {}, [], None
-    res = subprocess.run(["addr2line", "-a", "-f", "-i", "-C", "-e", path] + ["0x%x" % o for o in sorted(offs)],
+    res = subprocess.run(ADDR2LINE + ["-a", "-f", "-i", "-C", "-e", path] + ["0x%x" % o for o in sorted(offs)],
                          capture_output=True, text=True).stdout.splitlines()
     for ln in res:
         if ln.startswith("0x") and len(ln.split()) == 1:
@@ -74,7 +77,7 @@ def main(n_calls=4096, top=40):
     S.sg_sampler_stacks.restype = C.POINTER(C.c_uint64)
     depth = S.sg_sampler_depth()
     calls = bench.c5_calls(int(n_calls))
-    batch.Plan(calls[:64], None).close()  # load the library, warm the caches
+    batch.Plan(calls[:max(64, len(calls) // 4)], None).close()  # load the library, warm the size estimates
     S.sg_sampler_start(2000, 1)
     t0 = time.perf_counter()
     p = batch.Plan(calls, None)
@@ -97,6 +100,7 @@ def main(n_calls=4096, top=40):
         samples.append((leaf_path, leaf_off, mine))
     sym = _symbolize(lib, {o for _, _, m in samples for o in m}) if lib else {}
     self_fn, incl_fn, leaf_obj = collections.Counter(), collections.Counter(), collections.Counter()
+    self_line = collections.Counter()
     for leaf_path, leaf_off, mine in samples:
         leaf_obj[os.path.basename(leaf_path or "?")] += 1
         if not mine:
@@ -105,6 +109,7 @@ def main(n_calls=4096, top=40):
         chain = sym.get(mine[0], [("??", "")])
         where = "" if leaf_path and "libsoundgen_hip" in leaf_path else "  [in %s]" % os.path.basename(leaf_path or "?")
         self_fn[_short(chain[0][0]) + where] += 1
+        self_line["%s @ %s%s" % (_short(chain[0][0]), chain[0][1].split("/")[-1], where)] += 1
         seen = set()
         for o in mine:
             for fn, _ in sym.get(o, []):
@@ -115,6 +120,7 @@ def main(n_calls=4096, top=40):
     tot = max(n, 1)
     print("calls %d, wall %.2f s, samples %d" % (int(n_calls), wall, n))
     for title, ctr in (("self (innermost planner frame; [in X] = time inside library X)", self_fn),
+                       ("self by source line", self_line),
                        ("inclusive (any planner frame on the stack)", incl_fn), ("leaf object", leaf_obj)):
         print("\n== %s" % title)
         for k, v in ctr.most_common(int(top)):
