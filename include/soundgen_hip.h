@@ -257,6 +257,15 @@ int sg_dtw_symmetric2(const double* x, int64_t n, const double* y, int64_t m, do
  * mode 0 never, 1 when the conditioning estimate exceeds rho (default 300),
  * 2 every filtered bout. SG_E_ARG for an invalid mode or rho. */
 int sg_set_fp64_policy(int32_t mode, double rho);
+/* Process-wide source of the harmonic amplitude matrices for later
+ * sg_plan_batch calls: 0 (default) built on the device at upload from
+ * per-glottal-cycle parameters, 1 built on the host and uploaded (the
+ * reference-order host restatement; tests compare the two). */
+int sg_set_amp_policy(int32_t host_built);
+/* The amplitude blocks sg_amp_build writes at upload, evaluated on the host by
+ * the same code (tests; no device needed): n = sg_plan_amp_count(plan) floats. */
+int64_t sg_plan_amp_count(const sg_plan* plan);
+int sg_plan_debug_amps(const sg_plan* plan, float* out, int64_t n);
 
 /* ---- function-level entries mirroring the R API (synchronous) ---------- */
 int sg_generate_harmonics(sg_ctx* ctx, const double* pitch, int64_t len,

@@ -13,14 +13,17 @@ import numpy as np
 from . import _abi, native, rargs
 
 
-class Plan:
-    def __init__(self, calls, ctx=None):
-        """Plan `calls`. ctx may be None: planning is host-only."""
-        self.ctx = ctx
+class Marshalled:
+    """The C descriptors of a list of calls (sg_call_desc array) and the buffers
+    behind them: the Python half of planning, separable from the native half so
+    that the two overlap across chunks (plan_uploaded)."""
+
+    def __init__(self, calls):
         self.holder = rargs.Holder()
-        n = len(calls)
+        n = self.n = len(calls)
         descs = (_abi.sg_call_desc * max(n, 1))()
-        self._structs = []
+        args = (_abi.sg_soundgen_args * max(n, 1))()
+        self._structs = [args]
         for i, c in enumerate(calls):
             d = descs[i]
             kind = c.get("kind", "soundgen")
@@ -35,9 +38,21 @@ class Plan:
                 d.amplAnchors = self.holder.anchors(rargs.as_anchors(c.get("amplAnchors")))
             else:
                 d.kind = _abi.SG_CALL_SOUNDGEN
-                a = rargs.fill_soundgen_args(self.holder, c.get("args", {}))
-                self._structs.append(a)
-                d.args = C.pointer(a)
+                rargs.fill_soundgen_args(self.holder, c.get("args", {}), out=args[i])
+                d.args = C.pointer(args[i])
+        self.descs = descs
+
+
+class Plan:
+    def __init__(self, calls, ctx=None, marshalled=None):
+        """Plan `calls` (or the already marshalled ones). ctx may be None: planning
+        is host-only."""
+        self.ctx = ctx
+        m = marshalled if marshalled is not None else Marshalled(calls)
+        self._m = m  # keeps the descriptors' buffers alive
+        self.holder = m.holder
+        n = m.n
+        descs = m.descs
         self._descs = descs
         self.ptr = C.c_void_p()
         L = native.lib()
@@ -128,21 +143,26 @@ def execute_plans(ctx, plans, d_out_ptrs, stream_ptr=None):
 
 def plan_uploaded(calls, ctx, chunk):
     """Plan `calls` in chunks of `chunk` and upload each plan, yielding
-    (plan, first call index) in order. Chunk k + 1 is planned on a worker thread
-    while chunk k uploads: both native calls run without the GIL (ctypes), so
-    the host planner's threads overlap the pageable H2D copy of the previous
-    plan. Each yielded plan is uploaded and its host arrays released."""
+    (plan, first call index) in order. A three-stage pipeline: while chunk k
+    uploads (main thread), chunk k + 1 is planned natively and chunk k + 2 is
+    marshalled (two workers). The native calls run without the GIL (ctypes), so
+    only marshalling holds it. Each yielded plan is uploaded and its host arrays
+    released."""
     from concurrent.futures import ThreadPoolExecutor
     starts = list(range(0, len(calls), chunk))
     if not starts:
         return
-    with ThreadPoolExecutor(1) as ex:
-        fut = ex.submit(Plan, calls[0:chunk], ctx)
+
+    def piece(i):
+        return calls[starts[i]:starts[i] + chunk]
+    with ThreadPoolExecutor(2) as ex:
+        pfut = ex.submit(Plan, None, ctx, Marshalled(piece(0)))
+        mfut = ex.submit(Marshalled, piece(1)) if len(starts) > 1 else None
         for i, a in enumerate(starts):
-            p = fut.result()
-            if i + 1 < len(starts):
-                b = starts[i + 1]
-                fut = ex.submit(Plan, calls[b:b + chunk], ctx)
+            p = pfut.result()
+            if mfut is not None:
+                pfut = ex.submit(Plan, None, ctx, mfut.result())
+                mfut = ex.submit(Marshalled, piece(i + 2)) if i + 2 < len(starts) else None
             p.upload()
             p.release_host()
             yield p, a

@@ -16,6 +16,7 @@
 
 #include "sg_plan.h"
 #include "sg_exec.h"
+#include "sg_amp.h"
 #include "sg_prof.h"
 
 #include <cstdio>
@@ -70,16 +71,17 @@ int guarded(sg_ctx* ctx, F&& f) {
 
 // Rolls a Batch back to a checkpoint when planning one call fails.
 struct Checkpoint {
-  size_t segs, epochs, knots, amps, tasks, pieces, syls, syl_tiles, cknots, fl, items;
+  size_t segs, epochs, knots, ampsrc, ampcols, ampjobs, tasks, pieces, syls, syl_tiles, cknots, fl, items;
   size_t frames[2], olas[2], mixes[2], copies, eterms, ecols, envjobs, frames64;
-  int64_t w_total, harm_samples, harm_terms, harm_amp_bytes, fft_frames, fs_total, fe_total, w64_total, fh_total,
+  int64_t amp_total, w_total, harm_samples, harm_terms, harm_amp_bytes, fft_frames, fs_total, fe_total, w64_total, fh_total,
       hp_bouts;
   double fft_flops;
   explicit Checkpoint(const sg::Batch& B)
-      : segs(B.segs.size()), epochs(B.epochs.size()), knots(B.knots.size()), amps(B.amps.size()),
+      : segs(B.segs.size()), epochs(B.epochs.size()), knots(B.knots.size()), ampsrc(B.ampsrc.size()),
+        ampcols(B.ampcols.size()), ampjobs(B.ampjobs.size()),
         tasks(B.tasks.size()), pieces(B.pieces.size()), syls(B.syls.size()), syl_tiles(B.syl_tiles.size()),
         cknots(B.cknots.size()), fl(B.fl.size()), items(B.items.size()), copies(B.copies.size()),
-        eterms(B.eterms.size()), ecols(B.ecols.size()), envjobs(B.envjobs.size()), w_total(B.w_total),
+        eterms(B.eterms.size()), ecols(B.ecols.size()), envjobs(B.envjobs.size()), amp_total(B.amp_total), w_total(B.w_total),
         harm_samples(B.harm_samples), harm_terms(B.harm_terms), harm_amp_bytes(B.harm_amp_bytes),
         fft_frames(B.fft_frames), fs_total(B.fs_total), fe_total(B.fe_total), w64_total(B.w64_total),
         fh_total(B.fh_total), hp_bouts(B.hp_bouts), fft_flops(B.fft_flops) {
@@ -87,7 +89,8 @@ struct Checkpoint {
     for (int p = 0; p < 2; ++p) { frames[p] = B.frames[p].size(); olas[p] = B.olas[p].size(); mixes[p] = B.mixes[p].size(); }
   }
   void restore(sg::Batch& B) const {
-    B.segs.resize(segs); B.epochs.resize(epochs); B.knots.resize(knots); B.amps.resize(amps);
+    B.segs.resize(segs); B.epochs.resize(epochs); B.knots.resize(knots); B.ampsrc.resize(ampsrc);
+    B.ampcols.resize(ampcols); B.ampjobs.resize(ampjobs); B.amp_total = amp_total;
     B.tasks.resize(tasks); B.pieces.resize(pieces); B.syls.resize(syls); B.syl_tiles.resize(syl_tiles);
     B.cknots.resize(cknots); B.fl.resize(fl); B.items.resize(items); B.copies.resize(copies);
     for (int p = 0; p < 2; ++p) {
@@ -109,7 +112,7 @@ struct Checkpoint {
 // doubling, whose relocation copies and fresh-page faults were ~20 % of
 // planning time. Only the first parts planned in a process grow.
 struct GrowthEstimate {
-  static constexpr int N = 16;
+  static constexpr int N = 17;
   std::atomic<int64_t> calls{0};
   std::atomic<int64_t> elems[N];
   GrowthEstimate() {
@@ -123,10 +126,10 @@ struct GrowthEstimate {
   }
   template <class F>
   static void each(sg::Batch& B, F&& f) {
-    f(0, B.segs); f(1, B.epochs); f(2, B.knots); f(3, B.amps); f(4, B.tasks);
+    f(0, B.segs); f(1, B.epochs); f(2, B.knots); f(3, B.ampsrc); f(4, B.tasks);
     f(5, B.pieces); f(6, B.syl_tiles); f(7, B.fl); f(8, B.cknots); f(9, B.eterms);
     f(10, B.frames[0]); f(11, B.frames[1]); f(12, B.frame_geom[0]); f(13, B.frame_geom[1]); f(14, B.syls);
-    f(15, B.ecols);
+    f(15, B.ecols); f(16, B.ampcols);
   }
   void reserve(sg::Batch& B, int64_t n_calls) const {
     const int64_t c = calls.load();
@@ -207,7 +210,8 @@ int plan_threads(int64_t n_calls) {
 
 // Where one part's arrays land in the merged batch.
 struct PartBase {
-  int64_t out, fs, fl, w, amp, knot, ck, task, seg, syl, piece, st, item, copy, call, epoch, fe, term, col, job;
+  int64_t out, fs, fl, w, amp, asrc, acol, ajob, knot, ck, task, seg, syl, piece, st, item, copy, call, epoch, fe, term,
+      col, job;
   int64_t w64, fh, fr64;
   int64_t fr[2], ola[2], mix[2];
 };
@@ -243,7 +247,10 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
     }
     c.out += S.total_out; c.fs += S.fs_total; c.fl += (int64_t)S.fl.size();
     c.w = (c.w + S.w_total + 3) / 4 * 4;  // keeps the parts' 16-B alignment of epoch waveforms
-    c.amp += (int64_t)S.amps.size(); c.knot += (int64_t)S.knots.size(); c.ck += (int64_t)S.cknots.size();
+    c.amp += S.amp_total; c.asrc += (int64_t)S.ampsrc.size(); c.acol += (int64_t)S.ampcols.size();
+    c.ajob += (int64_t)S.ampjobs.size();
+    D.amp_lg_rows = std::max(D.amp_lg_rows, S.amp_lg_rows);
+    c.knot += (int64_t)S.knots.size(); c.ck += (int64_t)S.cknots.size();
     c.task += (int64_t)S.tasks.size(); c.seg += (int64_t)S.segs.size(); c.syl += (int64_t)S.syls.size();
     c.piece += (int64_t)S.pieces.size(); c.st += (int64_t)S.syl_tiles.size(); c.item += (int64_t)S.items.size();
     c.copy += (int64_t)S.copies.size(); c.call += (int64_t)S.call_len.size(); c.epoch += (int64_t)S.epochs.size();
@@ -264,7 +271,8 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
   D.ecols.resize(c.col); D.envjobs.resize(c.job);
   D.call_len.resize(c.call); D.call_off.resize(c.call); D.call_status.resize(c.call); D.call_msg.resize(c.call);
   D.call_fp64.resize(c.call); D.call_rows.resize(c.call); D.call_flops.resize(c.call);
-  D.epochs.resize(c.epoch); D.knots.resize(c.knot); D.pieces.resize(c.piece); D.syls.resize(c.syl); D.syl_tiles.resize(c.st);
+  D.epochs.resize(c.epoch); D.knots.resize(c.knot); D.pieces.resize(c.piece);
+  D.amp_total = c.amp; D.ampsrc.resize(c.asrc); D.ampcols.resize(c.acol); D.ampjobs.resize(c.ajob); D.syls.resize(c.syl); D.syl_tiles.resize(c.st);
   D.cknots.resize(c.ck); D.items.resize(c.item);
   // the largest arrays stay in the parts' blocks (moved below, not copied)
   auto blocks = [&](auto& x, int64_t n) {
@@ -272,7 +280,7 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
     x.base.resize(np);
     x.n = n;
   };
-  blocks(D.segs_x, c.seg); blocks(D.amps_x, c.amp); blocks(D.tasks_x, c.task); blocks(D.fl_x, c.fl);
+  blocks(D.segs_x, c.seg); blocks(D.tasks_x, c.task); blocks(D.fl_x, c.fl);
   blocks(D.eterms_x, c.term); D.copies.resize(c.copy);
   for (int ph = 0; ph < 2; ++ph) {
     D.frames[ph].resize(c.fr[ph]); D.frame_geom[ph].resize(c.fr[ph]);
@@ -353,7 +361,13 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
       x.blocks[k] = std::move(v);
       x.base[k] = at;
     };
-    move(D.eterms_x, S.eterms, b.term); move(D.segs_x, S.segs, b.seg); move(D.amps_x, S.amps, b.amp);
+    for (auto& j : S.ampjobs) {
+      j.amp_off += b.amp; j.da_off += b.amp;
+      if (j.src_off >= 0) j.src_off += b.asrc;
+      if (j.col0 >= 0) j.col0 += b.acol;
+    }
+    put(D.ampsrc, S.ampsrc, b.asrc); put(D.ampcols, S.ampcols, b.acol); put(D.ampjobs, S.ampjobs, b.ajob);
+    move(D.eterms_x, S.eterms, b.term); move(D.segs_x, S.segs, b.seg);
     move(D.tasks_x, S.tasks, b.task); move(D.fl_x, S.fl, b.fl);
     put(D.ecols, S.ecols, b.col); put(D.envjobs, S.envjobs, b.job);
     put(D.epochs, S.epochs, b.epoch); put(D.knots, S.knots, b.knot); put(D.pieces, S.pieces, b.piece);
@@ -484,7 +498,7 @@ int sg_plan_batch(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, sg_pl
         std::fprintf(stderr, "sg_plan_prof %-14s %.3f s\n", names[i], sg::g_prof_ns[i].exchange(0) * 1e-9);
       std::fprintf(stderr, "sg_plan_prof host MB: fl %.1f amps %.1f knots %.1f cknots %.1f tasks %.1f segs %.1f "
                    "frames %.1f pieces %.1f syl_tiles %.1f; scratch MB: fs %.1f w %.1f\n",
-                   bulk_size(B.fl_x, B.fl) * 4e-6, bulk_size(B.amps_x, B.amps) * 4e-6, B.knots.size() * 8e-6,
+                   bulk_size(B.fl_x, B.fl) * 4e-6, B.amp_total * 4e-6, B.knots.size() * 8e-6,
                    B.cknots.size() * 8e-6, bulk_size(B.tasks_x, B.tasks) * sizeof(SgWTask) * 1e-6,
                    bulk_size(B.segs_x, B.segs) * sizeof(SgSeg) * 1e-6,
                    (B.frames[0].size() + B.frames[1].size()) * sizeof(SgFrame) * 1e-6,
@@ -539,23 +553,21 @@ int sg_plan_release_host(sg_plan* plan) {
   // detached thread: unmapping them took ~1.2 s on the caller, which then plans
   // or uploads the next chunk meanwhile.
   struct Bulk {
-    decltype(B.amps) amps;
     decltype(B.fl) fl;
     decltype(B.tasks) tasks;
     decltype(B.segs) segs;
     decltype(B.eterms) eterms;
     decltype(B.cknots) cknots;
     decltype(B.knots) knots;
-    decltype(B.amps_x) amps_x;
     decltype(B.fl_x) fl_x;
     decltype(B.tasks_x) tasks_x;
     decltype(B.segs_x) segs_x;
     decltype(B.eterms_x) eterms_x;
   };
-  auto* bulk = new Bulk{std::move(B.amps),   std::move(B.fl),     std::move(B.tasks), std::move(B.segs),
-                        std::move(B.eterms), std::move(B.cknots), std::move(B.knots), std::move(B.amps_x),
-                        std::move(B.fl_x),   std::move(B.tasks_x), std::move(B.segs_x), std::move(B.eterms_x)};
-  B.amps_x = {}; B.fl_x = {}; B.tasks_x = {}; B.segs_x = {}; B.eterms_x = {};
+  auto* bulk = new Bulk{std::move(B.fl),     std::move(B.tasks),   std::move(B.segs), std::move(B.eterms),
+                        std::move(B.cknots), std::move(B.knots),   std::move(B.fl_x), std::move(B.tasks_x),
+                        std::move(B.segs_x), std::move(B.eterms_x)};
+  B.fl_x = {}; B.tasks_x = {}; B.segs_x = {}; B.eterms_x = {};
   try {
     std::thread([bulk]() { delete bulk; }).detach();
   } catch (...) {
@@ -563,7 +575,7 @@ int sg_plan_release_host(sg_plan* plan) {
   }
   // what sg_execute reads from the host plan stays: slices, ranges and splits,
   // the table sizes it launches over, the copy list, the envelope area base
-  drop(B.segs); drop(B.epochs); drop(B.knots); drop(B.amps); drop(B.tasks); drop(B.pieces); drop(B.syls);
+  drop(B.segs); drop(B.epochs); drop(B.knots); drop(B.ampsrc); drop(B.ampcols); drop(B.ampjobs); drop(B.tasks); drop(B.pieces); drop(B.syls);
   drop(B.syl_tiles); drop(B.fin_tiles); drop(B.copy_tiles); drop(B.ptiles); drop(B.cknots); drop(B.fl);
   drop(B.fgroups); drop(B.olasegs); drop(B.items); drop(B.mixes_dev); drop(B.eterms); drop(B.ecols); drop(B.envjobs);
   for (int ph = 0; ph < 2; ++ph) { drop(B.frames[ph]); drop(B.frame_geom[ph]); drop(B.olas[ph]); drop(B.mixes[ph]); }
@@ -663,6 +675,29 @@ int sg_plan_stft_stats(const sg_plan* plan, int64_t* samples, int64_t* alg_bytes
   *samples = plan->B.stft_samples;
   *alg_bytes = plan->B.stft_bytes;
   *flops = plan->B.stft_flops;
+  return SG_OK;
+}
+
+int64_t sg_plan_amp_count(const sg_plan* plan) { return plan && !plan->host_released ? plan->B.amp_total : 0; }
+
+int sg_plan_debug_amps(const sg_plan* plan, float* out, int64_t n) {
+  if (!plan || plan->host_released || !out || n < plan->B.amp_total) return SG_E_ARG;
+  const sg::Batch& B = plan->B;
+  std::vector<double> lg((size_t)B.amp_lg_rows + 1);
+  for (size_t k = 0; k < lg.size(); ++k) lg[k] = std::log2((double)(k + 1));
+  for (const SgAmpJob& J : B.ampjobs)  // sg_amp_build, one job after the other
+    for (int32_t r = 0; r < J.Rp; ++r) {
+      float prev = 0.f;
+      for (int32_t g = 0; g < J.G; ++g) {
+        float a;
+        if (r >= J.R) a = 0.f;
+        else if (J.src_off >= 0) a = B.ampsrc[J.src_off + (int64_t)g * J.Rp + r];
+        else a = (float)sg::amp_value(B.ampcols.data() + J.col0, J, lg.data(), g, r);
+        out[J.amp_off + (int64_t)g * J.Rp + r] = a;
+        if (g > 0) out[J.da_off + (int64_t)(g - 1) * J.Rp + r] = a - prev;
+        prev = a;
+      }
+    }
   return SG_OK;
 }
 

@@ -396,3 +396,30 @@ struct SgPcmStat {
   double mean, level, m, min, max;
   int32_t scale, pad;
 };
+
+// ------------------------------------------------------------------------
+// Harmonic amplitude matrices built on the device at upload (sg_amp_build,
+// SURVEY K3): getRolloff (R/sourceSpectrum.R:71-186), shimmer (R/source.R:
+// 316-323) and getVocalFry_per_epoch (R/subharmonics.R:25-86) from per-glottal-
+// cycle parameters. The host keeps every integer decision (kept rows, epochs,
+// rows per task) and sends 80 B per cycle instead of the [G][R] matrices.
+struct SgAmpCol {     // one glottal cycle
+  double pitch;       // f0 (Hz) after jitter, drift and clamping
+  double slope;       // rolloff + rolloffKHz (pitch - 200) / 1000 (dB/oct)
+  double oct;         // rolloffOct (dB/oct per kHz above 200 Hz)
+  double mx;          // column max of the thresholded dB (normalisation)
+  double sh;          // shimmer factor (1 without shimmer)
+  double rph;         // parabolic-rolloff harmonics (R's rounded value)
+  double pa, pb, pc;  // parabola a k^2 + b k + c over harmonics k <= rph
+  double sbw;         // subharmonic bandwidth subDep (Hz; vocal-fry epochs)
+};
+struct SgAmpJob {     // one epoch's [G][Rp] block A and [G-1][Rp] block dA = A[g+1] - A[g]
+  int64_t amp_off, da_off;  // destinations in the device amplitude array
+  int64_t src_off;          // >= 0: copy [G][Rp] floats from the uploaded source (host-built fallback)
+  int64_t col0;             // SgAmpCol of the syllable's glottal cycle 0
+  int32_t g0, G;            // the epoch's cycles [g0, g0 + G) of the syllable
+  int32_t R, Rp;            // rows computed (ranks 1..R), row stride (padded)
+  int32_t H, nsub;          // kept rolloff rows; subharmonics per harmonic (0: plain epoch)
+  double thr, nyq, parab, t01, baseline;  // throwaway (dB), sr / 2, rolloffParab, 2^(throwaway / 10), 200 Hz
+  int32_t any_oct, pad;
+};

@@ -24,7 +24,7 @@ size_t up(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 struct Layout {
   size_t tall, tlong, tshort, tallp, thp, fin_tiles_hp, W64, fh, frames64, frames64_tab, roots64, roots64_wl,
       roots64_off;
-  size_t segs, epochs, knots, amps, tasks, pieces, syls, syl_tiles, copy_tiles, ptiles, cknots, W, taskmax, ptilemax, maxes, total;
+  size_t segs, epochs, knots, amps, ampcols, ampjobs, ampsrc, tasks, pieces, syls, syl_tiles, copy_tiles, ptiles, cknots, W, taskmax, ptilemax, maxes, total;
   size_t geoms, frames, fgroups, olas, olatiles, olasegs, olatilemax, olamax, items, mixes, mixtiles, fl, fs;
   size_t eterms, ecols, envjobs, envtasks, elog2;
   explicit Layout(const Batch& B) {
@@ -34,7 +34,10 @@ struct Layout {
     segs = take((size_t)bulk_size(B.segs_x, B.segs) * sizeof(SgSeg));
     epochs = take(B.epochs.size() * sizeof(SgEpoch));
     knots = take(B.knots.size() * sizeof(double));
-    amps = take((size_t)bulk_size(B.amps_x, B.amps) * sizeof(float) + 64 * sizeof(float));
+    amps = take((size_t)B.amp_total * sizeof(float) + 64 * sizeof(float));
+    ampcols = take(B.ampcols.size() * sizeof(SgAmpCol));
+    ampjobs = take(B.ampjobs.size() * sizeof(SgAmpJob));
+    ampsrc = take(B.ampsrc.size() * sizeof(float));
     tasks = take(ntask * sizeof(SgWTask));
     tall = take(ntask * sizeof(int32_t));
     tlong = take(ntask * sizeof(int32_t));
@@ -154,7 +157,6 @@ void finalize_plan(Batch& B) {
     }
     std::vector<SgWTask> tasks;  // the merged task list (debug statistics only)
     bulk_each(B.tasks_x, B.tasks, [&](int64_t, const SgWTask* p, int64_t n) { tasks.insert(tasks.end(), p, p + n); });
-    auto amp = [&](int64_t i) { return bulk_at(B.amps_x, B.amps, i); };
     // sine-bank work: (sample, row) terms of the fp32 and the tall tasks, rows histogram of the tall ones
     double terms[2] = {0, 0};
     int64_t ntask[2] = {0, 0}, rmax = 0, samples[2] = {0, 0};
@@ -188,19 +190,6 @@ void finalize_plan(Batch& B) {
     std::fprintf(stderr, "sg plan: sine tasks fp32 %lld (%lld samples, %.3g chain terms), tall %lld (%lld samples, %.3g chain terms, max R %lld; R<256 %lld, <512 %lld, <1024 %lld, <2048 %lld, more %lld)\n",
                  (long long)ntask[0], (long long)samples[0], terms[0], (long long)ntask[1], (long long)samples[1], terms[1],
                  (long long)rmax, (long long)rh[0], (long long)rh[1], (long long)rh[2], (long long)rh[3], (long long)rh[4]);
-    {  // rows above the last nonzero amplitude (A or dA) of each task
-      double rsum[2] = {0, 0}, reff[2] = {0, 0};
-      for (const SgWTask& t : tasks) {
-        const int k = t.R > SG_ROWS_F32 ? 1 : 0;
-        int last = 0;
-        for (int r = 0; r < t.R; ++r)
-          if (amp(t.a_off + r) != 0.f || (!(t.flags & SG_TASK_CONST) && amp(t.d_off + r) != 0.f)) last = r + 1;
-        rsum[k] += (double)t.R * t.len;
-        reff[k] += (double)((last + 3) / 4 * 4) * t.len;
-      }
-      std::fprintf(stderr, "sg plan: row work incl. trailing zero rows: fp32 %.3g -> %.3g, tall %.3g -> %.3g\n", rsum[0],
-                   reff[0], rsum[1], reff[1]);
-    }
     for (int k = 0; k < 2; ++k)
       std::fprintf(stderr, "sg plan: %s tasks <= 64 samples: %lld (%.3g chain terms); len <=64/128/256/512/more: %lld %lld %lld %lld %lld\n",
                    k ? "tall" : "fp32", (long long)nshort[k], sterms[k], (long long)lh[k][0], (long long)lh[k][1],
@@ -278,6 +267,9 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   D.epochs = (SgEpoch*)(a + L.epochs);
   D.knots = (double*)(a + L.knots);
   D.amps = (float*)(a + L.amps);
+  D.ampcols = (const SgAmpCol*)(a + L.ampcols);
+  D.ampjobs = (const SgAmpJob*)(a + L.ampjobs);
+  D.ampsrc = (const float*)(a + L.ampsrc);
   D.tasks = (SgWTask*)(a + L.tasks);
   D.tall = (int32_t*)(a + L.tall);
   D.tlong = (int32_t*)(a + L.tlong);
@@ -326,7 +318,9 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   bulk_each(B.segs_x, B.segs, [&](int64_t o, const SgSeg* p, int64_t n) { cp(D.segs + o, p, n * sizeof(SgSeg)); });
   cp(D.epochs, B.epochs.data(), B.epochs.size() * sizeof(SgEpoch));
   cp(D.knots, B.knots.data(), B.knots.size() * sizeof(double));
-  bulk_each(B.amps_x, B.amps, [&](int64_t o, const float* p, int64_t n) { cp(D.amps + o, p, n * sizeof(float)); });
+  cp((void*)D.ampcols, B.ampcols.data(), B.ampcols.size() * sizeof(SgAmpCol));
+  cp((void*)D.ampjobs, B.ampjobs.data(), B.ampjobs.size() * sizeof(SgAmpJob));
+  cp((void*)D.ampsrc, B.ampsrc.data(), B.ampsrc.size() * sizeof(float));
   bulk_each(B.tasks_x, B.tasks, [&](int64_t o, const SgWTask* p, int64_t n) { cp(D.tasks + o, p, n * sizeof(SgWTask)); });
   // task classes (each task's class depends on the task alone): tall (sg_sine_bank_tall),
   // short fp32 (two per wave, sg_sine_bank_pairs), other fp32 (sg_sine_bank)
@@ -379,6 +373,7 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   cp(D.envjobs, B.envjobs.data(), B.envjobs.size() * sizeof(SgEnvJob));
   cp(D.envtasks, B.envtasks.data(), B.envtasks.size() * sizeof(SgEnvTask));
   cp(D.elog2, B.elog2.data(), B.elog2.size() * sizeof(double));
+  launch_amp_build(D, (int64_t)B.ampjobs.size(), s);  // the amplitude blocks, from the jobs just copied
   HIPCHK(hipStreamSynchronize(s));
   while (D.ev_slice.size() < B.slices.size()) {
     hipEvent_t e;

@@ -29,6 +29,9 @@ struct DevicePlan {
   SgEpoch* epochs = nullptr;
   double* knots = nullptr;
   float* amps = nullptr;
+  const SgAmpCol* ampcols = nullptr;  // sg_amp_build inputs (read at upload)
+  const SgAmpJob* ampjobs = nullptr;
+  const float* ampsrc = nullptr;
   SgWTask* tasks = nullptr;
   int32_t* tall = nullptr;           // indices of tasks with R > SG_ROWS_F32 (sg_sine_bank_tall)
   std::vector<int32_t> tall_host;
@@ -105,6 +108,7 @@ void device_execute_spec(const Batch& B, const DevicePlan& D, float* d_out, hipS
                          std::vector<SgProfEvent>* prof, bool join = false, hipEvent_t harm_done = nullptr);
 
 // launchers (sg_harm.hip)
+void launch_amp_build(const DevicePlan& D, int64_t n_jobs, hipStream_t s);
 void launch_sine_bank(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s);
 void launch_sine_bank_pairs(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s);
 void launch_sine_bank_tall(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s);

@@ -18,6 +18,7 @@
 
 #include "sg_dev.h"
 
+#include "sg_amp.h"
 #include "sg_devfn.h"
 
 using sgd::contour_at;
@@ -1132,6 +1133,30 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize_hp(
 }
 
 // ---------------------------------------------------------------- launchers
+// ------------------------------------------------- amplitude blocks (K3)
+// One workgroup per epoch job (run once, at upload): thread r owns row r of
+// every glottal cycle, walks the cycles in order and writes A[g][r] and
+// dA[g - 1][r] = A[g][r] - A[g - 1][r] in fp32, as the sine banks read them.
+// The values come from the shared formula (sg_amp.h) or, for the host-built
+// fallback, from the uploaded blocks.
+__global__ __launch_bounds__(256) void sg_amp_build(const SgAmpJob* __restrict__ jobs,
+                                                    const SgAmpCol* __restrict__ cols, const float* __restrict__ src,
+                                                    const double* __restrict__ lg, float* __restrict__ amps) {
+  const SgAmpJob J = jobs[blockIdx.x];
+  for (int r = threadIdx.x; r < J.Rp; r += blockDim.x) {
+    float prev = 0.f;
+    for (int g = 0; g < J.G; ++g) {
+      float a;
+      if (r >= J.R) a = 0.f;
+      else if (J.src_off >= 0) a = src[J.src_off + (int64_t)g * J.Rp + r];
+      else a = (float)sg::amp_value(cols + J.col0, J, lg, g, r);
+      amps[J.amp_off + (int64_t)g * J.Rp + r] = a;
+      if (g > 0) amps[J.da_off + (int64_t)(g - 1) * J.Rp + r] = a - prev;
+      prev = a;
+    }
+  }
+}
+
 #include "sg_exec.h"
 namespace sg {
 #define SG_LAUNCHED(name)                                                                       \
@@ -1140,6 +1165,12 @@ namespace sg {
     if (_e != hipSuccess) throw SgError(SG_E_DEVICE, std::string("launch " name ": ") + hipGetErrorString(_e)); \
   } while (0)
 
+void launch_amp_build(const DevicePlan& D, int64_t n_jobs, hipStream_t s) {
+  if (n_jobs <= 0) return;
+  hipLaunchKernelGGL(sg_amp_build, dim3((unsigned)n_jobs), dim3(256), 0, s, D.ampjobs, D.ampcols, D.ampsrc, D.elog2,
+                     D.amps);
+  SG_LAUNCHED("sg_amp_build");
+}
 void launch_sine_bank(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(sg_sine_bank, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, D.tlong + k0, n, D.tasks, D.amps,

@@ -92,7 +92,13 @@ struct Batch {
   bulk<SgSeg> segs;
   bulk<SgEpoch> epochs;
   bulk<double> knots;
-  bulk<float> amps;
+  // amplitude blocks: device-only (amp_total floats, sg_amp_build at upload) from
+  // one SgAmpJob per epoch: the formula over ampcols, or a copy of ampsrc
+  int64_t amp_total = 0;
+  bulk<SgAmpCol> ampcols;
+  std::vector<SgAmpJob> ampjobs;
+  bulk<float> ampsrc;         // host-built [G][Rp] blocks (the fallback path)
+  int64_t amp_lg_rows = 0;    // largest H: the log2 table the device formula reads
   bulk<SgWTask> tasks;
   bulk<SgPiece> pieces;
   std::vector<SgSyllable> syls;
@@ -147,9 +153,9 @@ struct Batch {
   // the end of the uploaded fl floats, fixed at finalize_spec). Until then a
   // frame's env < 0 encodes envelope-area offset -(env + 1).
   bulk<SgEnvTerm> eterms;
-  // merged batch: the parts' blocks ahead of segs, amps, tasks, fl, eterms (Blocks)
+  // merged batch: the parts' blocks ahead of segs, tasks, fl, eterms (Blocks)
   Blocks<SgSeg> segs_x;
-  Blocks<float> amps_x, fl_x;
+  Blocks<float> fl_x;
   Blocks<SgWTask> tasks_x;
   Blocks<SgEnvTerm> eterms_x;
   std::vector<SgEnvCol> ecols;

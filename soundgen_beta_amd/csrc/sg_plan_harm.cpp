@@ -8,10 +8,12 @@
 // samples the zero-crossing searches visit. The per-sample work — the sine
 // bank, the crossfades, normalisation, fades, envelopes — runs on the GPU.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
 
+#include "sg_amp.h"
 #include "sg_loess.h"
 #include "sg_plan.h"
 #include "sg_prof.h"
@@ -315,12 +317,55 @@ vec get_rolloff(const vec& pitch, int64_t nH, const vec& rolloff, const vec& rol
 }
 
 // ---------------------------------------------------------- vocal fry
+// A syllable's amplitude parameters for the device build (sg_amp.h): one
+// SgAmpCol per glottal cycle, the shared constants in a job template.
+struct AmpSpec {
+  std::vector<SgAmpCol> cols;
+  SgAmpJob J{};
+  vec lg;          // log2(h + 1), as getRolloff and the device table (elog2) hold it
+  vec lsh;         // log2 of each cycle's shimmer factor (0 without shimmer)
+};
+
 struct EpochMat {
   int64_t g0, g1;     // 0-based gc range (inclusive)
   int64_t D;          // nSubharm + 1
   int64_t R;          // max rank
-  vec A;              // [G][R] by rank, fp64 (zero rows for dropped ranks)
+  vec A;              // host-built: [G][R] by rank, fp64 (zero rows for dropped ranks)
   vec mult;           // [R]: R's times_f0 for ranks present (0 if absent)
+  // device-built (spec set): columns computed here only where the host needs
+  // values (zero-crossing searches), by the formula sg_amp_build runs
+  const AmpSpec* spec = nullptr;
+  SgAmpJob job{};
+  mutable std::vector<vec> cache;
+  // per column: rows up to the last nonzero A (lnz); eq[g]: column g + 1 equals column g
+  std::vector<int32_t> lnz;
+  std::vector<char> eq;
+  const double* col(int64_t g) const {
+    if (!spec) return A.data() + g * R;
+    if (cache.empty()) cache.resize((size_t)(g1 - g0 + 1));
+    vec& c = cache[(size_t)g];
+    if ((int64_t)c.size() != R) {
+      c.resize((size_t)R);
+      for (int64_t r = 0; r < R; ++r) c[r] = amp_value(spec->cols.data(), job, spec->lg.data(), (int)g, (int)r);
+    }
+    return c.data();
+  }
+  // lnz / eq of a host-built matrix from its fp32 values (what the device reads)
+  void float_pattern() {
+    const int64_t G = g1 - g0 + 1;
+    lnz.assign((size_t)G, 0);
+    eq.assign((size_t)G, 0);
+    for (int64_t g = 0; g < G; ++g) {
+      int32_t l = 0;
+      for (int64_t r = 0; r < R; ++r) if ((float)A[g * R + r] != 0.0f) l = (int32_t)(r + 1);
+      lnz[g] = l;
+      if (g + 1 < G) {
+        bool e = true;
+        for (int64_t r = 0; r < R && e; ++r) e = (float)A[g * R + r] == (float)A[(g + 1) * R + r];
+        eq[g] = e;
+      }
+    }
+  }
 };
 
 static double rowname_num(double x) {
@@ -395,9 +440,11 @@ static EpochMat fry_per_epoch(const double* roll, int64_t H, int64_t g0, int64_t
   return m;
 }
 
-// getVocalFry(), R/subharmonics.R:108-163
-static std::vector<EpochMat> get_vocal_fry(const vec& roll, int64_t H, const vec& pitch, const vec& subFreq,
-                                           const vec& subDep, double throwaway, double shortestEpoch) {
+// getVocalFry()'s epochs: runs of glottal cycles with one number of
+// subharmonics (clumped to shortestEpoch), [g0, g1] inclusive
+//   R/subharmonics.R:108-163
+struct FryEpoch { int64_t g0, g1, nsub; };
+static std::vector<FryEpoch> fry_epochs(const vec& pitch, const vec& subFreq, double shortestEpoch) {
   const int64_t nGC = (int64_t)pitch.size();
   vec nsub(nGC);
   double mx = -INFINITY;
@@ -406,20 +453,190 @@ static std::vector<EpochMat> get_vocal_fry(const vec& roll, int64_t H, const vec
     if (v < 0) v = 0;
     nsub[g] = v; mx = std::max(mx, v);
   }
-  std::vector<EpochMat> out;
-  if (mx < 1) { out.push_back(fry_per_epoch(roll.data(), H, 0, nGC - 1, pitch, 0, subDep, 0)); return out; }
-  const double throwaway01 = std::pow(2.0, throwaway / 10);
+  if (mx < 1) return {FryEpoch{0, nGC - 1, 0}};
   vec minlen(nGC);
   for (int64_t g = 0; g < nGC; ++g) minlen[g] = r_round(shortestEpoch / (1000 / pitch[g]));
   if (nGC > 1) clumper(nsub, minlen);
+  std::vector<FryEpoch> out;
   int64_t s0 = 0;
   for (int64_t g = 1; g <= nGC; ++g) {
     if (g == nGC || nsub[g] != nsub[g - 1]) {
-      out.push_back(fry_per_epoch(roll.data(), H, s0, g - 1, pitch, (int64_t)nsub[g - 1], subDep, throwaway01));
+      out.push_back(FryEpoch{s0, g - 1, (int64_t)nsub[g - 1]});
       s0 = g;
     }
   }
   return out;
+}
+
+// getVocalFry(), R/subharmonics.R:108-163
+static std::vector<EpochMat> get_vocal_fry(const vec& roll, int64_t H, const vec& pitch, const vec& subFreq,
+                                           const vec& subDep, double throwaway, double shortestEpoch) {
+  const std::vector<FryEpoch> eps = fry_epochs(pitch, subFreq, shortestEpoch);
+  const double throwaway01 = eps.size() == 1 && eps[0].nsub == 0 ? 0.0 : std::pow(2.0, throwaway / 10);
+  std::vector<EpochMat> out;
+  for (const FryEpoch& e : eps) out.push_back(fry_per_epoch(roll.data(), H, e.g0, e.g1, pitch, e.nsub, subDep, throwaway01));
+  return out;
+}
+
+// ------------------------------------------- device-built amplitude matrices
+// getRolloff() without the matrix: per cycle its parameters and column max,
+// the kept rows H, each column's last finite row (lf, 1-based). The device
+// builds the values (sg_amp_build). false -> the host-built path: kept rows
+// that are not 0..H-1 (R renumbers them), a column without a finite value, or
+// a dynamic range whose powers could underflow.
+//   R/sourceSpectrum.R:71-186 (rolloffParabCeiling NA, as generateHarmonics calls it)
+static bool rolloff_spec(const vec& pitch, int64_t nH, const vec& rolloff, const vec& rolloffOct, double rolloffParab,
+                         double rolloffParabHarm, const vec& rolloffKHz, double baseline, double throwaway, double sr,
+                         AmpSpec& S, int64_t& H, std::vector<int32_t>& lf) {
+  ProfScope ps(PF_ROLLOFF);
+  const int64_t nGC = (int64_t)pitch.size();
+  if (nH < 1) throw SgError(SG_E_DOMAIN, "getRolloff: nHarmonics < 1");
+  bool anyOct = false;
+  for (double v : rolloffOct) if (v != 0) anyOct = true;
+  S.lg.resize((size_t)nH);
+  for (int64_t h = 0; h < nH; ++h) S.lg[h] = std::log2((double)(h + 1));
+  SgAmpJob& J = S.J;
+  J = SgAmpJob{};
+  J.thr = throwaway;
+  J.nyq = sr / 2;
+  J.parab = rolloffParab;
+  J.t01 = std::pow(2.0, throwaway / 10);
+  J.baseline = baseline;
+  J.any_oct = anyOct;
+  double rph = r_round(rolloffParabHarm), a = 0, b = 0, c = 0;
+  if (rph == 2) rph = 3;
+  if (rolloffParab != 0) {
+    a = -4 * rolloffParab / ((rph - 1) * (rph - 1));
+    b = -a * (1 + rph);
+    c = a * rph;
+    if (rph >= 3 && rph > nH && nGC > 0)
+      throw SgError(SG_E_DOMAIN, "getRolloff: subscript out of bounds (rolloffParabHarm > nHarmonics)");
+  }
+  S.cols.resize((size_t)nGC);
+  std::vector<char> kept((size_t)nH, 0);
+  lf.assign((size_t)nGC, 0);
+  double vmin = INFINITY;
+  for (int64_t g = 0; g < nGC; ++g) {
+    SgAmpCol& P = S.cols[g];
+    P = SgAmpCol{};
+    P.pitch = pitch[g];
+    P.slope = rolloff[g] + rolloffKHz[g] * (pitch[g] - baseline) / 1000;
+    P.oct = rolloffOct[g];
+    P.sh = 1;
+    P.rph = rph;
+    P.pa = a; P.pb = b; P.pc = c;
+    double mx = -INFINITY, v;
+    int32_t last = 0;
+    for (int64_t h = 0; h < nH; ++h) {
+      if ((double)(h + 1) * P.pitch >= J.nyq) break;  // -Inf from here up
+      if (!roll_db(P, J, S.lg.data(), (int)h, &v)) continue;
+      kept[h] = 1;
+      last = (int32_t)(h + 1);
+      if (v > mx) mx = v;
+      if (v < vmin) vmin = v;
+    }
+    if (mx == -INFINITY) return false;
+    P.mx = mx;
+    lf[g] = last;
+    if (mx - vmin > 9000) return false;  // 2^(-900) and below: keep R's underflow decisions on the host
+  }
+  H = 0;
+  while (H < nH && kept[H]) ++H;
+  for (int64_t h = H; h < nH; ++h) if (kept[h]) return false;
+  return H > 0;
+}
+
+// a plain epoch (no subharmonics): the kept rolloff rows as they are
+static void plain_spec(const AmpSpec& S, int64_t H, int64_t g0, int64_t g1, const std::vector<int32_t>& lf,
+                       EpochMat& m) {
+  const int64_t ncol = g1 - g0 + 1;
+  m.g0 = g0; m.g1 = g1; m.D = 1; m.R = H;
+  m.mult.resize((size_t)H);
+  for (int64_t h = 0; h < H; ++h) m.mult[h] = (double)(h + 1);
+  m.spec = &S;
+  m.job = S.J;
+  m.job.g0 = (int32_t)g0; m.job.G = (int32_t)ncol; m.job.H = (int32_t)H; m.job.nsub = 0; m.job.R = (int32_t)H;
+  m.lnz.assign(lf.begin() + g0, lf.begin() + g1 + 1);
+  m.eq.assign((size_t)ncol, 0);
+  for (int64_t g = 0; g + 1 < ncol; ++g)
+    m.eq[g] = std::memcmp(&S.cols[g0 + g], &S.cols[g0 + g + 1], sizeof(SgAmpCol)) == 0;
+}
+
+// getVocalFry_per_epoch()'s kept ranks, multipliers and per-cycle nonzero rows
+// without the matrix. Harmonic rows are decided in the log domain (exponent
+// against throwaway / 10), sidebands from exact end points and weights. false
+// -> host path: a value within rounding of the threshold, where the device's
+// pow / exp might decide the other way.   R/subharmonics.R:25-86
+static bool fry_spec(const AmpSpec& S, int64_t H, int64_t g0, int64_t g1, int64_t nSub, EpochMat& m) {
+  const int64_t D = nSub + 1, ncol = g1 - g0 + 1;
+  const vec gseq = r_seq_by(0, (double)(H + 1), 1.0 / (double)D);
+  const int64_t nr = (int64_t)gseq.size();
+  if (nr != (H + 1) * D + 1) return false;
+  for (int64_t h = 0; h < H; ++h)  // rownames match at row (h + 1) D (15 significant digits)
+    if (std::fabs(gseq[(h + 1) * D] - (double)(h + 1)) > 1e-13 * (double)(h + 1)) return false;
+  SgAmpJob J = S.J;
+  J.g0 = (int32_t)g0; J.G = (int32_t)ncol; J.H = (int32_t)H; J.nsub = (int32_t)nSub;
+  const double* lg = S.lg.data();
+  vec r0((size_t)H);
+  for (int64_t h = 0; h < H; ++h) r0[h] = roll_value(S.cols[g0], J, lg, (int)h);
+  vec ml((size_t)(nSub * ncol));
+  for (int64_t q = 1; q <= nSub; ++q)
+    for (int64_t g = 0; g < ncol; ++g) ml[(q - 1) * ncol + g] = fry_ml(S.cols[g0 + g], J, (int)q);
+  std::vector<char> keep((size_t)nr, 0);
+  m.lnz.assign((size_t)ncol, 0);
+  const double thr10 = J.thr / 10;
+  for (int64_t g = 0; g < ncol; ++g) {
+    const SgAmpCol& P = S.cols[g0 + g];
+    const double lsh = S.lsh.empty() ? 0.0 : S.lsh[g0 + g];
+    int32_t last = 0;
+    for (int64_t i = 1; i < nr; ++i) {
+      bool nz;
+      if (i % D == 0) {
+        const int64_t h = i / D - 1;
+        double v;
+        if (h >= H || !roll_db(P, J, lg, (int)h, &v)) {
+          nz = false;
+        } else {
+          const double y = (v - P.mx) / 10 + lsh;
+          if (y > thr10 + 1e-9) nz = true;
+          else if (y < thr10 - 1e-9) nz = false;
+          else return false;
+        }
+      } else {
+        const int64_t block = i / D + 1, gg = i % D;
+        const double a = block >= 2 ? r0[block - 2] : 0.0, b = block - 1 < H ? r0[block - 1] : 0.0;
+        const double val = a * ml[(gg - 1) * ncol + g] + b * ml[(nSub - gg) * ncol + g];
+        if (std::isnan(val) || std::fabs(val - J.t01) <= 1e-12 * J.t01) return false;
+        nz = val >= J.t01;
+      }
+      if (nz) { keep[i] = 1; last = (int32_t)i; }
+    }
+    m.lnz[g] = last;
+  }
+  int64_t R = 0;
+  for (int64_t i = nr - 1; i > 0 && !R; --i) if (keep[i]) R = i;
+  m.g0 = g0; m.g1 = g1; m.D = D; m.R = R;
+  m.mult.assign((size_t)std::max<int64_t>(R, 1), 0.0);
+  for (int64_t i = 1; i <= R; ++i) if (keep[i]) m.mult[i - 1] = rowname_num(gseq[i]);
+  m.spec = &S;
+  m.job = J;
+  m.job.R = (int32_t)R;
+  m.eq.assign((size_t)ncol, 0);
+  for (int64_t g = 0; g + 1 < ncol; ++g)
+    m.eq[g] = std::memcmp(&S.cols[g0 + g], &S.cols[g0 + g + 1], sizeof(SgAmpCol)) == 0;
+  return true;
+}
+
+// 1: every call takes the host-built path (tests compare the two); default
+// from SG_AMP_HOST, changed by sg_set_amp_policy
+static std::atomic<int> g_amp_host{-1};
+static bool amp_device_enabled() {
+  int h = g_amp_host.load();
+  if (h < 0) {
+    h = std::getenv("SG_AMP_HOST") != nullptr ? 1 : 0;
+    g_amp_host.store(h);
+  }
+  return h == 0;
 }
 
 // ---------------------------------------------------- host evaluator
@@ -455,10 +672,11 @@ struct HostEpoch {
     while (i < jj - 1) { int64_t ij = (i + jj) / 2; if (v < knots[ij]) jj = ij; else i = ij; }
     const double t = (v - knots[i]) / (knots[jj] - knots[i]);
     const double integ = S->integr(u0 + j);
+    const double *A0 = M->col(i), *A1 = M->col(jj);
     double acc = 0;
     for (int64_t r = 0; r < M->R; ++r) {
       if (M->mult[r] == 0) continue;
-      const double y0 = M->A[i * M->R + r], y1 = M->A[jj * M->R + r];
+      const double y0 = A0[r], y1 = A1[r];
       double am;
       if (v == knots[jj]) am = y1;
       else if (v == knots[i]) am = y0;
@@ -481,8 +699,9 @@ struct HostEpoch {
     x -= std::rint(x);
     const double th = 2 * M_PI * x, c2 = 2 * std::cos(th);
     double b1 = 0, b2 = 0, sabs = 0;
+    const double *A0 = M->col(i), *A1 = M->col(jj);
     for (int64_t r = M->R - 1; r >= 0; --r) {
-      const double y0 = M->A[i * M->R + r], y1 = M->A[jj * M->R + r];
+      const double y0 = A0[r], y1 = A1[r];
       double am = (M->mult[r] == 0) ? 0.0 : (v == knots[jj] ? y1 : (v == knots[i] ? y0 : y0 + (y1 - y0) * t));
       const double b = am + c2 * b1 - b2;
       b2 = b1;
@@ -749,22 +968,63 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
     roo[g] = P.rolloffOct * w * w * w;
     rk[g] = P.rolloffKHz * w;
   }
+  // amplitude matrices: built on the device from per-cycle parameters (spec),
+  // or on the host (roll, mats[].A) where the formula path does not apply
   int64_t H = 0;
-  vec roll = get_rolloff(ppg, nH, ro, roo, P.rolloffParab, P.rolloffParabHarm, rk, 200, P.throwaway, sr, H);
-  if (P.shimmerDep > 0 && P.nonlinBalance > 0)
+  AmpSpec spec;
+  std::vector<int32_t> lastf;  // per cycle: last finite rolloff row (1-based)
+  bool dev_amps = amp_device_enabled() && rolloff_spec(ppg, nH, ro, roo, P.rolloffParab, P.rolloffParabHarm, rk, 200,
+                                                       P.throwaway, sr, spec, H, lastf);
+  vec roll;
+  if (!dev_amps) roll = get_rolloff(ppg, nH, ro, roo, P.rolloffParab, P.rolloffParabHarm, rk, 200, P.throwaway, sr, H);
+  const bool shimmer = P.shimmerDep > 0 && P.nonlinBalance > 0;
+  if (dev_amps) spec.lsh.assign((size_t)nGC, 0.0);
+  if (shimmer)
     for (int64_t g = 0; g < nGC; ++g) {
       const double z = R.rnorm(0, P.shimmerDep / 100);
-      const double sh = std::pow(2.0, z * rw[g] * jit_on[g]);
-      for (int64_t h = 0; h < H; ++h) roll[g * H + h] *= sh;
+      const double e = z * rw[g] * jit_on[g];
+      const double sh = std::pow(2.0, e);
+      if (dev_amps) {
+        spec.cols[g].sh = sh;
+        spec.lsh[g] = e;
+      } else {
+        for (int64_t h = 0; h < H; ++h) roll[g * H + h] *= sh;
+      }
     }
   std::vector<EpochMat> mats;
   ProfScope pfry(PF_FRY);
-  if (P.subDep > 0 && P.nonlinBalance > 0) {
-    vec sf(nGC), sd(nGC);
+  const bool fry = P.subDep > 0 && P.nonlinBalance > 0;
+  vec sf, sd;
+  if (fry) {
+    sf.resize(nGC);
+    sd.resize(nGC);
     for (int64_t g = 0; g < nGC; ++g) { const double w4 = std::pow(rw[g], 4); sf[g] = P.subFreq * w4; sd[g] = P.subDep * w4 * vf_on[g]; }
-    mats = get_vocal_fry(roll, H, ppg, sf, sd, P.throwaway, P.shortestEpoch);
-  } else {
-    mats.push_back(fry_per_epoch(roll.data(), H, 0, nGC - 1, ppg, 0, vec(nGC, 0.0), 0));
+  }
+  if (dev_amps) {
+    if (fry)
+      for (int64_t g = 0; g < nGC; ++g) spec.cols[g].sbw = sd[g];
+    const std::vector<FryEpoch> eps = fry ? fry_epochs(ppg, sf, P.shortestEpoch) : std::vector<FryEpoch>{{0, nGC - 1, 0}};
+    for (const FryEpoch& e : eps) {
+      mats.emplace_back();
+      if (e.nsub == 0) {
+        plain_spec(spec, H, e.g0, e.g1, lastf, mats.back());
+      } else if (!fry_spec(spec, H, e.g0, e.g1, e.nsub, mats.back())) {
+        dev_amps = false;  // a threshold call too close to decide for the device: host path
+        break;
+      }
+    }
+    if (!dev_amps) {
+      mats.clear();
+      roll = get_rolloff(ppg, nH, ro, roo, P.rolloffParab, P.rolloffParabHarm, rk, 200, P.throwaway, sr, H);
+      if (shimmer)
+        for (int64_t g = 0; g < nGC; ++g)
+          for (int64_t h = 0; h < H; ++h) roll[g * H + h] *= spec.cols[g].sh;
+    }
+  }
+  if (!dev_amps) {
+    if (fry) mats = get_vocal_fry(roll, H, ppg, sf, sd, P.throwaway, P.shortestEpoch);
+    else mats.push_back(fry_per_epoch(roll.data(), H, 0, nGC - 1, ppg, 0, vec(nGC, 0.0), 0));
+    for (EpochMat& m : mats) m.float_pattern();
   }
   // upsample(): gcLen, gc_up, cumulative-pitch segments
   vec gcl(nGC);
@@ -822,7 +1082,12 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
       HarmProbe hp;
       hp.t = (int64_t)gc_up[g] - 1;
       hp.f0 = ppg[g];
-      hp.amp.assign(roll.begin() + g * H, roll.begin() + (g + 1) * H);
+      if (dev_amps) {
+        hp.amp.resize((size_t)H);
+        for (int64_t h = 0; h < H; ++h) hp.amp[h] = roll_value(spec.cols[g], spec.J, spec.lg.data(), (int)h);
+      } else {
+        hp.amp.assign(roll.begin() + g * H, roll.begin() + (g + 1) * H);
+      }
       probes->push_back(std::move(hp));
     }
   }
@@ -864,6 +1129,12 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
     g.c4 = (double)((d / 4) * isr);
     B.segs.push_back(g);
   }
+  int64_t col0 = -1;
+  if (dev_amps) {
+    col0 = (int64_t)B.ampcols.size();
+    B.ampcols.insert(B.ampcols.end(), spec.cols.begin(), spec.cols.end());
+    B.amp_lg_rows = std::max<int64_t>(B.amp_lg_rows, H);
+  }
   std::vector<int32_t> ep_index(mats.size());
   // destination offset of each epoch's direct piece, to keep the fp32 copy
   // in the finalize kernel 16-byte aligned on both sides
@@ -890,20 +1161,33 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
     d.invD = 1.0 / (double)m.D;
     d.knot_off = (int64_t)B.knots.size();
     B.knots.insert(B.knots.end(), he.knots.begin(), he.knots.end());
-    // [G][R] amplitudes then [G-1][R] column differences, 64-B aligned rows
-    d.amp_off = (int64_t)B.amps.size();
+    // [G][R] amplitudes then [G-1][R] column differences (device array, built by
+    // sg_amp_build at upload from the job: formula, or the host-built values)
+    d.amp_off = B.amp_total;
     d.da_off = d.amp_off + (int64_t)d.G * d.R;
-    B.amps.resize(B.amps.size() + (size_t)(2 * d.G - 1) * d.R);  // every element written below
+    B.amp_total += (int64_t)(2 * d.G - 1) * d.R;
     {
-      float* a = B.amps.data() + d.amp_off;
-      float* da = B.amps.data() + d.da_off;
-      for (int64_t g = 0; g < he.G; ++g) {
-        float* row = a + g * d.R;
-        for (int64_t r = 0; r < m.R; ++r) row[r] = (float)m.A[g * m.R + r];
-        std::fill(row + m.R, row + d.R, 0.0f);
+      SgAmpJob j = dev_amps ? m.job : SgAmpJob{};
+      j.amp_off = d.amp_off;
+      j.da_off = d.da_off;
+      j.G = d.G;
+      j.R = (int32_t)m.R;
+      j.Rp = d.R;
+      if (dev_amps) {
+        j.src_off = -1;
+        j.col0 = col0;
+      } else {
+        j.src_off = (int64_t)B.ampsrc.size();
+        j.col0 = -1;
+        B.ampsrc.resize(B.ampsrc.size() + (size_t)d.G * d.R);
+        float* a = B.ampsrc.data() + j.src_off;
+        for (int64_t g = 0; g < he.G; ++g) {
+          float* row = a + g * d.R;
+          for (int64_t r = 0; r < m.R; ++r) row[r] = (float)m.A[g * m.R + r];
+          std::fill(row + m.R, row + d.R, 0.0f);
+        }
       }
-      for (int64_t g = 0; g + 1 < he.G; ++g)
-        for (int64_t r = 0; r < d.R; ++r) da[g * d.R + r] = a[(g + 1) * d.R + r] - a[g * d.R + r];
+      B.ampjobs.push_back(j);
     }
     d.syl = syl_idx;
     d.dj0 = d.dj1 = 0;
@@ -965,14 +1249,11 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
       }
       jb[i] = g;
       ja = g;
-      bool c = true;
-      for (int64_t r = 0; r < ep.R && c; ++r) c = B.amps[ep.da_off + i * ep.R + r] == 0.0f;
+      const EpochMat& m = mats[e];
+      const bool c = m.eq[i] != 0;  // dA[i] = 0: one chain
       cst[i] = c;
       // rows the device recurrence needs: up to the last nonzero A (or dA) row
-      int64_t last = ep.R;
-      const float* ar = B.amps.data() + ep.amp_off + i * ep.R;
-      const float* dr = B.amps.data() + ep.da_off + i * ep.R;
-      while (last > 0 && ar[last - 1] == 0.0f && (c || dr[last - 1] == 0.0f)) --last;
+      const int64_t last = std::max<int64_t>(m.lnz[i], c ? 0 : m.lnz[i + 1]);
       rn[i] = (int32_t)((last + 3) / 4 * 4);
     }
     int64_t k = 0;
@@ -1125,3 +1406,9 @@ void tile_syllables(Batch& B, int first_syl) {
 }
 
 }  // namespace sg
+
+extern "C" int sg_set_amp_policy(int32_t host_built) {
+  if (host_built < 0 || host_built > 1) return SG_E_ARG;
+  sg::g_amp_host.store(host_built);
+  return SG_OK;
+}

@@ -686,7 +686,9 @@ void finalize_spec(Batch& B) {
     maxnr = std::max(maxnr, j.nr);
     if (j.ntr > 2 * 64) throw SgError(SG_E_DEVICE, "spectral envelope: more than 128 formant tracks (planner check)");
   }
-  B.elog2.resize((size_t)maxnr + 64);  // log2(k) for k = 1.. (padded to whole 64-bin chunks)
+  // log2(k) for k = 1.. (padded to whole 64-bin chunks): spectral envelopes' bins and
+  // the device amplitude formula's rolloff rows (sg_amp.h)
+  B.elog2.resize((size_t)std::max<int64_t>(maxnr, B.amp_lg_rows) + 64);
   for (size_t k = 0; k < B.elog2.size(); ++k) B.elog2[k] = std::log2((double)(k + 1));
   B.envtasks.clear();
   for (size_t j = 0; j < B.envjobs.size(); ++j)

@@ -74,6 +74,10 @@ def lib():
     L.sg_plan_stft_stats.argtypes = [vp, i64p, i64p, dp]
     L.sg_plan_precision.argtypes = [vp, C.POINTER(C.c_int32), i64p, i64p]
     L.sg_set_fp64_policy.argtypes = [C.c_int32, C.c_double]
+    L.sg_set_amp_policy.argtypes = [C.c_int32]
+    L.sg_plan_amp_count.restype = C.c_int64
+    L.sg_plan_amp_count.argtypes = [C.c_void_p]
+    L.sg_plan_debug_amps.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.c_int64]
     L.sg_plan_call_work.argtypes = [vp, dp, dp]
     L.sg_dtw_symmetric2.argtypes = [dp, i64, dp, i64, dp]
     L.sg_rrng_create.argtypes = [C.c_int32, C.POINTER(vp)]

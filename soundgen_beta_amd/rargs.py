@@ -219,6 +219,31 @@ class Holder:
         self.keep.append(a)
         return a
 
+    def anchors_of(self, x, time_to=1.0):
+        """sg_anchors of an R anchors argument, converted once per distinct value
+        (a batch repeats a few anchor sets: presets, defaults, NA)."""
+        if isinstance(x, dict):
+            t, v = x["time"], x["value"]
+            key = ("d", tuple(t) if isinstance(t, (list, tuple, np.ndarray)) else (t,),
+                   tuple(v) if isinstance(v, (list, tuple, np.ndarray)) else (v,))
+        elif isinstance(x, (list, tuple, np.ndarray)):
+            key = ("v", tuple(x), time_to)
+        else:
+            key = ("s", x if not (isinstance(x, float) and math.isnan(x)) else "NA", time_to)
+        hit = self._amemo.get(key)
+        if hit is None:
+            an = as_anchors(x, time_to=time_to)
+            if an is None:
+                hit = (0, None, None)
+            else:
+                t, v = self.arr(an[0]), self.arr(an[1])
+                hit = (len(t), _abi.dptr(t), _abi.dptr(v))
+            self._amemo[key] = hit
+        s = _abi.sg_anchors()
+        if hit[0]:
+            s.n, s.time, s.value = hit
+        return s
+
     def anchors(self, an):
         if an is None:
             s = _abi.sg_anchors()
@@ -290,34 +315,51 @@ def resolve_soundgen_kwargs(kw):
     return a
 
 
-def fill_soundgen_args(h, kw):
-    """kwargs (R names) -> sg_soundgen_args (buffers kept alive by h)."""
+# the scalar (double) fields of sg_soundgen_args, written in one structured-array
+# store per call instead of one ctypes setattr each
+_SG_SCALARS = [f for f, t in _abi.sg_soundgen_args._fields_ if t is _abi.C.c_double]
+_SG_SCALAR_DT = np.dtype({"names": _SG_SCALARS, "formats": ["<f8"] * len(_SG_SCALARS),
+                          "offsets": [getattr(_abi.sg_soundgen_args, f).offset for f in _SG_SCALARS],
+                          "itemsize": _abi.C.sizeof(_abi.sg_soundgen_args)})
+_NAN = float("nan")
+_ACTIONS = {"adjust": 0, "abort": 1, "ignore": 2}
+
+
+def _scalar(v):
+    if v is None or (isinstance(v, str) and v == "NA"):
+        return _NAN
+    return float(v)
+
+
+def fill_soundgen_args(h, kw, out=None):
+    """kwargs (R names) -> sg_soundgen_args (buffers kept alive by h); fills `out`
+    in place when given."""
     a = resolve_soundgen_kwargs(kw)
-    s = _abi.sg_soundgen_args()
-    for f, _ in _abi.sg_soundgen_args._fields_:
-        if f in ("pitchAnchors", "pitchAnchorsGlobal", "noiseAnchors", "mouthAnchors",
-                 "amplAnchors", "amplAnchorsGlobal", "formants", "formantsNoise",
-                 "tempEffects", "invalidArgAction", "formantsNoise_rlen"):
-            continue
-        v = a[f]
-        setattr(s, f, float("nan") if _is_na(v) else float(v))
-    s.tempEffects = (C_double8())(*[float(a["tempEffects"][k]) for k in TEMP_EFFECTS_ORDER])
-    s.pitchAnchors = h.anchors(as_anchors(a["pitchAnchors"]))
-    s.pitchAnchorsGlobal = h.anchors(as_anchors(a["pitchAnchorsGlobal"]))
-    s.amplAnchors = h.anchors(as_anchors(a["amplAnchors"]))
-    s.amplAnchorsGlobal = h.anchors(as_anchors(a["amplAnchorsGlobal"]))
-    s.mouthAnchors = h.anchors(as_anchors(a["mouthAnchors"]))
-    s.noiseAnchors = h.anchors(as_anchors(a["noiseAnchors"], time_to=a["sylLen"]))
+    s = _abi.sg_soundgen_args() if out is None else out
+    vals = tuple(map(a.__getitem__, _SG_SCALARS))
+    if None in vals or "NA" in vals:
+        vals = tuple(map(_scalar, vals))
+    np.frombuffer(s, dtype=_SG_SCALAR_DT, count=1)[0] = vals
+    te = a["tempEffects"]
+    s.tempEffects = (C_double8())(*[float(te[k]) for k in TEMP_EFFECTS_ORDER])
+    s.pitchAnchors = h.anchors_of(a["pitchAnchors"])
+    s.pitchAnchorsGlobal = h.anchors_of(a["pitchAnchorsGlobal"])
+    s.amplAnchors = h.anchors_of(a["amplAnchors"])
+    s.amplAnchorsGlobal = h.anchors_of(a["amplAnchorsGlobal"])
+    s.mouthAnchors = h.anchors_of(a["mouthAnchors"])
+    s.noiseAnchors = h.anchors_of(a["noiseAnchors"], time_to=a["sylLen"])
     s.formants = h.formants_of(a["formants"])
     s.formantsNoise = h.formants_of(a["formantsNoise"])
     s.formantsNoise_rlen = r_max_lengths(a["formantsNoise"])
-    s.invalidArgAction = {"adjust": 0, "abort": 1, "ignore": 2}[a["invalidArgAction"]]
+    s.invalidArgAction = _ACTIONS[a["invalidArgAction"]]
     return s
 
 
+_D8 = _abi.C.c_double * 8
+
+
 def C_double8():
-    import ctypes
-    return ctypes.c_double * 8
+    return _D8
 
 
 def fill_harm_params(kw):
