@@ -567,7 +567,8 @@ static void plain_spec(const AmpSpec& S, int64_t H, int64_t g0, int64_t g1, cons
 // against throwaway / 10), sidebands from exact end points and weights. false
 // -> host path: a value within rounding of the threshold, where the device's
 // pow / exp might decide the other way.   R/subharmonics.R:25-86
-static bool fry_spec(const AmpSpec& S, int64_t H, int64_t g0, int64_t g1, int64_t nSub, EpochMat& m) {
+static bool fry_spec(const AmpSpec& S, int64_t H, int64_t g0, int64_t g1, int64_t nSub, const std::vector<int32_t>& lf,
+                     EpochMat& m) {
   const int64_t D = nSub + 1, ncol = g1 - g0 + 1;
   const vec gseq = r_seq_by(0, (double)(H + 1), 1.0 / (double)D);
   const int64_t nr = (int64_t)gseq.size();
@@ -582,36 +583,57 @@ static bool fry_spec(const AmpSpec& S, int64_t H, int64_t g0, int64_t g1, int64_
   vec ml((size_t)(nSub * ncol));
   for (int64_t q = 1; q <= nSub; ++q)
     for (int64_t g = 0; g < ncol; ++g) ml[(q - 1) * ncol + g] = fry_ml(S.cols[g0 + g], J, (int)q);
-  std::vector<char> keep((size_t)nr, 0);
-  m.lnz.assign((size_t)ncol, 0);
   const double thr10 = J.thr / 10;
-  for (int64_t g = 0; g < ncol; ++g) {
-    const SgAmpCol& P = S.cols[g0 + g];
-    const double lsh = S.lsh.empty() ? 0.0 : S.lsh[g0 + g];
-    int32_t last = 0;
-    for (int64_t i = 1; i < nr; ++i) {
-      bool nz;
-      if (i % D == 0) {
-        const int64_t h = i / D - 1;
-        double v;
-        if (h >= H || !roll_db(P, J, lg, (int)h, &v)) {
-          nz = false;
-        } else {
-          const double y = (v - P.mx) / 10 + lsh;
-          if (y > thr10 + 1e-9) nz = true;
-          else if (y < thr10 - 1e-9) nz = false;
-          else return false;
-        }
-      } else {
-        const int64_t block = i / D + 1, gg = i % D;
-        const double a = block >= 2 ? r0[block - 2] : 0.0, b = block - 1 < H ? r0[block - 1] : 0.0;
-        const double val = a * ml[(gg - 1) * ncol + g] + b * ml[(nSub - gg) * ncol + g];
-        if (std::isnan(val) || std::fabs(val - J.t01) <= 1e-12 * J.t01) return false;
-        nz = val >= J.t01;
-      }
-      if (nz) { keep[i] = 1; last = (int32_t)i; }
+  // element (i, g) nonzero? 0 / 1, or -1: too close to the threshold to decide for the device
+  auto nz_at = [&](int64_t i, int64_t g) -> int {
+    if (i % D == 0) {
+      const int64_t h = i / D - 1;
+      double v;
+      if (h >= H || !roll_db(S.cols[g0 + g], J, lg, (int)h, &v)) return 0;
+      const double y = (v - S.cols[g0 + g].mx) / 10 + (S.lsh.empty() ? 0.0 : S.lsh[g0 + g]);
+      if (y > thr10 + 1e-9) return 1;
+      if (y < thr10 - 1e-9) return 0;
+      return -1;
     }
-    m.lnz[g] = last;
+    const int64_t block = i / D + 1, gg = i % D;
+    const double a = block >= 2 ? r0[block - 2] : 0.0, b = block - 1 < H ? r0[block - 1] : 0.0;
+    const double val = a * ml[(gg - 1) * ncol + g] + b * ml[(nSub - gg) * ncol + g];
+    if (std::isnan(val) || std::fabs(val - J.t01) <= 1e-12 * J.t01) return -1;
+    return val >= J.t01 ? 1 : 0;
+  };
+  // bounds that decide whole rows at once: harmonic rows at or above every
+  // cycle's last finite rolloff row, sideband rows whose end points times the
+  // largest weights stay clearly under the threshold
+  int64_t hmax = 0;
+  for (int64_t g = 0; g < ncol; ++g) hmax = std::max<int64_t>(hmax, lf[g0 + g]);
+  vec mlmax((size_t)nSub, 0.0);
+  for (int64_t q = 0; q < nSub; ++q)
+    for (int64_t g = 0; g < ncol; ++g) mlmax[q] = std::max(mlmax[q], ml[q * ncol + g]);
+  auto row_zero = [&](int64_t i) -> bool {
+    if (i % D == 0) return i / D - 1 >= std::min<int64_t>(H, hmax);
+    const int64_t block = i / D + 1, gg = i % D;
+    const double a = block >= 2 ? r0[block - 2] : 0.0, b = block - 1 < H ? r0[block - 1] : 0.0;
+    return a * mlmax[gg - 1] + b * mlmax[nSub - gg] < J.t01 * (1 - 1e-9);
+  };
+  // per cycle: the last nonzero rank (scan down from the top possible row)
+  m.lnz.assign((size_t)ncol, 0);
+  const int64_t itop = std::min<int64_t>(nr - 1, (std::min<int64_t>(H, hmax) + 1) * D);
+  for (int64_t g = 0; g < ncol; ++g)
+    for (int64_t i = itop; i > 0; --i) {
+      if (row_zero(i)) continue;
+      const int z = nz_at(i, g);
+      if (z < 0) return false;
+      if (z) { m.lnz[g] = (int32_t)i; break; }
+    }
+  // kept rows (rowSums > 0): any cycle nonzero
+  std::vector<char> keep((size_t)nr, 0);
+  for (int64_t i = 1; i <= itop; ++i) {
+    if (row_zero(i)) continue;
+    for (int64_t g = 0; g < ncol; ++g) {
+      const int z = nz_at(i, g);
+      if (z < 0) return false;
+      if (z) { keep[i] = 1; break; }
+    }
   }
   int64_t R = 0;
   for (int64_t i = nr - 1; i > 0 && !R; --i) if (keep[i]) R = i;
@@ -1008,7 +1030,7 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
       mats.emplace_back();
       if (e.nsub == 0) {
         plain_spec(spec, H, e.g0, e.g1, lastf, mats.back());
-      } else if (!fry_spec(spec, H, e.g0, e.g1, e.nsub, mats.back())) {
+      } else if (!fry_spec(spec, H, e.g0, e.g1, e.nsub, lastf, mats.back())) {
         dev_amps = false;  // a threshold call too close to decide for the device: host path
         break;
       }

@@ -241,12 +241,22 @@ static IstftGeom istft_geom(int wl, int64_t nc, double ovlp) {
   IstftGeom g;
   g.h = (double)wl * (100 - ovlp) / 100;
   g.xlen = (int64_t)((double)wl + (double)(nc - 1) * g.h);  // numeric(xlen) truncates
-  long double W0 = 0;
-  for (int i = 0; i < wl; ++i) {
-    const double w = 0.5 - 0.5 * std::cos(2 * M_PI * (double)i / (double)(wl - 1));
-    W0 += w * w;
+  // sum(hanning(wl)^2) depends on wl alone: once per window length and thread
+  thread_local std::vector<std::pair<int, double>> w0_memo;
+  double W0d = -1;
+  for (const auto& e : w0_memo)
+    if (e.first == wl) { W0d = e.second; break; }
+  if (W0d < 0) {
+    long double W0 = 0;
+    for (int i = 0; i < wl; ++i) {
+      const double w = 0.5 - 0.5 * std::cos(2 * M_PI * (double)i / (double)(wl - 1));
+      W0 += w * w;
+    }
+    W0d = (double)W0;
+    if (w0_memo.size() >= 64) w0_memo.erase(w0_memo.begin());
+    w0_memo.emplace_back(wl, W0d);
   }
-  g.scale = (float)(g.h / (double)W0);
+  g.scale = (float)(g.h / W0d);
   return g;
 }
 
