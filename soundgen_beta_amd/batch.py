@@ -23,6 +23,7 @@ class Marshalled:
         n = self.n = len(calls)
         descs = (_abi.sg_call_desc * max(n, 1))()
         args = (_abi.sg_soundgen_args * max(n, 1))()
+        scal = rargs.scalar_view(args, max(n, 1))
         self._structs = [args]
         for i, c in enumerate(calls):
             d = descs[i]
@@ -38,7 +39,7 @@ class Marshalled:
                 d.amplAnchors = self.holder.anchors(rargs.as_anchors(c.get("amplAnchors")))
             else:
                 d.kind = _abi.SG_CALL_SOUNDGEN
-                rargs.fill_soundgen_args(self.holder, c.get("args", {}), out=args[i])
+                rargs.fill_soundgen_args(self.holder, c.get("args", {}), out=args[i], scalars=scal, i=i)
                 d.args = C.pointer(args[i])
         self.descs = descs
 

@@ -205,6 +205,14 @@ class Holder:
         self._amemo = {}  # anchors by value: one pair of buffers per distinct anchor set
         self._rmemo = {}  # injected draw arrays by identity (a batch often shares one stream)
 
+    def max_lengths_of(self, x):
+        """r_max_lengths(x), once per string or (live) object."""
+        key = ("L", x) if isinstance(x, str) or x is None else ("Lo", id(x))
+        hit = self._fmemo.get(key)
+        if hit is None:
+            hit = self._fmemo[key] = (r_max_lengths(x), x)
+        return hit[0]
+
     def formants_of(self, x):
         """sg_formants of an R formants argument (vowel string, formant lists or NA);
         the same string or the same (live) object is converted once per Holder."""
@@ -231,18 +239,22 @@ class Holder:
         else:
             key = ("s", x if not (isinstance(x, float) and math.isnan(x)) else "NA", time_to)
         hit = self._amemo.get(key)
-        if hit is None:
-            an = as_anchors(x, time_to=time_to)
-            if an is None:
-                hit = (0, None, None)
+        if hit is None:  # one sg_anchors per distinct value; assigning it into a struct copies it
+            hit = _abi.sg_anchors()
+            if key[0] == "d" and len(key[1]) == len(key[2]) and key[1]:
+                # time and value in one buffer; the pointers keep it alive
+                a = np.array(key[1] + key[2], dtype=np.float64)
+                n = len(key[1])
+                hit.n = n
+                hit.time = _abi.C.pointer(_abi.C.c_double.from_buffer(a))
+                hit.value = _abi.C.pointer(_abi.C.c_double.from_buffer(a, 8 * n))
             else:
-                t, v = self.arr(an[0]), self.arr(an[1])
-                hit = (len(t), _abi.dptr(t), _abi.dptr(v))
+                an = as_anchors(x, time_to=time_to)
+                if an is not None:
+                    t, v = self.arr(an[0]), self.arr(an[1])
+                    hit.n, hit.time, hit.value = len(t), _abi.dptr(t), _abi.dptr(v)
             self._amemo[key] = hit
-        s = _abi.sg_anchors()
-        if hit[0]:
-            s.n, s.time, s.value = hit
-        return s
+        return hit
 
     def anchors(self, an):
         if an is None:
@@ -303,7 +315,7 @@ class Holder:
 
 def resolve_soundgen_kwargs(kw):
     """Fill soundgen() defaults for missing args; returns a plain dict."""
-    unknown = set(kw) - set(SOUNDGEN_DEFAULTS)
+    unknown = kw.keys() - SOUNDGEN_DEFAULTS.keys()
     if unknown:
         raise TypeError("soundgen(): unused argument(s) %s" % sorted(unknown))
     a = dict(SOUNDGEN_DEFAULTS)
@@ -331,15 +343,24 @@ def _scalar(v):
     return float(v)
 
 
-def fill_soundgen_args(h, kw, out=None):
+def scalar_view(args_array, n):
+    """Structured numpy view of the scalar fields of a ctypes sg_soundgen_args array
+    (fill_soundgen_args writes a call's scalars with one store into it)."""
+    return np.frombuffer(args_array, dtype=_SG_SCALAR_DT, count=n)
+
+
+def fill_soundgen_args(h, kw, out=None, scalars=None, i=0):
     """kwargs (R names) -> sg_soundgen_args (buffers kept alive by h); fills `out`
-    in place when given."""
+    in place when given (scalars: scalar_view of the array `out` belongs to, i:
+    its index there)."""
     a = resolve_soundgen_kwargs(kw)
     s = _abi.sg_soundgen_args() if out is None else out
     vals = tuple(map(a.__getitem__, _SG_SCALARS))
     if None in vals or "NA" in vals:
         vals = tuple(map(_scalar, vals))
-    np.frombuffer(s, dtype=_SG_SCALAR_DT, count=1)[0] = vals
+    if scalars is None:
+        scalars, i = np.frombuffer(s, dtype=_SG_SCALAR_DT, count=1), 0
+    scalars[i] = vals
     te = a["tempEffects"]
     s.tempEffects = (C_double8())(*[float(te[k]) for k in TEMP_EFFECTS_ORDER])
     s.pitchAnchors = h.anchors_of(a["pitchAnchors"])
@@ -350,7 +371,7 @@ def fill_soundgen_args(h, kw, out=None):
     s.noiseAnchors = h.anchors_of(a["noiseAnchors"], time_to=a["sylLen"])
     s.formants = h.formants_of(a["formants"])
     s.formantsNoise = h.formants_of(a["formantsNoise"])
-    s.formantsNoise_rlen = r_max_lengths(a["formantsNoise"])
+    s.formantsNoise_rlen = h.max_lengths_of(a["formantsNoise"])
     s.invalidArgAction = _ACTIONS[a["invalidArgAction"]]
     return s
 
