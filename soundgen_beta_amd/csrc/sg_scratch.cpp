@@ -10,6 +10,8 @@
 #include <sys/mman.h>
 
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -95,17 +97,76 @@ void scratch_free(void* q, size_t bytes) noexcept {
   }
 }
 
+// Freed bulk blocks are kept for the next plan (up to SG_HOST_CACHE_MB, default
+// 8192): a plan's host arrays are GBs, freed once uploaded, and the next plan
+// of a batch asks for blocks of about the same sizes; reusing resident pages
+// skips the page faults and the kernel's zeroing of fresh ones. Blocks are
+// sized in classes of 1/16 of a power of two (<= 6.25 % slack), so a freed
+// block serves any request of its class.
+namespace {
+constexpr size_t HUGE_PAGE = size_t(2) << 20;
+size_t bulk_class(size_t bytes) {
+  size_t sz = (bytes + HUGE_PAGE - 1) / HUGE_PAGE * HUGE_PAGE;
+  int top = 63 - __builtin_clzll(sz);
+  const size_t step = top > 4 ? size_t(1) << (top - 4) : 1;
+  sz = (sz + step - 1) / step * step;
+  return (sz + HUGE_PAGE - 1) / HUGE_PAGE * HUGE_PAGE;
+}
+struct BulkCache {
+  std::mutex mu;
+  std::multimap<size_t, void*> blocks;
+  size_t bytes = 0;
+  const size_t cap = [] {
+    const char* e = std::getenv("SG_HOST_CACHE_MB");
+    return (size_t)(e ? std::atoll(e) : 8192) << 20;
+  }();
+  ~BulkCache() {
+    for (auto& b : blocks) std::free(b.second);
+  }
+};
+BulkCache& bulk_cache() {
+  static BulkCache* c = new BulkCache();  // never destroyed: frees may run on detached threads at exit
+  return *c;
+}
+}  // namespace
+
 void* bulk_alloc(size_t bytes) {
-  constexpr size_t HUGE = size_t(2) << 20;
-  const size_t sz = (bytes + HUGE - 1) / HUGE * HUGE;
-  void* q = std::aligned_alloc(HUGE, sz);
+  const size_t sz = bulk_class(bytes);
+  {
+    BulkCache& c = bulk_cache();
+    std::lock_guard<std::mutex> g(c.mu);
+    auto it = c.blocks.find(sz);
+    if (it != c.blocks.end()) {
+      void* q = it->second;
+      c.blocks.erase(it);
+      c.bytes -= sz;
+      return q;
+    }
+  }
+  void* q = std::aligned_alloc(HUGE_PAGE, sz);
   if (!q) throw std::bad_alloc();
   static const bool no_thp = std::getenv("SG_NO_THP") != nullptr;  // experiment knob
   if (!no_thp) (void)madvise(q, sz, MADV_HUGEPAGE);  // advisory: 4 KB pages when THP is off
   return q;
 }
 
-void bulk_free(void* q, size_t) noexcept { std::free(q); }
+void bulk_free(void* q, size_t bytes) noexcept {
+  if (!q) return;
+  const size_t sz = bulk_class(bytes);
+  BulkCache& c = bulk_cache();
+  {
+    std::lock_guard<std::mutex> g(c.mu);
+    if (c.bytes + sz <= c.cap) {
+      try {
+        c.blocks.emplace(sz, q);
+        c.bytes += sz;
+        return;
+      } catch (...) {
+      }
+    }
+  }
+  std::free(q);
+}
 
 void scratch_trim() noexcept {
   if (slot.p) slot.p->clear();
