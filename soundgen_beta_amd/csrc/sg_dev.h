@@ -228,7 +228,7 @@ constexpr int SG_FFT_DFT = 2;   // M with a prime factor > 31: Bluestein (SgCdft
 constexpr int SG_FFT_ODD = 3;
 constexpr int SG_WAVE_STATE = 24;  // complex butterfly points a lane holds per stage in sg_stft_ola
 #ifndef SG_FFT_WAVES_N
-#define SG_FFT_WAVES_N 12  // build knob: 3 waves per SIMD at <= 168 VGPRs (round 3; 8 before)
+#define SG_FFT_WAVES_N 8  // build knob
 #endif
 constexpr int SG_FFT_WAVES = SG_FFT_WAVES_N;    // wavefronts (segments) per sg_stft_ola workgroup: one workgroup per CU
 #ifndef SG_FFT_WAVES_NOISE_N

@@ -22,7 +22,7 @@
 
 #include "sg_dev.h"
 #ifndef SG_FFT_WPE
-#define SG_FFT_WPE (SG_FFT_WAVES_N > 8 ? 3 : 2)  // waves per SIMD for sg_stft_ola
+#define SG_FFT_WPE 2  // build knob: waves per SIMD for sg_stft_ola
 #endif
 #ifndef SG_FFT_WPE_NOISE
 #define SG_FFT_WPE_NOISE (SG_FFT_WAVES_NOISE_N > 8 ? 3 : 2)  // waves per SIMD for sg_stft_ola_noise
@@ -636,10 +636,10 @@ extern "C" __global__ __launch_bounds__(SG_FFT_THREADS) void sg_fft_frames(
 }
 
 // ------------------------------------------------ fused frame pipeline
-// Inputs of one frame, loaded into registers before its transform:
-//   FILTER: s[i] = sound (y[2n], y[2n+1]), n = 64 i + lane; the envelope column
-//           (envp) is read where the untangle uses it: held in registers across the
-//           forward FFT it kept the filter kernel at 2 waves per SIMD
+// Inputs of one frame, prefetched into registers one frame ahead (their HBM
+// latency overlaps the previous frame's inverse FFT and overlap-add):
+//   FILTER: s[i] = sound (y[2n], y[2n+1]), n = 64 i + lane; a[i] = envelope
+//           (env[k], env[M - k]) with k = 64 i + lane (k = 0: env[0], env[M-1]); xh = env[half]
 //   NOISE:  a[i] = uniforms (u[k], u[M - k]), b[i] = filter (f[k], f[M - k]) (k = 0: M - 1); xh, xh2 at half
 // NOISE's filter pairs share the FILTER sound registers (b[i] = s[i]): the mode is
 // wave-uniform but not a compile-time constant, so separate arrays would both be allocated
@@ -648,7 +648,6 @@ struct FramePf {
   float2 s[SG_PF_SRC];
   float2 a[SG_PF_PAIR];
   float xh, xh2;
-  const float* envp;  // FILTER: the frame's envelope column (env[k], k < M)
   __device__ __forceinline__ float2& b(int i) { return s[i]; }
   __device__ __forceinline__ const float2& b(int i) const { return s[i]; }
 };
@@ -664,7 +663,12 @@ __device__ __forceinline__ void frame_prefetch(FramePf& P, const SgFrame& F, int
       const int n = 64 * i + lane;
       if (n < M) P.s[i] = make_float2(src[2 * n], src[2 * n + 1]);
     }
-    P.envp = env;
+#pragma unroll
+    for (int i = 0; i < SG_PF_PAIR; ++i) {
+      const int k = 64 * i + lane;
+      if (k <= half) P.a[i] = make_float2(env[k], env[k == 0 ? M - 1 : M - k]);
+    }
+    P.xh = env[half];
   } else {
     const float* u = fl + F.src;
     const float* flt = fl + F.env;
@@ -731,7 +735,7 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
         const float2 o = make_float2(0.5f * dd.y, -0.5f * dd.x);
         return cadd(e, cmul(o, twN[t]));
       };
-      const float ek = P.envp[kk] * invN, em = P.envp[kk == 0 ? M - 1 : km] * invN;  // k = 0: env[0], env[M - 1]
+      const float ek = P.a[i].x * invN, em = P.a[i].y * invN;  // k = 0: env[0], env[M - 1]
       if (kk == 0) {
         const float2 x0 = X_at(za, za, 0), xl = X_at(zM1, z1, M - 1);
         const float y0 = x0.x * ek;
@@ -739,7 +743,7 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
         A[0] = make_float2(y0 + nyq, y0 - nyq);
         if (M % 2 == 0) {
           const float2 xk = X_at(zh, zh, half);
-          const float eh = P.envp[half] * invN;
+          const float eh = P.xh * invN;
           const float2 yk = make_float2(xk.x * eh, xk.y * eh);
           float2 a, b;
           pack_pair(yk, yk, twN[half], a, b);
@@ -799,9 +803,8 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
                                              const SgFrame* __restrict__ frames, const SgFftGeom& g,
                                              const float* __restrict__ fl, float* __restrict__ fs,
                                              float* __restrict__ slotmax, float2* twS, const float2* twN,
-                                             const float* ham, const float* han, int w, int lane0) {
+                                             const float* ham, const float* han, int w, int lane) {
   const int M = CM ? CM : g.M, N = CM ? 2 * CM : g.wl;
-  int lane = lane0;
   const int mode = MODE;  // the launch's phase fixes it (noise: phase 0, filter: phase 1)
   const SgOla& O = olas[S.ola];
   float2* A = twS + M * (4 + w);
@@ -833,10 +836,6 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
   }
 #endif
   for (int k = 0; k < S.nf; ++k) {
-    // lane-derived LDS addresses and masks are recomputed per frame: hoisted out of the
-    // frame loop they held ~50 VGPRs (3 waves per SIMD need <= 168)
-    lane = lane0;
-    __asm__ __volatile__("" : "+v"(lane));
 #if !SG_PF_AHEAD
     {
       int Mk = M;
