@@ -302,6 +302,14 @@ int sg_formant_filter(sg_ctx* ctx, const double* sound, int64_t len,
                       const double* env, int32_t env_nc,
                       int32_t windowLength_points, double overlap,
                       double* out, int64_t cap, int64_t* out_len);
+/* getSmoothContour(anchors, len, thisIsPitch, method, valueFloor,
+ * valueCeiling, samplingRate)  R/smoothContours.R:53-227 (exported,
+ * NAMESPACE:10); method 0 = 'loess' (R's default), 1 = 'spline'. The
+ * planner's own contour (host, fp64). out holds len doubles; *out_len = 0 when
+ * R returns NA (no anchors, len 0). */
+int sg_get_smooth_contour(sg_anchors anchors, int64_t len, int32_t thisIsPitch, int32_t method, int32_t has_floor,
+                          double valueFloor, int32_t has_ceil, double valueCeiling, double samplingRate, double* out,
+                          int64_t* out_len);
 /* getRolloff() (host helper; R returns H x nGC). out cap = nHarmonics*nGC.
  * rolloffParabCeiling NaN = NULL (R/sourceSpectrum.R:77, :105-107). */
 int sg_get_rolloff(const double* pitch_per_gc, int32_t n_gc,

@@ -148,3 +148,111 @@ def getRolloff(pitch_per_gc=(440,), nHarmonics=100, rolloff=-12, rolloffOct=-2, 
     native.check(rc)
     H = rows.value
     return out[:H * len(p)].reshape(len(p), H).T.copy()
+
+
+def getSmoothContour(anchors=None, len=None, thisIsPitch=False, method="loess", valueFloor=None,
+                     valueCeiling=None, samplingRate=16000):
+    """getSmoothContour() — R/smoothContours.R:53-227 (exported; host helper through the
+    planner's own contour code). anchors: {"time": ..., "value": ...}, a numeric vector
+    (time spread over 0..1), or NA/None. len None: anchors' time is the duration in ms
+    and len = floor(duration_ms * samplingRate / 1000) (R/smoothContours.R:92-96; the
+    times are then normalised like a given len, which can differ from R by rounding).
+    Returns a float64 array, or None where R returns NA."""
+    an = rargs.as_anchors(anchors)
+    if an is None:
+        return None
+    t, v = an
+    if len is None:
+        len = int(np.floor((np.max(t) - np.min(t)) * samplingRate / 1000))
+    len = int(len)
+    if len <= 0:
+        return None
+    h = rargs.Holder()
+    s = h.anchors(an)
+    out = np.zeros(len)
+    n = C.c_int64()
+    L = native.lib()
+    rc = L.sg_get_smooth_contour(s, len, int(bool(thisIsPitch)), 1 if method == "spline" else 0,
+                                 int(valueFloor is not None), float(valueFloor or 0.0),
+                                 int(valueCeiling is not None), float(valueCeiling or 0.0), float(samplingRate),
+                                 _abi.dptr(out), C.byref(n))
+    native.check(rc)
+    return out[:n.value].copy() if n.value else None
+
+
+def findZeroCrossing(ampl, location):
+    """findZeroCrossing(ampl, location) — R/utilities_soundgen.R:255-295: the index
+    (1-based) of the upward zero crossing nearest to `location`, None for NA."""
+    a = np.asarray(ampl, dtype=np.float64)
+    n = a.size
+    location = int(location)
+    if n < 1 or location < 1 or location > n:
+        return None
+    if n == 1 and location == 1:
+        return location
+    zl = zr = None
+    i = location
+    if location > 1:
+        while i > 1:
+            if a[i - 1] > 0 and a[i - 2] < 0:
+                zl = i - 1
+                break
+            i -= 1
+    if location < n:
+        i = location
+    while i < n - 1:  # R: i keeps the left search's value when location == len
+        if a[i] > 0 and a[i - 1] < 0:
+            zr = i
+            break
+        i += 1
+    if zl is None and zr is None:
+        return None
+    if zl is None:
+        return zr
+    if zr is None:
+        return zl
+    return zl if abs(zl - location) <= abs(zr - location) else zr
+
+
+def crossFade(ampl1, ampl2, samplingRate, crossLen=15, crossLenPoints=None):
+    """crossFade() — R/utilities_soundgen.R:328-375: both waveforms cut at their zero
+    crossings, then joined by a linear cross-fade over crossLenPoints samples."""
+    a1 = np.asarray(ampl1, dtype=np.float64)
+    a2 = np.asarray(ampl2, dtype=np.float64)
+    zc1 = findZeroCrossing(a1, a1.size)
+    if zc1 is not None:
+        a1 = np.concatenate([a1[:zc1], [0.0]])
+    zc2 = findZeroCrossing(a2, 1)
+    if zc2 is not None:
+        a2 = a2[zc2:]
+    if crossLenPoints is None:
+        cl = min(np.floor(crossLen * samplingRate / 1000), a1.size - 1, a2.size - 1)
+    else:
+        cl = min(crossLenPoints, a1.size - 1, a2.size - 1)
+    if cl < 2:
+        return np.concatenate([a1, a2])
+    cl = int(cl)
+    # seq(0, 1, length.out = cl) as R computes it
+    multipl = np.arange(cl, dtype=np.float64) * (1.0 / (cl - 1))
+    multipl[-1] = 1.0
+    idx1 = a1.size - cl
+    cross = multipl[::-1] * a1[idx1:] + multipl * a2[:cl]
+    return np.concatenate([a1[:idx1], cross, a2[cl:]])
+
+
+def addVectors(v1, v2, insertionPoint):
+    """addVectors() — R/utilities_math.R:500-525 (exported): v2 added into v1 from
+    index insertionPoint (1-based, may be <= 0), both zero-padded, NA as 0."""
+    a = np.nan_to_num(np.asarray(v1, dtype=np.float64), nan=0.0)
+    b = np.nan_to_num(np.asarray(v2, dtype=np.float64), nan=0.0)
+    ip = int(insertionPoint)
+    if ip > 1:
+        b = np.concatenate([np.zeros(ip), b])
+    elif ip < 1:
+        a = np.concatenate([np.zeros(1 - ip), a])
+    d = b.size - a.size
+    if d > 0:
+        a = np.concatenate([a, np.zeros(d)])
+    elif d < 0:
+        b = np.concatenate([b, np.zeros(-d)])
+    return a + b

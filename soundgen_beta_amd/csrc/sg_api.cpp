@@ -1006,6 +1006,22 @@ int sg_wav_write(const char* path, const int16_t* pcm, int64_t n, int32_t sampli
   return std::fclose(f) == 0 && ok ? SG_OK : SG_E_ARG;
 }
 
+int sg_get_smooth_contour(sg_anchors anchors, int64_t len, int32_t thisIsPitch, int32_t method, int32_t has_floor,
+                          double valueFloor, int32_t has_ceil, double valueCeiling, double samplingRate, double* out,
+                          int64_t* out_len) {
+  return guarded(nullptr, [&]() {
+    if (!out_len || len < 0 || (len > 0 && !out)) throw sg::SgError(SG_E_ARG, "sg_get_smooth_contour: arguments");
+    sg::vec v;
+    *out_len = 0;
+    if (!sg::smooth_contour(anchors, len, thisIsPitch != 0, method, has_floor != 0, valueFloor, has_ceil != 0,
+                            valueCeiling, v, samplingRate))
+      return SG_OK;  // NA anchors or len 0: R returns NA
+    std::memcpy(out, v.data(), v.size() * sizeof(double));
+    *out_len = (int64_t)v.size();
+    return SG_OK;
+  });
+}
+
 int sg_get_rolloff(const double* pitch_per_gc, int32_t n_gc, int32_t nHarmonics, double rolloff, double rolloffOct,
                    double rolloffParab, double rolloffParabHarm, double rolloffParabCeiling, double rolloffKHz,
                    double baseline, double throwaway, double samplingRate, double* out, int32_t* out_rows) {
