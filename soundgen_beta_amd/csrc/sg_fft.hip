@@ -1113,10 +1113,14 @@ __device__ __forceinline__ double2 cmul64(double2 a, double2 b) {
   return make_double2(fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x));
 }
 __device__ __forceinline__ double2 conj_if(double2 w, bool c) { return c ? make_double2(w.x, -w.y) : w; }
-// one radix-R stage of an M-point frame, src -> dst; TN = W_N^t, t < N = 2M; rt = W_R^t
-template <int R>
-__device__ void stage64(double2* __restrict__ src, double2* __restrict__ dst, int M, int Ns,
+// one radix-R stage of an M-point frame, src -> dst; TN = W_N^t, t < N = 2M; rt = W_R^t.
+// CM, CNS > 0: frame size and stage stride as compile-time constants (the dominant
+// geometry, M = 1102 = 2 x 19 x 29): every division and modulo folds to shifts and
+// multiplies, the odd butterflies' root index steps by k instead of (m k) mod R.
+template <int R, int CM = 0, int CNS = 0>
+__device__ void stage64(double2* __restrict__ src, double2* __restrict__ dst, int M_, int Ns_,
                         const double2* __restrict__ TN, const double2* __restrict__ rt, bool inv) {
+  const int M = CM ? CM : M_, Ns = CNS ? CNS : Ns_;
   const int nR = M / R, tstep2 = 2 * (M / (Ns * R));  // W_{Ns R}^e = W_N^(2 e M / (Ns R))
   if (Ns > 1) {  // (a) input j + r nR of butterfly j times W_{Ns R}^(r (j mod Ns)), in place
     for (int q = threadIdx.x; q < M; q += SG_F64_THREADS) {
@@ -1156,10 +1160,13 @@ __device__ void stage64(double2* __restrict__ src, double2* __restrict__ dst, in
       double2* y = dst + (j - jm) * R + jm;
       const double2 x0 = x[0];
       double2 P = make_double2(0.0, 0.0), Q = make_double2(0.0, 0.0);
-#pragma unroll 1
+      int t = 0;  // (m k) mod R
+#pragma unroll 2
       for (int m = 1; m <= H; ++m) {
+        t += k;
+        if (t >= R) t -= R;
         const double2 u = x[m * nR], v = x[(R - m) * nR];
-        const double2 w = k == 0 ? make_double2(1.0, 0.0) : rt[(m * k) % R];  // (cos, -sin) of 2 pi m k / R
+        const double2 w = k == 0 ? make_double2(1.0, 0.0) : rt[t];  // (cos, -sin) of 2 pi m k / R
         P.x = fma(u.x + v.x, w.x, P.x);
         P.y = fma(u.y + v.y, w.x, P.y);
         Q.x = fma(u.x - v.x, -w.y, Q.x);
@@ -1180,6 +1187,17 @@ __device__ void stage64(double2* __restrict__ src, double2* __restrict__ dst, in
 // M-point complex DFT of *a (result in *a, *b scratch); TN: W_N^t (t < 2M), global; rt: LDS (32)
 __device__ void fft64(double2*& a, double2*& b, int M, const double2* __restrict__ TN,
                                    double2* __restrict__ rt, bool inv) {
+  if (M == 1102) {  // 2 x 19 x 29, the stage order of the loop below, sizes folded
+    stage64<2, 1102, 1>(a, b, M, 1, TN, rt, inv);
+    if (threadIdx.x < 19) rt[threadIdx.x] = TN[threadIdx.x * (2 * 1102 / 19)];
+    __syncthreads();
+    stage64<19, 1102, 2>(b, a, M, 2, TN, rt, inv);  // ends with a barrier: its root reads are done
+    if (threadIdx.x < 29) rt[threadIdx.x] = TN[threadIdx.x * (2 * 1102 / 29)];
+    __syncthreads();
+    stage64<29, 1102, 38>(a, b, M, 38, TN, rt, inv);
+    double2* t = a; a = b; b = t;  // three stages: the result is in b -> swap as the loop does
+    return;
+  }
   int rest = M, Ns = 1;
   while (rest > 1) {
     int R = rest % 4 == 0 ? 4 : rest % 2 == 0 ? 2 : 0;
@@ -1204,16 +1222,23 @@ __device__ void fft64(double2*& a, double2*& b, int M, const double2* __restrict
 }
 }  // namespace
 
-// W_N^t = exp(-2 pi i t / N), t < N, for every window length of the plan's fp64 frames
+// Per window length N = 2M of the plan's fp64 frames: W_N^t = exp(-2 pi i t / N), t < N,
+// then seewave's hamming and hanning (ftwindow) as pairs (w[2n], w[2n + 1]), n < M
 extern "C" __global__ __launch_bounds__(256) void sg_roots64(const int32_t* __restrict__ wls,
                                                              const int64_t* __restrict__ offs,
                                                              double2* __restrict__ tabs) {
-  const int N = wls[blockIdx.y];
+  const int N = wls[blockIdx.y], M = N / 2;
   double2* T = tabs + offs[blockIdx.y];
+  const double wd = (double)(N - 1);
   for (int t = blockIdx.x * 256 + threadIdx.x; t < N; t += gridDim.x * 256) {
     double sn, cs;
     sincospi(-2.0 * (double)t / (double)N, &sn, &cs);
     T[t] = make_double2(cs, sn);
+  }
+  for (int n = blockIdx.x * 256 + threadIdx.x; n < M; n += gridDim.x * 256) {
+    const double c0 = cospi(2.0 * (double)(2 * n) / wd), c1 = cospi(2.0 * (double)(2 * n + 1) / wd);
+    T[N + n] = make_double2(0.54 - 0.46 * c0, 0.54 - 0.46 * c1);
+    T[N + M + n] = make_double2(0.5 - 0.5 * c0, 0.5 - 0.5 * c1);
   }
 }
 
@@ -1227,12 +1252,12 @@ extern "C" __global__ __launch_bounds__(SG_F64_THREADS) void sg_fft_frames64(
   double2* a = lds64;        // M points
   double2* b = a + M;        // M points
   double2* rt = b + M;       // radix roots (<= 31)
-  const double wd = (double)(N - 1);
+  const double2* __restrict__ ham = TN + N;  // window pairs (sg_roots64)
+  const double2* __restrict__ han = ham + M;
   const double* x = fh + F.src;
   for (int n = threadIdx.x; n < M; n += SG_F64_THREADS) {  // hamming (seewave ftwindow), packed pairs
-    const double h0 = 0.54 - 0.46 * cospi(2.0 * (double)(2 * n) / wd);
-    const double h1 = 0.54 - 0.46 * cospi(2.0 * (double)(2 * n + 1) / wd);
-    a[n] = make_double2(x[2 * n] * h0, x[2 * n + 1] * h1);
+    const double2 h = ham[n];
+    a[n] = make_double2(x[2 * n] * h.x, x[2 * n + 1] * h.y);
   }
   __syncthreads();
   fft64(a, b, M, TN, rt, false);
@@ -1262,10 +1287,9 @@ extern "C" __global__ __launch_bounds__(SG_F64_THREADS) void sg_fft_frames64(
   fft64(c, d, M, TN, rt, true);
   float* out = fs + F.dst;
   for (int n = threadIdx.x; n < M; n += SG_F64_THREADS) {
-    const double h0 = 0.5 - 0.5 * cospi(2.0 * (double)(2 * n) / wd);
-    const double h1 = 0.5 - 0.5 * cospi(2.0 * (double)(2 * n + 1) / wd);
-    out[2 * n] = (float)(c[n].x * invN * h0);
-    out[2 * n + 1] = (float)(c[n].y * invN * h1);
+    const double2 h = han[n];
+    out[2 * n] = (float)(c[n].x * invN * h.x);
+    out[2 * n + 1] = (float)(c[n].y * invN * h.y);
   }
 }
 

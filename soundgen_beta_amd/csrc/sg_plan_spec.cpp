@@ -686,7 +686,7 @@ void finalize_spec(Batch& B) {
     if (w == B.roots64_wl.size()) {
       B.roots64_wl.push_back(f.wl);
       B.roots64_off.push_back(B.roots64_total);
-      B.roots64_total += f.wl;
+      B.roots64_total += 2 * (int64_t)f.wl;  // W_N^t (N), then the fp64 hamming and hanning pairs (M each)
     }
     B.frames64_tab.push_back(B.roots64_off[w]);
     B.frames64_maxwl = std::max(B.frames64_maxwl, f.wl);
