@@ -104,14 +104,18 @@ def c5_calls(n_calls):
     """C5: calls drawn uniformly from the 33 presets (R/presets.R:158-399,
     extracted to soundgen_beta_amd/presets.json); sylLen x U(0.5, 2) clamped to [20, 5000],
     pitch anchor values x 2^U(-0.5, 0.5), samplingRate 44100, addSilence 0, the
-    preset's own temperature. Random draws come from one shared pre-drawn stream
-    (every call reads it from the start; synthetic data)."""
+    preset's own temperature. Random draws: every call reads its own window of one
+    pre-drawn stream (a per-call offset from a second generator, so the call
+    parameters are those of earlier rounds; synthetic data)."""
     from soundgen_beta_amd import presets as P
     rng = _rng(5)
     names = P.names()
     base = {k: P.args(*k) for k in names}  # one copy per preset: calls share its formant lists
     Z = rng.standard_normal(200000)
     U = rng.uniform(size=4000000)
+    orng = _rng(55)  # window offsets: <= 100k of the 200k normals, <= 2M of the 4M uniforms
+    oz = orng.integers(0, 100000, size=n_calls)
+    ou = orng.integers(0, 2000000, size=n_calls)
     calls = []
     for i in range(n_calls):
         spk, nm = names[int(rng.integers(len(names)))]
@@ -125,7 +129,8 @@ def c5_calls(n_calls):
             a["pitchAnchors"] = {"time": pa["time"], "value": list(np.asarray(pa["value"], float) * f)}
         a["samplingRate"] = 44100
         a["addSilence"] = 0
-        calls.append({"kind": "soundgen", "args": a, "normals": Z, "uniforms": U, "preset": spk + "$" + nm})
+        calls.append({"kind": "soundgen", "args": a, "normals": Z[oz[i]:], "uniforms": U[ou[i]:],
+                      "preset": spk + "$" + nm})
     return calls
 
 
