@@ -294,8 +294,13 @@ class Holder:
         def buf(x):
             hit = self._rmemo.get(id(x))
             if hit is None or hit[0] is not x:
-                a = self.arr(x)
-                hit = self._rmemo[id(x)] = (x, _abi.dptr(a), len(a))
+                if type(x) is np.ndarray and x.dtype == np.float64 and x.flags.c_contiguous and x.flags.writeable:
+                    # a window of one stream (kept alive by the memo): pointer without a copy or a cast
+                    p, n = _abi.C.pointer(_abi.C.c_double.from_buffer(x)), x.shape[0]
+                else:
+                    a = self.arr(x)
+                    p, n = _abi.dptr(a), len(a)
+                hit = self._rmemo[id(x)] = (x, p, n)
             return hit[1], hit[2]
         if normals is not None:
             r.normals, r.n_normals = buf(normals)
