@@ -155,6 +155,29 @@ def test_c5_presets_one_batch(oracle):
     print("C5 worst rms", worst, "over", len(outs), "calls")
 
 
+def test_c5_1024_calls_spread_over_the_batch(oracle):
+    """1,024 calls spread over the 65,536-call C5 batch (every 64th, each reading its own
+    draw window) planned as one batch and compared with the oracle at RMS <= 1e-5 with
+    exact lengths; the oracle runs on a 16-thread pool (its ctypes calls release the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+    bench = _bench()
+    from soundgen_beta_amd import batch
+    calls = bench.c5_calls(65536)[::64]
+    outs = batch.synthesize(calls)
+    bad = [i for i, y in enumerate(outs) if isinstance(y, Exception)]
+    assert not bad, [(i, str(outs[i])) for i in bad[:5]]
+    with ThreadPoolExecutor(16) as ex:
+        refs = list(ex.map(lambda c: bench.oracle_call(oracle, c), calls))
+    worst, where = 0.0, None
+    for i, (y, ref) in enumerate(zip(outs, refs)):
+        assert len(y) == len(ref), (i, calls[i]["preset"])
+        r = _rms(y, ref)
+        if r > worst:
+            worst, where = r, calls[i]["preset"]
+        assert r <= TOL, (i, calls[i]["preset"], r)
+    print("C5 1024 calls: worst rms", worst, where)
+
+
 def _per_preset(bench, k):
     """The first k calls of each of the 33 presets in the C5 stream."""
     calls, seen = [], {}
