@@ -1110,7 +1110,10 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize(
   for (int q = 0; q < 4; ++q) finalize_tile(tl, pieces, syls, cknots, W, maxes, out_buf, fs, lenv, q, lkw);
 #else
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#pragma unroll 1
+#ifndef SG_FIN_UNROLL
+#define SG_FIN_UNROLL 1  // build knob: tiles of a workgroup unrolled (their descriptor chains may overlap)
+#endif
+#pragma unroll SG_FIN_UNROLL
   for (int i = 0; i < SG_FIN_TILES; ++i) {
     const int64_t t = (int64_t)blockIdx.x * SG_FIN_TILES + i;
     if (t >= ntiles) break;
