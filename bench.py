@@ -335,7 +335,8 @@ def main():
     failed = 0
     first_msg = None
     # chunk k + 1 plans on the host while chunk k uploads (batch.plan_uploaded)
-    for p, a in batch.plan_uploaded(mine, ctx, args.plan_chunk):
+    plan_stages = []
+    for p, a in batch.plan_uploaded(mine, ctx, args.plan_chunk, plan_stages):
         bad = np.nonzero(p.status)[0]
         failed += len(bad)
         if len(bad) and first_msg is None:
@@ -483,6 +484,7 @@ def main():
             "value_device_resident": (samples_all * args.device_steps / dt_dev) if dt_dev else None,
             "ms_per_step_device_resident": (dt_dev / args.device_steps * 1e3) if dt_dev else None,
             "plan_s": t_plan_max, "calls_gen_s": t_gen,
+            "plan_stages": [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in t.items()} for t in plan_stages],
             "value_incl_planning": samples_all / (t_plan_max + dt / args.steps),
             "rms_error_vs_oracle": max(rms) if rms else None,
             "roofline": roof,

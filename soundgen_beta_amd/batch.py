@@ -142,30 +142,51 @@ def execute_plans(ctx, plans, d_out_ptrs, stream_ptr=None):
                  ctx.ptr)
 
 
-def plan_uploaded(calls, ctx, chunk):
+def plan_uploaded(calls, ctx, chunk, timings=None):
     """Plan `calls` in chunks of `chunk` and upload each plan, yielding
     (plan, first call index) in order. A three-stage pipeline: while chunk k
     uploads (main thread), chunk k + 1 is planned natively and chunk k + 2 is
     marshalled (two workers). The native calls run without the GIL (ctypes), so
     only marshalling holds it. Each yielded plan is uploaded and its host arrays
-    released."""
+    released. `timings` (a list) receives per chunk the seconds of each stage and
+    the main thread's wait for the planner."""
+    import time
     from concurrent.futures import ThreadPoolExecutor
     starts = list(range(0, len(calls), chunk))
     if not starts:
         return
+    stage = {}
 
     def piece(i):
         return calls[starts[i]:starts[i] + chunk]
+
+    def marshal(i):
+        t = time.perf_counter()
+        m = Marshalled(piece(i))
+        stage[("marshal", i)] = time.perf_counter() - t
+        return m
+
+    def plan(i, m):
+        t = time.perf_counter()
+        p = Plan(None, ctx, m)
+        stage[("plan", i)] = time.perf_counter() - t
+        return p
     with ThreadPoolExecutor(2) as ex:
-        pfut = ex.submit(Plan, None, ctx, Marshalled(piece(0)))
-        mfut = ex.submit(Marshalled, piece(1)) if len(starts) > 1 else None
+        pfut = ex.submit(plan, 0, marshal(0))
+        mfut = ex.submit(marshal, 1) if len(starts) > 1 else None
         for i, a in enumerate(starts):
+            t0 = time.perf_counter()
             p = pfut.result()
             if mfut is not None:
-                pfut = ex.submit(Plan, None, ctx, mfut.result())
-                mfut = ex.submit(Marshalled, piece(i + 2)) if i + 2 < len(starts) else None
+                pfut = ex.submit(plan, i + 1, mfut.result())
+                mfut = ex.submit(marshal, i + 2) if i + 2 < len(starts) else None
+            t1 = time.perf_counter()
             p.upload()
             p.release_host()
+            t2 = time.perf_counter()
+            if timings is not None:
+                timings.append(dict(chunk=i, marshal_s=stage.get(("marshal", i)), plan_s=stage.get(("plan", i)),
+                                    wait_s=t1 - t0, upload_s=t2 - t1))
             yield p, a
 
 

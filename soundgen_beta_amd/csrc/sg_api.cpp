@@ -74,7 +74,7 @@ struct Checkpoint {
   size_t segs, epochs, knots, ampsrc, ampcols, ampjobs, tasks, pieces, syls, syl_tiles, cknots, fl, items;
   size_t frames[2], olas[2], mixes[2], copies, eterms, ecols, envjobs, frames64;
   int64_t amp_total, w_total, harm_samples, harm_terms, harm_amp_bytes, fft_frames, fs_total, fe_total, w64_total, fh_total,
-      hp_bouts;
+      hp_bouts, hp_noise_bouts;
   double fft_flops;
   explicit Checkpoint(const sg::Batch& B)
       : segs(B.segs.size()), epochs(B.epochs.size()), knots(B.knots.size()), ampsrc(B.ampsrc.size()),
@@ -84,7 +84,7 @@ struct Checkpoint {
         eterms(B.eterms.size()), ecols(B.ecols.size()), envjobs(B.envjobs.size()), amp_total(B.amp_total), w_total(B.w_total),
         harm_samples(B.harm_samples), harm_terms(B.harm_terms), harm_amp_bytes(B.harm_amp_bytes),
         fft_frames(B.fft_frames), fs_total(B.fs_total), fe_total(B.fe_total), w64_total(B.w64_total),
-        fh_total(B.fh_total), hp_bouts(B.hp_bouts), fft_flops(B.fft_flops) {
+        fh_total(B.fh_total), hp_bouts(B.hp_bouts), hp_noise_bouts(B.hp_noise_bouts), fft_flops(B.fft_flops) {
     frames64 = B.frames64.size();
     for (int p = 0; p < 2; ++p) { frames[p] = B.frames[p].size(); olas[p] = B.olas[p].size(); mixes[p] = B.mixes[p].size(); }
   }
@@ -101,6 +101,7 @@ struct Checkpoint {
     B.harm_amp_bytes = harm_amp_bytes; B.fft_frames = fft_frames; B.fs_total = fs_total;
     B.eterms.resize(eterms); B.ecols.resize(ecols); B.envjobs.resize(envjobs); B.fe_total = fe_total;
     B.frames64.resize(frames64); B.w64_total = w64_total; B.fh_total = fh_total; B.hp_bouts = hp_bouts;
+    B.hp_noise_bouts = hp_noise_bouts;
     B.fft_flops = fft_flops;
   }
 };
@@ -258,6 +259,7 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
     c.job += (int64_t)S.envjobs.size();
     c.w64 += S.w64_total; c.fh += S.fh_total; c.fr64 += (int64_t)S.frames64.size();
     D.hp_bouts += S.hp_bouts;
+    D.hp_noise_bouts += S.hp_noise_bouts;
     for (int ph = 0; ph < 2; ++ph) {
       c.fr[ph] += (int64_t)S.frames[ph].size(); c.ola[ph] += (int64_t)S.olas[ph].size();
       c.mix[ph] += (int64_t)S.mixes[ph].size();
@@ -345,7 +347,7 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
       }
     }
     for (auto& f : S.frames64) {
-      f.src += b.fh;
+      f.src += f.mode == SG_F64_NOISE ? b.fl : b.fh;  // uniforms (fl) / pre-filter sound (fh)
       f.env = f.env < 0 ? f.env - b.fe : f.env + b.fl;
       f.dst += b.fs;
     }
@@ -451,7 +453,11 @@ int sg_plan_batch(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, sg_pl
       plan_range(B, calls, 0, n_calls);
       g_growth.record(B, n_calls);
     } else {
-      const int64_t nchunk = std::min<int64_t>(n_calls, (int64_t)threads * 8);
+      static const int per_thread = [] {  // parts per thread (SG_PLAN_PARTS: experiments)
+        const char* e = std::getenv("SG_PLAN_PARTS");
+        return e ? std::max(1, std::atoi(e)) : 8;
+      }();
+      const int64_t nchunk = std::min<int64_t>(n_calls, (int64_t)threads * per_thread);
       std::vector<sg::Batch> parts((size_t)nchunk);
       std::vector<std::exception_ptr> errs((size_t)nchunk);
       std::atomic<int64_t> next{0};
@@ -504,6 +510,9 @@ int sg_plan_batch(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, sg_pl
                    (B.frames[0].size() + B.frames[1].size()) * sizeof(SgFrame) * 1e-6,
                    B.pieces.size() * sizeof(SgPiece) * 1e-6, B.syl_tiles.size() * sizeof(SgSylTile) * 1e-6,
                    B.fs_total * 4e-6, B.w_total * 4e-6);
+      std::fprintf(stderr, "sg_plan_prof fp64: filter bouts %lld, noise bouts %lld, frames %lld (noise %lld) of %lld\n",
+                   (long long)B.hp_bouts, (long long)B.hp_noise_bouts, (long long)B.frames64.size(),
+                   (long long)B.frames64_noise, (long long)(B.frames[0].size() + B.frames[1].size() + B.frames64.size()));
     }
     sg::scratch_trim();
     *out = P.release();

@@ -251,13 +251,17 @@ struct SgFrame {
 // A formant-filter frame of an ill-conditioned call (sg_fft_frames64): the fp64
 // sound fh[src .. src + wl) -> hamming -> fp64 DFT / wl -> x env (fp32 envelope
 // area / fl) -> fp64 inverse DFT / 2M -> x hann -> fs[dst .. dst + wl) (fp32, for sg_ola)
+// A noise frame of such a call (mode SG_F64_NOISE, generateNoise's istft): the
+// real spectrum fl[src + k] x fl[env + k] -> fp64 inverse DFT / 2M -> x hann -> fs.
 struct SgFrame64 {
   int64_t src;
   int64_t env;
   int64_t dst;
   int32_t wl;
-  int32_t pad;
+  int32_t mode;  // SG_F64_FILTER, SG_F64_NOISE
 };
+constexpr int32_t SG_F64_FILTER = 0;
+constexpr int32_t SG_F64_NOISE = 1;
 struct SgFrameGroup {  // frames of one workgroup: same geometry and mode
   int32_t geom, mode;
   int32_t f0, nf;

@@ -498,7 +498,7 @@ void device_execute_spec(const Batch& B, const DevicePlan& D, float* d_out, hipS
       prof->push_back({SG_PROF_STFT_OLA, e0, e1});
     }
     launch_fft_frames(D, r[1], r[2] - r[1], B.fgroup_lds[ph][1], s);
-    if (ph == 1) launch_fft_frames64(D, B, s);
+    launch_fft_frames64(D, B, ph, s);  // fp64 noise frames (phase 0), fp64 filter frames (phase 1)
     const int64_t t0 = ph == 0 ? 0 : B.olatile_split, t1 = ph == 0 ? B.olatile_split : (int64_t)B.olatiles.size();
     const int64_t o0 = ph == 0 ? 0 : B.ola_split, o1 = ph == 0 ? B.ola_split : (int64_t)B.olas_dev.size();
     launch_ola(D, t0, t1 - t0, s);

@@ -122,7 +122,7 @@ void launch_sine_bank_hp(const DevicePlan& D, int64_t n, hipStream_t s);
 void launch_piece_max_hp(const DevicePlan& D, int64_t p0, int64_t n_ptiles, hipStream_t s);
 void launch_harm_finalize_hp(const DevicePlan& D, int64_t n_stiles, hipStream_t s);
 void launch_mix_hp(const DevicePlan& D, int64_t t0, int64_t n_tiles, hipStream_t s);
-void launch_fft_frames64(const DevicePlan& D, const Batch& B, hipStream_t s);
+void launch_fft_frames64(const DevicePlan& D, const Batch& B, int ph, hipStream_t s);
 // sg_fft.hip
 void launch_fft_frames(const DevicePlan& D, int64_t g0, int64_t n_groups, int lds_bytes, hipStream_t s);
 void launch_stft_ola(const DevicePlan& D, int phase, int64_t s0, int64_t n_segs, int lds_bytes, hipStream_t s);

@@ -1254,17 +1254,23 @@ extern "C" __global__ __launch_bounds__(SG_F64_THREADS) void sg_fft_frames64(
   double2* rt = b + M;       // radix roots (<= 31)
   const double2* __restrict__ ham = TN + N;  // window pairs (sg_roots64)
   const double2* __restrict__ han = ham + M;
-  const double* x = fh + F.src;
-  for (int n = threadIdx.x; n < M; n += SG_F64_THREADS) {  // hamming (seewave ftwindow), packed pairs
-    const double2 h = ham[n];
-    a[n] = make_double2(x[2 * n] * h.x, x[2 * n + 1] * h.y);
+  const bool noise = F.mode == SG_F64_NOISE;
+  if (!noise) {
+    const double* x = fh + F.src;
+    for (int n = threadIdx.x; n < M; n += SG_F64_THREADS) {  // hamming (seewave ftwindow), packed pairs
+      const double2 h = ham[n];
+      a[n] = make_double2(x[2 * n] * h.x, x[2 * n + 1] * h.y);
+    }
+    __syncthreads();
+    fft64(a, b, M, TN, rt, false);
   }
-  __syncthreads();
-  fft64(a, b, M, TN, rt, false);
-  // untangle, / N, x env (Y_k, k < M), Hermitian extension, pack for the inverse (a -> b)
+  // FILTER: untangle, / N, x env; NOISE: uniforms x filter (real); Y_k, k < M; then
+  // seewave's Hermitian extension, packed for the inverse (-> b)
   const double invN = 1.0 / (double)N;
   const float* env = fl + F.env;
+  const float* uni = fl + F.src;
   auto Yat = [&](int kk) -> double2 {  // Y_kk, 0 <= kk < M
+    if (noise) return make_double2((double)uni[kk] * (double)env[kk], 0.0);
     const double2 p = a[kk], q = a[kk == 0 ? 0 : M - kk], w = TN[kk];
     const double2 e = make_double2(0.5 * (p.x + q.x), 0.5 * (p.y - q.y));
     const double2 o = make_double2(0.5 * (p.y + q.y), -0.5 * (p.x - q.x));
@@ -1481,16 +1487,21 @@ void launch_fft_probe(const SgFftGeom* geom, const float* fl, float* data, int M
                      reinterpret_cast<float2*>(data), inverse);
   SG_LAUNCHED("sg_fft_probe");
 }
-void launch_fft_frames64(const DevicePlan& D, const Batch& B, hipStream_t s) {
-  const int64_t n = (int64_t)B.frames64.size();
-  if (n <= 0) return;
-  hipLaunchKernelGGL(sg_roots64, dim3(16, (unsigned)B.roots64_wl.size()), dim3(256), 0, s, D.roots64_wl, D.roots64_off,
-                     reinterpret_cast<double2*>(D.roots64));
-  SG_LAUNCHED("sg_roots64");
+// phase 0: the noise frames [0, frames64_noise); phase 1: the filter frames after them.
+// The root tables are built before the first of the two launches that has frames.
+void launch_fft_frames64(const DevicePlan& D, const Batch& B, int ph, hipStream_t s) {
+  const int64_t n0 = B.frames64_noise, n = (int64_t)B.frames64.size();
+  const int64_t f0 = ph == 0 ? 0 : n0, nf = ph == 0 ? n0 : n - n0;
+  if (nf <= 0) return;
+  if (ph == 0 || n0 == 0) {
+    hipLaunchKernelGGL(sg_roots64, dim3(16, (unsigned)B.roots64_wl.size()), dim3(256), 0, s, D.roots64_wl,
+                       D.roots64_off, reinterpret_cast<double2*>(D.roots64));
+    SG_LAUNCHED("sg_roots64");
+  }
   const int lds = (B.frames64_maxwl + 32) * (int)sizeof(double2);  // two M-point buffers + radix roots
   lds_opt_in(reinterpret_cast<const void*>(&sg_fft_frames64), lds, "sg_fft_frames64");
-  hipLaunchKernelGGL(sg_fft_frames64, dim3((unsigned)n), dim3(SG_F64_THREADS), lds, s, D.frames64, D.frames64_tab,
-                     reinterpret_cast<const double2*>(D.roots64), D.fl, D.fh, D.fs);
+  hipLaunchKernelGGL(sg_fft_frames64, dim3((unsigned)nf), dim3(SG_F64_THREADS), lds, s, D.frames64 + f0,
+                     D.frames64_tab + f0, reinterpret_cast<const double2*>(D.roots64), D.fl, D.fh, D.fs);
   SG_LAUNCHED("sg_fft_frames64");
 }
 void launch_mix_hp(const DevicePlan& D, int64_t t0, int64_t n_tiles, hipStream_t s) {

@@ -116,13 +116,14 @@ struct Batch {
   std::vector<SgFrame> frames[2];        // [0] noise frames, [1] filter frames
   std::vector<int32_t> frame_geom[2];
   std::vector<SgOla> olas[2];            // [0] noise OLAs, [1] filter OLAs (device: [0] then [1])
-  std::vector<SgFrame64> frames64;       // filter frames of fp64 (ill-conditioned) calls: sg_fft_frames64
+  std::vector<SgFrame64> frames64;       // filter / noise frames of fp64 (ill-conditioned) bouts: sg_fft_frames64
   // derived (finalize_spec): the window lengths of the fp64 frames, their root tables
   // W_N^t (offsets in double2 units), each frame's table offset, the largest window
   std::vector<int32_t> roots64_wl;
   std::vector<int64_t> roots64_off, frames64_tab;
   int64_t roots64_total = 0;
   int32_t frames64_maxwl = 0;
+  int64_t frames64_noise = 0;  // finalize_spec: frames64 holds the noise frames first
   std::vector<SgNoiseItem> items;        // items[].ola indexes the device OLA table
   std::vector<SgMix> mixes[2];           // [0] pre-filter sounds (fs), [1] final output
   struct Copy { int64_t fl_off, fs_off, n; };
@@ -148,6 +149,7 @@ struct Batch {
   int64_t w64_total = 0;        // fp64 epoch-waveform scratch W64 (doubles; SG_TASK_HP tasks)
   int64_t fh_total = 0;         // fp64 sound scratch fh (doubles): voiced parts and sounds of fp64 bouts
   int64_t hp_bouts = 0;         // bouts whose formant filter runs the fp64 path
+  int64_t hp_noise_bouts = 0;   // bouts whose pre-filter noise runs the fp64 frame kernel
   // device spectral envelopes (sg_spec_env): per-column/track terms, per-column
   // factors, jobs; outputs in the envelope area (fe_total floats after fe_base,
   // the end of the uploaded fl floats, fixed at finalize_spec). Until then a
@@ -237,6 +239,11 @@ int plan_filter(Batch& B, int64_t sound, int64_t L, int wl, double overlap, int6
 bool plan_noise(Batch& B, Rng& R, int64_t len, const sg_anchors& noiseAnchors, double rolloffNoise,
                 double attackLen, int wl, double sr, double overlap, const double* filterNoise, int64_t fnc,
                 SgNoiseItem* item, int64_t filt_env = 0);
+// The noise items of an ill-conditioned bout (their OLAs, phase 0, the last
+// noises planned) on the fp64 frame kernel: the frames move from the phase-0
+// list to frames64 (SG_F64_NOISE) and the OLAs read their scratch (sg_ola).
+// False (nothing changed) when a window does not suit sg_fft_frames64.
+bool noise_to_fp64(Batch& B, const std::vector<int>& olas);
 // getSpectralEnvelope(), R/sourceSpectrum.R:261-566: the host part (tracks,
 // draws) plus one sg_spec_env job computing the nr x nc matrix on the device;
 // returns its envelope-area offset encoded as -(offset + 1). slope: dB per

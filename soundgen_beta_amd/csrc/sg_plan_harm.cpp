@@ -712,27 +712,50 @@ struct HostEpoch {
   // the recurrence (~R^2 eps), and R's 15-digit multipliers (rowname
   // round trip) against (r + 1) / D, times the row amplitudes.
   double Wfast(int64_t j, double* err) const {
-    const double v = r_seqint_at(knots.front(), knots.back(), n, j);
-    int64_t i = 0, jj = G - 1;
-    while (i < jj - 1) { int64_t ij = (i + jj) / 2; if (v < knots[ij]) jj = ij; else i = ij; }
-    const double t = (v - knots[i]) / (knots[jj] - knots[i]);
-    const double integ = S->integr(u0 + j);
-    double x = integ / (double)M->D;
-    x -= std::rint(x);
-    const double th = 2 * M_PI * x, c2 = 2 * std::cos(th);
-    double b1 = 0, b2 = 0, sabs = 0;
-    const double *A0 = M->col(i), *A1 = M->col(jj);
+    double f;
+    Wfast_n<1>(j, 1, &f, err);
+    return f;
+  }
+  // Wfast of the n <= K samples j0 .. j0 + n - 1: per sample the same operations
+  // in the same order, the K row recurrences interleaved (independent dependency
+  // chains keep the FP pipes busy; one chain is latency-bound)
+  template <int K>
+  void Wfast_n(int64_t j0, int n, double* f, double* err) const {
+    const double *A0[K], *A1[K];
+    double t[K], c2[K], th[K], integ[K], b1[K], b2[K], sabs[K];
+    int sel[K];  // 0: interpolate; 1: on knot jj (y1); 2: on knot i (y0)
+    for (int l = 0; l < K; ++l) {
+      const int64_t j = j0 + (l < n ? l : n - 1);
+      const double v = r_seqint_at(knots.front(), knots.back(), this->n, j);
+      int64_t i = 0, jj = G - 1;
+      while (i < jj - 1) { int64_t ij = (i + jj) / 2; if (v < knots[ij]) jj = ij; else i = ij; }
+      t[l] = (v - knots[i]) / (knots[jj] - knots[i]);
+      integ[l] = S->integr(u0 + j);
+      double x = integ[l] / (double)M->D;
+      x -= std::rint(x);
+      th[l] = 2 * M_PI * x;
+      c2[l] = 2 * std::cos(th[l]);
+      A0[l] = M->col(i);
+      A1[l] = M->col(jj);
+      sel[l] = v == knots[jj] ? 1 : (v == knots[i] ? 2 : 0);
+      b1[l] = b2[l] = sabs[l] = 0;
+    }
     for (int64_t r = M->R - 1; r >= 0; --r) {
-      const double y0 = A0[r], y1 = A1[r];
-      double am = (M->mult[r] == 0) ? 0.0 : (v == knots[jj] ? y1 : (v == knots[i] ? y0 : y0 + (y1 - y0) * t));
-      const double b = am + c2 * b1 - b2;
-      b2 = b1;
-      b1 = b;
-      sabs += std::fabs(am);
+      const bool zero = M->mult[r] == 0;
+      for (int l = 0; l < K; ++l) {
+        const double y0 = A0[l][r], y1 = A1[l][r];
+        const double am = zero ? 0.0 : (sel[l] == 1 ? y1 : (sel[l] == 2 ? y0 : y0 + (y1 - y0) * t[l]));
+        const double b = am + c2[l] * b1[l] - b2[l];
+        b2[l] = b1[l];
+        b1[l] = b;
+        sabs[l] += std::fabs(am);
+      }
     }
     const double Rr = (double)M->R;
-    *err = sabs * (Rr * Rr * 1e-15 + 1e-14 * std::fabs(integ) * Rr / (double)M->D) + 1e-300;
-    return b1 * std::sin(th);
+    for (int l = 0; l < n; ++l) {
+      err[l] = sabs[l] * (Rr * Rr * 1e-15 + 1e-14 * std::fabs(integ[l]) * Rr / (double)M->D) + 1e-300;
+      f[l] = b1[l] * std::sin(th[l]);
+    }
   }
   // sign-exact W for the zero-crossing search: the fast value where its error
   // bound cannot change the sign, else R's row-by-row sum
@@ -741,6 +764,16 @@ struct HostEpoch {
     double err;
     const double f = Wfast(j, &err);
     return std::fabs(f) > 1e3 * err ? f : W(j);
+  }
+  // Wsign of j0 .. j0 + n - 1 (n <= 4)
+  void Wsign_n(int64_t j0, int n, double* out) const {
+    if (!fast_ok) {
+      for (int l = 0; l < n; ++l) out[l] = W(j0 + l);
+      return;
+    }
+    double f[4], e[4];
+    Wfast_n<4>(j0, n, f, e);
+    for (int l = 0; l < n; ++l) out[l] = std::fabs(f[l]) > 1e3 * e[l] ? f[l] : W(j0 + l);
   }
   bool fast_ok = false;  // every present row's multiplier is (r + 1) / D
   void init_fast() {
@@ -786,17 +819,54 @@ struct Chain {
     }
     return std::fabs(v) > 1e3 * (err + 1e-300) ? v : at(k);
   }
+  // sign_at of k0 .. k0 + n - 1 (n <= 4): blocks of Wfast per term when the
+  // samples share a piece, the same per-sample sums and decisions as sign_at
+  void sign_at_n(int64_t k0, int n, double* out) const {
+    int64_t lo = 0, hi = (int64_t)P.size() - 1;
+    while (lo < hi) { int64_t m = (lo + hi + 1) / 2; if (P[m].start <= k0) lo = m; else hi = m - 1; }
+    const HPiece& p = P[lo];
+    bool block = k0 + n <= p.start + p.len;
+    for (const HTerm& t : p.t) block = block && (*E)[t.e].fast_ok;
+    if (!block) {
+      for (int l = 0; l < n; ++l) out[l] = sign_at(k0 + l);
+      return;
+    }
+    double v[4] = {0, 0, 0, 0}, err[4] = {0, 0, 0, 0}, f[4], e[4];
+    for (const HTerm& t : p.t) {
+      (*E)[t.e].Wfast_n<4>(t.j0 + (k0 - p.start), n, f, e);
+      for (int l = 0; l < n; ++l) {
+        const double q = (double)(k0 + l - p.start);
+        const double w = t.w0 + q * (t.w1 + q * t.w2);
+        v[l] += w * f[l];
+        err[l] += std::fabs(w) * e[l];
+      }
+    }
+    for (int l = 0; l < n; ++l) out[l] = std::fabs(v[l]) > 1e3 * (err[l] + 1e-300) ? v[l] : at(k0 + l);
+  }
   void truncate(int64_t newL) {
     while (!P.empty() && P.back().start >= newL) P.pop_back();
     if (!P.empty() && P.back().start + P.back().len > newL) P.back().len = newL - P.back().start;
   }
 };
 
-// findZeroCrossing(), R/utilities_soundgen.R:255-295, 1-based, 0 = NA
-template <class F>
-static int64_t find_zero_crossing(F&& a, int64_t len, int64_t location) {
+// findZeroCrossing(), R/utilities_soundgen.R:255-295, 1-based, 0 = NA.
+// ab(k0, n, out) evaluates the 0-based samples k0 .. k0 + n - 1 (n <= 4): the
+// scans read them through a 4-sample block in their direction of travel
+template <class FB>
+static int64_t find_zero_crossing(FB&& ab, int64_t len, int64_t location) {
   if (len < 1 || location < 1 || location > len) return 0;
   if (len == 1 && location == 1) return location;
+  double blk[4];
+  int64_t b0 = 0, bn = 0;
+  bool back = true;
+  auto a = [&](int64_t k) {
+    if (k < b0 || k >= b0 + bn) {
+      b0 = back ? std::max<int64_t>(0, k - 3) : k;
+      bn = back ? k - b0 + 1 : std::min<int64_t>(4, len - k);
+      ab(b0, (int)bn, blk);
+    }
+    return blk[k - b0];
+  };
   int64_t zl = 0, zr = 0, i = 0;
   if (location > 1) {
     i = location;
@@ -809,6 +879,7 @@ static int64_t find_zero_crossing(F&& a, int64_t len, int64_t location) {
     }
   }
   if (location < len) i = location;
+  back = false;
   if (i < len - 1) {
     double cur = a(i - 1);
     while (i < (len - 1)) {
@@ -836,12 +907,12 @@ static HTerm rebase(const HTerm& t, double s) {  // weight polynomial shifted by
 // crossFade(A, W_e), R/utilities_soundgen.R:328-375
 static void cross_fade(Chain& A, const HostEpoch& W, int64_t e, double sr, double crossLen) {
   const int64_t LA = A.L();
-  const int64_t zc1 = find_zero_crossing([&](int64_t k) { return A.sign_at(k); }, LA, LA);
+  const int64_t zc1 = find_zero_crossing([&](int64_t k0, int n, double* o) { A.sign_at_n(k0, n, o); }, LA, LA);
   if (zc1) {
     A.truncate(zc1);
     A.P.push_back(HPiece{zc1, 1, {}});
   }
-  const int64_t zc2 = find_zero_crossing([&](int64_t j) { return W.Wsign(j); }, W.n, 1);
+  const int64_t zc2 = find_zero_crossing([&](int64_t j0, int n, double* o) { W.Wsign_n(j0, n, o); }, W.n, 1);
   const int64_t w0 = zc2;  // W' = W[zc2 ..] (0-based)
   const int64_t lenW = W.n - w0;
   const int64_t L1 = A.L();

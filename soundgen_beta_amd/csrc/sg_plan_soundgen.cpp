@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <optional>
 
 #include "sg_plan.h"
 
@@ -256,7 +257,7 @@ SgNoiseItem raw_item(int64_t fs_off, int64_t len, int64_t off) {
 double env_db_at(const Batch& B, const SgEnvJob& J, int64_t c, int64_t k) {
   const SgEnvTerm* tm = B.eterms.data() + J.term0 + c * J.ntr;
   const SgEnvCol& C = B.ecols[J.col0 + c];
-  const double lk = std::log2((double)k);
+  const double lk = log2_int(k);
   double acc = 0;
   for (int32_t t = 0; t < J.ntr; ++t) {
     const SgEnvTerm& e = tm[t];
@@ -267,25 +268,44 @@ double env_db_at(const Batch& B, const SgEnvJob& J, int64_t c, int64_t k) {
   return (acc + C.lip * lk) * C.boost + J.slope * lk;
 }
 
+// env^2 of a bout's envelope on the bins 1, 1 + st, .. nr (st = nr / 256), per
+// column asked for, computed once for both estimates below
+struct EnvGrid {
+  const Batch& B;
+  const SgEnvJob& J;
+  int64_t st;
+  std::vector<std::pair<int64_t, vec>> cols;
+  EnvGrid(const Batch& b, const SgEnvJob& j) : B(b), J(j), st(std::max<int64_t>(1, j.nr / 256)) {}
+  const vec& col(int64_t c) {
+    for (const auto& p : cols)
+      if (p.first == c) return p.second;
+    vec v;
+    for (int64_t k = 1; k <= J.nr; k += st) v.push_back(std::exp2(env_db_at(B, J, c, k) / 5));
+    cols.emplace_back(c, std::move(v));
+    return cols.back().second;
+  }
+};
+
 struct ProbeAt {
   int64_t pos;  // sample of the bout's pre-filter sound
   const HarmProbe* p;
 };
 
-double filter_conditioning(const Batch& B, const SgEnvJob& J, const std::vector<ProbeAt>& probes, double hop, int wl,
-                           double sr) {
+double filter_conditioning(EnvGrid& G, const std::vector<ProbeAt>& probes, double hop, int wl, double sr) {
+  const Batch& B = G.B;
+  const SgEnvJob& J = G.J;
   double worst = 0;
   const int64_t nr = J.nr;
-  const int64_t st = std::max<int64_t>(1, nr / 256);
   for (const ProbeAt& pa : probes) {
     int64_t c = 0;
     if (J.nc > 1) {
       c = (int64_t)std::llround(((double)pa.pos - wl / 2.0) / hop);
       c = std::min<int64_t>(std::max<int64_t>(c, 0), J.nc - 1);
     }
+    const vec& e2 = G.col(c);
     double n2 = 0;
-    int64_t nk = 0;
-    for (int64_t k = 1; k <= nr; k += st, ++nk) n2 += std::exp2(env_db_at(B, J, c, k) / 5);  // env^2
+    for (double v : e2) n2 += v;  // env^2
+    const int64_t nk = (int64_t)e2.size();
     double s2 = 0, a2 = 0;
     const HarmProbe& hp = *pa.p;
     for (size_t h = 0; h < hp.amp.size(); ++h) {
@@ -298,6 +318,32 @@ double filter_conditioning(const Batch& B, const SgEnvJob& J, const std::vector<
     }
     if (a2 <= 0 || s2 <= 0 || nk == 0) continue;
     worst = std::max(worst, std::sqrt(n2 / (double)nk) / std::sqrt(s2 / a2));
+  }
+  return worst;
+}
+
+// The same rho for the pre-filter noise, whose fp32 round-off (its inverse
+// STFT, ~eps x the noise level, white) meets the envelope against the noise's
+// own spectrum: generateNoise's rolloffNoise filter (R/source.R:97-105), at the
+// filter's bins (k x wl_noise / wl), over up to 4 envelope columns.
+double noise_conditioning(EnvGrid& G, double rolloffNoise, int wl_noise, int wl) {
+  const SgEnvJob& J = G.J;
+  double worst = 0;
+  const int64_t ncol = std::min<int64_t>(4, J.nc);
+  for (int64_t q = 0; q < ncol; ++q) {
+    const int64_t c = (2 * q + 1) * J.nc / (2 * ncol);
+    const vec& e2 = G.col(c);
+    double n2 = 0, s2 = 0, w2 = 0;
+    int64_t i = 0;
+    for (int64_t k = 1; k <= J.nr; k += G.st, ++i) {
+      const double lk = wl_noise == wl ? log2_int(k) : std::log2((double)k * wl_noise / wl);
+      const double p2 = std::exp2(rolloffNoise / 5 * lk);  // filter^2
+      n2 += e2[(size_t)i];
+      s2 += p2 * e2[(size_t)i];
+      w2 += p2;
+    }
+    if (i == 0 || s2 <= 0 || w2 <= 0) continue;
+    worst = std::max(worst, std::sqrt(n2 / (double)i) / std::sqrt(s2 / w2));
   }
   return worst;
 }
@@ -320,6 +366,13 @@ int hp_mode() {
     g_hp_mode.store(m);
   }
   return m;
+}
+double hp_rho_noise() {
+  static const double r = [] {
+    const char* e = std::getenv("SG_HP_RHO_NOISE");
+    return e ? std::atof(e) : 30.0;
+  }();
+  return r;
 }
 double hp_rho() {
   double r = g_hp_rho.load();
@@ -545,6 +598,7 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
     int wl = 0;
     int64_t filt_env = 0, nInt = 1;
     bool hp = false;
+    std::optional<EnvGrid> grid;  // env^2 samples of the bout's filter envelope (conditioning estimates)
     if (ncontent > 0) {
       const double fl2 = std::floor((double)Ls / 2);
       if (fl2 < wlp) wlp = fl2;  // persists into later bouts and their noise
@@ -558,6 +612,7 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
       nInt = moving ? nc : 1;
       filt_env = plan_envelope(B, R, (double)wl / 2, nInt, &Fm, A.formantDep, A.rolloffLip, mouthA.view(), 0, 0,
                                A.vocalTract, T, A.tempEffects[1], A.tempEffects[2], A.formantDepStoch, 1, sr, 35400);
+      grid.emplace(B, B.envjobs.back());
       const int mode = hp_mode();
       // the fp64 frame kernel takes even windows with a 31-smooth half M <= 2048
       if (mode > 0 && !bout_syls.empty() && wl % 2 == 0 && wl <= 4096 && smooth31(wl / 2)) {  // M <= 2048
@@ -566,9 +621,19 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
         } else {
           std::vector<ProbeAt> pa;
           for (size_t q = 0; q < probes.size(); ++q) pa.push_back(ProbeAt{probe_pos[q], &probes[q]});
-          hp = filter_conditioning(B, B.envjobs.back(), pa, (double)wl - A.overlap * wl / 100, wl, sr) > hp_rho();
+          hp = filter_conditioning(*grid, pa, (double)wl - A.overlap * wl / 100, wl, sr) > hp_rho();
         }
       }
+    }
+    // the pre-filter noise of an ill-conditioned bout: fp64 inverse transforms
+    if (!postNoise && grid && hp_mode() > 0) {
+      std::vector<int> nolas;
+      for (const SgNoiseItem& it : noises)
+        if (it.ola >= 0 && !(it.flags & SG_ITEM_ZERO)) nolas.push_back(it.ola);
+      if (!nolas.empty() &&
+          (hp_mode() == 2 || noise_conditioning(*grid, A.rolloffNoise, B.olas[0][nolas[0]].wl, wl) > hp_rho_noise()) &&
+          noise_to_fp64(B, nolas))
+        ++B.hp_noise_bouts;
     }
     if (hp) {  // voiced syllables to the fp64 path; their items read fh
       ++B.hp_bouts;

@@ -11,6 +11,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <string>
 
 #include "sg_plan.h"
@@ -20,6 +22,26 @@ namespace sg {
 
 namespace {
 constexpr int kRadices[] = {4, 2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31};
+
+// The fp64 trig tables of a transform depend on its length alone: each is
+// computed once per process (every batch part plans its own geometries, so
+// without this each part would redo them) and copied into the part's fl.
+// kind: 0 windows (wl), 1 twiddles (wl), 2 stage twiddles (wl), 3 Bluestein chirp (n), 4 its DFT (n)
+template <class Make>
+std::shared_ptr<const vec> trig_table(int kind, int n, Make&& make) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, std::shared_ptr<const vec>> memo;
+  const std::pair<int, int> key(kind, n);
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = memo.find(key);
+    if (it != memo.end()) return it->second;
+  }
+  auto t = std::make_shared<const vec>(make());
+  std::lock_guard<std::mutex> lk(mu);
+  if (memo.size() >= 4096) memo.clear();  // bounded: windows of every length would otherwise accumulate
+  return memo.emplace(key, t).first->second;
+}
 constexpr int kFftSlots = 8192;  // complex points per FFT workgroup (sg_fft.hip SG_FFT_SLOTS)
 }  // namespace
 
@@ -40,12 +62,15 @@ int64_t fl_push(Batch& B, const double* v, int64_t n) {
 
 // seewave ftwindow: hamming.w (seewave.r:7431-7437), hanning.w (:7444-7450)
 static int64_t push_windows(Batch& B, int wl) {
-  vec win(2 * (size_t)wl);
-  for (int i = 0; i < wl; ++i) {
-    win[i] = 0.54 - 0.46 * std::cos(2 * M_PI * (double)i / (double)(wl - 1));
-    win[wl + i] = 0.5 - 0.5 * std::cos(2 * M_PI * (double)i / (double)(wl - 1));
-  }
-  return fl_push(B, win.data(), (int64_t)win.size());
+  const auto win = trig_table(0, wl, [wl] {
+    vec w(2 * (size_t)wl);
+    for (int i = 0; i < wl; ++i) {
+      w[i] = 0.54 - 0.46 * std::cos(2 * M_PI * (double)i / (double)(wl - 1));
+      w[wl + i] = 0.5 - 0.5 * std::cos(2 * M_PI * (double)i / (double)(wl - 1));
+    }
+    return w;
+  });
+  return fl_push(B, win->data(), (int64_t)win->size());
 }
 
 // ---- complex DFTs of any length for sg_fft_frames (SgCdft, sg_dev.h)
@@ -97,23 +122,31 @@ static SgCdft make_cdft(Batch& B, int n) {
   if (L > kFftSlots) throw SgError(SG_E_UNSUPPORTED, "FFT: Bluestein length " + std::to_string(L) + " exceeds LDS");
   c.L = L;
   c.geom = geometry(B, 2 * L);
-  vec ch(2 * (size_t)n);
-  std::vector<std::complex<double>> b((size_t)L, 0.0), bf;
-  for (int m = 0; m < n; ++m) {
-    const double a = -M_PI * (double)(((int64_t)m * m) % (2 * (int64_t)n)) / (double)n;
-    ch[2 * m] = std::cos(a);
-    ch[2 * m + 1] = std::sin(a);
-    b[m] = std::complex<double>(ch[2 * m], -ch[2 * m + 1]);
-    if (m > 0) b[L - m] = b[m];
-  }
-  dft_smooth(b, bf);
-  vec bv(2 * (size_t)L);
-  for (int k = 0; k < L; ++k) {
-    bv[2 * k] = bf[k].real() / L;
-    bv[2 * k + 1] = bf[k].imag() / L;
-  }
-  c.chirp = fl_push(B, ch.data(), (int64_t)ch.size());
-  c.bf = fl_push(B, bv.data(), (int64_t)bv.size());
+  const auto ch = trig_table(3, n, [n] {
+    vec h(2 * (size_t)n);
+    for (int m = 0; m < n; ++m) {
+      const double a = -M_PI * (double)(((int64_t)m * m) % (2 * (int64_t)n)) / (double)n;
+      h[2 * m] = std::cos(a);
+      h[2 * m + 1] = std::sin(a);
+    }
+    return h;
+  });
+  const auto bv = trig_table(4, n, [n, L, &ch] {
+    std::vector<std::complex<double>> b((size_t)L, 0.0), bf;
+    for (int m = 0; m < n; ++m) {
+      b[m] = std::complex<double>((*ch)[2 * m], -(*ch)[2 * m + 1]);
+      if (m > 0) b[L - m] = b[m];
+    }
+    dft_smooth(b, bf);
+    vec v(2 * (size_t)L);
+    for (int k = 0; k < L; ++k) {
+      v[2 * k] = bf[k].real() / L;
+      v[2 * k + 1] = bf[k].imag() / L;
+    }
+    return v;
+  });
+  c.chirp = fl_push(B, ch->data(), (int64_t)ch->size());
+  c.bf = fl_push(B, bv->data(), (int64_t)bv->size());
   return c;
 }
 static int cdft_size(const SgCdft& c) { return c.L ? c.L : c.n; }
@@ -165,31 +198,39 @@ int geometry(Batch& B, int wl) {
       if (B.geoms[i].wl == wl) return (int)i;
   }
   // twiddles W_M^t (t < M), W_N^k (k < M), fp64 -> fp32
-  vec tw(4 * (size_t)g.M);
-  for (int t = 0; t < g.M; ++t) {
-    const double a = -2.0 * M_PI * (double)t / (double)g.M;
-    tw[2 * t] = std::cos(a);
-    tw[2 * t + 1] = std::sin(a);
-    const double b = -2.0 * M_PI * (double)t / (double)wl;
-    tw[2 * g.M + 2 * t] = std::cos(b);
-    tw[2 * g.M + 2 * t + 1] = std::sin(b);
-  }
-  g.tw = fl_push(B, tw.data(), (int64_t)tw.size());
-  {
-    vec ts(2 * (size_t)std::max(1, g.M - 1), 0.0);
-    int ns = 1;
-    for (int s = 0; s < g.nstages; ++s) {
-      const int r = g.radix[s];
-      for (int q = 1; q < r; ++q)
-        for (int jm = 0; jm < ns; ++jm) {
-          const size_t e = (size_t)(ns - 1 + (q - 1) * ns + jm);
-          const double a = -2.0 * M_PI * (double)q * (double)jm / ((double)ns * r);
-          ts[2 * e] = std::cos(a);
-          ts[2 * e + 1] = std::sin(a);
-        }
-      ns *= r;
+  const int M = g.M;
+  const auto tw = trig_table(1, wl, [M, wl] {
+    vec w(4 * (size_t)M);
+    for (int t = 0; t < M; ++t) {
+      const double a = -2.0 * M_PI * (double)t / (double)M;
+      w[2 * t] = std::cos(a);
+      w[2 * t + 1] = std::sin(a);
+      const double b = -2.0 * M_PI * (double)t / (double)wl;
+      w[2 * M + 2 * t] = std::cos(b);
+      w[2 * M + 2 * t + 1] = std::sin(b);
     }
-    g.tws = fl_push(B, ts.data(), (int64_t)ts.size());
+    return w;
+  });
+  g.tw = fl_push(B, tw->data(), (int64_t)tw->size());
+  {
+    const SgFftGeom& gc = g;  // the stage radices are a function of wl
+    const auto ts = trig_table(2, wl, [&gc] {
+      vec t(2 * (size_t)std::max(1, gc.M - 1), 0.0);
+      int ns = 1;
+      for (int s = 0; s < gc.nstages; ++s) {
+        const int r = gc.radix[s];
+        for (int q = 1; q < r; ++q)
+          for (int jm = 0; jm < ns; ++jm) {
+            const size_t e = (size_t)(ns - 1 + (q - 1) * ns + jm);
+            const double a = -2.0 * M_PI * (double)q * (double)jm / ((double)ns * r);
+            t[2 * e] = std::cos(a);
+            t[2 * e + 1] = std::sin(a);
+          }
+        ns *= r;
+      }
+      return t;
+    });
+    g.tws = fl_push(B, ts->data(), (int64_t)ts->size());
   }
   g.win = push_windows(B, wl);
   // frames per workgroup: one in-place LDS buffer of fb * M complex points,
@@ -412,6 +453,38 @@ bool plan_noise(Batch& B, Rng& R, int64_t len, const sg_anchors& noiseAnchors, d
   return true;
 }
 
+bool noise_to_fp64(Batch& B, const std::vector<int>& olas) {
+  std::vector<SgFrame>& F = B.frames[0];
+  int64_t first = (int64_t)F.size(), nf = 0;
+  for (int o : olas) {
+    const SgOla& O = B.olas[0][o];
+    const int wl = O.wl;
+    if (O.fidx < 0 || wl % 2 || wl > 4096 || !smooth31(wl / 2)) return false;  // sg_fft_frames64: M <= 2048, 31-smooth
+    first = std::min<int64_t>(first, O.fidx);
+    nf += O.nframes;
+  }
+  if (first + nf != (int64_t)F.size()) return false;  // not the tail of the frame list
+  for (int o : olas) {
+    SgOla& O = B.olas[0][o];
+    if (O.fused) O.frames = fs_alloc(B, (int64_t)O.nframes * O.wl);  // frame scratch for sg_ola
+    for (int32_t c = 0; c < O.nframes; ++c) {
+      const SgFrame& f = F[(size_t)(O.fidx + c)];
+      SgFrame64 g{};
+      g.src = f.src;
+      g.env = f.env;
+      g.dst = O.frames + (int64_t)c * O.wl;
+      g.wl = O.wl;
+      g.mode = SG_F64_NOISE;
+      B.frames64.push_back(g);
+    }
+    O.fidx = -1;
+    O.fused = 0;
+  }
+  F.resize((size_t)first);
+  B.frame_geom[0].resize((size_t)first);
+  return true;
+}
+
 vec sigmoid_half(double sr, double freq, double shape, double spikiness) {
   // getSigmoid(), R/utilities_math.R:639-653: seq(from, to, length.out = sr / freq / 2)
   // (length.out rounded up), logistic, zeroOne
@@ -628,7 +701,8 @@ int64_t plan_envelope(Batch& B, Rng& R, double nrd, int64_t nc, const sg_formant
         e = SgEnvTerm{};
         e.A = shape - 1;
         e.Rr = rate * L2E;
-        auto l2 = [&](double x) { return e.A * std::log2(x) - e.Rr * x; };  // log2 density (+ const), as the device
+        // log2 density (+ const) at the integer bins k0, k1, as the device
+        auto l2 = [&](double x) { return e.A * log2_int((int64_t)x) - e.Rr * x; };
         double kmax = 1;
         if (e.A > 0 && rate > 0) kmax = std::min((double)nr, std::max(1.0, e.A / rate));
         const double k0 = std::floor(kmax), k1 = std::min((double)nr, std::ceil(kmax));
@@ -679,6 +753,11 @@ void finalize_spec(Batch& B) {
   B.frames64_tab.clear();
   B.roots64_total = 0;
   B.frames64_maxwl = 0;
+  // noise frames first (launched in phase 0, before the noise OLAs), then the filter frames;
+  // OLAs address the frames' scratch outputs, not their order
+  B.frames64_noise = std::stable_partition(B.frames64.begin(), B.frames64.end(),
+                                           [](const SgFrame64& f) { return f.mode == SG_F64_NOISE; }) -
+                     B.frames64.begin();
   for (SgFrame64& f : B.frames64) {
     if (f.env < 0) f.env = B.fe_base + (-f.env - 1);
     size_t w = 0;

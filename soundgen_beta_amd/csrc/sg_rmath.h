@@ -197,6 +197,15 @@ inline vec r_spline(const vec& x, const vec& y, int64_t n) {
   for (int64_t l = 0; l < n; ++l) out[l] = s.eval(r_seqint_at(x.front(), x.back(), n, l), i);
   return out;
 }
+// std::log2(k) of a positive integer k, from a table for the bins of any window
+inline double log2_int(int64_t k) {
+  static const std::vector<double> tab = [] {
+    std::vector<double> t(16385);
+    for (size_t i = 1; i < t.size(); ++i) t[i] = std::log2((double)i);
+    return t;
+  }();
+  return k > 0 && k < (int64_t)tab.size() ? tab[(size_t)k] : std::log2((double)k);
+}
 // approx1 (stats/src/approx.c), rule = 1
 inline double approx1(double v, const double* x, const double* y, int64_t n) {
   int64_t i = 0, j = n - 1;

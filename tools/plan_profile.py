@@ -77,7 +77,9 @@ def main(n_calls=4096, top=40):
     S.sg_sampler_stacks.restype = C.POINTER(C.c_uint64)
     depth = S.sg_sampler_depth()
     calls = bench.c5_calls(int(n_calls))
-    batch.Plan(calls[:max(64, len(calls) // 4)], None).close()  # load the library, warm the size estimates
+    # load the library, warm the size estimates (SG_PP_WARM=1: a whole plan first, so that the
+    # host block cache is as warm as for bench.py's later chunks)
+    batch.Plan(calls if os.environ.get("SG_PP_WARM") else calls[:max(64, len(calls) // 4)], None).close()
     S.sg_sampler_start(2000, 1)
     t0 = time.perf_counter()
     p = batch.Plan(calls, None)
