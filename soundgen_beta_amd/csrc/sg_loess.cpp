@@ -147,6 +147,52 @@ double LoessFit::hermite(int p, double z) const {
   return phi0 * val[a] + phi1 * val[b] + (psi0 * slope[a] + psi1 * slope[b]) * (v1 - v0);
 }
 
+namespace {
+// Is T(u) < thr for some u = 1..len (the valueFloor test of the refit loop)?
+// On a leaf cell the Hermite cubic's minimum over its part of [1, len]
+// (endpoints and stationary points, power basis) bounds its values at the
+// integers there; only a cell whose bound comes within a rounding margin of
+// thr has its integers evaluated one by one, as are integers outside the
+// vertex range. Same answer as evaluating all len points.
+bool dips_below(const LoessFit& T, int64_t len, double thr) {
+  double vmin = INFINITY, vmax = -INFINITY;
+  for (double v : T.vx) {
+    vmin = std::min(vmin, v);
+    vmax = std::max(vmax, v);
+  }
+  auto scan = [&](int64_t z0, int64_t z1) {
+    for (int64_t z = std::max<int64_t>(z0, 1); z <= std::min<int64_t>(z1, len); ++z)
+      if (T.eval((double)z) < thr) return true;
+    return false;
+  };
+  if (!(vmin <= vmax) || scan(1, (int64_t)std::ceil(vmin) - 1) || scan((int64_t)std::floor(vmax) + 1, len)) return true;
+  for (size_t p = 0; p < T.split.size(); ++p) {
+    if (T.split[p]) continue;
+    const int a = T.cv0[p], b = T.cv1[p];
+    const double v0 = T.vx[a], v1 = T.vx[b];
+    const double lo = std::max(std::min(v0, v1), 1.0), hi = std::min(std::max(v0, v1), (double)len);
+    if (!(lo <= hi) || std::ceil(lo) > std::floor(hi)) continue;
+    const double D = v1 - v0, y0 = T.val[a], y1 = T.val[b], m0 = T.slope[a] * D, m1 = T.slope[b] * D;
+    const double c1 = m0, c2 = 3 * (y1 - y0) - 2 * m0 - m1, c3 = 2 * (y0 - y1) + m0 + m1;
+    auto f = [&](double h) { return y0 + h * (c1 + h * (c2 + h * c3)); };
+    const double hlo = std::min((lo - v0) / D, (hi - v0) / D), hhi = std::max((lo - v0) / D, (hi - v0) / D);
+    double fmin = std::min(f(hlo), f(hhi));
+    // stationary points: qa h^2 + qb h + qc = 0 (the cancellation-free pair of roots;
+    // qa may be a rounding residue of a quadratic piece)
+    const double qa = 3 * c3, qb = 2 * c2, qc = c1;
+    const double disc = qb * qb - 4 * qa * qc;
+    if (disc >= 0) {
+      const double q = -0.5 * (qb + std::copysign(std::sqrt(disc), qb));
+      for (double r : {q != 0 ? qc / q : NAN, qa != 0 ? q / qa : NAN})
+        if (r > hlo && r < hhi) fmin = std::min(fmin, f(r));
+    }
+    const double margin = 1e-9 * (std::fabs(y0) + std::fabs(y1) + std::fabs(m0) + std::fabs(m1) + 1);
+    if (!(fmin >= thr + margin) && scan((int64_t)std::ceil(lo), (int64_t)std::floor(hi))) return true;
+  }
+  return false;
+}
+}  // namespace
+
 bool loess_fit(const double* x, const double* y, int n, double f, LoessFit& T) {
   if (n < 1) throw SgError(SG_E_DOMAIN, "loess: no data");
   if (std::floor(n * f + 1e-5) <= 0) throw SgError(SG_E_DOMAIN, "loess: span is too small");
@@ -256,11 +302,7 @@ LoessFit smooth_loess(const double* t, const double* v, int64_t n, int64_t len, 
       if (!loess_fit(x.data(), y.data(), (int)x.size(), span, T))
         throw SgError(SG_E_UNSUPPORTED, "loess: zero-width fit inside the valueFloor refits");
     }
-    bool below = false;
-    if (has_floor) {
-      int leaf = -1;
-      for (int64_t k = 0; k < len && !below; ++k) below = T.eval_seq((double)(k + 1), leaf) < vfloor - 1e-6;
-    }
+    const bool below = has_floor && dips_below(T, len, vfloor - 1e-6);
     if (!below) return T;
     span = span / 1.1;  // less smoothing while the contour dips below the floor
   }

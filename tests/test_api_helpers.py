@@ -30,6 +30,26 @@ def test_get_smooth_contour_vs_oracle(oracle, case):
     np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-12)
 
 
+def test_get_smooth_contour_floor_refits_vs_oracle(oracle):
+    """Anchors dipping below valueFloor drive the loess refit loop (span / 1.1 while a
+    value of 1..len falls below the floor, R/smoothContours.R:144-151): the planner's
+    per-cell bound must pick the same span as the oracle's point-by-point test."""
+    rng = np.random.default_rng(11)
+    n_refit = 0
+    for trial in range(300):
+        n = int(rng.integers(3, 11))
+        t = np.sort(rng.uniform(0, 1, n))
+        t[0], t[-1] = 0, 1
+        v = rng.normal(0, 3, n) if trial % 2 else rng.uniform(-5, 40, n)
+        case = dict(anchors={"time": list(t), "value": list(v)}, len=int(rng.integers(5, 3000)), valueFloor=0.0)
+        got = api.getSmoothContour(**case)
+        want = oracle.smooth_contour(**case)
+        n_refit += bool(np.min(v) < 0)
+        assert got.shape == want.shape, trial
+        np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-12, err_msg=str(trial))
+    assert n_refit > 50
+
+
 def test_get_smooth_contour_na():
     assert api.getSmoothContour(None, len=100) is None
     assert api.getSmoothContour({"time": [0, 1], "value": [1, 2]}, len=0) is None
