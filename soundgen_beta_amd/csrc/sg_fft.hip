@@ -28,7 +28,17 @@
 #define SG_FFT_WPE_NOISE (SG_FFT_WAVES_NOISE_N > 8 ? 3 : 2)  // waves per SIMD for sg_stft_ola_noise
 #endif
 #ifndef SG_PF_AHEAD
-#define SG_PF_AHEAD 0  // build knob: issue the next frame's input loads before this frame's inverse FFT
+#define SG_PF_AHEAD 0  // build knob (filter kernel): 1 the next frame's inputs before this frame's inverse FFT;
+                       // 2 the next frame's sound after it, this frame's envelope before the forward FFT
+#endif
+#ifndef SG_PF_AHEAD_NOISE
+#define SG_PF_AHEAD_NOISE 0  // the same for sg_stft_ola_noise (2: the next frame's input after the inverse FFT)
+#endif
+#ifndef SG_UNT_HOIST
+#define SG_UNT_HOIST 0  // build knob: the untangle reads all its LDS pairs before its first write (r03i A/B: neutral)
+#endif
+#ifndef SG_OUT_BATCH
+#define SG_OUT_BATCH 1  // build knob: output samples and the next carry read from LDS in batches (no per-sample waits)
 #endif
 #include "sg_devfn.h"
 #include "sg_roots.h"
@@ -419,6 +429,9 @@ __device__ __forceinline__ void fft_wc(float2* X, const float2* twS, int lane SG
   stage_w<R2, INV, CM, R0 * R1>(X, CM, R0 * R1, twS, 0u, lane);
   SG_ST(INV ? 7 : 3);
 }
+#ifndef SG_STFT_CP13
+#define SG_STFT_CP13 0  // build knob: the M = 1102 path with 13 carry pairs when the OLA's tail fits (hop >= 540)
+#endif
 #ifndef SG_STFT_SPEC
 #define SG_STFT_SPEC 1  // build knob: compile-time specialisation of sg_stft_ola for M = 1102 = 2 x 19 x 29
 #endif
@@ -652,24 +665,31 @@ struct FramePf {
   __device__ __forceinline__ const float2& b(int i) const { return s[i]; }
 };
 
+// PART: 0 everything; 1 what the frame front consumes first (FILTER: the sound;
+// NOISE: everything); 2 the rest (FILTER: the envelope, consumed after the forward FFT)
+template <int PART = 0>
 __device__ __forceinline__ void frame_prefetch(FramePf& P, const SgFrame& F, int mode, int M,
                                                const float* __restrict__ fl, const float* __restrict__ fs, int lane) {
   const int half = M / 2;
   if (mode == SG_FRAME_FILTER) {
     const float* src = fs + F.src;
     const float* env = fl + F.env;
+    if (PART != 2) {
 #pragma unroll
-    for (int i = 0; i < SG_PF_SRC; ++i) {
-      const int n = 64 * i + lane;
-      if (n < M) P.s[i] = make_float2(src[2 * n], src[2 * n + 1]);
+      for (int i = 0; i < SG_PF_SRC; ++i) {
+        const int n = 64 * i + lane;
+        if (n < M) P.s[i] = make_float2(src[2 * n], src[2 * n + 1]);
+      }
     }
+    if (PART != 1) {
 #pragma unroll
-    for (int i = 0; i < SG_PF_PAIR; ++i) {
-      const int k = 64 * i + lane;
-      if (k <= half) P.a[i] = make_float2(env[k], env[k == 0 ? M - 1 : M - k]);
+      for (int i = 0; i < SG_PF_PAIR; ++i) {
+        const int k = 64 * i + lane;
+        if (k <= half) P.a[i] = make_float2(env[k], env[k == 0 ? M - 1 : M - k]);
+      }
+      P.xh = env[half];
     }
-    P.xh = env[half];
-  } else {
+  } else if (PART != 2) {
     const float* u = fl + F.src;
     const float* flt = fl + F.env;
 #pragma unroll
@@ -708,7 +728,25 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
     else fft_w<false>(A, g, twS, lane SG_ST_ARGS);
     // untangle X[k] = E + W_N^k O (E, O from Z_k, conj Z_{M-k}), Y = X / wl x env,
     // pack for the inverse; pair k owns slots k and M - k, the k = 0 lane also
-    // reads slots 1, M - 1 and half; every read of an iteration precedes its writes
+    // reads slots 1, M - 1 and half. SG_UNT_HOIST: every read of every pair
+    // before the first write (the slots of different pairs are disjoint, so the
+    // LDS latency is paid once per frame, not once per 64 pairs); else every read
+    // of an iteration precedes its writes
+#if SG_UNT_HOIST
+    float2 zav[SG_PF_PAIR], zbv[SG_PF_PAIR];
+#pragma unroll
+    for (int i = 0; i < SG_PF_PAIR; ++i) {
+      const int k0 = 64 * i;
+      if (k0 > half) break;
+      const int k = k0 + lane;
+      const bool act = k <= half && (k == 0 || k < M - k);
+      const int kk = act ? k : 0;
+      zav[i] = A[kk];
+      zbv[i] = A[kk == 0 ? 0 : M - kk];
+    }
+    const float2 z1h = A[1], zM1h = A[M - 1], zhh = A[half];
+    sg_wave_fence();
+#endif
 #pragma unroll
     for (int i = 0; i < SG_PF_PAIR; ++i) {
       const int k0 = 64 * i;
@@ -717,6 +755,10 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
       const bool act = k <= half && (k == 0 || k < M - k);
       const int kk = act ? k : 0;
       const int km = kk == 0 ? 0 : M - kk;
+#if SG_UNT_HOIST
+      const float2 za = zav[i], zb = zbv[i];
+      const float2 z1 = z1h, zM1 = zM1h, zh = zhh;
+#else
       const float2 za = A[kk], zb = A[km];
       float2 z1 = za, zM1 = za, zh = za;
       if (i == 0) {
@@ -728,6 +770,7 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
       // thread the compiler may sink them into the k = 0 branch, which the
       // SIMT code runs after the other branch
       sg_wave_fence();
+#endif
       if (!act) continue;
       auto X_at = [&](float2 a, float2 b, int t) -> float2 {
         const float2 e = make_float2(0.5f * (a.x + b.x), 0.5f * (a.y - b.y));
@@ -798,7 +841,7 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
 // summation is in frame order, so results are deterministic.
 // LDS: twS (M pairs), twN (M pairs), ham + han (M pairs each), SG_FFT_WAVES slices (M pairs each).
 // One segment of sg_stft_ola (CM > 0: the M = CM geometry with radices R0 x R1 x R2, sizes folded)
-template <int CM, int R0, int R1, int R2, int MODE>
+template <int CM, int R0, int R1, int R2, int MODE, int CP = SG_CARRY_PAIRS>
 __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __restrict__ olas,
                                              const SgFrame* __restrict__ frames, const SgFftGeom& g,
                                              const float* __restrict__ fl, float* __restrict__ fs,
@@ -817,9 +860,9 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
   const float scale = O.scale;
   float* out = fs + O.out;
   float m = -INFINITY;
-  float2 C[SG_CARRY_PAIRS];
+  float2 C[CP];
 #pragma unroll
-  for (int r = 0; r < SG_CARRY_PAIRS; ++r) C[r] = make_float2(0.f, 0.f);
+  for (int r = 0; r < CP; ++r) C[r] = make_float2(0.f, 0.f);
   FramePf P;
 #ifdef SG_STFT_STAMPS
   uint64_t st_accv[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -828,45 +871,51 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
   uint64_t* st_last = &st_lastv;
 #endif
   int bf = bstart(S.f0);
-#if SG_PF_AHEAD
-  {
+  constexpr int PFA = MODE == SG_FRAME_NOISE ? SG_PF_AHEAD_NOISE : SG_PF_AHEAD;
+  if constexpr (PFA != 0) {
     int Mk = M;
     if (!CM) __asm__ __volatile__("" : "+s"(Mk));
-    frame_prefetch(P, frames[S.fdev], mode, Mk, fl, fs, lane);
+    frame_prefetch<PFA == 2 ? 1 : 0>(P, frames[S.fdev], mode, Mk, fl, fs, lane);
   }
-#endif
   for (int k = 0; k < S.nf; ++k) {
-#if !SG_PF_AHEAD
-    {
+    if constexpr (PFA == 0) {
       int Mk = M;
       if (!CM) __asm__ __volatile__("" : "+s"(Mk));
       frame_prefetch(P, frames[S.fdev + k], mode, Mk, fl, fs, lane);
-    }
-#endif
-    frame_front<CM, R0, R1, R2>(A, P, mode, g, twS, twN, ham, lane SG_ST_ARGS);
-#if SG_PF_AHEAD
-    // the next frame's inputs are in flight during this frame's inverse FFT and overlap-add
-    if (k + 1 < S.nf) {
+    } else if constexpr (PFA == 2) {  // the envelope: in flight during the forward FFT
       int Mk = M;
       if (!CM) __asm__ __volatile__("" : "+s"(Mk));
-      frame_prefetch(P, frames[S.fdev + k + 1], mode, Mk, fl, fs, lane);
+      frame_prefetch<2>(P, frames[S.fdev + k], mode, Mk, fl, fs, lane);
     }
-#endif
+    frame_front<CM, R0, R1, R2>(A, P, mode, g, twS, twN, ham, lane SG_ST_ARGS);
+    if constexpr (PFA == 1) {
+      // the next frame's inputs are in flight during this frame's inverse FFT and overlap-add
+      if (k + 1 < S.nf) {
+        int Mk = M;
+        if (!CM) __asm__ __volatile__("" : "+s"(Mk));
+        frame_prefetch(P, frames[S.fdev + k + 1], mode, Mk, fl, fs, lane);
+      }
+    }
     SG_ST(4);
     if constexpr (CM != 0) fft_wc<true, CM, R0, R1, R2>(A, twS, lane SG_ST_ARGS);
     else fft_w<true>(A, g, twS, lane SG_ST_ARGS);
     int Mk = M, Nk = N;
     if (!CM) __asm__ __volatile__("" : "+s"(Mk), "+s"(Nk));
+    if constexpr (PFA == 2) {
+      // the next frame's sound (noise: its whole input): in flight during the
+      // overlap-add, the output and the carry reload (the FFT state is dead here)
+      if (k + 1 < S.nf) frame_prefetch<1>(P, frames[S.fdev + k + 1], mode, Mk, fl, fs, lane);
+    }
     // window (/wl x hanning) and add the carry (pairs n = 64 r + lane)
 #pragma unroll
-    for (int r = 0; r < SG_CARRY_PAIRS; ++r) {
+    for (int r = 0; r < CP; ++r) {
       const int n = 64 * r + lane;
       if (n < Mk) {
         const float2 v = A[n];
         A[n] = make_float2(fmaf(v.x * invN, han[2 * n], C[r].x), fmaf(v.y * invN, han[2 * n + 1], C[r].y));
       }
     }
-    for (int n = 64 * SG_CARRY_PAIRS + lane; n < Mk; n += 64) {
+    for (int n = 64 * CP + lane; n < Mk; n += 64) {
       const float2 v = A[n];
       A[n] = make_float2(v.x * invN * han[2 * n], v.y * invN * han[2 * n + 1]);
     }
@@ -878,7 +927,20 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
     if (bf >= S.pa && bf - first >= 0 && bn - first <= len && D <= Nk) {
       // interior frame (wave-uniform): every final sample is owned, inside the trim and the frame
       float* __restrict__ o = out + (bf - first);
-      for (int i = lane; i < D; i += 64) {
+      int i = lane;
+#if SG_OUT_BATCH
+      for (; i + 192 < D; i += 256) {  // four LDS reads in flight per lane before the stores
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = Af[i + 64 * e] * scale;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[i + 64 * e] = v[e];
+          m = fmaxf(m, v[e]);
+        }
+      }
+#endif
+      for (; i < D; i += 64) {
         const float v = Af[i] * scale;
         o[i] = v;
         m = fmaxf(m, v);
@@ -896,8 +958,19 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
     }
     if (!lastf) {
       const int tail = Nk - D;  // carried samples (pairs beyond it are zero)
+#if SG_OUT_BATCH
+      // every read unconditional (index clamped into the slice): all in flight at once;
+      // i0 >= Nk exactly when the pair lies past the tail
+      (void)tail;
 #pragma unroll
-      for (int r = 0; r < SG_CARRY_PAIRS; ++r) {
+      for (int r = 0; r < CP; ++r) {
+        const int i0 = 2 * (64 * r + lane) + D;
+        const float a = Af[min(i0, Nk - 1)], b = Af[min(i0 + 1, Nk - 1)];
+        C[r] = make_float2(i0 < Nk ? a : 0.f, i0 + 1 < Nk ? b : 0.f);
+      }
+#else
+#pragma unroll
+      for (int r = 0; r < CP; ++r) {
         if (128 * r < tail) {  // wave-uniform
           const int i0 = 2 * (64 * r + lane) + D;
           C[r] = make_float2(i0 < Nk ? Af[i0] : 0.f, i0 + 1 < Nk ? Af[i0 + 1] : 0.f);
@@ -905,6 +978,7 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
           C[r] = make_float2(0.f, 0.f);
         }
       }
+#endif
     }
     sg_wave_fence();  // the next frame overwrites the slice
     bf = bn;
@@ -961,7 +1035,10 @@ __device__ __forceinline__ void stft_ola_body(
   if (S.nf <= 0) return;  // padding segment
 #if SG_STFT_SPEC
   if (M == 1102 && g.nstages == 3 && g.radix[0] == 2 && g.radix[1] == 19 && g.radix[2] == 29)
-    stft_segment<1102, 2, 19, 29, MODE>(S, olas, frames, g, fl, fs, slotmax, twS, twN, ham, han, w, lane);
+    if (SG_STFT_CP13 && 2204 - (olas[S.ola].hi > 0 ? olas[S.ola].hi : (int)floor(olas[S.ola].h)) <= 128 * 13)
+      stft_segment<1102, 2, 19, 29, MODE, 13>(S, olas, frames, g, fl, fs, slotmax, twS, twN, ham, han, w, lane);
+    else
+      stft_segment<1102, 2, 19, 29, MODE>(S, olas, frames, g, fl, fs, slotmax, twS, twN, ham, han, w, lane);
   else
 #endif
 #ifndef SG_STFT_ONLY_SPEC  // diagnostic: the specialised path alone (register budget)
