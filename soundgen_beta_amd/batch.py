@@ -19,16 +19,26 @@ class Marshalled:
     that the two overlap across chunks (plan_uploaded)."""
 
     def __init__(self, calls):
-        self.holder = rargs.Holder()
+        self.holder = h = rargs.Holder()
         n = self.n = len(calls)
-        descs = (_abi.sg_call_desc * max(n, 1))()
-        args = (_abi.sg_soundgen_args * max(n, 1))()
-        scal = rargs.scalar_view(args, max(n, 1))
+        N = max(n, 1)
+        descs = (_abi.sg_call_desc * N)()
+        args = (_abi.sg_soundgen_args * N)()
         self._structs = [args]
+        # soundgen() calls with injected draws go through the bulk writers: their
+        # argument structs (ArgsWriter) and descriptor fields are written for all
+        # calls at once; harmonics calls and draw callbacks take the per-call path
+        aw = rargs.ArgsWriter(h, args, N)
+        fast, rand = [], []
         for i, c in enumerate(calls):
-            d = descs[i]
             kind = c.get("kind", "soundgen")
-            d.random = self.holder.random(c.get("normals"), c.get("uniforms"), c.get("rng"))
+            if kind != "harmonics" and c.get("rng") is None:
+                aw.add(i, c.get("args", {}))
+                fast.append(i)
+                rand.append(h.random_addrs(c.get("normals"), c.get("uniforms")))
+                continue
+            d = descs[i]
+            d.random = h.random(c.get("normals"), c.get("uniforms"), c.get("rng"))
             if kind == "harmonics":
                 d.kind = _abi.SG_CALL_HARMONICS
                 p = self.holder.arr(c["pitch"])
@@ -39,9 +49,31 @@ class Marshalled:
                 d.amplAnchors = self.holder.anchors(rargs.as_anchors(c.get("amplAnchors")))
             else:
                 d.kind = _abi.SG_CALL_SOUNDGEN
-                rargs.fill_soundgen_args(self.holder, c.get("args", {}), out=args[i], scalars=scal, i=i)
+                aw.add(i, c.get("args", {}))
                 d.args = C.pointer(args[i])
+        aw.finish()
+        if fast:
+            dv = np.frombuffer(descs, dtype=_DESC_VIEW, count=N)
+            idx = np.asarray(fast, dtype=np.int64)
+            r = np.array(rand, dtype=np.uint64).reshape(-1, 4)
+            dv["kind"][idx] = _abi.SG_CALL_SOUNDGEN
+            dv["args"][idx] = C.addressof(args) + idx.astype(np.uint64) * C.sizeof(_abi.sg_soundgen_args)
+            dv["normals"][idx], dv["n_normals"][idx] = r[:, 0], r[:, 1]
+            dv["uniforms"][idx], dv["n_uniforms"][idx] = r[:, 2], r[:, 3]
         self.descs = descs
+
+
+def _desc_view():
+    D, R = _abi.sg_call_desc, _abi.sg_random
+    o = D.random.offset
+    f = [("kind", "<i4", D.kind.offset), ("args", "<u8", D.args.offset),
+         ("normals", "<u8", o + R.normals.offset), ("n_normals", "<i8", o + R.n_normals.offset),
+         ("uniforms", "<u8", o + R.uniforms.offset), ("n_uniforms", "<i8", o + R.n_uniforms.offset)]
+    return np.dtype({"names": [x[0] for x in f], "formats": [x[1] for x in f], "offsets": [x[2] for x in f],
+                     "itemsize": C.sizeof(D)})
+
+
+_DESC_VIEW = _desc_view()
 
 
 class Plan:

@@ -204,6 +204,7 @@ class Holder:
         self._fmemo = {}  # formants converted once per object (a batch shares preset formant lists)
         self._amemo = {}  # anchors by value: one pair of buffers per distinct anchor set
         self._rmemo = {}  # injected draw arrays by identity (a batch often shares one stream)
+        self._ramemo = {}  # the same for random_addrs: (array, address, count)
 
     def max_lengths_of(self, x):
         """r_max_lengths(x), once per string or (live) object."""
@@ -284,6 +285,27 @@ class Holder:
         s.n_points = _abi.iptr(npnt)
         s.time, s.freq, s.amp, s.width = (_abi.dptr(c) for c in cat)
         return s
+
+    def random_addrs(self, normals=None, uniforms=None):
+        """(normals address, count, uniforms address, count) of injected draw arrays
+        for the bulk descriptor writer (0, 0 for an absent array); the arrays are
+        kept alive, float64 C-contiguous ones without a copy."""
+        out = []
+        for x in (normals, uniforms):
+            if x is None:
+                out += (0, 0)
+                continue
+            hit = self._ramemo.get(id(x))
+            if hit is None or hit[0] is not x:
+                if type(x) is np.ndarray and x.dtype == np.float64 and x.flags.c_contiguous and x.flags.writeable:
+                    p = _abi.C.addressof(_abi.C.c_double.from_buffer(x)) if x.shape[0] else 0
+                    n = x.shape[0]
+                else:
+                    a = self.arr(x)
+                    p, n = (a.ctypes.data if len(a) else 0), len(a)
+                hit = self._ramemo[id(x)] = (x, p, n)
+            out += (hit[1], hit[2])
+        return out
 
     def random(self, normals=None, uniforms=None, rng=None):
         """sg_random from injected arrays and/or a draw source `rng` (an object
@@ -386,6 +408,145 @@ _D8 = _abi.C.c_double * 8
 
 def C_double8():
     return _D8
+
+
+# ---------------------------------------------------------------- bulk writer
+# Marshalling a batch one ctypes field at a time cost ~90 us per call (a 16k-call
+# C5 chunk took longer to marshal than to plan natively). ArgsWriter keeps, per
+# call, one Python tuple of plain numbers (scalars, tempEffects, and the
+# (n, address, address) of every anchor and formant struct) and writes all calls
+# at the end through a structured numpy view of the sg_soundgen_args array, field
+# by field. Anchor and formant buffers are converted once per object (identity)
+# or value and kept alive by the Holder. The bytes written equal those of
+# fill_soundgen_args (tests/test_planner.py compares them).
+_ANCHOR_FIELDS = ("pitchAnchors", "pitchAnchorsGlobal", "amplAnchors", "amplAnchorsGlobal", "mouthAnchors",
+                  "noiseAnchors")
+_FORMANT_FIELDS = ("formants", "formantsNoise")
+_FORMANT_SUB = ("n_formants", "f1_index", "n_points", "time", "freq", "amp", "width")
+
+
+def _addr(p):
+    """Address held by a ctypes pointer (0 for NULL)."""
+    return _abi.C.cast(p, _abi.C.c_void_p).value or 0
+
+
+def _wide_dtypes():
+    S = _abi.sg_soundgen_args
+    names, formats, offsets = [], [], []
+
+    def add(name, fmt, off):
+        names.append(name)
+        formats.append(fmt)
+        offsets.append(off)
+    for f in _SG_SCALARS:
+        add(f, "<f8", getattr(S, f).offset)
+    add("tempEffects", ("<f8", (8,)), S.tempEffects.offset)
+    for f in _ANCHOR_FIELDS:
+        o = getattr(S, f).offset
+        add(f + ".n", "<i4", o + _abi.sg_anchors.n.offset)
+        add(f + ".time", "<u8", o + _abi.sg_anchors.time.offset)
+        add(f + ".value", "<u8", o + _abi.sg_anchors.value.offset)
+    for f in _FORMANT_FIELDS:
+        o = getattr(S, f).offset
+        for sub in _FORMANT_SUB:
+            add(f + "." + sub, "<i4" if sub in ("n_formants", "f1_index") else "<u8",
+                o + getattr(_abi.sg_formants, sub).offset)
+    add("invalidArgAction", "<i4", S.invalidArgAction.offset)
+    add("formantsNoise_rlen", "<i4", S.formantsNoise_rlen.offset)
+    view = np.dtype({"names": names, "formats": formats, "offsets": offsets, "itemsize": _abi.C.sizeof(S)})
+    packed = np.dtype({"names": names, "formats": formats})
+    return view, packed
+
+
+_WIDE_VIEW, _WIDE_PACKED = _wide_dtypes()
+_TE_DEFAULT = tuple(float(TEMP_EFFECTS_DEFAULT[k]) for k in TEMP_EFFECTS_ORDER)
+_DEFAULT_KEYS = SOUNDGEN_DEFAULTS.keys()
+
+
+class ArgsWriter:
+    """Collects soundgen() calls for one sg_soundgen_args array and writes them
+    all in finish() (fields equal to fill_soundgen_args')."""
+
+    def __init__(self, h, args_array, n):
+        self.h, self.args, self.n = h, args_array, n
+        self.rows, self.idx = [], []
+        self._tmemo = {}   # anchors by (identity, time_to): (object, (n, time, value))
+        self._ftmemo = {}  # formants by identity / string: (object, 7-tuple)
+
+    def _anchor(self, x, time_to):
+        if type(x) is dict:  # a well-formed data frame does not depend on time_to
+            hit = self._tmemo.get(id(x))
+            if hit is not None and hit[0] is x:
+                return hit[1]
+            t, v = x["time"], x["value"]
+            tt = t if isinstance(t, (list, tuple, np.ndarray)) else (t,)
+            vv = v if isinstance(v, (list, tuple, np.ndarray)) else (v,)
+            n = len(tt)
+            if n and n == len(vv):  # anchors_of' time-and-value buffer, built directly
+                a = np.fromiter((*tt, *vv), dtype=np.float64, count=2 * n)
+                self.h.keep.append(a)
+                p = _abi.C.addressof(_abi.C.c_double.from_buffer(a))
+                trip = (n, p, p + 8 * n)
+                self._tmemo[id(x)] = (x, trip)
+                return trip
+        key = (id(x), time_to)
+        hit = self._tmemo.get(key)
+        if hit is not None and hit[0] is x:
+            return hit[1]
+        trip = None
+        if trip is None:
+            s = self.h.anchors_of(x, time_to=time_to)
+            trip = (s.n, _addr(s.time), _addr(s.value))
+        self._tmemo[key] = (x, trip)
+        return trip
+
+    def _formants(self, x):
+        key = ("s", x) if isinstance(x, str) else ("o", id(x))
+        hit = self._ftmemo.get(key)
+        if hit is None or (key[0] == "o" and hit[0] is not x):
+            s = self.h.formants_of(x)
+            hit = self._ftmemo[key] = (x, (s.n_formants, s.f1_index, _addr(s.n_points), _addr(s.time),
+                                           _addr(s.freq), _addr(s.amp), _addr(s.width)))
+        return hit[1]
+
+    def add(self, i, kw):
+        unknown = kw.keys() - _DEFAULT_KEYS
+        if unknown:
+            raise TypeError("soundgen(): unused argument(s) %s" % sorted(unknown))
+        a = dict(SOUNDGEN_DEFAULTS)
+        a.update(kw)
+        vals = tuple(map(a.__getitem__, _SG_SCALARS))
+        if None in vals or "NA" in vals:
+            vals = tuple(map(_scalar, vals))
+        te_in = kw.get("tempEffects")
+        if te_in:
+            te = dict(TEMP_EFFECTS_DEFAULT)
+            te.update(te_in)
+            te = tuple(float(te[k]) for k in TEMP_EFFECTS_ORDER)
+        else:
+            te = _TE_DEFAULT
+        an = self._anchor
+        row = (vals + (te,) + an(a["pitchAnchors"], 1.0) + an(a["pitchAnchorsGlobal"], 1.0)
+               + an(a["amplAnchors"], 1.0) + an(a["amplAnchorsGlobal"], 1.0) + an(a["mouthAnchors"], 1.0)
+               + an(a["noiseAnchors"], a["sylLen"]) + self._formants(a["formants"])
+               + self._formants(a["formantsNoise"])
+               + (_ACTIONS[a["invalidArgAction"]], self.h.max_lengths_of(a["formantsNoise"])))
+        self.rows.append(row)
+        self.idx.append(i)
+
+    def finish(self):
+        if not self.rows:
+            return
+        packed = np.array(self.rows, dtype=_WIDE_PACKED)
+        view = np.frombuffer(self.args, dtype=_WIDE_VIEW, count=self.n)
+        idx = np.asarray(self.idx, dtype=np.int64)
+        whole = len(idx) == self.n
+        for name in _WIDE_PACKED.names:
+            if whole:
+                view[name] = packed[name]
+            else:
+                view[name][idx] = packed[name]
+        self.rows, self.idx = [], []
 
 
 def fill_harm_params(kw):

@@ -178,3 +178,68 @@ def test_precision_path_flags_ill_conditioned_presets():
         assert L.sg_set_fp64_policy(3, 300.0) != 0
     finally:
         L.sg_set_fp64_policy(1, 300.0)
+
+
+def _decode_args(s):
+    """Every field of an sg_soundgen_args, pointers followed to their values."""
+    import ctypes as C
+
+    from soundgen_beta_amd import _abi
+    out = []
+    for name, t in _abi.sg_soundgen_args._fields_:
+        v = getattr(s, name)
+        if t is _abi.sg_anchors:
+            out.append((v.n, [v.time[i] for i in range(v.n)], [v.value[i] for i in range(v.n)]))
+        elif t is _abi.sg_formants:
+            if v.n_formants == 0:
+                out.append((0, v.f1_index))
+                continue
+            npnt = [v.n_points[i] for i in range(v.n_formants)]
+            out.append((v.n_formants, v.f1_index, npnt,
+                        [[getattr(v, k)[i] for i in range(sum(npnt))] for k in ("time", "freq", "amp", "width")]))
+        elif t is C.c_double:
+            out.append(np.float64(v).tobytes())  # NaN-safe
+        elif name == "tempEffects":
+            out.append(np.asarray(list(v)).tobytes())
+        else:
+            out.append(v)
+    return out
+
+
+def test_bulk_marshalling_equals_per_call_fill():
+    """batch.Marshalled's bulk writer (rargs.ArgsWriter + the descriptor view)
+    fills the same argument values, draws and descriptors as the per-call
+    fill_soundgen_args, on a mixed batch: C3/C4/C5 calls, NA and numeric anchors,
+    vowel strings, tempEffects, harmonics calls and draw callbacks."""
+    import ctypes as C
+
+    import bench
+    from soundgen_beta_amd import rargs
+    rng = np.random.default_rng(3)
+    calls = bench.c5_calls(300)[::3] + bench.c3_calls(12) + bench.c4_calls(6)
+    calls += [{"kind": "soundgen", "args": {"pitchAnchors": [120, 180, 90], "noiseAnchors": None,
+                                            "tempEffects": {"formDrift": 0.5}, "formants": "aoi",
+                                            "amplAnchors": {"time": 0, "value": 50}}},
+              {"kind": "harmonics", "pitch": np.full(300, 150.0), "params": {"samplingRate": 44100}},
+              {"kind": "soundgen", "args": {"sylLen": 100, "temperature": 0.1}, "rng": rng},
+              {"kind": "soundgen", "args": {"sylLen": 120, "pitchAnchors": {"time": [0, 1], "value": [200, 300]}},
+               "normals": [0.1, -0.2], "uniforms": np.zeros(0)}]
+    m = batch.Marshalled(calls)
+    h = rargs.Holder()
+    for i, c in enumerate(calls):
+        d = m.descs[i]
+        if c.get("kind") == "harmonics":
+            assert d.kind == 1
+            continue
+        assert d.kind == 0
+        assert _decode_args(d.args.contents) == _decode_args(rargs.fill_soundgen_args(h, c.get("args", {})))
+        for key, p, n in (("normals", d.random.normals, d.random.n_normals),
+                          ("uniforms", d.random.uniforms, d.random.n_uniforms)):
+            x = c.get(key)
+            if x is None:
+                assert n == 0
+                continue
+            x = np.asarray(x, dtype=np.float64)
+            assert n == len(x)
+            if n:
+                assert np.array_equal(np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_double)), (n,)), x)
