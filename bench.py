@@ -294,6 +294,8 @@ def main():
     ap.add_argument("--calls", type=int, default=0, help="calls in the whole batch (default: the config's)")
     ap.add_argument("--plan-chunk", type=int, default=16384,
                     help="calls per plan (each uploaded, then its host copy freed)")
+    ap.add_argument("--no-plan-ramp", action="store_true",
+                    help="equal plan chunks (default: a first chunk of plan-chunk / 4 calls, a short pipeline fill)")
     ap.add_argument("--no-d2h", action="store_true",
                     help="profiling runs only: the timed steps leave the outputs in HBM (no copy kernels beside them)")
     ap.add_argument("--device-steps", type=int, default=5,
@@ -336,15 +338,16 @@ def main():
     first_msg = None
     # chunk k + 1 plans on the host while chunk k uploads (batch.plan_uploaded)
     plan_stages = []
-    for p, a in batch.plan_uploaded(mine, ctx, args.plan_chunk, plan_stages):
+    sizes = batch.chunk_sizes(len(mine), args.plan_chunk, ramp=not args.no_plan_ramp)
+    for p, a in batch.plan_uploaded(mine, ctx, sizes, plan_stages):
         bad = np.nonzero(p.status)[0]
         failed += len(bad)
         if len(bad) and first_msg is None:
             first_msg = p.message(int(bad[0]))
-        plans.append((p, base, idx[a:a + args.plan_chunk]))
+        plans.append((p, base, idx[a:a + p.n]))
         base += (p.total + 63) // 64 * 64
         if rank == 0:
-            print("bench: planned + uploaded %d/%d calls (%.1f s)" % (min(a + args.plan_chunk, len(mine)), len(mine),
+            print("bench: planned + uploaded %d/%d calls (%.1f s)" % (a + p.n, len(mine),
                                                                       time.perf_counter() - t_plan), file=sys.stderr)
     t_plan = time.perf_counter() - t_plan
     if failed:

@@ -262,6 +262,13 @@ int sg_set_fp64_policy(int32_t mode, double rho);
  * per-glottal-cycle parameters, 1 built on the host and uploaded (the
  * reference-order host restatement; tests compare the two). */
 int sg_set_amp_policy(int32_t host_built);
+/* Process-wide handling of generateNoise()'s uniforms read from injected draw
+ * arrays, for later sg_plan_batch calls: 1 (default) the planner records each
+ * noise item's range of the caller's array, copies the union of the ranges
+ * once and the device expands the items at upload; 0 each item's draws are
+ * copied into the plan (the same values either way; tests compare the two).
+ * The arrays are read during sg_plan_batch only. */
+int sg_set_uniform_gather(int32_t on);
 /* The amplitude blocks sg_amp_build writes at upload, evaluated on the host by
  * the same code (tests; no device needed): n = sg_plan_amp_count(plan) floats. */
 int64_t sg_plan_amp_count(const sg_plan* plan);

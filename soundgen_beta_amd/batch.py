@@ -174,9 +174,22 @@ def execute_plans(ctx, plans, d_out_ptrs, stream_ptr=None):
                  ctx.ptr)
 
 
+def chunk_sizes(n, chunk, ramp=True):
+    """Chunk sizes for plan_uploaded: `chunk` calls each; with ramp, a first chunk
+    of chunk / 4 calls, so that the pipeline's fill (marshal + plan of the first
+    chunk, nothing to overlap with) is short."""
+    sizes = []
+    if ramp and n > chunk:
+        sizes.append(max(1, chunk // 4))
+    while sum(sizes) < n:
+        sizes.append(min(chunk, n - sum(sizes)))
+    return sizes
+
+
 def plan_uploaded(calls, ctx, chunk, timings=None):
-    """Plan `calls` in chunks of `chunk` and upload each plan, yielding
-    (plan, first call index) in order. A three-stage pipeline: while chunk k
+    """Plan `calls` in chunks of `chunk` calls (an int, or a list of chunk sizes)
+    and upload each plan, yielding (plan, first call index) in order. A
+    three-stage pipeline: while chunk k
     uploads (main thread), chunk k + 1 is planned natively and chunk k + 2 is
     marshalled (two workers). The native calls run without the GIL (ctypes), so
     only marshalling holds it. Each yielded plan is uploaded and its host arrays
@@ -184,13 +197,14 @@ def plan_uploaded(calls, ctx, chunk, timings=None):
     the main thread's wait for the planner."""
     import time
     from concurrent.futures import ThreadPoolExecutor
-    starts = list(range(0, len(calls), chunk))
-    if not starts:
+    sizes = list(chunk) if isinstance(chunk, (list, tuple)) else chunk_sizes(len(calls), chunk, ramp=False)
+    starts = [sum(sizes[:i]) for i in range(len(sizes))]
+    if not starts or not len(calls):
         return
     stage = {}
 
     def piece(i):
-        return calls[starts[i]:starts[i] + chunk]
+        return calls[starts[i]:starts[i] + sizes[i]]
 
     def marshal(i):
         t = time.perf_counter()

@@ -72,9 +72,9 @@ int guarded(sg_ctx* ctx, F&& f) {
 // Rolls a Batch back to a checkpoint when planning one call fails.
 struct Checkpoint {
   size_t segs, epochs, knots, ampsrc, ampcols, ampjobs, tasks, pieces, syls, syl_tiles, cknots, fl, items;
-  size_t frames[2], olas[2], mixes[2], copies, eterms, ecols, envjobs, frames64;
+  size_t frames[2], olas[2], mixes[2], copies, eterms, ecols, envjobs, frames64, ugath;
   int64_t amp_total, w_total, harm_samples, harm_terms, harm_amp_bytes, fft_frames, fs_total, fe_total, w64_total, fh_total,
-      hp_bouts, hp_noise_bouts;
+      hp_bouts, hp_noise_bouts, fu_total;
   double fft_flops;
   explicit Checkpoint(const sg::Batch& B)
       : segs(B.segs.size()), epochs(B.epochs.size()), knots(B.knots.size()), ampsrc(B.ampsrc.size()),
@@ -86,6 +86,8 @@ struct Checkpoint {
         fft_frames(B.fft_frames), fs_total(B.fs_total), fe_total(B.fe_total), w64_total(B.w64_total),
         fh_total(B.fh_total), hp_bouts(B.hp_bouts), hp_noise_bouts(B.hp_noise_bouts), fft_flops(B.fft_flops) {
     frames64 = B.frames64.size();
+    ugath = B.ugath.size();
+    fu_total = B.fu_total;
     for (int p = 0; p < 2; ++p) { frames[p] = B.frames[p].size(); olas[p] = B.olas[p].size(); mixes[p] = B.mixes[p].size(); }
   }
   void restore(sg::Batch& B) const {
@@ -102,6 +104,8 @@ struct Checkpoint {
     B.eterms.resize(eterms); B.ecols.resize(ecols); B.envjobs.resize(envjobs); B.fe_total = fe_total;
     B.frames64.resize(frames64); B.w64_total = w64_total; B.fh_total = fh_total; B.hp_bouts = hp_bouts;
     B.hp_noise_bouts = hp_noise_bouts;
+    B.ugath.resize(ugath);
+    B.fu_total = fu_total;
     B.fft_flops = fft_flops;
   }
 };
@@ -213,7 +217,7 @@ int plan_threads(int64_t n_calls) {
 struct PartBase {
   int64_t out, fs, fl, w, amp, asrc, acol, ajob, knot, ck, task, seg, syl, piece, st, item, copy, call, epoch, fe, term,
       col, job;
-  int64_t w64, fh, fr64;
+  int64_t w64, fh, fr64, fu, ug;
   int64_t fr[2], ola[2], mix[2];
 };
 
@@ -258,6 +262,7 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
     c.fe += S.fe_total; c.term += (int64_t)S.eterms.size(); c.col += (int64_t)S.ecols.size();
     c.job += (int64_t)S.envjobs.size();
     c.w64 += S.w64_total; c.fh += S.fh_total; c.fr64 += (int64_t)S.frames64.size();
+    c.fu += S.fu_total; c.ug += (int64_t)S.ugath.size();
     D.hp_bouts += S.hp_bouts;
     D.hp_noise_bouts += S.hp_noise_bouts;
     for (int ph = 0; ph < 2; ++ph) {
@@ -270,6 +275,7 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
   }
   D.total_out = c.out; D.fs_total = c.fs; D.w_total = c.w; D.fe_total = c.fe;
   D.w64_total = c.w64; D.fh_total = c.fh; D.frames64.resize(c.fr64);
+  D.fu_total = c.fu; D.ugath.resize(c.ug);
   D.ecols.resize(c.col); D.envjobs.resize(c.job);
   D.call_len.resize(c.call); D.call_off.resize(c.call); D.call_status.resize(c.call); D.call_msg.resize(c.call);
   D.call_fp64.resize(c.call); D.call_rows.resize(c.call); D.call_flops.resize(c.call);
@@ -327,7 +333,8 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
     }
     for (int ph = 0; ph < 2; ++ph) {
       for (auto& f : S.frames[ph]) {
-        f.src += ph == 0 ? b.fl : b.fs;  // noise: uniforms in fl; filter: the sound in fs
+        // noise: uniforms in fl, or gathered (uniform area, encoded); filter: the sound in fs
+        f.src = ph == 1 ? f.src + b.fs : (f.src < 0 ? f.src - b.fu : f.src + b.fl);
         f.env = f.env < 0 ? f.env - b.fe : f.env + b.fl;  // envelope area (encoded) or fl
         if (f.dst >= 0) f.dst += b.fs;
       }
@@ -347,7 +354,8 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
       }
     }
     for (auto& f : S.frames64) {
-      f.src += f.mode == SG_F64_NOISE ? b.fl : b.fh;  // uniforms (fl) / pre-filter sound (fh)
+      // uniforms (fl, or the uniform area encoded) / pre-filter sound (fh)
+      f.src = f.mode == SG_F64_NOISE ? (f.src < 0 ? f.src - b.fu : f.src + b.fl) : f.src + b.fh;
       f.env = f.env < 0 ? f.env - b.fe : f.env + b.fl;
       f.dst += b.fs;
     }
@@ -359,6 +367,8 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
     }
     for (auto& x : S.copies) { x.fl_off += b.fl; x.fs_off += b.fs; }
     for (auto& j : S.envjobs) { j.out += b.fe; j.term0 += b.term; j.col0 += b.col; }
+    for (auto& g : S.ugath) g.dst += b.fu;
+    put(D.ugath, S.ugath, b.ug);
     auto move = [&](auto& x, auto& v, int64_t at) {
       x.blocks[k] = std::move(v);
       x.base[k] = at;
@@ -588,6 +598,7 @@ int sg_plan_release_host(sg_plan* plan) {
   drop(B.syl_tiles); drop(B.fin_tiles); drop(B.copy_tiles); drop(B.ptiles); drop(B.cknots); drop(B.fl);
   drop(B.fgroups); drop(B.olasegs); drop(B.items); drop(B.mixes_dev); drop(B.eterms); drop(B.ecols); drop(B.envjobs);
   for (int ph = 0; ph < 2; ++ph) { drop(B.frames[ph]); drop(B.frame_geom[ph]); drop(B.olas[ph]); drop(B.mixes[ph]); }
+  drop(B.ustream); drop(B.ujobs);
   plan->host_released = true;
   return SG_OK;
 }

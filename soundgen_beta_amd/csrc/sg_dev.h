@@ -308,6 +308,13 @@ struct SgOlaTile {
   int64_t q0;  // first sample of the tile (relative to `first`)
 };
 
+// Noise uniforms of one noise item copied on the device at upload (sg_ugather):
+// fl[dst + j] = us[src + j] for j < n, 0 for n <= j < ntot (us: the union of the
+// injected draw ranges the batch reads, as floats)
+struct SgUJob {
+  int64_t src, dst, n, ntot;
+};
+
 // Noise of one syllable, as generateNoise() returns it (R/source.R:124-131):
 // matchLengths()-trimmed OLA output / its max * 2^(dB/10) contour, faded.
 struct SgNoiseItem {

@@ -78,8 +78,10 @@ struct Layout {
     envjobs = take(B.envjobs.size() * sizeof(SgEnvJob));
     envtasks = take(B.envtasks.size() * sizeof(SgEnvTask));
     elog2 = take(B.elog2.size() * sizeof(double));
-    // uploaded floats, then the device-computed envelopes from fe_base on
-    fl = take((size_t)std::max<int64_t>(bulk_size(B.fl_x, B.fl), B.fe_base + B.fe_total) * sizeof(float));
+    // uploaded floats, then the device-computed envelopes from fe_base on, then the
+    // noise uniforms expanded at upload from fu_base on
+    fl = take((size_t)std::max<int64_t>(std::max<int64_t>(bulk_size(B.fl_x, B.fl), B.fe_base + B.fe_total),
+                                        B.fu_base + B.fu_total) * sizeof(float));
     fs = take((size_t)B.fs_total * sizeof(float) + 256);
     total = o;
   }
@@ -374,7 +376,18 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   cp(D.envtasks, B.envtasks.data(), B.envtasks.size() * sizeof(SgEnvTask));
   cp(D.elog2, B.elog2.data(), B.elog2.size() * sizeof(double));
   launch_amp_build(D, (int64_t)B.ampjobs.size(), s);  // the amplitude blocks, from the jobs just copied
+  // gathered noise uniforms: the union of the draw ranges and the item jobs in a
+  // temporary buffer, expanded into the uniform area
+  void* ug = nullptr;
+  if (!B.ujobs.empty()) {
+    const size_t ub = up(B.ustream.size() * sizeof(float)), jb = B.ujobs.size() * sizeof(SgUJob);
+    HIPCHK(hipMalloc(&ug, ub + jb));
+    cp(ug, B.ustream.data(), B.ustream.size() * sizeof(float));
+    cp((char*)ug + ub, B.ujobs.data(), jb);
+    launch_ugather((const SgUJob*)((char*)ug + ub), (int64_t)B.ujobs.size(), (const float*)ug, D.fl, s);
+  }
   HIPCHK(hipStreamSynchronize(s));
+  if (ug) (void)hipFree(ug);
   while (D.ev_slice.size() < B.slices.size()) {
     hipEvent_t e;
     HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));

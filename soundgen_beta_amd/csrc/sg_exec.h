@@ -109,6 +109,7 @@ void device_execute_spec(const Batch& B, const DevicePlan& D, float* d_out, hipS
 
 // launchers (sg_harm.hip)
 void launch_amp_build(const DevicePlan& D, int64_t n_jobs, hipStream_t s);
+void launch_ugather(const SgUJob* jobs, int64_t n_jobs, const float* us, float* fl, hipStream_t s);
 void launch_sine_bank(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s);
 void launch_sine_bank_pairs(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s);
 void launch_sine_bank_tall(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s);

@@ -1376,6 +1376,14 @@ extern "C" __global__ __launch_bounds__(SG_F64_THREADS) void sg_fft_frames64(
   }
 }
 
+// Gathered noise uniforms (upload time): one workgroup per noise item copies its
+// draws from the union of the injected ranges into the uniform area, zero-padded
+extern "C" __global__ __launch_bounds__(256) void sg_ugather(const SgUJob* __restrict__ jobs,
+                                                             const float* __restrict__ us, float* __restrict__ fl) {
+  const SgUJob J = jobs[blockIdx.x];
+  for (int64_t j = threadIdx.x; j < J.ntot; j += 256) fl[J.dst + j] = j < J.n ? us[J.src + j] : 0.f;
+}
+
 // HP: the pre-filter sound of an fp64 bout: fp64 sum into fh (X.to_fs == 2), voiced
 // items (SG_ITEM_F64) read from fh, noise items from fs
 template <bool HP>
@@ -1604,6 +1612,13 @@ void launch_mix(const DevicePlan& D, int64_t t0, int64_t n_tiles, float* out, hi
   hipLaunchKernelGGL(sg_mix, dim3((unsigned)n_tiles), dim3(256), 0, s, D.mixtiles + t0, D.mixes, D.items, D.olamax,
                      D.cknots, D.fl, D.fs, out);
   SG_LAUNCHED("sg_mix");
+}
+void launch_ugather(const SgUJob* jobs, int64_t n_jobs, const float* us, float* fl, hipStream_t s) {
+  for (int64_t j0 = 0; j0 < n_jobs; j0 += 1 << 30) {
+    const int64_t n = std::min<int64_t>(n_jobs - j0, 1 << 30);
+    hipLaunchKernelGGL(sg_ugather, dim3((unsigned)n), dim3(256), 0, s, jobs + j0, us, fl);
+    SG_LAUNCHED("sg_ugather");
+  }
 }
 }  // namespace sg
 

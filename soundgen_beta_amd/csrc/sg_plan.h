@@ -164,6 +164,20 @@ struct Batch {
   std::vector<SgEnvJob> envjobs;
   int64_t fe_total = 0, fe_base = 0;
   std::vector<SgEnvTask> envtasks;  // derived (finalize_spec)
+  // generateNoise()'s runif(nr * nc) read from an injected draw array are not
+  // copied per item: the item records the caller's range and its offset in the
+  // uniform area (fu_total floats after fu_base, device-only, after the envelope
+  // area); finalize_spec copies the union of the ranges once (ustream, floats) and
+  // sg_ugather expands the items at upload. Until then a noise frame's src < 0
+  // encodes uniform-area offset -(src + 1).
+  struct UGather {
+    const double* src;
+    int64_t n, dst, ntot;
+  };
+  std::vector<UGather> ugath;
+  int64_t fu_total = 0, fu_base = 0;
+  std::vector<float> ustream;  // derived (finalize_spec)
+  std::vector<SgUJob> ujobs;   // derived (finalize_spec)
   std::vector<double> elog2;        // derived: log2(k), k = 1..max nr
   // ---- per call ----
   std::vector<int64_t> call_len, call_off;

@@ -5,6 +5,7 @@
 // Lengths, frame starts and trims are integers computed here in fp64 with
 // R's operation order; per-sample work runs in sg_fft.hip.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <complex>
 #include <cstdio>
@@ -44,6 +45,19 @@ std::shared_ptr<const vec> trig_table(int kind, int n, Make&& make) {
 }
 constexpr int kFftSlots = 8192;  // complex points per FFT workgroup (sg_fft.hip SG_FFT_SLOTS)
 }  // namespace
+// 0: noise uniforms copied into fl per item by the planner (the pre-round-3
+// path); 1 (default; SG_UGATHER=0 in the environment turns it off) gathered on
+// the device at upload. sg_set_uniform_gather changes it (tests compare the two).
+std::atomic<int> g_ugather{-1};
+bool ugather_on() {
+  int v = g_ugather.load();
+  if (v < 0) {
+    const char* e = std::getenv("SG_UGATHER");
+    v = (e && std::atoi(e) == 0) ? 0 : 1;
+    g_ugather.store(v);
+  }
+  return v == 1;
+}
 
 int64_t fs_alloc(Batch& B, int64_t n) {
   const int64_t o = B.fs_total;
@@ -413,17 +427,28 @@ bool plan_noise(Batch& B, Rng& R, int64_t len, const sg_anchors& noiseAnchors, d
   // (nr = wl / 2 is x.5 for an odd wl: floor(nr * nc) draws, matrix(nrow = nr)
   // keeps as.integer(nr) rows of them)
   const int64_t ndraw = (int64_t)((double)wl / 2 * (double)nc);
-  const int64_t u_off = bulk_size(B.fl_x, B.fl), u_loc = (int64_t)B.fl.size();
   const int64_t nu = std::min<int64_t>(ndraw, nr * nc);
-  B.fl.resize((size_t)(u_loc + (nr * nc + 3) / 4 * 4));  // the draws, then zeros to the 16-B pad
-  R.unif_f32(nu, B.fl.data() + u_loc);
-  std::fill(B.fl.begin() + u_loc + nu, B.fl.end(), 0.f);
-  if (ndraw > nr * nc) R.unif_f32(ndraw - nr * nc, nullptr);
+  int64_t u_off;
+  if (ugather_on() && R.s && R.s->uniforms && R.iu + ndraw <= R.s->n_uniforms) {
+    // every draw from the injected array: recorded, expanded on the device at upload
+    const int64_t at = B.fu_total;
+    B.fu_total += (nr * nc + 63) / 64 * 64;
+    B.ugath.push_back(Batch::UGather{R.s->uniforms + R.iu, nu, at, (nr * nc + 3) / 4 * 4});
+    R.iu += ndraw;
+    u_off = -(at + 1);  // frame c: -(at + c nr + 1)
+  } else {
+    u_off = bulk_size(B.fl_x, B.fl);
+    const int64_t u_loc = (int64_t)B.fl.size();
+    B.fl.resize((size_t)(u_loc + (nr * nc + 3) / 4 * 4));  // the draws, then zeros to the 16-B pad
+    R.unif_f32(nu, B.fl.data() + u_loc);
+    std::fill(B.fl.begin() + u_loc + nu, B.fl.end(), 0.f);
+    if (ndraw > nr * nc) R.unif_f32(ndraw - nr * nc, nullptr);
+  }
   const bool fused = fusable(B.geoms[gi], (double)wl * (100 - overlap) / 100);
   const int64_t fr = fused ? 0 : fs_alloc(B, nc * wl);
   for (int64_t c = 0; c < nc; ++c) {
     SgFrame f{};
-    f.src = u_off + c * nr;
+    f.src = u_off < 0 ? u_off - c * nr : u_off + c * nr;
     const int64_t col = ((int64_t)fri[c] - 1) * nr;
     f.env = dev ? filt_off - col : filt_off + col;
     f.dst = fused ? -1 : fr + c * wl;
@@ -744,9 +769,42 @@ void finalize_spec(Batch& B) {
   // envelope area after the uploaded floats: decode frame envelope offsets;
   // sg_spec_env wave tasks of SG_ENV_COLS columns
   B.fe_base = (bulk_size(B.fl_x, B.fl) + 63) / 64 * 64;
+  B.fu_base = B.fe_base + (B.fe_total + 63) / 64 * 64;
   for (int ph = 0; ph < 2; ++ph)
-    for (SgFrame& f : B.frames[ph])
+    for (SgFrame& f : B.frames[ph]) {
       if (f.env < 0) f.env = B.fe_base + (-f.env - 1);
+      if (ph == 0 && f.src < 0) f.src = B.fu_base + (-f.src - 1);
+    }
+  // gathered noise uniforms: the union of the callers' draw ranges, once, as floats
+  // (C5: every call reads a window of one stream); one device job per item
+  B.ustream.clear();
+  B.ujobs.assign(B.ugath.size(), SgUJob{});
+  if (!B.ugath.empty()) {
+    std::vector<int64_t> ord(B.ugath.size());
+    for (size_t i = 0; i < ord.size(); ++i) ord[i] = (int64_t)i;
+    auto lo = [&](int64_t i) { return (uintptr_t)B.ugath[i].src; };
+    std::sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) { return lo(a) < lo(b); });
+    size_t k = 0;
+    while (k < ord.size()) {
+      const double* r0 = B.ugath[ord[k]].src;
+      uintptr_t end = lo(ord[k]) + 8 * (uintptr_t)B.ugath[ord[k]].n;
+      size_t k1 = k + 1;
+      while (k1 < ord.size() && lo(ord[k1]) <= end) {
+        end = std::max<uintptr_t>(end, lo(ord[k1]) + 8 * (uintptr_t)B.ugath[ord[k1]].n);
+        ++k1;
+      }
+      const int64_t base = (int64_t)B.ustream.size(), n = (int64_t)((end - (uintptr_t)r0) / 8);
+      B.ustream.resize((size_t)(base + n));
+      for (int64_t j = 0; j < n; ++j) B.ustream[(size_t)(base + j)] = (float)r0[j];
+      for (size_t q = k; q < k1; ++q) {
+        const Batch::UGather& g = B.ugath[ord[q]];
+        B.ujobs[ord[q]] = SgUJob{base + (g.src - r0), B.fu_base + g.dst, g.n, g.ntot};
+      }
+      k = k1;
+    }
+  }
+  B.ugath.clear();
+  B.ugath.shrink_to_fit();
   // fp64 frames: one root table W_N^t per window length (sg_roots64)
   B.roots64_wl.clear();
   B.roots64_off.clear();
@@ -760,6 +818,7 @@ void finalize_spec(Batch& B) {
                      B.frames64.begin();
   for (SgFrame64& f : B.frames64) {
     if (f.env < 0) f.env = B.fe_base + (-f.env - 1);
+    if (f.mode == SG_F64_NOISE && f.src < 0) f.src = B.fu_base + (-f.src - 1);
     size_t w = 0;
     while (w < B.roots64_wl.size() && B.roots64_wl[w] != f.wl) ++w;
     if (w == B.roots64_wl.size()) {
@@ -1017,3 +1076,9 @@ void finalize_spec(Batch& B) {
 }
 
 }  // namespace sg
+
+extern "C" int sg_set_uniform_gather(int32_t on) {
+  if (on < 0 || on > 1) return SG_E_ARG;
+  sg::g_ugather.store(on);
+  return SG_OK;
+}

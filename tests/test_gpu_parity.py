@@ -243,3 +243,27 @@ def test_execute_plans_equals_per_plan_execute():
         batch.execute_plans(ctx, [plans[0], plans[0]], [outs[0].data_ptr()] * 2, sptr)
     for p in plans:
         p.close()
+
+
+def test_gathered_noise_uniforms_byte_equal():
+    """generateNoise()'s uniforms expanded on the device at upload from the union
+    of the injected draw ranges (sg_set_uniform_gather(1), the default) synthesize
+    the same bytes as the per-item host copy (0): C5 calls reading windows of one
+    stream, C3 vowels with breathing noise, and calls on separate arrays."""
+    import bench
+    from soundgen_beta_amd import batch, native
+    rng = np.random.default_rng(11)
+    calls = bench.c5_calls(400)[::2] + bench.c3_calls(8)
+    calls += [{"kind": "soundgen", "args": {"sylLen": 300, "noiseAnchors": {"time": [0, 300], "value": [-20, -30]},
+                                            "samplingRate": 44100, "addSilence": 0},
+               "normals": rng.standard_normal(20000), "uniforms": rng.uniform(size=200000)} for _ in range(3)]
+    L = native.lib()
+    outs = []
+    for on in (0, 1):
+        assert L.sg_set_uniform_gather(on) == 0
+        try:
+            outs.append(batch.synthesize(calls))
+        finally:
+            L.sg_set_uniform_gather(1)
+    for a, b in zip(*outs):
+        assert a.tobytes() == b.tobytes()

@@ -243,3 +243,26 @@ def test_bulk_marshalling_equals_per_call_fill():
             assert n == len(x)
             if n:
                 assert np.array_equal(np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_double)), (n,)), x)
+
+
+def test_uniform_gather_plans_the_same_calls():
+    """With the noise uniforms gathered at upload (sg_set_uniform_gather(1)) the
+    plan's lengths, offsets, status and kernel work equal the per-item copy's
+    (the GPU test compares the synthesized bytes)."""
+    import bench
+    from soundgen_beta_amd import native
+    L = native.lib()
+    calls = bench.c5_calls(240) + bench.c3_calls(6)
+    res = []
+    for on in (0, 1):
+        assert L.sg_set_uniform_gather(on) == 0
+        try:
+            p = batch.Plan(calls, None)
+            res.append((p.lengths.copy(), p.offsets.copy(), p.status.copy(), p.stats()))
+            p.close()
+        finally:
+            L.sg_set_uniform_gather(1)
+    (l0, o0, s0, st0), (l1, o1, s1, st1) = res
+    assert np.array_equal(l0, l1) and np.array_equal(o0, o1) and np.array_equal(s0, s1)
+    assert st0 == st1
+    assert L.sg_set_uniform_gather(2) != 0
