@@ -29,13 +29,24 @@
 #endif
 #ifndef SG_PF_AHEAD
 #define SG_PF_AHEAD 0  // build knob (filter kernel): 1 the next frame's inputs before this frame's inverse FFT;
-                       // 2 the next frame's sound after it, this frame's envelope before the forward FFT
+                       // 2 the next frame's sound after it, this frame's envelope before the forward FFT;
+                       // 3 the next frame's envelope right after this frame's untangle; 4: 3 and the next
+                       // frame's sound after this frame's inverse FFT
 #endif
 #ifndef SG_PF_AHEAD_NOISE
 #define SG_PF_AHEAD_NOISE 0  // the same for sg_stft_ola_noise (2: the next frame's input after the inverse FFT)
 #endif
 #ifndef SG_UNT_HOIST
 #define SG_UNT_HOIST 0  // build knob: the untangle reads all its LDS pairs before its first write (r03i A/B: neutral)
+#endif
+#ifndef SG_UNT_PACK
+#define SG_UNT_PACK 1  // build knob: the filter untangle + inverse packing in packed (re, im) arithmetic
+#endif
+#ifndef SG_NOISE_PACK
+#define SG_NOISE_PACK 1  // build knob: the noise spectrum's inverse packing from the real products directly
+#endif
+#ifndef SG_HAN_SCALED
+#define SG_HAN_SCALED 1  // build knob: the LDS hanning table pre-scaled by 1 / wl (one packed FMA per windowed pair)
 #endif
 #ifndef SG_OUT_BATCH
 #define SG_OUT_BATCH 1  // build knob: output samples and the next carry read from LDS in batches (no per-sample waits)
@@ -76,6 +87,16 @@ __device__ __forceinline__ v2 add_miq(v2 p, v2 q) {  // p - i q = (p.x + q.y, p.
 __device__ __forceinline__ v2 add_piq(v2 p, v2 q) {  // p + i q = (p.x - q.y, p.y + q.x)
   v2 r;
   __asm__("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(p), "v"(q));
+  return r;
+}
+__device__ __forceinline__ v2 add_conjb(v2 a, v2 b) {  // a + conj b = (a.x + b.x, a.y - b.y)
+  v2 r;
+  __asm__("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ v2 sub_conjb(v2 a, v2 b) {  // a - conj b = (a.x - b.x, a.y + b.y)
+  v2 r;
+  __asm__("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) { return F(vmul(V(a), V(b))); }
@@ -793,6 +814,23 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
           A[half] = a;
         }
       } else {
+#if SG_UNT_PACK
+        // packed form (v_pk_* on (re, im)): with s = Z_k + conj Z_{M-k}, d = Z_k - conj Z_{M-k},
+        // p = d W_N^k: 2 X_k = s - i p and 2 X_{M-k} = conj(s + i p) (W_N^{M-k} = -conj W_N^k:
+        // no second twiddle read); the inverse packing Z'_k = e + i q, Z'_{M-k} = conj(e - i q)
+        // with e = Y_k + conj Y_{M-k}, q = (Y_k - conj Y_{M-k}) conj W_N^k (pack_pair)
+        const v2 a = V(za), b = V(zb);
+        const v2 s = add_conjb(a, b), d = sub_conjb(a, b);
+        const v2 wk = V(twN[kk]);
+        const v2 p = vmul(d, wk);
+        const v2 yk = add_miq(s, p) * splat(0.5f * ek);
+        const v2 um = add_piq(s, p) * splat(0.5f * em);  // conj Y_{M-k}
+        const v2 q = vmulc(yk - um, wk);
+        const v2 e = yk + um;
+        const v2 zk = add_piq(e, q), zm = add_miq(e, q);
+        A[kk] = F(zk);
+        A[km] = make_float2(zm.x, -zm.y);
+#else
         const float2 xk = X_at(za, zb, kk), xm = X_at(zb, za, km);
         const float2 yk = make_float2(xk.x * ek, xk.y * ek);
         const float2 ym = make_float2(xm.x * em, xm.y * em);
@@ -800,6 +838,7 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
         pack_pair(yk, ym, twN[kk], a, b);
         A[kk] = a;
         A[km] = b;
+#endif
       }
     }
   } else {  // SG_FRAME_NOISE: real spectrum u x filter, packed
@@ -817,11 +856,21 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
           A[half] = a;
         }
       } else if (k < M - k) {
+#if SG_NOISE_PACK
+        // pack_pair of the real Y_k = a, Y_{M-k} = b: with e = a + b, r = a - b,
+        // Z'_k = (e + r Im W, r Re W), Z'_{M-k} = (e - r Im W, r Re W)
+        const float a = P.a[i].x * P.b(i).x, b = P.a[i].y * P.b(i).y;
+        const float2 w = twN[k];
+        const float e = a + b, r = a - b, im = r * w.x;
+        A[k] = make_float2(fmaf(r, w.y, e), im);
+        A[M - k] = make_float2(fmaf(-r, w.y, e), im);
+#else
         const float2 yk = make_float2(P.a[i].x * P.b(i).x, 0.f), ym = make_float2(P.a[i].y * P.b(i).y, 0.f);
         float2 a, b;
         pack_pair(yk, ym, twN[k], a, b);
         A[k] = a;
         A[M - k] = b;
+#endif
       }
     }
   }
@@ -852,7 +901,7 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
   const SgOla& O = olas[S.ola];
   float2* A = twS + M * (4 + w);
   const float* Af = reinterpret_cast<const float*>(A);
-  const float invN = 1.f / (float)N;
+  [[maybe_unused]] const float invN = 1.f / (float)N;  // the windowing without SG_HAN_SCALED
   const int hi = O.hi;
   const double h = O.h;
   auto bstart = [&](int f) -> int { return hi > 0 ? f * hi : (int)floor((double)f * h); };
@@ -875,10 +924,14 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
   if constexpr (PFA != 0) {
     int Mk = M;
     if (!CM) __asm__ __volatile__("" : "+s"(Mk));
-    frame_prefetch<PFA == 2 ? 1 : 0>(P, frames[S.fdev], mode, Mk, fl, fs, lane);
+    frame_prefetch<PFA == 2 ? 1 : (PFA == 3 ? 2 : 0)>(P, frames[S.fdev], mode, Mk, fl, fs, lane);  // 4: both
   }
   for (int k = 0; k < S.nf; ++k) {
-    if constexpr (PFA == 0) {
+    if constexpr (PFA == 3) {  // this frame's sound; its envelope is in flight since the previous untangle
+      int Mk = M;
+      if (!CM) __asm__ __volatile__("" : "+s"(Mk));
+      frame_prefetch<1>(P, frames[S.fdev + k], mode, Mk, fl, fs, lane);
+    } else if constexpr (PFA == 0) {
       int Mk = M;
       if (!CM) __asm__ __volatile__("" : "+s"(Mk));
       frame_prefetch(P, frames[S.fdev + k], mode, Mk, fl, fs, lane);
@@ -888,6 +941,15 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
       frame_prefetch<2>(P, frames[S.fdev + k], mode, Mk, fl, fs, lane);
     }
     frame_front<CM, R0, R1, R2>(A, P, mode, g, twS, twN, ham, lane SG_ST_ARGS);
+    if constexpr (PFA == 3 || PFA == 4) {
+      // the next frame's envelope: in flight during this frame's inverse FFT, overlap-add
+      // and the next forward FFT (its registers take the place the forward FFT's env held)
+      if (k + 1 < S.nf) {
+        int Mk = M;
+        if (!CM) __asm__ __volatile__("" : "+s"(Mk));
+        frame_prefetch<2>(P, frames[S.fdev + k + 1], mode, Mk, fl, fs, lane);
+      }
+    }
     if constexpr (PFA == 1) {
       // the next frame's inputs are in flight during this frame's inverse FFT and overlap-add
       if (k + 1 < S.nf) {
@@ -901,12 +963,22 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
     else fft_w<true>(A, g, twS, lane SG_ST_ARGS);
     int Mk = M, Nk = N;
     if (!CM) __asm__ __volatile__("" : "+s"(Mk), "+s"(Nk));
-    if constexpr (PFA == 2) {
+    if constexpr (PFA == 2 || PFA == 4) {
       // the next frame's sound (noise: its whole input): in flight during the
       // overlap-add, the output and the carry reload (the FFT state is dead here)
       if (k + 1 < S.nf) frame_prefetch<1>(P, frames[S.fdev + k + 1], mode, Mk, fl, fs, lane);
     }
     // window (/wl x hanning) and add the carry (pairs n = 64 r + lane)
+#if SG_HAN_SCALED
+    // han holds hanning / wl: one packed FMA per pair
+    const float2* han2 = reinterpret_cast<const float2*>(han);
+#pragma unroll
+    for (int r = 0; r < CP; ++r) {
+      const int n = 64 * r + lane;
+      if (n < Mk) A[n] = F(pfma(V(A[n]), V(han2[n]), V(C[r])));
+    }
+    for (int n = 64 * CP + lane; n < Mk; n += 64) A[n] = F(V(A[n]) * V(han2[n]));
+#else
 #pragma unroll
     for (int r = 0; r < CP; ++r) {
       const int n = 64 * r + lane;
@@ -919,6 +991,7 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
       const float2 v = A[n];
       A[n] = make_float2(v.x * invN * han[2 * n], v.y * invN * han[2 * n + 1]);
     }
+#endif
     sg_wave_fence();
     SG_ST(8);
     const bool lastf = k == S.nf - 1;
@@ -1028,7 +1101,9 @@ __device__ __forceinline__ void stft_ola_body(
       if (t < M - 1) twS[t] = tsg[t];
       twN[t] = tng[t];
     }
-    for (int t = threadIdx.x; t < 2 * N; t += NT) ham[t] = wg[t];  // hamming then hanning
+    // hamming, then hanning (SG_HAN_SCALED: times 1 / wl, the inverse transform's scale)
+    const float hs = SG_HAN_SCALED ? 1.f / (float)N : 1.f;
+    for (int t = threadIdx.x; t < 2 * N; t += NT) ham[t] = t < N ? wg[t] : wg[t] * hs;
   }
   __syncthreads();
   const SgSegment S = segs[blockIdx.x * W + w];
