@@ -175,14 +175,19 @@ def execute_plans(ctx, plans, d_out_ptrs, stream_ptr=None):
 
 
 def chunk_sizes(n, chunk, ramp=True):
-    """Chunk sizes for plan_uploaded: `chunk` calls each; with ramp, a first chunk
-    of chunk / 4 calls, so that the pipeline's fill (marshal + plan of the first
-    chunk, nothing to overlap with) is short."""
+    """Chunk sizes for plan_uploaded: `chunk` calls each; with ramp, a first and a
+    last chunk of chunk / 4 calls, so that the pipeline's fill (marshal + plan of
+    the first chunk, nothing to overlap with) and drain (the last upload) are short."""
     sizes = []
+    q = max(1, chunk // 4)
     if ramp and n > chunk:
-        sizes.append(max(1, chunk // 4))
+        sizes.append(q)
     while sum(sizes) < n:
-        sizes.append(min(chunk, n - sum(sizes)))
+        left = n - sum(sizes)
+        if ramp and len(sizes) > 0 and chunk >= left > q:  # the tail: [left - q, q]
+            sizes += [left - q, q]
+            break
+        sizes.append(min(chunk, left))
     return sizes
 
 
