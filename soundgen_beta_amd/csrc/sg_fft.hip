@@ -48,6 +48,9 @@
 #ifndef SG_HAN_SCALED
 #define SG_HAN_SCALED 1  // build knob: the LDS hanning table pre-scaled by 1 / wl (one packed FMA per windowed pair)
 #endif
+#ifndef SG_OUT_REG
+#define SG_OUT_REG 0  // build knob: interior frames' final samples stored from the windowing registers (r03n A/B: 2 % slower, off)
+#endif
 #ifndef SG_OUT_BATCH
 #define SG_OUT_BATCH 1  // build knob: output samples and the next carry read from LDS in batches (no per-sample waits)
 #endif
@@ -741,7 +744,7 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
 #pragma unroll
     for (int i = 0; i < SG_PF_SRC; ++i) {
       const int n = 64 * i + lane;
-      if (n < M) A[n] = make_float2(P.s[i].x * ham[2 * n], P.s[i].y * ham[2 * n + 1]);
+      if (n < M) A[n] = F(V(P.s[i]) * V(reinterpret_cast<const float2*>(ham)[n]));
     }
     sg_wave_fence();
     SG_ST(0);
@@ -975,7 +978,10 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
 #pragma unroll
     for (int r = 0; r < CP; ++r) {
       const int n = 64 * r + lane;
-      if (n < Mk) A[n] = F(pfma(V(A[n]), V(han2[n]), V(C[r])));
+      if (n < Mk) {
+        C[r] = F(pfma(V(A[n]), V(han2[n]), V(C[r])));  // C[r] now holds the windowed pair (SG_OUT_REG)
+        A[n] = C[r];
+      }
     }
     for (int n = 64 * CP + lane; n < Mk; n += 64) A[n] = F(V(A[n]) * V(han2[n]));
 #else
@@ -997,7 +1003,24 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
     const bool lastf = k == S.nf - 1;
     const int bn = lastf ? S.pb : bstart(S.f0 + k + 1);
     const int D = bn - bf;  // samples [bf, bn) are final
-    if (bf >= S.pa && bf - first >= 0 && bn - first <= len && D <= Nk) {
+    if (SG_OUT_REG && SG_HAN_SCALED && MODE == SG_FRAME_FILTER && bf >= S.pa && bf - first >= 0 && bn - first <= len && D <= 128 * CP) {
+      // interior frame whose final samples all lie in the carried pairs: written from
+      // the registers the windowing left them in (pair n = 64 r + lane: samples 2n, 2n + 1)
+      float* __restrict__ o = out + (bf - first);
+#pragma unroll
+      for (int r = 0; r < CP; ++r) {
+        const int i = 2 * (64 * r + lane);
+        const float vx = C[r].x * scale, vy = C[r].y * scale;
+        if (i < D) {
+          o[i] = vx;
+          m = fmaxf(m, vx);
+        }
+        if (i + 1 < D) {
+          o[i + 1] = vy;
+          m = fmaxf(m, vy);
+        }
+      }
+    } else if (bf >= S.pa && bf - first >= 0 && bn - first <= len && D <= Nk) {
       // interior frame (wave-uniform): every final sample is owned, inside the trim and the frame
       float* __restrict__ o = out + (bf - first);
       int i = lane;
