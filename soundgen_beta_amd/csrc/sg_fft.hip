@@ -1284,7 +1284,7 @@ __device__ __forceinline__ float fade_in_out(int lf, int64_t L, int64_t k) {  //
 // in global memory, one per window length (sg_roots64), L2-resident.
 constexpr int SG_F64_THREADS = 256;
 #ifndef SG_F64_KG
-#define SG_F64_KG 3  // build knob: outputs per work item of an odd-radix fp64 stage (1: one per item)
+#define SG_F64_KG 1  // build knob: outputs per work item of an odd-radix fp64 stage (1: one per item)
 #endif
 namespace {
 __device__ __forceinline__ double2 cmul64(double2 a, double2 b) {
