@@ -350,6 +350,7 @@ def main():
             print("bench: planned + uploaded %d/%d calls (%.1f s)" % (a + p.n, len(mine),
                                                                       time.perf_counter() - t_plan), file=sys.stderr)
     t_plan = time.perf_counter() - t_plan
+    native.lib().sg_host_cache_trim()  # planning is over: give the planner's cached host blocks back
     if failed:
         print("bench: %d of %d calls not synthesized: %s" % (failed, len(mine), first_msg), file=sys.stderr)
     out = torch.empty(max(base, 1), dtype=torch.float32, device=dev)

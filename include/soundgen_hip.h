@@ -269,6 +269,10 @@ int sg_set_amp_policy(int32_t host_built);
  * copied into the plan (the same values either way; tests compare the two).
  * The arrays are read during sg_plan_batch only. */
 int sg_set_uniform_gather(int32_t on);
+/* Release the planner's process-wide cache of freed host blocks (kept for the
+ * next plan, capped by SG_HOST_CACHE_MB or 8 GB / LOCAL_WORLD_SIZE). Returns
+ * the bytes released. Safe at any time; later plans refill it. */
+int64_t sg_host_cache_trim(void);
 /* The amplitude blocks sg_amp_build writes at upload, evaluated on the host by
  * the same code (tests; no device needed): n = sg_plan_amp_count(plan) floats. */
 int64_t sg_plan_amp_count(const sg_plan* plan);

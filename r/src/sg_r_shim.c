@@ -9,7 +9,10 @@
  *   C_sg_generate_harmonics  R/source.R:173-471     (do.call(generateHarmonics, ...) at R/soundgen.R:616-620)
  *   C_sg_soundgen            R/soundgen.R:208-862
  *   C_sg_generate_noise      R/source.R:57-138      (R/soundgen.R:686-696)
+ *   C_sg_spectral_envelope   R/sourceSpectrum.R:261-566 (R/soundgen.R:668-680, :762-775)
  *   C_sg_formant_filter      R/soundgen.R:743-807   (seewave::stft x env -> seewave::istft)
+ *   C_sg_soundgen_batch      a list of soundgen() calls planned as ONE batch
+ *                            (the loops of R/morph.R:200-208, R/matchPars.R:176-190)
  *
  * Randomness: the sg_random callbacks are bound to R's own norm_rand(),
  * unif_rand() and rgamma() between GetRNGstate()/PutRNGstate(), so a
@@ -123,12 +126,37 @@ SEXP C_sg_generate_harmonics(SEXP pitch, SEXP pars, SEXP amplAnchors) {
   return run_planned(&d);
 }
 
+/* list(n_points = integer, f1_index = integer, time, freq, amp, width), as
+ * .sg_flatten_formants() builds it, or NULL (NA formants) -> sg_formants
+ * (views into R memory) */
+static void flat_formants(SEXP v, sg_formants* f) {
+  memset(f, 0, sizeof *f);
+  f->f1_index = -1;
+  if (Rf_isNull(v)) return;
+  if (!Rf_isNewList(v) || Rf_xlength(v) != 6 || TYPEOF(VECTOR_ELT(v, 0)) != INTSXP)
+    Rf_error("soundgen_hip: formants must be flattened by .sg_flatten_formants()");
+  SEXP np = VECTOR_ELT(v, 0);
+  R_xlen_t tot = 0;
+  for (R_xlen_t k = 0; k < Rf_xlength(np); ++k) tot += INTEGER(np)[k];
+  for (int j = 2; j < 6; ++j)
+    if (TYPEOF(VECTOR_ELT(v, j)) != REALSXP || Rf_xlength(VECTOR_ELT(v, j)) != tot)
+      Rf_error("soundgen_hip: formant time/freq/amp/width must be double, one value per row");
+  f->n_formants = (int32_t)Rf_xlength(np);
+  f->n_points = INTEGER(np);
+  f->f1_index = Rf_asInteger(VECTOR_ELT(v, 1));
+  f->time = REAL(VECTOR_ELT(v, 2));
+  f->freq = REAL(VECTOR_ELT(v, 3));
+  f->amp = REAL(VECTOR_ELT(v, 4));
+  f->width = REAL(VECTOR_ELT(v, 5));
+}
+
 /* soundgen(...) with the formals of R/soundgen.R:208-277 already resolved by
- * the R wrapper (anchors as data.frames, formants as lists of data.frames) */
-SEXP C_sg_soundgen(SEXP args) {
-  sg_soundgen_args a;
-  sg_default_soundgen_args(&a);
-#define F(nm) a.nm = num(args, #nm, a.nm)
+ * the R wrapper (.sg_soundgen_args: anchors as data.frames, formants
+ * flattened) -> sg_soundgen_args (views into R memory) */
+static void soundgen_args(SEXP args, sg_soundgen_args* a) {
+  if (!Rf_isNewList(args)) Rf_error("soundgen_hip: soundgen arguments must be a named list");
+  sg_default_soundgen_args(a);
+#define F(nm) a->nm = num(args, #nm, a->nm)
   F(repeatBout); F(nSyl); F(sylLen); F(pauseLen); F(temperature); F(maleFemale); F(creakyBreathy);
   F(nonlinBalance); F(nonlinDep); F(jitterLen); F(jitterDep); F(vibratoFreq); F(vibratoDep); F(shimmerDep);
   F(attackLen); F(rolloff); F(rolloffOct); F(rolloffKHz); F(rolloffParab); F(rolloffParabHarm); F(rolloffLip);
@@ -140,34 +168,24 @@ SEXP C_sg_soundgen(SEXP args) {
   for (R_xlen_t i = 0; i < Rf_xlength(args); ++i) {
     const char* k = CHAR(STRING_ELT(nms, i));
     SEXP v = VECTOR_ELT(args, i);
-    if (!strcmp(k, "pitchAnchors")) a.pitchAnchors = anchors(v);
-    else if (!strcmp(k, "pitchAnchorsGlobal")) a.pitchAnchorsGlobal = anchors(v);
-    else if (!strcmp(k, "noiseAnchors")) a.noiseAnchors = anchors(v);
-    else if (!strcmp(k, "mouthAnchors")) a.mouthAnchors = anchors(v);
-    else if (!strcmp(k, "amplAnchors")) a.amplAnchors = anchors(v);
-    else if (!strcmp(k, "amplAnchorsGlobal")) a.amplAnchorsGlobal = anchors(v);
-    else if (!strcmp(k, "formantsNoise_rlen")) a.formantsNoise_rlen = Rf_asInteger(v);
-    else if (!strcmp(k, "invalidArgAction")) a.invalidArgAction = Rf_asInteger(v);
+    if (!strcmp(k, "pitchAnchors")) a->pitchAnchors = anchors(v);
+    else if (!strcmp(k, "pitchAnchorsGlobal")) a->pitchAnchorsGlobal = anchors(v);
+    else if (!strcmp(k, "noiseAnchors")) a->noiseAnchors = anchors(v);
+    else if (!strcmp(k, "mouthAnchors")) a->mouthAnchors = anchors(v);
+    else if (!strcmp(k, "amplAnchors")) a->amplAnchors = anchors(v);
+    else if (!strcmp(k, "amplAnchorsGlobal")) a->amplAnchorsGlobal = anchors(v);
+    else if (!strcmp(k, "formantsNoise_rlen")) a->formantsNoise_rlen = Rf_asInteger(v);
+    else if (!strcmp(k, "invalidArgAction")) a->invalidArgAction = Rf_asInteger(v);
     else if (!strcmp(k, "tempEffects") && TYPEOF(v) == REALSXP && Rf_xlength(v) == 8)
-      memcpy(a.tempEffects, REAL(v), sizeof a.tempEffects);
+      memcpy(a->tempEffects, REAL(v), sizeof a->tempEffects);
+    else if (!strcmp(k, "formants_flat")) flat_formants(v, &a->formants);
+    else if (!strcmp(k, "formantsNoise_flat")) flat_formants(v, &a->formantsNoise);
   }
-  /* formants / formantsNoise arrive flattened by the R wrapper as
-   * list(n_points = integer, f1_index = integer, time, freq, amp, width) */
-  sg_formants* fs[2] = {&a.formants, &a.formantsNoise};
-  const char* fk[2] = {"formants_flat", "formantsNoise_flat"};
-  for (int f = 0; f < 2; ++f) {
-    for (R_xlen_t i = 0; i < Rf_xlength(args); ++i) {
-      if (strcmp(CHAR(STRING_ELT(nms, i)), fk[f])) continue;
-      SEXP v = VECTOR_ELT(args, i);
-      fs[f]->n_formants = (int32_t)Rf_xlength(VECTOR_ELT(v, 0));
-      fs[f]->n_points = INTEGER(VECTOR_ELT(v, 0));
-      fs[f]->f1_index = Rf_asInteger(VECTOR_ELT(v, 1));
-      fs[f]->time = REAL(VECTOR_ELT(v, 2));
-      fs[f]->freq = REAL(VECTOR_ELT(v, 3));
-      fs[f]->amp = REAL(VECTOR_ELT(v, 4));
-      fs[f]->width = REAL(VECTOR_ELT(v, 5));
-    }
-  }
+}
+
+SEXP C_sg_soundgen(SEXP args) {
+  sg_soundgen_args a;
+  soundgen_args(args, &a);
   sg_call_desc d;
   memset(&d, 0, sizeof d);
   d.kind = SG_CALL_SOUNDGEN;
@@ -176,22 +194,110 @@ SEXP C_sg_soundgen(SEXP args) {
   return run_planned(&d);
 }
 
-/* istft-based filtered noise, R/source.R:57-138 */
+/* soundgen_batch(calls): a list of resolved soundgen() argument lists (as
+ * .sg_soundgen_args builds each) planned as ONE sg_plan_batch and executed in
+ * one pass; returns the list of waveforms in call order. R's RNG is drawn in
+ * call order, each call's draws in the reference's order, so the result equals
+ * lapply(calls, function(a) do.call(soundgen, a)) after the same set.seed().
+ * A call R would stop() on stops the batch with that call's message, as the
+ * loop would (its draws and those of the calls before it are consumed). */
+SEXP C_sg_soundgen_batch(SEXP calls) {
+  if (!Rf_isNewList(calls)) Rf_error("soundgen_hip: calls must be a list of argument lists");
+  const R_xlen_t n = Rf_xlength(calls);
+  SEXP res = PROTECT(Rf_allocVector(VECSXP, n));
+  if (n == 0) {
+    UNPROTECT(1);
+    return res;
+  }
+  sg_soundgen_args* a = (sg_soundgen_args*)R_alloc((size_t)n, sizeof(sg_soundgen_args));
+  sg_call_desc* d = (sg_call_desc*)R_alloc((size_t)n, sizeof(sg_call_desc));
+  memset(d, 0, (size_t)n * sizeof(sg_call_desc));
+  for (R_xlen_t i = 0; i < n; ++i) {
+    soundgen_args(VECTOR_ELT(calls, i), &a[i]);
+    d[i].kind = SG_CALL_SOUNDGEN;
+    d[i].args = &a[i];
+    d[i].random = r_rng();
+  }
+  sg_plan* plan = NULL;
+  GetRNGstate();
+  int rc = sg_plan_batch(ctx(), d, (int64_t)n, &plan);
+  PutRNGstate();
+  check(rc);
+  int32_t* st = (int32_t*)R_alloc((size_t)n, sizeof(int32_t));
+  int64_t* len = (int64_t*)R_alloc((size_t)n, sizeof(int64_t));
+  int64_t* off = (int64_t*)R_alloc((size_t)n, sizeof(int64_t));
+  sg_plan_status(plan, st);
+  sg_plan_lengths(plan, len, off);
+  for (R_xlen_t i = 0; i < n; ++i)
+    if (st[i]) {
+      char msg[512];
+      snprintf(msg, sizeof msg, "call %ld: %s", (long)(i + 1), sg_plan_call_message(plan, (int64_t)i));
+      sg_plan_destroy(plan);
+      Rf_error("soundgen_hip: %s", msg);
+    }
+  const int64_t tot = sg_plan_total_samples(plan);
+  SEXP all = PROTECT(Rf_allocVector(REALSXP, tot > 0 ? tot : 1));
+  rc = sg_execute_to_host(ctx(), plan, REAL(all));
+  sg_plan_destroy(plan);
+  check(rc);
+  for (R_xlen_t i = 0; i < n; ++i) {
+    SEXP y = Rf_allocVector(REALSXP, len[i]);
+    SET_VECTOR_ELT(res, i, y);
+    if (len[i]) memcpy(REAL(y), REAL(all) + off[i], (size_t)len[i] * sizeof(double));
+  }
+  UNPROTECT(2);
+  return res;
+}
+
+/* generateNoise(len, noiseAnchors, <scalar formals as a named list>,
+ * filterNoise): istft-based filtered noise, R/source.R:57-138. filterNoise is
+ * NULL (NA) or an nr x nc double matrix, nr = windowLength_points / 2. */
 SEXP C_sg_generate_noise(SEXP len, SEXP noiseAnchors, SEXP pars, SEXP filterNoise) {
-  const int64_t L = (int64_t)Rf_asReal(len);
+  const double Ld = Rf_asReal(len);
+  if (!(Ld >= 0)) Rf_error("soundgen_hip: len must be a non-negative number");
+  const int64_t L = (int64_t)Ld;
   SEXP out = PROTECT(Rf_allocVector(REALSXP, L));
   const double* fn = NULL;
   int32_t fnc = 0;
-  if (TYPEOF(filterNoise) == REALSXP && Rf_isMatrix(filterNoise)) {
+  const int32_t wl = (int32_t)num(pars, "windowLength_points", 1024);
+  if (!Rf_isNull(filterNoise)) {
+    if (TYPEOF(filterNoise) != REALSXP || !Rf_isMatrix(filterNoise) || Rf_nrows(filterNoise) != wl / 2)
+      Rf_error("soundgen_hip: filterNoise must be a double matrix with windowLength_points / 2 rows");
     fn = REAL(filterNoise);
     fnc = Rf_ncols(filterNoise);
   }
   sg_random rnd = r_rng();
   GetRNGstate();
   int rc = sg_generate_noise(ctx(), L, anchors(noiseAnchors), num(pars, "rolloffNoise", -6),
-                             num(pars, "attackLen", 10), (int32_t)num(pars, "windowLength_points", 1024),
+                             num(pars, "attackLen", 10), wl,
                              num(pars, "samplingRate", 16000), num(pars, "overlap", 75), num(pars, "throwaway", -120),
                              fn, fnc, &rnd, REAL(out));
+  PutRNGstate();
+  check(rc);
+  UNPROTECT(1);
+  return out;
+}
+
+/* getSpectralEnvelope(nr, nc, <formants flattened>, <scalar formals as a
+ * named list>, mouthAnchors) -> the nr x nc double matrix R returns
+ * (R/sourceSpectrum.R:261-566). vocalTract NULL travels as NA (NaN). The
+ * tracks and stochastic formants are planned on the host with R's RNG; the
+ * matrix is computed on the device. */
+SEXP C_sg_spectral_envelope(SEXP nr, SEXP nc, SEXP formants, SEXP pars, SEXP mouthAnchors) {
+  const int NR = Rf_asInteger(nr), NC = Rf_asInteger(nc);
+  if (NR == NA_INTEGER || NC == NA_INTEGER || NR < 1 || NC < 1)
+    Rf_error("soundgen_hip: nr and nc must be positive integers");
+  sg_formants F;
+  flat_formants(formants, &F);
+  SEXP out = PROTECT(Rf_allocMatrix(REALSXP, NR, NC));
+  sg_random rnd = r_rng();
+  GetRNGstate();
+  int rc = sg_spectral_envelope(ctx(), NR, NC, &F, num(pars, "formantDep", 1), num(pars, "rolloffLip", 6),
+                                anchors(mouthAnchors), num(pars, "mouthOpenThres", 0),
+                                num(pars, "openMouthBoost", 0), num(pars, "vocalTract", NA_REAL),
+                                num(pars, "temperature", 0), num(pars, "formDrift", .3), num(pars, "formDisp", .2),
+                                num(pars, "formantDepStoch", 30), num(pars, "smoothLinearFactor", 1),
+                                num(pars, "samplingRate", 16000), num(pars, "speedSound", 35400), &rnd, REAL(out));
   PutRNGstate();
   check(rc);
   UNPROTECT(1);
@@ -213,7 +319,9 @@ static const R_CallMethodDef CALLS[] = {
     {"C_sg_generate_harmonics", (DL_FUNC)&C_sg_generate_harmonics, 3},
     {"C_sg_soundgen", (DL_FUNC)&C_sg_soundgen, 1},
     {"C_sg_generate_noise", (DL_FUNC)&C_sg_generate_noise, 4},
+    {"C_sg_spectral_envelope", (DL_FUNC)&C_sg_spectral_envelope, 5},
     {"C_sg_formant_filter", (DL_FUNC)&C_sg_formant_filter, 4},
+    {"C_sg_soundgen_batch", (DL_FUNC)&C_sg_soundgen_batch, 1},
     {NULL, NULL, 0}};
 
 void R_init_soundgen(DllInfo* dll) {

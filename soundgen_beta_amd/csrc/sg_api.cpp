@@ -124,10 +124,17 @@ struct GrowthEstimate {
     for (auto& e : elems) e.store(0);
   }
   // one sample per part: keep the estimate a running mean over recent plans
+  // (concurrent sg_plan_batch calls: the CAS lets one of them halve a given
+  // count; each element is halved atomically)
   void decay() {
-    if (calls.load() < (int64_t(1) << 20)) return;
-    calls = calls.load() / 2;
-    for (auto& e : elems) e = e.load() / 2;
+    int64_t c = calls.load();
+    if (c < (int64_t(1) << 20)) return;
+    if (!calls.compare_exchange_strong(c, c / 2)) return;  // another plan is decaying it
+    for (auto& e : elems) {
+      int64_t v = e.load();
+      while (!e.compare_exchange_weak(v, v / 2)) {
+      }
+    }
   }
   template <class F>
   static void each(sg::Batch& B, F&& f) {
@@ -640,6 +647,8 @@ int sg_execute_plans(sg_ctx* ctx, sg_plan* const* plans, float* const* d_outs, i
     return SG_OK;
   });
 }
+
+int64_t sg_host_cache_trim(void) { return (int64_t)sg::bulk_trim(); }
 
 int sg_set_profiling(sg_ctx* ctx, int on) {
   ctx->profiling = on != 0;

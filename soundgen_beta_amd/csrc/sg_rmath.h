@@ -27,6 +27,7 @@ void scratch_trim() noexcept;  // return the calling thread's pool to the system
 // the planning threads, then again in the merge) cost more than writing them.
 void* bulk_alloc(size_t bytes);
 void bulk_free(void* p, size_t bytes) noexcept;
+size_t bulk_trim() noexcept;  // free every cached bulk block; returns the bytes released
 constexpr size_t SG_BULK_HUGE = size_t(8) << 20;
 
 template <class T>

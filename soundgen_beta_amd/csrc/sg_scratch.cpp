@@ -98,7 +98,8 @@ void scratch_free(void* q, size_t bytes) noexcept {
 }
 
 // Freed bulk blocks are kept for the next plan (up to SG_HOST_CACHE_MB, default
-// 8192): a plan's host arrays are GBs, freed once uploaded, and the next plan
+// 8192 / LOCAL_WORLD_SIZE: one rank per GPU shares the node's memory; at least
+// 1024; sg_host_cache_trim() returns them): a plan's host arrays are GBs, freed once uploaded, and the next plan
 // of a batch asks for blocks of about the same sizes; reusing resident pages
 // skips the page faults and the kernel's zeroing of fresh ones. Blocks are
 // sized in classes of 1/16 of a power of two (<= 6.25 % slack), so a freed
@@ -118,7 +119,10 @@ struct BulkCache {
   size_t bytes = 0;
   const size_t cap = [] {
     const char* e = std::getenv("SG_HOST_CACHE_MB");
-    return (size_t)(e ? std::atoll(e) : 8192) << 20;
+    if (e) return (size_t)std::atoll(e) << 20;
+    const char* w = std::getenv("LOCAL_WORLD_SIZE");
+    const long long ranks = w ? std::max(1LL, std::atoll(w)) : 1;
+    return (size_t)std::max(1024LL, 8192LL / ranks) << 20;
   }();
   ~BulkCache() {
     for (auto& b : blocks) std::free(b.second);
@@ -166,6 +170,20 @@ void bulk_free(void* q, size_t bytes) noexcept {
     }
   }
   std::free(q);
+}
+
+size_t bulk_trim() noexcept {
+  BulkCache& c = bulk_cache();
+  std::multimap<size_t, void*> blocks;
+  size_t held = 0;
+  {
+    std::lock_guard<std::mutex> g(c.mu);
+    blocks.swap(c.blocks);
+    held = c.bytes;
+    c.bytes = 0;
+  }
+  for (auto& b : blocks) std::free(b.second);
+  return held;
 }
 
 void scratch_trim() noexcept {

@@ -46,14 +46,33 @@ def _anchors_len(a):
     return len(np.atleast_1d(a))
 
 
+def _is_na(v):
+    return v is None or (isinstance(v, str) and v.upper() == "NA")
+
+
+def _finite(v):
+    """Finite values of an anchor list or pitch vector; NaN / None / "NA" are
+    R's NA (unvoiced), the planner treats them as absent."""
+    if _is_na(v):
+        return np.zeros(0)
+    v = np.atleast_1d(np.asarray([np.nan if _is_na(x) else x for x in np.atleast_1d(v).tolist()],
+                                 dtype=np.float64))
+    return v[np.isfinite(v)]
+
+
 def _anchor_values(pa, default):
-    if pa is None:
+    """Pitch anchor values of a call, or None when it has no voiced part
+    (pitchAnchors NULL / NA / all NA: R/soundgen.R:465 builds a pitch contour only
+    from a list)."""
+    if _is_na(pa):
         return None
     if isinstance(pa, dict):
-        return np.atleast_1d(np.asarray(pa.get("value", default), dtype=np.float64))
-    if isinstance(pa, str):
-        return np.atleast_1d(np.asarray(default, dtype=np.float64))
-    return np.atleast_1d(np.asarray(pa, dtype=np.float64))
+        v = _finite(pa.get("value", default))
+    elif isinstance(pa, str):
+        v = _finite(default)
+    else:
+        v = _finite(pa)
+    return v if len(v) else None
 
 
 def harmonic_rows(f0, sr, rolloff=-12.0, rolloffOct=-12.0, rolloffKHz=-6.0, throwaway=-120.0):
@@ -79,11 +98,13 @@ def call_cost(call):
         p = call.get("params", {})
         sr = float(p.get("samplingRate", 16000))
         psr = float(p.get("pitchSamplingRate", 3500))
-        pitch = np.asarray(call["pitch"], dtype=np.float64)
+        pitch = np.atleast_1d(call["pitch"])
         n = len(pitch) / psr * sr
-        f0 = float(np.nanmedian(pitch)) if len(pitch) else 100.0
-        rows = harmonic_rows(f0, sr, p.get("rolloff", -18), p.get("rolloffOct", -2), p.get("rolloffKHz", -6),
-                             p.get("throwaway", -120))
+        voiced = _finite(pitch)
+        rows = 0
+        if len(voiced):  # all-NA pitch: nothing voiced, no sine-bank rows
+            rows = harmonic_rows(float(np.median(voiced)), sr, p.get("rolloff", -18), p.get("rolloffOct", -2),
+                                 p.get("rolloffKHz", -6), p.get("throwaway", -120))
         return n * (rows * W_ROW + W_SAMPLE)
     a = call.get("args", {})
     sr = float(a.get("samplingRate", 16000))
@@ -93,7 +114,7 @@ def call_cost(call):
     n = dur / 1000.0 * sr
     vals = _anchor_values(a.get("pitchAnchors", "default"), [100.0, 150.0, 135.0, 100.0])
     rows = 0.0
-    if vals is not None and len(vals):
+    if vals is not None:
         f0 = float(np.exp(np.mean(np.log(np.maximum(vals, 1.0)))))
         rows = harmonic_rows(f0, sr, a.get("rolloff", -12), a.get("rolloffOct", -12), a.get("rolloffKHz", -6),
                              a.get("throwaway", -120))
@@ -131,13 +152,14 @@ def shard(calls, rank, world):
     return idx, [calls[i] for i in idx], owner
 
 
-def gather_packed(data, offsets, lengths, owner, rank, world, root=0):
+def gather_packed(data, offsets, lengths, owner, rank, world, root=0, to_host=False):
     """The exchange step: every rank holds its shard's outputs packed in `data`
     (a 1-D float32 tensor on the communication device: the rank's GPU under
     RCCL, the CPU under gloo), call i of the shard at offsets[i] with lengths[i]
     samples (-1: the call failed). Returns, on the root, one entry per call of
-    the batch in call order: a 1-D view of a received (device) buffer or an
-    exception; None elsewhere."""
+    the batch in call order: a 1-D float32 tensor view of the received buffer
+    (on the communication device: a GPU tensor under RCCL) or, with to_host, a
+    float32 numpy array; an exception for a failed call. None elsewhere."""
     import torch
     import torch.distributed as dist
     dev = data.device
@@ -176,7 +198,10 @@ def gather_packed(data, offsets, lengths, owner, rank, world, root=0):
             buf, off, ln = data, np.asarray(offsets, np.int64), np.asarray(lengths, np.int64)
         else:
             t = tables[r].cpu().numpy().reshape(2, -1)
-            buf, off, ln = bufs.get(r), t[0], t[1]
+            # a peer whose packed size is 0 (only empty or failed calls) sent no buffer
+            buf, off, ln = bufs.get(r, torch.empty(0, dtype=torch.float32, device=dev)), t[0], t[1]
+        if to_host:
+            buf = buf.cpu().numpy()
         for i, o, n in zip(idx, off, ln):
             result[i] = RuntimeError("call %d failed on rank %d" % (i, r)) if n < 0 else buf[int(o):int(o) + int(n)]
     return result
@@ -197,11 +222,13 @@ def pack_outputs(outs, device="cpu"):
     return torch.from_numpy(data).to(device), offs, lens
 
 
-def synthesize_sharded(calls, rank, world, device=None, synth=None, root=0, comm_device=None):
+def synthesize_sharded(calls, rank, world, device=None, synth=None, root=0, comm_device=None, to_host=False):
     """Every rank synthesizes its LPT shard and the root gathers the batch in call
     order (gather_packed). Default: batch.synthesize_packed on the rank's GPU
     (LOCAL_RANK), the packed device buffer sent as is (RCCL). `synth` maps a list
-    of calls to host outputs instead (packed on `comm_device`, e.g. "cpu" for gloo)."""
+    of calls to host outputs instead (packed on `comm_device`, e.g. "cpu" for gloo).
+    The root's entries are float32 tensor views on the communication device, on
+    every path (world 1 included); to_host=True returns float32 numpy arrays."""
     if device is None:
         device = int(os.environ.get("LOCAL_RANK", "0"))
     idx, mine, owner = shard(calls, rank, world)
@@ -210,9 +237,8 @@ def synthesize_sharded(calls, rank, world, device=None, synth=None, root=0, comm
         data, offs, lens = batch.synthesize_packed(mine, device)
     else:
         outs = synth(mine) if mine else []
-        if world == 1:
-            return outs
         data, offs, lens = pack_outputs(outs, comm_device or "cpu")
     if world == 1:
-        return [RuntimeError("call failed") if n < 0 else data[o:o + n] for o, n in zip(offs, lens)]
-    return gather_packed(data, offs, lens, owner, rank, world, root)
+        buf = data.cpu().numpy() if to_host else data
+        return [RuntimeError("call failed") if n < 0 else buf[int(o):int(o) + int(n)] for o, n in zip(offs, lens)]
+    return gather_packed(data, offs, lens, owner, rank, world, root, to_host)

@@ -60,6 +60,29 @@ def test_lpt_assignment_balanced_and_deterministic():
     assert sgd.call_cost(_calls()[0]) > 0 and sgd.call_cost(_calls()[-2]) > 0
 
 
+def test_cost_na_pitch():
+    """R's NA (NaN, None, "NA", all-NA anchors or pitch) means no voiced part:
+    the call costs its per-sample work only, and never raises (shard() runs it on
+    every rank)."""
+    base = dict(sylLen=300, samplingRate=16000, temperature=0, addSilence=0)
+    voiced = sgd.call_cost({"kind": "soundgen", "args": dict(base, pitchAnchors=[120, 180])})
+    unvoiced = sgd.call_cost({"kind": "soundgen", "args": dict(base, pitchAnchors=None)})
+    assert voiced > unvoiced > 0
+    for pa in (float("nan"), "NA", [float("nan"), float("nan")], {"time": [0, 1], "value": [float("nan")] * 2},
+               {"time": [0, 1], "value": [None, None]}):
+        assert sgd.call_cost({"kind": "soundgen", "args": dict(base, pitchAnchors=pa)}) == unvoiced, pa
+    # NA values among finite ones are dropped, not propagated
+    part = sgd.call_cost({"kind": "soundgen", "args": dict(base, pitchAnchors=[120, float("nan"), 180])})
+    assert np.isfinite(part) and part > unvoiced
+    h = {"kind": "harmonics", "params": dict(samplingRate=16000)}
+    assert sgd.call_cost(dict(h, pitch=np.full(700, np.nan))) > 0
+    assert sgd.call_cost(dict(h, pitch=np.full(700, np.nan))) < sgd.call_cost(dict(h, pitch=np.full(700, 150.0)))
+    mixed = np.full(700, 150.0)
+    mixed[:300] = np.nan
+    assert np.isfinite(sgd.call_cost(dict(h, pitch=mixed)))
+    sgd.shard([dict(h, pitch=np.full(700, np.nan)), {"kind": "soundgen", "args": dict(base, pitchAnchors="NA")}], 0, 2)
+
+
 def test_cost_rows_follow_get_rolloff(oracle):
     """harmonic_rows() counts the rows getRolloff keeps (the oracle's, no cap)."""
     for f0, kw in ((100.0, dict(rolloff=-12, rolloffOct=-12, rolloffKHz=-6)),
@@ -76,6 +99,10 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         res = sgd.synthesize_sharded(_calls(), rank, world, synth=_oracle_synth, comm_device="cpu")
+        # a peer whose shard packs to 0 samples (its only call is refused) sends no
+        # buffer; the root still returns every call, as host arrays with to_host
+        two = [_calls()[0], _calls()[-1]]
+        res0 = sgd.synthesize_sharded(two, rank, world, synth=_oracle_synth, comm_device="cpu", to_host=True)
         # the real host planner on this rank's shard of 96 C5 calls (CPU planning)
         from soundgen_beta_amd import batch
         calls = _bench().c5_calls(96)
@@ -85,6 +112,9 @@ def _worker(rank, world, port, q):
         plans = [None] * world
         dist.all_gather_object(plans, mine_plan)
         if rank == 0:
+            assert sgd.lpt_assign([sgd.call_cost(c) for c in two], world).tolist() == [0, 1]
+            assert isinstance(res0[0], np.ndarray) and res0[0].dtype == np.float32 and len(res0[0]) > 0
+            assert isinstance(res0[1], Exception)
             q.put(([np.asarray(y, np.float64) if not isinstance(y, Exception) else None for y in res], plans))
     finally:
         dist.destroy_process_group()

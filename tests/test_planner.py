@@ -266,3 +266,27 @@ def test_uniform_gather_plans_the_same_calls():
     assert np.array_equal(l0, l1) and np.array_equal(o0, o1) and np.array_equal(s0, s1)
     assert st0 == st1
     assert L.sg_set_uniform_gather(2) != 0
+
+
+def test_host_cache_trim_between_plans():
+    """sg_host_cache_trim releases the planner's cached host blocks; the next plan
+    refills the cache and plans the same batch."""
+    import time
+
+    import bench
+    from soundgen_beta_amd import native
+    L = native.lib()
+    calls = bench.c5_calls(1200)
+    p = batch.Plan(calls, None)
+    want = (p.lengths.copy(), p.offsets.copy(), p.stats())
+    p.close()
+    released = 0
+    for _ in range(40):  # large host arrays are freed on a detached thread after close
+        released += L.sg_host_cache_trim()
+        if released:
+            break
+        time.sleep(0.05)
+    assert released >= 0 and L.sg_host_cache_trim() >= 0
+    q = batch.Plan(calls, None)
+    assert np.array_equal(q.lengths, want[0]) and np.array_equal(q.offsets, want[1]) and q.stats() == want[2]
+    q.close()
