@@ -14,7 +14,7 @@ import numpy as np
 from soundgen_beta_amd import _abi, rargs
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "_build", "libsg_oracle.so")
+_LIB_PATH = os.environ.get("SG_ORACLE_LIB") or os.path.join(_HERE, "_build", "libsg_oracle.so")  # override: sanitizer build
 _lib = None
 
 
