@@ -213,6 +213,40 @@ def cpu_baseline(calls, budget_s):
             "note": "R unavailable; CPU baseline = C restatement of the R algorithm"}
 
 
+def rms_check(plans, out, calls, n_check):
+    """RMS error vs the oracle (after the timed region) of n_check calls spread
+    evenly over every plan's synthesized calls, on the /max-normalised waveform
+    both return (R/soundgen.R:807); lengths must match exactly. The calls the
+    planner sent to the fp64 filter path are all included when present."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import oracle as O
+    O.lib()
+    per = max(1, -(-n_check // max(1, len(plans))))
+    picks = []  # (global offset, length, call index, fp64 path)
+    for p, b, ix in plans:
+        ok = np.nonzero(p.status == 0)[0]
+        if not len(ok):
+            continue
+        hp = p.precision()[0]
+        sel = set(ok[np.linspace(0, len(ok) - 1, min(per, len(ok))).round().astype(int)].tolist())
+        sel |= set(ok[hp[ok] > 0][:2].tolist())  # fp64-path calls, two per plan
+        picks += [(b + int(p.offsets[i]), int(p.lengths[i]), int(ix[i]), bool(hp[i] > 0)) for i in sorted(sel)]
+    ys = [out[lo:lo + n].double().cpu().numpy() for lo, n, _, _ in picks]
+
+    def one(k):
+        ref = oracle_call(O, calls[picks[k][2]])
+        y = ys[k]
+        return float(np.sqrt(np.mean((y - ref) ** 2))) if len(ref) == len(y) else float("inf")
+    with ThreadPoolExecutor(host_cores()) as ex:
+        errs = list(ex.map(one, range(len(picks))))
+    if not errs:
+        return None
+    presets = sorted({calls[pk[2]].get("preset", calls[pk[2]].get("kind")) for pk in picks})
+    return {"calls": len(errs), "plans": len(plans), "max": max(errs), "median": float(np.median(errs)),
+            "fp64_path_calls": int(sum(pk[3] for pk in picks)), "presets": len(presets),
+            "tolerance": 1e-5, "within_tolerance": int(sum(e <= 1e-5 for e in errs))}
+
+
 def traffic_from_profiles(config, kernel, launches_per_step):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of
     this workload (profiles/rNN_<config>_traffic.json by tools/gpu_traffic.sh:
@@ -233,12 +267,44 @@ def traffic_from_profiles(config, kernel, launches_per_step):
     return per_step / max(1, launches_per_step), os.path.relpath(files[-1], ROOT)
 
 
-def roofline(st, prof, steps, config):
-    """Roofline of the step's dominant kernel (the one with the most event time):
-    achieved = algorithmic bytes per launch / average launch duration (HIP events on
-    the launch stream), SURVEY.md §8d per-unit bytes."""
-    tot = {k: v[0] * v[1] for k, v in prof.items()}
-    kern = max(tot, key=tot.get) if any(tot.values()) else "sg_sine_bank"
+def pmc_from_profiles(config, kernel):
+    """Issue profile of `kernel` from the newest committed rocprofv3 SQ-counter
+    summary of this workload (profiles/rNN_<config>_pmc.json, tools/pmc_summary.py):
+    the fraction of its waves' cycles with a VALU / LDS instruction issued and
+    parked on s_waitcnt, averaged over its launches (each counter from its own
+    pass)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_%s_pmc.json" % config)))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    acc = {}
+    for k, v in d.get("kernels", {}).items():
+        if k.split(" ")[0] != kernel or not v.get("SQ_WAVE_CYCLES"):
+            continue
+        for c in ("SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS", "SQ_WAIT_INST_ANY"):
+            if c in v:
+                acc.setdefault(c, []).append(v[c] / v["SQ_WAVE_CYCLES"])
+    if not acc:
+        return None
+    m = {c: float(np.mean(x)) for c, x in acc.items()}
+    return {"valu_issue_per_wave": m.get("SQ_ACTIVE_INST_VALU"), "lds_issue_per_wave": m.get("SQ_ACTIVE_INST_LDS"),
+            "waitcnt_per_wave": m.get("SQ_WAIT_INST_ANY"), "source": os.path.relpath(files[-1], ROOT)}
+
+
+# waves per SIMD the kernels run at (hipcc -Rpass-analysis=kernel-resource-usage, gfx950)
+WAVES_PER_SIMD = {"sg_stft_ola": 2, "sg_stft_ola_noise": 3, "sg_sine_bank": 7, "sg_sine_bank_pairs": 8,
+                  "sg_sine_bank_tall": 5, "sg_sine_bank_tall_pairs": 8}
+
+
+def roofline(st, prof, steps, config, kern):
+    """Roofline of one profiled kernel group: achieved = algorithmic bytes per launch
+    (SURVEY.md §8d per-unit bytes) / average launch duration (HIP events
+    on the launch stream, every kernel alone: profiling serialises the two streams).
+    `bound` names the unit whose fraction is the larger: HBM bytes against 8 TB/s, or
+    the VALU's work (sine bank: 2 lane-ops per (sample, row, chain) against the packed
+    issue peak; STFT: the nominal 5 wl log2 wl flops per transform against the fp32
+    peak). `frac` is always the HBM fraction of the algorithmic bytes."""
     ms, n = prof[kern]
     lps = max(1, n // steps)  # launches per step
     sec = ms / 1e3
@@ -246,30 +312,40 @@ def roofline(st, prof, steps, config):
         # fp32 epoch waveform write + the amplitude blocks it reads (A and dA columns)
         alg = (4 * st["harm_samples"] + st["harm_amp_bytes"]) / lps
         valu_ops = 2.0 * st["harm_terms"] / lps  # Clenshaw: 2 lane-ops per (sample, row, chain)
+        vfrac = valu_ops / sec / VALU_PEAK_OPS if sec else 0
         extra = {"valu": {"ops_per_launch": valu_ops, "achieved_ops_s": valu_ops / sec if sec else 0,
-                          "peak_ops_s": VALU_PEAK_OPS, "frac": valu_ops / sec / VALU_PEAK_OPS if sec else 0}}
+                          "peak_ops_s": VALU_PEAK_OPS, "frac": vfrac}}
+        kernels = ("sg_sine_bank", "sg_sine_bank_pairs", "sg_sine_bank_tall", "sg_sine_bank_tall_pairs")
+        name = " + ".join(kernels)
     else:
         # source / uniforms + envelope columns read, trimmed output written
         alg = st["stft_bytes"] / lps
         fl = st["stft_flops"] / lps
+        vfrac = fl / sec / 1e12 / FP32_PEAK_TFLOPS if sec else 0
         extra = {"flops": {"nominal_per_launch": fl, "achieved_tflops": fl / sec / 1e12 if sec else 0,
-                           "peak_tflops": FP32_PEAK_TFLOPS,
-                           "frac": fl / sec / 1e12 / FP32_PEAK_TFLOPS if sec else 0}}
+                           "peak_tflops": FP32_PEAK_TFLOPS, "frac": vfrac}}
+        kernels = ("sg_stft_ola", "sg_stft_ola_noise")
+        name = "sg_stft_ola + sg_stft_ola_noise"
     achieved = alg / sec / 1e9 if sec > 0 else 0.0
+    hfrac = achieved / HBM_PEAK_GBS
     traffic, src = traffic_from_profiles(config, kern, lps)
-    r = {"bound": "hbm", "kernel": kern, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "alg_bytes_per_launch": alg,
-         "avg_launch_ms": ms, "launches_timed": n}
-    if kern == "sg_stft_ola":
-        # the fused STFT/ISTFT/OLA runs once per spectral phase of a plan: the noise
-        # phase as sg_stft_ola_noise, the formant-filter phase as sg_stft_ola; bytes,
-        # flops and event time are their sum over both launches, per launch
-        r["kernel"] = "sg_stft_ola + sg_stft_ola_noise"
-        r["rocprof_check"] = ("avg_launch_ms = (TotalDurationNs of sg_stft_ola + sg_stft_ola_noise) / "
-                              "(their Calls) in the kernel-stats summary")
+    r = {"bound": "valu" if vfrac > hfrac else "hbm", "kernel": name, "achieved": achieved, "peak": HBM_PEAK_GBS,
+         "unit": "GB/s", "frac": hfrac, "traffic": traffic, "alg_bytes_per_launch": alg, "avg_launch_ms": ms,
+         "launches_timed": n,
+         "rocprof_check": (("avg_launch_ms = (TotalDurationNs of %s) / (their Calls)" if kern != "sg_sine_bank" else
+                            "avg_launch_ms = (sum of TotalDurationNs of %s) / (Calls of one of them: one launch "
+                            "of each class per plan)") % " + ".join(kernels)
+                           + " in the SG_OVERLAP=0 kernel-stats summary")}
     if src:
         r["traffic_source"] = src
     r.update(extra)
+    issue = {k: pmc_from_profiles(config, k) for k in kernels}
+    issue = {k: dict(v, waves_per_simd=WAVES_PER_SIMD.get(k)) for k, v in issue.items() if v}
+    if issue:
+        r["issue"] = issue
+    if kern == "sg_stft_ola":
+        r["binding"] = ("VALU issue and latency at 2 waves/SIMD (241 VGPRs): the odd-prime radix-19/29 "
+                        "butterflies of M = 1102 = 2 x 19 x 29 are ~64 % of the VALU per frame")
     return r
 
 
@@ -302,8 +378,10 @@ def main():
                     help="extra steps timed with the outputs left in HBM (value_device_resident; 0: skip)")
     ap.add_argument("--cpu-budget", type=float, default=16.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--gather", action="store_true",
-                    help="after the timed steps, time the packed-output gather to rank 0 (RCCL point-to-point)")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="N>1: skip the timed gather of every rank's packed output to rank 0 after the timed steps")
+    ap.add_argument("--rms-calls", type=int, default=66,
+                    help="calls checked against the oracle after timing, spread over every plan")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(relaunch(args))
@@ -439,41 +517,33 @@ def main():
     value = samples_all * args.steps / dt
 
     gather_ms = None
-    if args.gather and dist:
-        # SURVEY §8e exchange step: every peer sends its packed output to rank 0
-        # concurrently (one xGMI link each); rank 0 receives into one buffer per peer
-        n_loc = torch.tensor([base], device=dev, dtype=torch.int64)
-        counts = [torch.zeros_like(n_loc) for _ in range(world)]
-        dist.all_gather(counts, n_loc)
-        counts = [int(c.item()) for c in counts]
-        dist.barrier()
-        torch.cuda.synchronize(dev)
-        tg = time.perf_counter()
-        if rank == 0:
-            bufs = [torch.empty(max(counts[r], 1), dtype=torch.float32, device=dev) for r in range(1, world)]
-            ops = [dist.P2POp(dist.irecv, bufs[r - 1][:counts[r]], r) for r in range(1, world) if counts[r]]
-        else:
-            ops = [dist.P2POp(dist.isend, out[:base], 0)] if base else []
-        for w in (dist.batch_isend_irecv(ops) if ops else []):
-            w.wait()
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        gather_ms = (time.perf_counter() - tg) * 1e3
+    if dist and not args.no_gather:
+        # SURVEY §8e exchange step, after the timed steps: every peer sends its packed
+        # output and (offset, length) table to rank 0 (dist.gather_packed: one RCCL
+        # point-to-point transfer per peer, each on its own xGMI link). Not part of
+        # `value` (every rank's outputs already reached its own pinned host memory
+        # over its own PCIe link); gathering to rank 0 and copying from there would
+        # put the whole node behind one link.
+        offs = np.concatenate([b + p.offsets for p, b, _ in plans]) if plans else np.zeros(0, np.int64)
+        lens = np.concatenate([np.where(p.status == 0, p.lengths, -1) for p, _, _ in plans]) if plans else \
+            np.zeros(0, np.int64)
+        got, gather_ms = sharding.gather_timed(out[:max(base, 1)], offs, lens, calls, rank, world)
+        if rank == 0:  # the gathered batch is complete and in call order
+            assert len(got) == n_calls
+            gathered_samples = sum(int(g.numel()) for g in got if not isinstance(g, Exception))
+            assert gathered_samples == int(samples_all), (gathered_samples, samples_all)
+        del got
 
     if rank == 0:
         st = {}
         for p, _, _ in plans:
             for k, v in p.stats().items():
                 st[k] = st.get(k, 0) + v
-        roof = roofline(st, prof, args.steps, args.config)
-        from oracle import oracle as O
-        rms = []
-        p0, b0, i0 = plans[0]
-        for i in [k for k in range(p0.n) if p0.status[k] == 0][:3]:
-            lo, n = b0 + int(p0.offsets[i]), int(p0.lengths[i])
-            y = out[lo:lo + n].double().cpu().numpy()
-            ref = oracle_call(O, calls[int(i0[i])])
-            rms.append(float(np.sqrt(np.mean((y - ref) ** 2))) if len(ref) == len(y) else float("inf"))
+        tot = {k: v[0] * v[1] for k, v in prof.items()}
+        dom = max(tot, key=tot.get) if any(tot.values()) else "sg_sine_bank"
+        roof = roofline(st, prof, args.steps, args.config, dom)
+        other = [k for k in prof if k != dom and prof[k][1] > 0]
+        rms = rms_check(plans, out, calls, args.rms_calls)
         res = {
             "metric": METRIC, "value": value, "unit": "samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
@@ -490,9 +560,13 @@ def main():
             "plan_s": t_plan_max, "calls_gen_s": t_gen,
             "plan_stages": [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in t.items()} for t in plan_stages],
             "value_incl_planning": samples_all / (t_plan_max + dt / args.steps),
-            "rms_error_vs_oracle": max(rms) if rms else None,
+            "rms_error_vs_oracle": rms["max"] if rms else None,
+            "rms_check": rms,
             "roofline": roof,
         }
+        for k in other:  # the other profiled kernel group (C5: the sine-bank classes)
+            res["roofline_" + ("sine_bank" if k == "sg_sine_bank" else "stft_ola")] = \
+                roofline(st, prof, args.steps, args.config, k)
         if gather_ms is not None:
             res["gather_ms"] = gather_ms
         if not args.no_cpu_baseline and world == 1:  # the CPU leg runs at N=1 only

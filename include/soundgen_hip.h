@@ -241,20 +241,56 @@ int sg_plan_stft_stats(const sg_plan* plan, int64_t* samples, int64_t* alg_bytes
 /* Precision path of the plan (ABI 2): per call, the number of its bouts whose
  * formant filter runs in fp64 (source, pre-filter mix and forward STFT; the
  * planner's conditioning estimate of the fp32 round-off through the envelope
- * exceeded its threshold, env SG_HP_RHO, default 300; SG_HP=0 never, 2 always);
+ * exceeded its threshold, env SG_HP_RHO, default 100; SG_HP=0 never, 2 always);
  * totals of fp64 filter frames and sine-bank tasks. Any pointer may be NULL.
  * No reference counterpart: the R path is fp64 throughout. */
 int sg_plan_precision(const sg_plan* plan, int32_t* call_fp64, int64_t* fp64_frames, int64_t* fp64_tasks);
+/* Per call: the planner's conditioning estimate of the formant filter in fp32
+ * (the largest over the call's filtered bouts; 0 when none was estimated):
+ * bouts above the fp64 policy's threshold take the fp64 filter path. */
+int sg_plan_conditioning(const sg_plan* plan, double* rho);
 /* Per-call device work the plan emits (ABI 2): sine-bank (sample, row) terms and
  * nominal FFT flops (5 wl log2 wl per transform), for load balancing across
  * GPUs (soundgen_beta_amd/dist.py). Either pointer may be NULL. */
 int sg_plan_call_work(const sg_plan* plan, double* rows, double* fft_flops);
+/* compareSounds() / getMelSpec() parameters (R/matchPars.R:313-325, :510-520
+ * formals): windowLength and step in ms, overlap in %, throwaway in dB; step
+ * NaN = windowLength * (1 - overlap / 100), maxFreq NaN = samplingRate / 2. */
+typedef struct sg_mel_params {
+  double samplingRate;
+  double windowLength;
+  double overlap;
+  double step;
+  double throwaway;
+  double maxFreq;
+  int32_t penalizeLengthDif;
+  int32_t pad;
+} sg_mel_params;
+/* getMelSpec(s, ...) (R/matchPars.R:510-560: tuneR melfcc(spec_out = TRUE)
+ * $aspectrum, frames with colMeans <= 2^(throwaway/10) dropped, log01) of one
+ * host waveform, computed on the GPU in fp64: out (cap doubles) receives the
+ * nb x nc matrix column-major; *nb and *nc are set (out may be NULL to size).
+ * Windows of more than 4096 FFT points: SG_E_UNSUPPORTED. */
+int sg_mel_spec(sg_ctx* ctx, const double* wave, int64_t len, const sg_mel_params* p, double* out, int64_t cap,
+                int32_t* nb, int32_t* nc);
+/* compareSounds(targetSpec = target, cand = candidate c, ...) for n candidates
+ * in DEVICE memory (fp32, candidate c at d_wave + offsets[c], lengths[c]
+ * samples; lengths[c] <= 0: skipped, NaN), against the host target spectrum
+ * (nb x nc_target column-major, as sg_mel_spec returns it): out[4 c + m] for
+ * m = cor, cosine, pixel, dtw (methods: bit m set = computed, else NaN; dtw is
+ * the dtw package's symmetric2 normalizedDistance), summary[c] the mean of the
+ * computed non-NA methods (compareSounds(summary = TRUE); may be NULL). One
+ * launch sequence for the whole batch (R/matchPars.R:313-416, called per
+ * candidate at :168, :202). */
+int sg_compare_sounds_batch(sg_ctx* ctx, const double* target_spec, int32_t nb, int32_t nc_target,
+                            const float* d_wave, const int64_t* offsets, const int64_t* lengths, int64_t n,
+                            const sg_mel_params* p, int32_t methods, double* out, double* summary);
 /* compareSounds' 'dtw' method (R/matchPars.R:372-376): dtw::dtw(x, y,
  * distance.only = TRUE)$normalizedDistance with the dtw package defaults
  * (|x_i - y_j|, symmetric2, / (n + m)). Host only (ABI 2). */
 int sg_dtw_symmetric2(const double* x, int64_t n, const double* y, int64_t m, double* out);
 /* Process-wide policy of the fp64 filter path for later sg_plan_batch calls:
- * mode 0 never, 1 when the conditioning estimate exceeds rho (default 300),
+ * mode 0 never, 1 when the conditioning estimate exceeds rho (default 100),
  * 2 every filtered bout. SG_E_ARG for an invalid mode or rho. */
 int sg_set_fp64_policy(int32_t mode, double rho);
 /* Process-wide source of the harmonic amplitude matrices for later

@@ -36,6 +36,12 @@ class sg_formants(C.Structure):
                 ("amp", _dp), ("width", _dp)]
 
 
+class sg_mel_params(C.Structure):
+    _fields_ = [("samplingRate", C.c_double), ("windowLength", C.c_double), ("overlap", C.c_double),
+                ("step", C.c_double), ("throwaway", C.c_double), ("maxFreq", C.c_double),
+                ("penalizeLengthDif", C.c_int32), ("pad", C.c_int32)]
+
+
 NORM_CB = C.CFUNCTYPE(C.c_double, C.c_void_p)
 UNIF_CB = C.CFUNCTYPE(C.c_double, C.c_void_p)
 GAMMA_CB = C.CFUNCTYPE(C.c_double, C.c_void_p, C.c_double, C.c_double)

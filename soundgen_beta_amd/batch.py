@@ -111,6 +111,13 @@ class Plan:
         return dict(harm_samples=v[0].value, harm_terms=v[1].value, harm_amp_bytes=v[2].value,
                     fft_frames=v[3].value, stft_samples=w[0].value, stft_bytes=w[1].value, stft_flops=w[2].value)
 
+    def conditioning(self):
+        """Per call: the planner's fp32 conditioning estimate of its formant filter
+        (the largest over its filtered bouts; bouts above the threshold go fp64)."""
+        v = np.zeros(self.n, dtype=np.float64)
+        native.check(native.lib().sg_plan_conditioning(self.ptr, v.ctypes.data_as(C.POINTER(C.c_double))))
+        return v
+
     def precision(self):
         """Per call: bouts on the fp64 filter path; totals of fp64 frames and tasks."""
         v = np.zeros(self.n, dtype=np.int32)

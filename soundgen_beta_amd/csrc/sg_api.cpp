@@ -18,6 +18,7 @@
 #include "sg_exec.h"
 #include "sg_amp.h"
 #include "sg_prof.h"
+#include "sg_mel.h"
 
 #include <cstdio>
 #include <cstdlib>
@@ -164,6 +165,7 @@ void plan_range(sg::Batch& B, const sg_call_desc* calls, int64_t c0, int64_t c1)
   B.call_off.assign(n, 0);
   B.call_status.assign(n, 0);
   B.call_fp64.assign(n, 0);
+  B.call_rho.assign(n, 0.0);
   B.call_rows.assign(n, 0.0);
   B.call_flops.assign(n, 0.0);
   B.call_msg.assign(n, "");
@@ -174,6 +176,7 @@ void plan_range(sg::Batch& B, const sg_call_desc* calls, int64_t c0, int64_t c1)
     const int first_syl = (int)B.syls.size();
     const int64_t hp0 = B.hp_bouts, rows0 = B.harm_terms;
     const double fl0 = B.fft_flops;
+    B.rho_cur = 0;
     try {
       sg::Rng R;
       R.s = &d.random;
@@ -197,6 +200,7 @@ void plan_range(sg::Batch& B, const sg_call_desc* calls, int64_t c0, int64_t c1)
       B.call_off[i] = off;
       B.call_len[i] = L;
       B.call_fp64[i] = (int32_t)(B.hp_bouts - hp0);
+      B.call_rho[i] = B.rho_cur;
       B.call_rows[i] = (double)(B.harm_terms - rows0);
       B.call_flops[i] = B.fft_flops - fl0;
       off += (L + 63) / 64 * 64;  // 256-B aligned call slots
@@ -285,7 +289,7 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
   D.fu_total = c.fu; D.ugath.resize(c.ug);
   D.ecols.resize(c.col); D.envjobs.resize(c.job);
   D.call_len.resize(c.call); D.call_off.resize(c.call); D.call_status.resize(c.call); D.call_msg.resize(c.call);
-  D.call_fp64.resize(c.call); D.call_rows.resize(c.call); D.call_flops.resize(c.call);
+  D.call_fp64.resize(c.call); D.call_rho.resize(c.call); D.call_rows.resize(c.call); D.call_flops.resize(c.call);
   D.epochs.resize(c.epoch); D.knots.resize(c.knot); D.pieces.resize(c.piece);
   D.amp_total = c.amp; D.ampsrc.resize(c.asrc); D.ampcols.resize(c.acol); D.ampjobs.resize(c.ajob); D.syls.resize(c.syl); D.syl_tiles.resize(c.st);
   D.cknots.resize(c.ck); D.items.resize(c.item);
@@ -311,6 +315,7 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
       D.call_off[b.call + i] = S.call_off[i] + b.out;
       D.call_status[b.call + i] = S.call_status[i];
       D.call_fp64[b.call + i] = S.call_fp64[i];
+      D.call_rho[b.call + i] = S.call_rho[i];
       D.call_rows[b.call + i] = S.call_rows[i];
       D.call_flops[b.call + i] = S.call_flops[i];
       D.call_msg[b.call + i] = std::move(S.call_msg[i]);
@@ -730,6 +735,13 @@ int sg_plan_debug_amps(const sg_plan* plan, float* out, int64_t n) {
   return SG_OK;
 }
 
+int sg_plan_conditioning(const sg_plan* plan, double* rho) {
+  if (!plan || !rho) return SG_E_ARG;
+  const sg::Batch& B = plan->B;
+  std::memcpy(rho, B.call_rho.data(), B.call_rho.size() * sizeof(double));
+  return SG_OK;
+}
+
 int sg_plan_precision(const sg_plan* plan, int32_t* call_fp64, int64_t* fp64_frames, int64_t* fp64_tasks) {
   if (!plan) return SG_E_ARG;
   const sg::Batch& B = plan->B;
@@ -749,6 +761,47 @@ int sg_plan_precision(const sg_plan* plan, int32_t* call_fp64, int64_t* fp64_fra
 // local distance |x_i - y_j| (Euclidean, 1-D), step pattern symmetric2
 //   g(i, j) = min(g(i-1, j-1) + 2 d(i, j), g(i-1, j) + d(i, j), g(i, j-1) + d(i, j)),
 // g(1, 1) = d(1, 1), normalised by n + m. Host code (compareSounds, R/matchPars.R:372-376).
+int sg_mel_spec(sg_ctx* ctx, const double* wave, int64_t len, const sg_mel_params* p, double* out, int64_t cap,
+                int32_t* nb, int32_t* nc) {
+  return guarded(ctx, [&]() {
+    if (!ctx || !p || !nb || !nc || len < 0 || (len > 0 && !wave)) throw sg::SgError(SG_E_ARG, "sg_mel_spec: bad arguments");
+    HIPCHK(hipSetDevice(ctx->device));
+    const sg::MelGeom g = sg::mel_geom(*p);
+    if (len == 0) throw sg::SgError(SG_E_ARG, "getMelSpec: empty sound");
+    double* d = nullptr;
+    HIPCHK(hipMalloc(&d, (size_t)len * sizeof(double)));
+    std::unique_ptr<double, void (*)(double*)> hold(d, [](double* q) { (void)hipFree(q); });
+    HIPCHK(hipMemcpyAsync(d, wave, (size_t)len * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    std::vector<double> spec;
+    int nk = 0;
+    sg::mel_spec_device(g, d, len, spec, &nk, ctx->stream);
+    *nb = g.nb;
+    *nc = nk;
+    if (out) {
+      if ((int64_t)spec.size() > cap) throw sg::SgError(SG_E_CAPACITY, "sg_mel_spec: output capacity too small");
+      std::memcpy(out, spec.data(), spec.size() * sizeof(double));
+    }
+    return SG_OK;
+  });
+}
+
+int sg_compare_sounds_batch(sg_ctx* ctx, const double* target_spec, int32_t nb, int32_t nc_target,
+                            const float* d_wave, const int64_t* offsets, const int64_t* lengths, int64_t n,
+                            const sg_mel_params* p, int32_t methods, double* out, double* summary) {
+  return guarded(ctx, [&]() {
+    if (!ctx || !p || !out || n < 0 || (n > 0 && (!offsets || !lengths || !d_wave)) || nc_target < 0 ||
+        (nc_target > 0 && !target_spec) || (methods & ~15) || methods == 0)
+      throw sg::SgError(SG_E_ARG, "sg_compare_sounds_batch: bad arguments");
+    HIPCHK(hipSetDevice(ctx->device));
+    const sg::MelGeom g = sg::mel_geom(*p);
+    if (nb != g.nb) throw sg::SgError(SG_E_ARG, "sg_compare_sounds_batch: target spectrum rows != mel bands");
+    if (n == 0) return SG_OK;
+    sg::compare_sounds_device(g, target_spec, nc_target, d_wave, offsets, lengths, n, methods,
+                              p->penalizeLengthDif != 0, out, summary, ctx->stream);
+    return SG_OK;
+  });
+}
+
 int sg_dtw_symmetric2(const double* x, int64_t n, const double* y, int64_t m, double* out) {
   if (!x || !y || !out || n < 1 || m < 1) return SG_E_ARG;
   std::vector<double> prev((size_t)m), cur((size_t)m);

@@ -39,6 +39,14 @@ constexpr int SG_LDS_ROWS = 256;
 #ifndef SG_NS_MAX
 #define SG_NS_MAX 8  // build knob: largest slot pass (8 or 4)
 #endif
+// Interpolated amplitudes (the dA chain). SG_FAMP 1: ONE chain over the per-sample
+// amplitude a_r(t) = A_r + t dA_r (fma, then the recurrence: 3 VALU ops per row
+// instead of 2 x 2 for the A and dA chains; Reinsch 4 instead of 6), so
+// W = (sum_r a_r(t) sin r theta) by linearity. SG_FAMP 0: the two chains,
+// W = (b_1 + t e_1) sin theta.
+#ifndef SG_FAMP
+#define SG_FAMP 1
+#endif
 
 
 template <bool TWO>
@@ -62,13 +70,20 @@ __device__ __forceinline__ f2 vfma(f2 a, f2 b, f2 c) { return __builtin_elementw
 #define SG_ROW(a, d)                                                  \
   {                                                                   \
     _Pragma("unroll") for (int s = 0; s < NS; ++s) {                  \
-      const Acc b = vfma(al[s], b1[s], (Acc)(a) - b2[s]);             \
-      b2[s] = b1[s];                                                  \
-      b1[s] = b;                                                      \
-      if (TWO) {                                                      \
-        const Acc e = vfma(al[s], e1[s], (Acc)(d) - e2[s]);           \
-        e2[s] = e1[s];                                                \
-        e1[s] = e;                                                    \
+      if (TWO && SG_FAMP) {                                           \
+        const Acc av = vfma(tt[s], (Acc)(d), (Acc)(a));               \
+        const Acc b = vfma(al[s], b1[s], av - b2[s]);                 \
+        b2[s] = b1[s];                                                \
+        b1[s] = b;                                                    \
+      } else {                                                        \
+        const Acc b = vfma(al[s], b1[s], (Acc)(a) - b2[s]);           \
+        b2[s] = b1[s];                                                \
+        b1[s] = b;                                                    \
+        if (TWO) {                                                    \
+          const Acc e = vfma(al[s], e1[s], (Acc)(d) - e2[s]);         \
+          e2[s] = e1[s];                                              \
+          e1[s] = e;                                                  \
+        }                                                             \
       }                                                               \
     }                                                                 \
   }
@@ -77,7 +92,7 @@ __device__ __forceinline__ f2 vfma(f2 a, f2 b, f2 c) { return __builtin_elementw
 #endif
 template <int NS, bool TWO, typename Acc>
 __device__ __forceinline__ void clenshaw_lds(const float* __restrict__ la, const float* __restrict__ ld, int n,
-                                             const Acc (&al)[NS], Acc (&b1)[NS], Acc (&b2)[NS],
+                                             const Acc (&al)[NS], const Acc (&tt)[NS], Acc (&b1)[NS], Acc (&b2)[NS],
                                              Acc (&e1)[NS], Acc (&e2)[NS]) {
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #ifdef SG_DIAG_NOROWS  // diagnostic timing build only: no row work
@@ -132,19 +147,20 @@ __device__ __forceinline__ void sample_setup(const SgWTask& T, int l, float& t, 
 // fp32 slots in pairs: each row is one v_pk_add_f32 + one v_pk_fma_f32 per two samples
 template <int NS, bool TWO>
 __device__ __forceinline__ void clenshaw_pk(const float* __restrict__ la, const float* __restrict__ ld, int n,
-                                            const float (&al)[NS], float (&b1)[NS], float (&b2)[NS], float (&e1)[NS],
-                                            float (&e2)[NS]) {
+                                            const float (&al)[NS], const float (&tt)[NS], float (&b1)[NS],
+                                            float (&b2)[NS], float (&e1)[NS], float (&e2)[NS]) {
   constexpr int NP = NS / 2;
-  f2 al2[NP], p1[NP], p2[NP], q1[NP], q2[NP];
+  f2 al2[NP], t2[NP], p1[NP], p2[NP], q1[NP], q2[NP];
 #pragma unroll
   for (int i = 0; i < NP; ++i) {
     al2[i] = f2{al[2 * i], al[2 * i + 1]};
+    t2[i] = f2{tt[2 * i], tt[2 * i + 1]};
     p1[i] = f2{b1[2 * i], b1[2 * i + 1]};
     p2[i] = f2{b2[2 * i], b2[2 * i + 1]};
     q1[i] = f2{e1[2 * i], e1[2 * i + 1]};
     q2[i] = f2{e2[2 * i], e2[2 * i + 1]};
   }
-  clenshaw_lds<NP, TWO, f2>(la, ld, n, al2, p1, p2, q1, q2);
+  clenshaw_lds<NP, TWO, f2>(la, ld, n, al2, t2, p1, p2, q1, q2);
 #pragma unroll
   for (int i = 0; i < NP; ++i) {
     b1[2 * i] = p1[i].x; b1[2 * i + 1] = p1[i].y;
@@ -155,12 +171,12 @@ __device__ __forceinline__ void clenshaw_pk(const float* __restrict__ la, const 
 }
 template <int NS, bool TWO, typename Acc>
 __device__ __forceinline__ void clenshaw_any(const float* __restrict__ la, const float* __restrict__ ld, int n,
-                                             const Acc (&al)[NS], Acc (&b1)[NS], Acc (&b2)[NS], Acc (&e1)[NS],
-                                             Acc (&e2)[NS]) {
+                                             const Acc (&al)[NS], const Acc (&tt)[NS], Acc (&b1)[NS], Acc (&b2)[NS],
+                                             Acc (&e1)[NS], Acc (&e2)[NS]) {
   if constexpr (SG_PK && sizeof(Acc) == 4 && NS % 2 == 0)
-    clenshaw_pk<NS, TWO>(la, ld, n, al, b1, b2, e1, e2);
+    clenshaw_pk<NS, TWO>(la, ld, n, al, tt, b1, b2, e1, e2);
   else
-    clenshaw_lds<NS, TWO, Acc>(la, ld, n, al, b1, b2, e1, e2);
+    clenshaw_lds<NS, TWO, Acc>(la, ld, n, al, tt, b1, b2, e1, e2);
 }
 
 // fp64 variant for tall tasks (T.R > SG_ROWS_F32, subharmonic sidebands): the
@@ -203,18 +219,21 @@ __device__ __forceinline__ void run_slots(const SgWTask& T, bool staged, float* 
       sample_setup<TWO, LIN>(T, valid[s] ? l[s] : 0, t[s], al[s], sn[s]);
     }
   }
+  Acc tt[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) tt[s] = (Acc)t[s];
   if (staged) {
-    clenshaw_any<NS, TWO, Acc>(la, ld, T.Rn, al, b1, b2, e1, e2);
+    clenshaw_any<NS, TWO, Acc>(la, ld, T.Rn, al, tt, b1, b2, e1, e2);
   } else {  // rare (subharmonic epochs with many rows): 256-row chunks, top first
     for (int r0 = (T.Rn - 1) / SG_LDS_ROWS * SG_LDS_ROWS; r0 >= 0; r0 -= SG_LDS_ROWS) {
       const int n = T.Rn - r0 < SG_LDS_ROWS ? T.Rn - r0 : SG_LDS_ROWS;
       stage_rows<TWO>(la, ld, amps + T.a_off, amps + T.d_off, r0, n, lane);
-      clenshaw_any<NS, TWO, Acc>(la, ld, n, al, b1, b2, e1, e2);
+      clenshaw_any<NS, TWO, Acc>(la, ld, n, al, tt, b1, b2, e1, e2);
     }
   }
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    const Acc yv = (TWO ? fma((Acc)t[s], e1[s], b1[s]) : b1[s]) * sn[s];
+    const Acc yv = (TWO && !SG_FAMP ? fma((Acc)t[s], e1[s], b1[s]) : b1[s]) * sn[s];
     const float y = (float)yv;
     const int j = T.j0 + l[s];
     if (valid[s]) W[T.w_off + j] = (WT)yv;
@@ -338,18 +357,25 @@ __device__ __forceinline__ void run_pair(const SgWTask& P, const SgWTask& Q, flo
   float tp, alp, snp, tq, alq, snq;
   sample_setup<TWO, false>(P, vp ? lane : 0, tp, alp, snp);
   sample_setup<TWO, false>(Q, vq ? lane : 0, tq, alq, snq);
-  const f2 al{alp, alq};
+  const f2 al{alp, alq}, tpq{tp, tq};
   f2 b1{0.f, 0.f}, b2{0.f, 0.f}, e1{0.f, 0.f}, e2{0.f, 0.f};
-#define SG_PROW(a, d)                      \
-  {                                        \
-    const f2 b = vfma(al, b1, (a) - b2);   \
-    b2 = b1;                               \
-    b1 = b;                                \
-    if (TWO) {                             \
-      const f2 e = vfma(al, e1, (d) - e2); \
-      e2 = e1;                             \
-      e1 = e;                              \
-    }                                      \
+#define SG_PROW(a, d)                          \
+  {                                            \
+    if (TWO && SG_FAMP) {                      \
+      const f2 av = vfma(tpq, (d), (a));       \
+      const f2 b = vfma(al, b1, av - b2);      \
+      b2 = b1;                                 \
+      b1 = b;                                  \
+    } else {                                   \
+      const f2 b = vfma(al, b1, (a) - b2);     \
+      b2 = b1;                                 \
+      b1 = b;                                  \
+      if (TWO) {                               \
+        const f2 e = vfma(al, e1, (d) - e2);   \
+        e2 = e1;                               \
+        e1 = e;                                \
+      }                                        \
+    }                                          \
   }
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll 1
@@ -364,8 +390,8 @@ __device__ __forceinline__ void run_pair(const SgWTask& P, const SgWTask& Q, flo
     SG_PROW((f2{A0.x, A0.y}), (f2{D0.x, D0.y}))
   }
 #undef SG_PROW
-  const float yp = (TWO ? fmaf(tp, e1.x, b1.x) : b1.x) * snp;
-  const float yq = (TWO ? fmaf(tq, e1.y, b1.y) : b1.y) * snq;
+  const float yp = (TWO && !SG_FAMP ? fmaf(tp, e1.x, b1.x) : b1.x) * snp;
+  const float yq = (TWO && !SG_FAMP ? fmaf(tq, e1.y, b1.y) : b1.y) * snq;
   const int jp = P.j0 + lane, jq = Q.j0 + lane;
   if (vp) W[P.w_off + jp] = yp;
   if (vq) W[Q.w_off + jq] = yq;
@@ -457,26 +483,27 @@ __device__ __forceinline__ void rs_setup(const SgWTask& T, int l, bool two, floa
   u = pos ? -4.f * s * s : 4.f * c * c;
 }
 
-#define SG_RROW(a, dd)                                   \
-  {                                                      \
-    _Pragma("unroll") for (int p = 0; p < NP; ++p) {     \
-      f2 q = vfma(sg[p], d[p], f2{(a), (a)});            \
-      q = vfma(u[p], b[p], q);                           \
-      b[p] = vfma(sg[p], b[p], q);                       \
-      d[p] = q;                                          \
-      if (TWO) {                                         \
-        f2 r = vfma(sg[p], g[p], f2{(dd), (dd)});        \
-        r = vfma(u[p], e[p], r);                         \
-        e[p] = vfma(sg[p], e[p], r);                     \
-        g[p] = r;                                        \
-      }                                                  \
-    }                                                    \
+#define SG_RROW(a, dd)                                             \
+  {                                                                \
+    _Pragma("unroll") for (int p = 0; p < NP; ++p) {               \
+      const f2 av = (TWO && SG_FAMP) ? vfma(tt[p], f2{(dd), (dd)}, f2{(a), (a)}) : f2{(a), (a)}; \
+      f2 q = vfma(sg[p], d[p], av);                                \
+      q = vfma(u[p], b[p], q);                                     \
+      b[p] = vfma(sg[p], b[p], q);                                 \
+      d[p] = q;                                                    \
+      if (TWO && !SG_FAMP) {                                       \
+        f2 r = vfma(sg[p], g[p], f2{(dd), (dd)});                  \
+        r = vfma(u[p], e[p], r);                                   \
+        e[p] = vfma(sg[p], e[p], r);                               \
+        g[p] = r;                                                  \
+      }                                                            \
+    }                                                              \
   }
 // rows n-1 .. 0 (n a multiple of 4) of the staged chunk, continuing (b, d) and (e, g)
 template <int NP, bool TWO>
 __device__ __forceinline__ void reinsch_lds(const float* __restrict__ la, const float* __restrict__ ld, int n,
-                                            const f2 (&u)[NP], const f2 (&sg)[NP], f2 (&b)[NP], f2 (&d)[NP],
-                                            f2 (&e)[NP], f2 (&g)[NP]) {
+                                            const f2 (&u)[NP], const f2 (&sg)[NP], const f2 (&tt)[NP], f2 (&b)[NP],
+                                            f2 (&d)[NP], f2 (&e)[NP], f2 (&g)[NP]) {
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll 1
   for (int r = n - 4; r >= 0; r -= 4) {
@@ -506,27 +533,28 @@ __device__ __forceinline__ void run_pairs_rs(const SgWTask& T, bool staged, floa
     valid[s] = l[s] < T.len;
     rs_setup(T, valid[s] ? l[s] : 0, TWO, t[s], uu[s], ss[s], sn[s]);
   }
-  f2 u[NP], sg[NP], b[NP], d[NP], e[NP], g[NP];
+  f2 u[NP], sg[NP], t2[NP], b[NP], d[NP], e[NP], g[NP];
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
     u[p] = f2{uu[2 * p], uu[2 * p + 1]};
     sg[p] = f2{ss[2 * p], ss[2 * p + 1]};
+    t2[p] = f2{t[2 * p], t[2 * p + 1]};
     b[p] = d[p] = e[p] = g[p] = f2{0.f, 0.f};
   }
   if (staged) {
-    reinsch_lds<NP, TWO>(la, ld, T.Rn, u, sg, b, d, e, g);
+    reinsch_lds<NP, TWO>(la, ld, T.Rn, u, sg, t2, b, d, e, g);
   } else {  // more than SG_LDS_ROWS rows: 256-row chunks, top first
     for (int r0 = (T.Rn - 1) / SG_LDS_ROWS * SG_LDS_ROWS; r0 >= 0; r0 -= SG_LDS_ROWS) {
       const int n = T.Rn - r0 < SG_LDS_ROWS ? T.Rn - r0 : SG_LDS_ROWS;
       stage_rows<TWO>(la, ld, amps + T.a_off, amps + T.d_off, r0, n, lane);
-      reinsch_lds<NP, TWO>(la, ld, n, u, sg, b, d, e, g);
+      reinsch_lds<NP, TWO>(la, ld, n, u, sg, t2, b, d, e, g);
     }
   }
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const float bs = (s & 1) ? b[s >> 1].y : b[s >> 1].x;
     const float es = (s & 1) ? e[s >> 1].y : e[s >> 1].x;
-    const float y = (TWO ? fmaf(t[s], es, bs) : bs) * sn[s];
+    const float y = (TWO && !SG_FAMP ? fmaf(t[s], es, bs) : bs) * sn[s];
     const int j = T.j0 + l[s];
     if (valid[s]) W[T.w_off + j] = y;
     const bool in = valid[s] && j >= T.dj0 && j < T.dj1;
@@ -570,20 +598,21 @@ __device__ __forceinline__ void run_pair_rs(const SgWTask& P, const SgWTask& Q, 
   float tp, up, sgp, snp, tq, uq, sgq, snq;
   rs_setup(P, vp ? lane : 0, TWO, tp, up, sgp, snp);
   rs_setup(Q, vq ? lane : 0, TWO, tq, uq, sgq, snq);
-  const f2 u{up, uq}, sg{sgp, sgq};
+  const f2 u{up, uq}, sg{sgp, sgq}, tpq{tp, tq};
   f2 b{0.f, 0.f}, d{0.f, 0.f}, e{0.f, 0.f}, g{0.f, 0.f};
-#define SG_RPROW(a, dd)                  \
-  {                                      \
-    f2 q = vfma(sg, d, (a));             \
-    q = vfma(u, b, q);                   \
-    b = vfma(sg, b, q);                  \
-    d = q;                               \
-    if (TWO) {                           \
-      f2 w = vfma(sg, g, (dd));          \
-      w = vfma(u, e, w);                 \
-      e = vfma(sg, e, w);                \
-      g = w;                             \
-    }                                    \
+#define SG_RPROW(a, dd)                                           \
+  {                                                               \
+    const f2 av = (TWO && SG_FAMP) ? vfma(tpq, (dd), (a)) : (a);  \
+    f2 q = vfma(sg, d, av);                                       \
+    q = vfma(u, b, q);                                            \
+    b = vfma(sg, b, q);                                           \
+    d = q;                                                        \
+    if (TWO && !SG_FAMP) {                                        \
+      f2 w = vfma(sg, g, (dd));                                   \
+      w = vfma(u, e, w);                                          \
+      e = vfma(sg, e, w);                                         \
+      g = w;                                                      \
+    }                                                             \
   }
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   constexpr int CH = SG_LDS_ROWS / 2;  // rows per interleaved chunk
@@ -612,8 +641,8 @@ __device__ __forceinline__ void run_pair_rs(const SgWTask& P, const SgWTask& Q, 
     }
   }
 #undef SG_RPROW
-  const float yp = (TWO ? fmaf(tp, e.x, b.x) : b.x) * snp;
-  const float yq = (TWO ? fmaf(tq, e.y, b.y) : b.y) * snq;
+  const float yp = (TWO && !SG_FAMP ? fmaf(tp, e.x, b.x) : b.x) * snp;
+  const float yq = (TWO && !SG_FAMP ? fmaf(tq, e.y, b.y) : b.y) * snq;
   const int jp = P.j0 + lane, jq = Q.j0 + lane;
   if (vp) W[P.w_off + jp] = yp;
   if (vq) W[Q.w_off + jq] = yq;

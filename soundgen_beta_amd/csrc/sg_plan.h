@@ -183,6 +183,8 @@ struct Batch {
   std::vector<int64_t> call_len, call_off;
   std::vector<int32_t> call_status;
   std::vector<int32_t> call_fp64;   // bouts of the call on the fp64 filter path
+  std::vector<double> call_rho;     // the largest conditioning estimate over the call's filtered bouts
+  double rho_cur = 0;               // (the call being planned)
   std::vector<std::string> call_msg;
   int64_t total_out = 0;
   // ---- stats ----

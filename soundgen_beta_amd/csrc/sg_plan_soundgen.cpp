@@ -378,7 +378,7 @@ double hp_rho() {
   double r = g_hp_rho.load();
   if (r < 0) {
     const char* e = std::getenv("SG_HP_RHO");
-    r = e ? std::atof(e) : 300.0;
+    r = e ? std::atof(e) : 100.0;  // measured: tools/selector_study.py (profiles/r04b_selector_study.json)
     g_hp_rho.store(r);
   }
   return r;
@@ -621,7 +621,9 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
         } else {
           std::vector<ProbeAt> pa;
           for (size_t q = 0; q < probes.size(); ++q) pa.push_back(ProbeAt{probe_pos[q], &probes[q]});
-          hp = filter_conditioning(*grid, pa, (double)wl - A.overlap * wl / 100, wl, sr) > hp_rho();
+          const double rho = filter_conditioning(*grid, pa, (double)wl - A.overlap * wl / 100, wl, sr);
+          B.rho_cur = std::max(B.rho_cur, rho);
+          hp = rho > hp_rho();
         }
       }
     }

@@ -242,3 +242,25 @@ def synthesize_sharded(calls, rank, world, device=None, synth=None, root=0, comm
         buf = data.cpu().numpy() if to_host else data
         return [RuntimeError("call failed") if n < 0 else buf[int(o):int(o) + int(n)] for o, n in zip(offs, lens)]
     return gather_packed(data, offs, lens, owner, rank, world, root, to_host)
+
+
+def gather_timed(data, offsets, lengths, calls, rank, world, root=0):
+    """The bench's exchange step at N > 1 (bench.py, default): every rank's packed
+    shard outputs (`data`, shard call i at offsets[i], lengths[i] samples, -1
+    failed; shard order as shard() lists it) gathered to the root in call order
+    by gather_packed, bracketed by barriers. Returns (root: the per-call list,
+    else None; wall ms of the exchange, the same on every rank's clock span)."""
+    import time
+
+    import torch
+    import torch.distributed as dist
+    owner = lpt_assign([call_cost(c) for c in calls], world)
+    sync = (lambda: torch.cuda.synchronize(data.device)) if data.is_cuda else (lambda: None)
+    dist.barrier()
+    sync()
+    t = time.perf_counter()
+    got = gather_packed(data, offsets, lengths, owner, rank, world, root)
+    sync()
+    dist.barrier()
+    return got, (time.perf_counter() - t) * 1e3
+

@@ -11,6 +11,12 @@ after morph().
   stripping (colMeans > 2^(throwaway / 10)) and log01.
 - compareSounds: per column cor / cosine / pixel / dtw of the two spectra
   (matchColumns pads the shorter with NA, central), averaged as R does.
+- On the GPU (sg_mel.hip, the product path of match_pars): get_mel_spec_gpu and
+  compare_sounds_batch run both for a whole generation of candidates in HBM in
+  one launch sequence (fp64 FFT frames, mel bands, kept columns, then one
+  wavefront per column for cor / cosine / pixel / dtw). The numpy functions
+  below (get_mel_spec, compare_sounds) are the host restatement the GPU tests
+  compare against.
   dtw: the dtw package's default (symmetric2 steps, Euclidean local distance,
   normalizedDistance = distance / (n + m)) computed by the library
   (sg_dtw_symmetric2); the dtw package is not vendored: parity unpinned.
@@ -401,6 +407,67 @@ def compare_sounds(target=None, targetSpec=None, cand=None, samplingRate=None,
     return out
 
 
+# ------------------------------------------------------- on the GPU (sg_mel.hip)
+_METHOD_BITS = {"cor": 1, "cosine": 2, "pixel": 4, "dtw": 8}
+_METHOD_ORDER = ("cor", "cosine", "pixel", "dtw")
+
+
+def _mel_params(samplingRate, windowLength=40, overlap=50, step=None, throwaway=-120, maxFreq=None,
+                penalizeLengthDif=True):
+    from . import _abi
+    return _abi.sg_mel_params(float(samplingRate), float(windowLength), float(overlap),
+                              math.nan if step is None else float(step), float(throwaway),
+                              math.nan if maxFreq is None else float(maxFreq), int(bool(penalizeLengthDif)), 0)
+
+
+def get_mel_spec_gpu(s, samplingRate, windowLength=40, overlap=50, step=None, throwaway=-120, maxFreq=None, device=0):
+    """getMelSpec() (R/matchPars.R:510-560) computed on the GPU (sg_mel_spec, fp64):
+    the same nb x nc matrix as get_mel_spec."""
+    L = native.lib()
+    ctx = native.default_context(device)
+    x = np.ascontiguousarray(np.asarray(s, dtype=np.float64))
+    P = _mel_params(samplingRate, windowLength, overlap, step, throwaway, maxFreq)
+    nb, nc = C.c_int32(), C.c_int32()
+    dp = C.POINTER(C.c_double)
+    native.check(L.sg_mel_spec(ctx.ptr, x.ctypes.data_as(dp), len(x), C.byref(P), None, 0, C.byref(nb), C.byref(nc)),
+                 ctx.ptr)
+    out = np.zeros(nb.value * nc.value)
+    native.check(L.sg_mel_spec(ctx.ptr, x.ctypes.data_as(dp), len(x), C.byref(P), out.ctypes.data_as(dp), len(out),
+                               C.byref(nb), C.byref(nc)), ctx.ptr)
+    return out.reshape(nc.value, nb.value).T
+
+
+def compare_sounds_batch(targetSpec, data, offsets, lengths, samplingRate, method=_METHOD_ORDER, windowLength=40,
+                         overlap=50, step=None, penalizeLengthDif=True, throwaway=-120, maxFreq=None, device=0):
+    """compareSounds(targetSpec = targetSpec, cand = c, ..., summary = FALSE) for a
+    batch of candidates already in HBM (`data`: a float32 CUDA tensor, candidate i
+    at offsets[i], lengths[i] samples, < 0 for a failed call -- the layout of
+    batch.synthesize_packed), in one launch sequence (sg_compare_sounds_batch):
+    returns (per method a float array over the candidates, the summary array:
+    the mean of the non-NA methods, compareSounds(summary = TRUE))."""
+    L = native.lib()
+    ctx = native.default_context(device)
+    mask = 0
+    for m in method:
+        mask |= _METHOD_BITS[m]
+    T = np.asfortranarray(np.asarray(targetSpec, dtype=np.float64))
+    nb, ncT = T.shape if T.ndim == 2 else (0, 0)
+    tflat = np.ascontiguousarray(T.T.ravel())  # column-major
+    offs = np.ascontiguousarray(np.asarray(offsets, dtype=np.int64))
+    lens = np.ascontiguousarray(np.asarray(lengths, dtype=np.int64))
+    n = len(offs)
+    out = np.full(4 * n, np.nan)
+    summ = np.full(n, np.nan)
+    P = _mel_params(samplingRate, windowLength, overlap, step, throwaway, maxFreq, penalizeLengthDif)
+    dp = C.POINTER(C.c_double)
+    i64p = C.POINTER(C.c_int64)
+    native.check(L.sg_compare_sounds_batch(ctx.ptr, tflat.ctypes.data_as(dp), int(nb), int(ncT), C.c_void_p(
+        data.data_ptr()), offs.ctypes.data_as(i64p), lens.ctypes.data_as(i64p), n, C.byref(P), mask,
+        out.ctypes.data_as(dp), summ.ctypes.data_as(dp)), ctx.ptr)
+    out = out.reshape(n, 4)
+    return {m: out[:, k] for k, m in enumerate(_METHOD_ORDER) if m in method}, summ
+
+
 # ---------------------------------------------------------------- matchPars
 def match_pars(target, samplingRate, pars, init=None, method=("cor", "cosine", "pixel", "dtw"), probMutation=.25,
                stepVariance=0.1, maxIter=50, minExpectedDelta=0.001, windowLength=40, overlap=50, step=None,
@@ -415,7 +482,7 @@ def match_pars(target, samplingRate, pars, init=None, method=("cor", "cosine", "
     D = _Draws(rng)
     kw = dict(windowLength=windowLength, overlap=overlap, step=step, penalizeLengthDif=penalizeLengthDif,
               throwaway=throwaway, maxFreq=maxFreq)
-    targetSpec = get_mel_spec(target, samplingRate, windowLength, overlap, step, throwaway, maxFreq)
+    targetSpec = get_mel_spec_gpu(target, samplingRate, windowLength, overlap, step, throwaway, maxFreq, device)
     defaults = MATCHPARS_DEFAULTS
     parDefault = {p: copy.deepcopy(defaults[p]) for p in pars}
     for k, v in (init or {}).items():
@@ -427,20 +494,26 @@ def match_pars(target, samplingRate, pars, init=None, method=("cor", "cosine", "
     def call(p):
         return {"kind": "soundgen", "args": _soundgen_args(p), "rng": rng}
 
-    first = batch.synthesize([call(parDefault)], device)[0]
-    if isinstance(first, Exception):
-        raise ValueError("Invalid initial pars: %s" % first)
-    sim0 = compare_sounds(None, targetSpec, first, samplingRate, method, summary=True, **kw)
+    def score(calls):
+        """One generation on the GPU: the candidates synthesized as one batch into
+        HBM, their spectra and similarities in one launch sequence; -inf for a
+        call the planner refused."""
+        data, offs, lens = batch.synthesize_packed(calls, device)
+        _, summ = compare_sounds_batch(targetSpec, data, offs, lens, samplingRate, method, device=device, **kw)
+        return [(-math.inf if n < 0 or math.isnan(v) else float(v)) for v, n in zip(summ, lens)], lens
+
+    sims, lens = score([call(parDefault)])
+    if lens[0] < 0:
+        raise ValueError("Invalid initial pars")
+    sim0 = sims[0]
     history = [{"pars": parDefault, "sim": sim0}]
     parLoop, i, evaluated = parDefault, 1, 1
     while i < maxIter:
         muts = [wiggle_pars(D, parLoop, list(pars), probMutation, stepVariance) for _ in range(pop)]
-        cands = batch.synthesize([call(m) for m in muts], device)
+        sims, _ = score([call(m) for m in muts])
         best, best_m = -math.inf, None
-        for m, y in zip(muts, cands):
+        for m, s in zip(muts, sims):
             evaluated += 1
-            s = -math.inf if isinstance(y, Exception) else compare_sounds(None, targetSpec, y, samplingRate, method,
-                                                                          summary=True, **kw)
             if s > best:
                 best, best_m = s, m
         if best - history[-1]["sim"] > minExpectedDelta:

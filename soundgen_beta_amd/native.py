@@ -15,6 +15,9 @@ LIB_PATH = os.environ.get("SG_HIP_LIB") or os.path.join(_HERE, "lib", "libsoundg
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "soundgen_hip.h")
 
 _lib = None
+# the planner's default threshold on its fp32 conditioning estimate of a formant
+# filter (sg_set_fp64_policy; DESIGN.md §5 "fp64 path")
+HP_RHO_DEFAULT = 100.0
 
 
 class SoundgenError(RuntimeError):
@@ -72,6 +75,7 @@ def lib():
     L.sg_profile_read.argtypes = [vp, dp, i64p]
     L.sg_profile_read_kernel.argtypes = [vp, C.c_int, dp, i64p]
     L.sg_plan_stft_stats.argtypes = [vp, i64p, i64p, dp]
+    L.sg_plan_conditioning.argtypes = [vp, dp]
     L.sg_plan_precision.argtypes = [vp, C.POINTER(C.c_int32), i64p, i64p]
     L.sg_set_fp64_policy.argtypes = [C.c_int32, C.c_double]
     L.sg_set_amp_policy.argtypes = [C.c_int32]
@@ -86,6 +90,10 @@ def lib():
     L.sg_plan_debug_amps.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.c_int64]
     L.sg_plan_call_work.argtypes = [vp, dp, dp]
     L.sg_dtw_symmetric2.argtypes = [dp, i64, dp, i64, dp]
+    L.sg_mel_spec.argtypes = [vp, dp, i64, C.POINTER(_abi.sg_mel_params), dp, i64, C.POINTER(C.c_int32),
+                              C.POINTER(C.c_int32)]
+    L.sg_compare_sounds_batch.argtypes = [vp, dp, C.c_int32, C.c_int32, vp, i64p, i64p, i64,
+                                          C.POINTER(_abi.sg_mel_params), C.c_int32, dp, dp]
     L.sg_rrng_create.argtypes = [C.c_int32, C.POINTER(vp)]
     L.sg_rrng_destroy.argtypes = [vp]
     L.sg_rrng_set_seed.argtypes = [vp, C.c_int32]

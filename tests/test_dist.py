@@ -103,6 +103,32 @@ def _worker(rank, world, port, q):
         # buffer; the root still returns every call, as host arrays with to_host
         two = [_calls()[0], _calls()[-1]]
         res0 = sgd.synthesize_sharded(two, rank, world, synth=_oracle_synth, comm_device="cpu", to_host=True)
+        # bench.py's default exchange at N > 1 (dist.gather_timed): the shard's outputs in
+        # several plan regions of one packed buffer (plan k at base b_k, its calls at
+        # b_k + offsets), gathered to rank 0 in call order
+        calls = _calls()
+        idx, mine, _ = sgd.shard(calls, rank, world)
+        outs = _oracle_synth(mine)
+        half = len(outs) // 2
+        parts = [sgd.pack_outputs(outs[:half]), sgd.pack_outputs(outs[half:])]
+        base = [0, int(parts[0][0].numel()) + 64]
+        import torch
+        data = torch.zeros(base[1] + int(parts[1][0].numel()), dtype=torch.float32)
+        offs, lens = [], []
+        for (d, o, n), b in zip(parts, base):
+            data[b:b + d.numel()] = d
+            offs.append(b + o)
+            lens.append(n)
+        gt, ms = sgd.gather_timed(data, np.concatenate(offs), np.concatenate(lens), calls, rank, world)
+        assert ms >= 0
+        if rank == 0:
+            assert len(gt) == len(calls)
+            for g, r in zip(gt, res):
+                assert isinstance(g, Exception) == isinstance(r, Exception)
+                if not isinstance(g, Exception):
+                    assert np.array_equal(g.numpy(), np.asarray(r))
+        else:
+            assert gt is None
         # the real host planner on this rank's shard of 96 C5 calls (CPU planning)
         from soundgen_beta_amd import batch
         calls = _bench().c5_calls(96)

@@ -193,19 +193,19 @@ def _per_preset(bench, k):
 def test_c5_every_preset_vs_oracle(oracle, policy):
     """Two calls of EACH of the 33 presets against the oracle at RMS <= 1e-5.
     policy 1: the default (fp64 filter path where the planner's conditioning
-    estimate exceeds 300: Misc$Cow); policy 2: every filtered bout on the fp64
+    estimate exceeds native.HP_RHO_DEFAULT: Misc$Cow, Misc$Elephant); policy 2: every filtered bout on the fp64
     path (sg_sine_bank_hp, sg_harm_finalize_hp, sg_mix_hp, sg_fft_frames64)."""
     bench = _bench()
     from soundgen_beta_amd import batch, native
     calls = _per_preset(bench, 2)
     L = native.lib()
-    assert L.sg_set_fp64_policy(policy, 300.0) == 0
+    assert L.sg_set_fp64_policy(policy, native.HP_RHO_DEFAULT) == 0
     try:
         plan = batch.Plan(calls, None)
         hp, nfr, ntk = plan.precision()
         outs = batch.synthesize(calls)
     finally:
-        L.sg_set_fp64_policy(1, 300.0)
+        L.sg_set_fp64_policy(1, native.HP_RHO_DEFAULT)
     cow = [i for i, c in enumerate(calls) if c["preset"] == "Misc$Cow"]
     assert all(hp[i] > 0 for i in cow)
     worst = {}

@@ -155,3 +155,59 @@ def test_match_pars_batch_equals_single_calls():
     for m, y in zip(muts, ys):
         ref = api.soundgen(**MP._soundgen_args(m))
         assert len(ref) == len(y) and np.array_equal(np.float32(ref), np.float32(y))
+
+
+def _mel_batch_calls(sr, n, seed):
+    rng = np.random.default_rng(seed)
+    calls = []
+    for i in range(n):
+        f0 = float(np.exp(rng.uniform(np.log(90), np.log(500))))
+        calls.append({"kind": "soundgen", "args": {
+            "sylLen": float(rng.uniform(150, 900)), "samplingRate": sr, "temperature": 0, "addSilence": 0,
+            "pitchAnchors": {"time": [0, 1], "value": [f0, f0 * float(rng.uniform(0.7, 1.5))]},
+            "formants": str(rng.choice(list("aoieu"))), "rolloff": float(rng.uniform(-18, -6)),
+            "noiseAnchors": {"time": [0, 300], "value": [float(rng.uniform(-40, -10))] * 2}},
+            "uniforms": rng.uniform(size=200000)})
+    return calls
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sr,wl,ov", [(16000, 40, 50), (44100, 40, 50), (22050, 25, 70)])
+def test_mel_spec_gpu_equals_numpy(sr, wl, ov):
+    """getMelSpec on the GPU (sg_mel_spec) vs the numpy restatement: same columns kept, <= 1e-9."""
+    from soundgen_beta_amd import api
+    y = api.soundgen(sylLen=700, samplingRate=sr, temperature=0, addSilence=50,
+                     pitchAnchors={"time": [0, 1], "value": [140, 260]}, formants="ai")
+    got = MP.get_mel_spec_gpu(y, sr, windowLength=wl, overlap=ov)
+    want = MP.get_mel_spec(y, sr, windowLength=wl, overlap=ov)
+    assert got.shape == want.shape
+    np.testing.assert_allclose(got, want, rtol=0, atol=1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("penalize", [True, False])
+def test_compare_sounds_batch_gpu_equals_numpy(penalize):
+    """compareSounds for a generation of 40 candidates in HBM (one launch sequence,
+    sg_compare_sounds_batch) vs the numpy compare_sounds per candidate: every
+    method (cor, cosine, pixel, dtw) and the summary within 1e-6; candidates both
+    shorter and longer than the target (matchColumns' NA padding on either side)."""
+    from soundgen_beta_amd import api, batch
+    sr = 16000
+    target = api.soundgen(sylLen=500, samplingRate=sr, temperature=0, addSilence=0,
+                          pitchAnchors={"time": [0, 1], "value": [150, 220]}, formants="ae")
+    tspec = MP.get_mel_spec(target, sr)
+    calls = _mel_batch_calls(sr, 40, 5)
+    data, offs, lens = batch.synthesize_packed(calls, 0)
+    assert (lens > 0).all()
+    got, summ = MP.compare_sounds_batch(tspec, data, offs, lens, sr, penalizeLengthDif=penalize)
+    host = data.cpu().numpy()
+    ncols = set()
+    for i in range(len(calls)):
+        y = host[offs[i]:offs[i] + lens[i]].astype(np.float64)
+        want = MP.compare_sounds(None, tspec, y, sr, summary=False, penalizeLengthDif=penalize)
+        ncols.add(np.sign(MP.get_mel_spec(y, sr).shape[1] - tspec.shape[1]))
+        for m in ("cor", "cosine", "pixel", "dtw"):
+            assert abs(got[m][i] - want[m]) <= 1e-6, (i, m, got[m][i], want[m])
+        vals = [v for v in want.values() if not math.isnan(v)]
+        assert abs(summ[i] - np.mean(vals)) <= 1e-6
+    assert ncols >= {-1, 1}  # shorter and longer candidates both exercised

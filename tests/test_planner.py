@@ -164,20 +164,20 @@ def test_precision_path_flags_ill_conditioned_presets():
     assert frames > 0 and tasks > 0
     from soundgen_beta_amd import native
     L = native.lib()
-    assert L.sg_set_fp64_policy(0, 300.0) == 0
+    assert L.sg_set_fp64_policy(0, native.HP_RHO_DEFAULT) == 0
     try:
         p0 = batch.Plan(calls, None)
         h0, f0, t0 = p0.precision()
         assert h0.sum() == 0 and f0 == 0 and t0 == 0
         assert np.array_equal(p0.lengths, plan.lengths) and np.array_equal(p0.offsets, plan.offsets)
-        assert L.sg_set_fp64_policy(2, 300.0) == 0
+        assert L.sg_set_fp64_policy(2, native.HP_RHO_DEFAULT) == 0
         p2 = batch.Plan(calls, None)
         h2, f2, t2 = p2.precision()
         assert (h2 >= hp).all() and f2 >= frames and t2 > tasks
         assert np.array_equal(p2.lengths, plan.lengths) and np.array_equal(p2.offsets, plan.offsets)
-        assert L.sg_set_fp64_policy(3, 300.0) != 0
+        assert L.sg_set_fp64_policy(3, native.HP_RHO_DEFAULT) != 0
     finally:
-        L.sg_set_fp64_policy(1, 300.0)
+        L.sg_set_fp64_policy(1, native.HP_RHO_DEFAULT)
 
 
 def _decode_args(s):
