@@ -353,7 +353,9 @@ int sg_formant_filter(sg_ctx* ctx, const double* sound, int64_t len,
  * valueCeiling, samplingRate)  R/smoothContours.R:53-227 (exported,
  * NAMESPACE:10); method 0 = 'loess' (R's default), 1 = 'spline'. The
  * planner's own contour (host, fp64). out holds len doubles; *out_len = 0 when
- * R returns NA (no anchors, len 0). */
+ * R returns NA (no anchors, len 0). len = -1 is R's len = NULL: the anchor
+ * times are in ms and len = floor(duration_ms * samplingRate / 1000) (out must
+ * then hold that many doubles). */
 int sg_get_smooth_contour(sg_anchors anchors, int64_t len, int32_t thisIsPitch, int32_t method, int32_t has_floor,
                           double valueFloor, int32_t has_ceil, double valueCeiling, double samplingRate, double* out,
                           int64_t* out_len);

@@ -289,9 +289,11 @@ def smooth_contour(anchors, len, thisIsPitch=False, method="loess", valueFloor=N
     """getSmoothContour(anchors, len, ...) (R/smoothContours.R:53-227)."""
     t = _f64(anchors["time"])
     v = _f64(anchors["value"])
-    n_out = int(len)
-    out = np.zeros(n_out)
-    _check(lib().or_smooth_contour(_abi.dptr(t), _abi.dptr(v), t.size, n_out, int(bool(thisIsPitch)),
+    # len None: R's len = NULL (times in ms, len = floor(duration_ms sr / 1000))
+    n_out = int(np.floor((t.max() - t.min()) * samplingRate / 1000)) if len is None else int(len)
+    out = np.zeros(max(n_out, 0))
+    _check(lib().or_smooth_contour(_abi.dptr(t), _abi.dptr(v), t.size, -1 if len is None else n_out,
+                                   int(bool(thisIsPitch)),
                                    0 if method == "loess" else 1, int(valueFloor is not None),
                                    float(valueFloor or 0.0), int(valueCeiling is not None),
                                    float(valueCeiling or 0.0), float(samplingRate), _abi.dptr(out)))

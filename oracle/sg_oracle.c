@@ -484,11 +484,21 @@ static int get_smooth_contour(sg_anchors an, int64_t len, int thisIsPitch,
     if (has_floor) vfloor = HzToSemitones(vfloor);
     if (has_ceil) vceil = HzToSemitones(vceil);
   }
+  /* R/smoothContours.R:92-101: len = NULL (here len < 0) keeps the times in ms,
+   * len = floor(duration_ms sr / 1000); a given len rescales them to 0..1 */
+  double dur_ms = (double)len / sr * 1000;
+  dv traw = dv_copy(t.v, n);
+  const int len_null = len < 0;
+  if (len_null) {
+    dur_ms = r_max(t.v, n) - r_min(t.v, n);
+    len = (int64_t)floor(dur_ms * sr / 1000);
+    if (!(dur_ms != 0)) len = 0;
+  }
   double tmin = r_min(t.v, n);
   for (int64_t i = 0; i < n; ++i) t.v[i] -= tmin;
   double tmax = r_max(t.v, n);
   for (int64_t i = 0; i < n; ++i) t.v[i] /= tmax;
-  if (len == 0) { dv_free(&t); dv_free(&val); return 0; }
+  if (len <= 0) { dv_free(&t); dv_free(&val); dv_free(&traw); return 0; }
   int rc = 0;
   if (n == 1) {
     *out = dv_new(len); for (int64_t i = 0; i < len; ++i) out->v[i] = val.v[0];
@@ -497,10 +507,10 @@ static int get_smooth_contour(sg_anchors an, int64_t len, int thisIsPitch,
   } else {
     if (method != 1) {
       *out = dv_new(len);
-      rc = smooth_loess(t.v, val.v, n, len, (double)len / sr * 1000, has_floor, vfloor, out->v);
+      rc = smooth_loess(t.v, val.v, n, len, dur_ms, has_floor, vfloor, out->v);
       if (rc) { dv_free(out); out->n = 0; goto done; }
     } else {
-      *out = r_spline(t.v, val.v, n, len);
+      *out = r_spline(len_null ? traw.v : t.v, val.v, n, len);
     }
     for (int64_t i = 0; i < len; ++i) {
       if (has_floor && out->v[i] < vfloor) out->v[i] = vfloor;
@@ -510,7 +520,7 @@ static int get_smooth_contour(sg_anchors an, int64_t len, int thisIsPitch,
   for (int64_t i = 0; i < out->n; ++i) if (isnan(out->v[i])) out->v[i] = 0;
   if (thisIsPitch) for (int64_t i = 0; i < out->n; ++i) out->v[i] = semitonesToHz(out->v[i]);
 done:
-  dv_free(&t); dv_free(&val);
+  dv_free(&t); dv_free(&val); dv_free(&traw);
   return rc;
 }
 
@@ -1508,6 +1518,7 @@ OR_API int or_smooth_contour(const double* time, const double* value, int64_t n,
   dv c;
   const int rc = get_smooth_contour(an, len, thisIsPitch, method, has_floor, vfloor, has_ceil, vceil, sr, &c);
   if (rc) return rc;
+  if (len < 0) len = c.n;  /* len = NULL: the caller sized out from the anchors' span */
   for (int64_t i = 0; i < len; ++i) out[i] = i < c.n ? c.v[i] : NAN;
   dv_free(&c);
   return 0;

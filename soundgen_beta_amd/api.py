@@ -155,21 +155,20 @@ def getSmoothContour(anchors=None, len=None, thisIsPitch=False, method="loess", 
     """getSmoothContour() — R/smoothContours.R:53-227 (exported; host helper through the
     planner's own contour code). anchors: {"time": ..., "value": ...}, a numeric vector
     (time spread over 0..1), or NA/None. len None: anchors' time is the duration in ms
-    and len = floor(duration_ms * samplingRate / 1000) (R/smoothContours.R:92-96; the
-    times are then normalised like a given len, which can differ from R by rounding).
-    Returns a float64 array, or None where R returns NA."""
+    and len = floor(duration_ms * samplingRate / 1000), the times kept in ms and the
+    loess span taken from that duration, as R/smoothContours.R:92-96 does (len = -1
+    at the C ABI). Returns a float64 array, or None where R returns NA."""
     an = rargs.as_anchors(anchors)
     if an is None:
         return None
     t, v = an
-    if len is None:
-        len = int(np.floor((np.max(t) - np.min(t)) * samplingRate / 1000))
-    len = int(len)
-    if len <= 0:
+    cap = int(np.floor((np.max(t) - np.min(t)) * samplingRate / 1000)) if len is None else int(len)
+    if cap <= 0:
         return None
+    len = -1 if len is None else cap
     h = rargs.Holder()
     s = h.anchors(an)
-    out = np.zeros(len)
+    out = np.zeros(cap)
     n = C.c_int64()
     L = native.lib()
     rc = L.sg_get_smooth_contour(s, len, int(bool(thisIsPitch)), 1 if method == "spline" else 0,

@@ -1092,7 +1092,7 @@ int sg_get_smooth_contour(sg_anchors anchors, int64_t len, int32_t thisIsPitch, 
                           double valueFloor, int32_t has_ceil, double valueCeiling, double samplingRate, double* out,
                           int64_t* out_len) {
   return guarded(nullptr, [&]() {
-    if (!out_len || len < 0 || (len > 0 && !out)) throw sg::SgError(SG_E_ARG, "sg_get_smooth_contour: arguments");
+    if (!out_len || len < -1 || (len != 0 && !out)) throw sg::SgError(SG_E_ARG, "sg_get_smooth_contour: arguments");
     sg::vec v;
     *out_len = 0;
     if (!sg::smooth_contour(anchors, len, thisIsPitch != 0, method, has_floor != 0, valueFloor, has_ceil != 0,

@@ -1280,12 +1280,10 @@ __device__ __forceinline__ float fade_in_out(int lf, int64_t L, int64_t k) {  //
 // wl = 2204: 4 workgroups per CU). Per stage of radix R: (a) every input times
 // its twiddle, in place; (b) odd R: one work item per (butterfly, output pair k,
 // R - k) from the symmetric sums x_m +- x_{R-m} (all threads busy for R = 19,
-// 29), R = 2, 4: one item per butterfly. Roots of unity W_N^t from an fp64 table
+// 29), R = 2, 4: one item per butterfly. (Grouping several outputs per item so each
+// input pair is read once measured no better: r04d, +2 % at 3, +21 % at 2 per item.) Roots of unity W_N^t from an fp64 table
 // in global memory, one per window length (sg_roots64), L2-resident.
 constexpr int SG_F64_THREADS = 256;
-#ifndef SG_F64_KG
-#define SG_F64_KG 1  // build knob: outputs per work item of an odd-radix fp64 stage (1: one per item)
-#endif
 namespace {
 __device__ __forceinline__ double2 cmul64(double2 a, double2 b) {
   return make_double2(fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x));
@@ -1332,54 +1330,6 @@ __device__ void stage64(double2* __restrict__ src, double2* __restrict__ dst, in
     // y_k = x_0 + sum_m A_m c_mk -/+ i sum_m B_m s_mk (forward -, inverse +), y_{R-k} the
     // other sign; A_m = x_m + x_{R-m}, B_m = x_m - x_{R-m}; item k = 0: y_0 = x_0 + sum A_m
     constexpr int H = (R - 1) / 2;
-#if SG_F64_KG > 1
-    // one work item per (butterfly, group of KG consecutive outputs k): each pair
-    // (x_m, x_{R-m}) is read once for the group (the per-k form re-read all of them per k)
-    constexpr int KG = SG_F64_KG, NG = (H + 1 + KG - 1) / KG;
-    for (int i = threadIdx.x; i < nR * NG; i += SG_F64_THREADS) {
-      const int g = i % NG, j = i / NG, jm = j % Ns;
-      const double2* x = src + j;
-      double2* y = dst + (j - jm) * R + jm;
-      const double2 x0 = x[0];
-      double2 P[KG], Q[KG];
-      int t[KG];
-#pragma unroll
-      for (int e = 0; e < KG; ++e) {
-        P[e] = make_double2(0.0, 0.0);
-        Q[e] = make_double2(0.0, 0.0);
-        t[e] = 0;
-      }
-#pragma unroll 1
-      for (int m = 1; m <= H; ++m) {
-        const double2 u = x[m * nR], v = x[(R - m) * nR];
-        const double2 A = make_double2(u.x + v.x, u.y + v.y), B = make_double2(u.x - v.x, u.y - v.y);
-#pragma unroll
-        for (int e = 0; e < KG; ++e) {
-          const int k = g * KG + e;
-          t[e] += k;  // (m k) mod R
-          if (t[e] >= R) t[e] -= R;
-          const double2 w = k == 0 ? make_double2(1.0, 0.0) : rt[t[e]];  // (cos, -sin) of 2 pi m k / R
-          P[e].x = fma(A.x, w.x, P[e].x);
-          P[e].y = fma(A.y, w.x, P[e].y);
-          Q[e].x = fma(B.x, -w.y, Q[e].x);
-          Q[e].y = fma(B.y, -w.y, Q[e].y);
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < KG; ++e) {
-        const int k = g * KG + e;
-        if (k > H) break;
-        const double2 ya = make_double2(x0.x + P[e].x + Q[e].y, x0.y + P[e].y - Q[e].x);
-        const double2 yb = make_double2(x0.x + P[e].x - Q[e].y, x0.y + P[e].y + Q[e].x);
-        if (k == 0) {
-          y[0] = ya;
-        } else {
-          y[k * Ns] = inv ? yb : ya;
-          y[(R - k) * Ns] = inv ? ya : yb;
-        }
-      }
-    }
-#else
     for (int i = threadIdx.x; i < nR * (H + 1); i += SG_F64_THREADS) {
       const int k = i % (H + 1), j = i / (H + 1), jm = j % Ns;
       const double2* x = src + j;
@@ -1407,7 +1357,6 @@ __device__ void stage64(double2* __restrict__ src, double2* __restrict__ dst, in
         y[(R - k) * Ns] = inv ? ya : yb;
       }
     }
-#endif
   }
   __syncthreads();
 }

@@ -36,16 +36,26 @@ bool smooth_contour(const sg_anchors& an, int64_t len, bool thisIsPitch, int met
     if (has_floor) vfloor = HzToSemitones(vfloor);
     if (has_ceil) vceil = HzToSemitones(vceil);
   }
+  // len = NULL (len < 0, R/smoothContours.R:92-96): the times are durations in ms
+  // and stay as they are (spline's x); len = floor(duration_ms * sr / 1000)
+  const vec traw = t;
+  const bool len_null = len < 0;
+  double dur_ms = (double)len / sr * 1000;
+  if (len_null) {
+    dur_ms = r_max(t) - r_min(t);
+    len = (int64_t)std::floor(dur_ms * sr / 1000);
+    if (!(dur_ms != 0)) return false;
+  }
   const double tmin = r_min(t);
   for (auto& x : t) x -= tmin;
   const double tmax = r_max(t);
-  for (auto& x : t) x /= tmax;
-  if (len == 0) return false;
+  for (auto& x : t) x /= tmax;  // (the loess anchor points: the same bits either way)
+  if (len <= 0) return false;
   if (n == 1) out.assign(len, v[0]);
   else if (n == 2) out = r_seq_len(v[0], v[1], len);
   else {
-    if (method != 1) {  // loess, R/smoothContours.R:119-154 (duration_ms = len / sr * 1000)
-      const LoessFit T = smooth_loess(t.data(), v.data(), n, len, (double)len / sr * 1000, has_floor, vfloor);
+    if (method != 1) {  // loess, R/smoothContours.R:119-154 (duration_ms: len / sr * 1000, or the anchors' span)
+      const LoessFit T = smooth_loess(t.data(), v.data(), n, len, dur_ms, has_floor, vfloor);
       out.resize(len);
       int leaf = -1;
       for (int64_t k = 0; k < len; ++k) {
@@ -53,7 +63,7 @@ bool smooth_contour(const sg_anchors& an, int64_t len, bool thisIsPitch, int met
         out[k] = (z < T.xmin || z > T.xmax) ? NAN : T.eval_seq(z, leaf);
       }
     } else {
-      out = r_spline(t, v, len);
+      out = r_spline(len_null ? traw : t, v, len);
     }
     for (auto& x : out) {
       if (has_floor && x < vfloor) x = vfloor;

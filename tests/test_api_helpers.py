@@ -18,14 +18,15 @@ from soundgen_beta_amd import api
          valueCeiling=8),
     dict(anchors={"time": [0, 50, 120, 300], "value": [200, 400, 250, 210]}, len=None, thisIsPitch=True,
          samplingRate=16000),
+    # len = NULL (R/smoothContours.R:92-96): times in ms, not starting at 0; loess span
+    # from the anchors' duration; spline over the raw times
+    dict(anchors={"time": [20, 95, 130, 333], "value": [200, 400, 250, 210]}, len=None, samplingRate=22050),
+    dict(anchors={"time": [20, 95, 130, 333, 400], "value": [1, 4, 2, 8, 3]}, len=None, method="spline",
+         samplingRate=44100),
 ])
 def test_get_smooth_contour_vs_oracle(oracle, case):
     got = api.getSmoothContour(**case)
-    c = dict(case)
-    if c.get("len") is None:
-        t = c["anchors"]["time"]
-        c["len"] = int(np.floor((max(t) - min(t)) * c.get("samplingRate", 16000) / 1000))
-    want = oracle.smooth_contour(**c)
+    want = oracle.smooth_contour(**case)
     assert got is not None and got.shape == want.shape
     np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-12)
 
@@ -53,6 +54,22 @@ def test_get_smooth_contour_floor_refits_vs_oracle(oracle):
 def test_get_smooth_contour_na():
     assert api.getSmoothContour(None, len=100) is None
     assert api.getSmoothContour({"time": [0, 1], "value": [1, 2]}, len=0) is None
+    assert api.getSmoothContour({"time": [5, 5], "value": [1, 2]}) is None  # len = NULL, zero duration
+
+
+def test_get_smooth_contour_len_null_uses_the_anchor_duration(oracle):
+    """len = NULL differs from the len it implies: the loess span is taken from
+    the anchors' duration, not from floor(duration sr / 1000) / sr (the API used
+    to pass the floored len, a rounding deviation from R)."""
+    # 365.47 ms: floor(4 span) = 2 from the anchors' duration, 3 from 5847 / 16 kHz
+    a = {"time": [0, 137.3, 261.9, 365.47], "value": [3, 9, 1, 4]}
+    sr = 16000
+    n = int(np.floor(365.47 * sr / 1000))
+    null = api.getSmoothContour(a, len=None, samplingRate=sr)
+    given = api.getSmoothContour(a, len=n, samplingRate=sr)
+    assert len(null) == len(given) == n
+    np.testing.assert_allclose(null, oracle.smooth_contour(a, None, samplingRate=sr), rtol=1e-12, atol=1e-12)
+    assert not np.allclose(null, given, rtol=0, atol=1e-12)
 
 
 def test_find_zero_crossing_vs_oracle(oracle):
