@@ -218,6 +218,8 @@ def rms_check(plans, out, calls, n_check):
     evenly over every plan's synthesized calls, on the /max-normalised waveform
     both return (R/soundgen.R:807); lengths must match exactly. The calls the
     planner sent to the fp64 filter path are all included when present."""
+    if n_check <= 0:
+        return None
     from concurrent.futures import ThreadPoolExecutor
     from oracle import oracle as O
     O.lib()
