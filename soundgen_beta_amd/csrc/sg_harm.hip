@@ -231,6 +231,22 @@ __device__ __forceinline__ void run_slots(const SgWTask& T, bool staged, float* 
       clenshaw_any<NS, TWO, Acc>(la, ld, n, al, tt, b1, b2, e1, e2);
     }
   }
+  // a pass whose samples all exist and all land 1:1 in the syllable (most of a long
+  // task's passes): no per-lane range tests in the epilogue
+#ifndef SG_FAST_EPI
+#define SG_FAST_EPI 1  // build knob
+#endif
+  const int jp0 = T.j0 + l0;
+  if (SG_FAST_EPI && !ENV && l0 + 64 * NS <= T.len && jp0 >= T.dj0 && jp0 + 64 * NS <= T.dj1) {
+    WT* __restrict__ wp = W + T.w_off + jp0 + lane;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const Acc yv = (TWO && !SG_FAMP ? fma((Acc)t[s], e1[s], b1[s]) : b1[s]) * sn[s];
+      wp[64 * s] = (WT)yv;
+      tmax = fmaxf(tmax, (float)yv);
+    }
+    return;
+  }
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const Acc yv = (TWO && !SG_FAMP ? fma((Acc)t[s], e1[s], b1[s]) : b1[s]) * sn[s];
@@ -399,7 +415,12 @@ __device__ __forceinline__ void run_pair(const SgWTask& P, const SgWTask& Q, flo
   mq = vq && jq >= Q.dj0 && jq < Q.dj1 ? yq : 0.f;
 }
 
-// Tasks of the fp32 class (listed in idx), one per wave.
+// Tasks of the fp32 class (listed in idx), one per wave; SG_SB_PERSIST: a grid of
+// resident waves, each walking the list with the grid's stride (no wave launch
+// per task).
+#ifndef SG_SB_PERSIST
+#define SG_SB_PERSIST 0  // build knob
+#endif
 extern "C" __global__ __launch_bounds__(256) void sg_sine_bank(
     const int32_t* __restrict__ idx, int64_t n, const SgWTask* __restrict__ tasks, const float* __restrict__ amps,
     const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, float* __restrict__ W,
@@ -407,12 +428,23 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank(
   __shared__ __attribute__((aligned(16))) float rows[4][2][SG_LDS_ROWS];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if SG_SB_PERSIST
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  for (int64_t k = (int64_t)blockIdx.x * 4 + wave; k < n; k += stride) {
+    const int64_t ti = idx[k];
+    const SgWTask T = tasks[ti];
+    const float wm = wave_max(run_one(T, rows[wave][0], rows[wave][1], amps, syls, cknots, W, lane));
+    if (lane == 0) taskmax[ti] = wm;
+    __builtin_amdgcn_wave_barrier();  // the next task's rows overwrite this one's LDS slot
+  }
+#else
   const int64_t k = (int64_t)blockIdx.x * 4 + wave;
   if (k >= n) return;
   const int64_t ti = idx[k];
   const SgWTask T = tasks[ti];
   const float wm = wave_max(run_one(T, rows[wave][0], rows[wave][1], amps, syls, cknots, W, lane));
   if (lane == 0) taskmax[ti] = wm;
+#endif
 }
 
 // Short fp32 tasks (<= 64 samples, no envelope; listed in idx), two per wave in
@@ -1205,7 +1237,12 @@ void launch_amp_build(const DevicePlan& D, int64_t n_jobs, hipStream_t s) {
 }
 void launch_sine_bank(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(sg_sine_bank, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, D.tlong + k0, n, D.tasks, D.amps,
+#if SG_SB_PERSIST
+  const int64_t nb = std::min<int64_t>((n + 3) / 4, SG_SB_PERSIST * 256);  // SG_SB_PERSIST workgroups per CU
+#else
+  const int64_t nb = (n + 3) / 4;
+#endif
+  hipLaunchKernelGGL(sg_sine_bank, dim3((unsigned)nb), dim3(256), 0, s, D.tlong + k0, n, D.tasks, D.amps,
                      D.syls, D.cknots, D.W, D.taskmax);
   SG_LAUNCHED("sg_sine_bank");
 }
