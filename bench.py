@@ -296,7 +296,7 @@ def pmc_from_profiles(config, kernel):
 
 # waves per SIMD the kernels run at (hipcc -Rpass-analysis=kernel-resource-usage, gfx950)
 WAVES_PER_SIMD = {"sg_stft_ola": 2, "sg_stft_ola_noise": 3, "sg_sine_bank": 7, "sg_sine_bank_pairs": 8,
-                  "sg_sine_bank_tall": 5, "sg_sine_bank_tall_pairs": 8}
+                  "sg_sine_bank_tall": 5, "sg_sine_bank_tall_pairs": 8, "sg_sine_bank_tab": 8, "sg_sine_bank_tab4k": 4}
 
 
 def roofline(st, prof, steps, config, kern):
@@ -317,7 +317,8 @@ def roofline(st, prof, steps, config, kern):
         vfrac = valu_ops / sec / VALU_PEAK_OPS if sec else 0
         extra = {"valu": {"ops_per_launch": valu_ops, "achieved_ops_s": valu_ops / sec if sec else 0,
                           "peak_ops_s": VALU_PEAK_OPS, "frac": vfrac}}
-        kernels = ("sg_sine_bank", "sg_sine_bank_pairs", "sg_sine_bank_tall", "sg_sine_bank_tall_pairs")
+        kernels = ("sg_sine_bank", "sg_sine_bank_pairs", "sg_sine_bank_tall", "sg_sine_bank_tall_pairs",
+                   "sg_sine_bank_tab", "sg_sine_bank_tab4k")
         name = " + ".join(kernels)
     else:
         # source / uniforms + envelope columns read, trimmed output written

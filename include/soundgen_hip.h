@@ -233,6 +233,10 @@ const char* sg_plan_call_message(const sg_plan* plan, int64_t i);
 int sg_plan_kernel_stats(const sg_plan* plan, int64_t* harm_samples,
                          int64_t* harm_terms, int64_t* harm_amp_bytes,
                          int64_t* fft_frames);
+/* Wavetable spans of an uploaded plan (sg_set_sine_table): workgroups that
+ * each build a table per execute, the samples they produce and the (sample, row) recurrence terms
+ * those samples stand in for; zeros before upload. */
+int sg_plan_table_stats(const sg_plan* plan, int64_t* tables, int64_t* samples, int64_t* terms);
 /* sg_stft_ola work of the plan (fused seewave stft x envelope -> istft -> OLA,
  * R/soundgen.R:743-807, and generateNoise's istft, R/source.R:88-131): trimmed
  * output samples, algorithmic HBM bytes (source/uniforms + envelope columns +
@@ -305,6 +309,13 @@ int sg_set_amp_policy(int32_t host_built);
  * copied into the plan (the same values either way; tests compare the two).
  * The arrays are read during sg_plan_batch only. */
 int sg_set_uniform_gather(int32_t on);
+/* Process-wide switch of the sine bank's wavetable path, for plans uploaded
+ * later (sg_plan_upload, or the first sg_execute of a plan): 1 (default)
+ * long runs of constant-amplitude, linear-phase tasks (static tones) sample a
+ * per-span table of the harmonic sum by cubic Hermite interpolation
+ * (sg_sine_bank_tab); 0 every task runs the row recurrence. SG_TABLE=0 in the
+ * environment sets the default off. */
+int sg_set_sine_table(int32_t on);
 /* Release the planner's process-wide cache of freed host blocks (kept for the
  * next plan, capped by SG_HOST_CACHE_MB or 8 GB / LOCAL_WORLD_SIZE). Returns
  * the bytes released. Safe at any time; later plans refill it. */

@@ -111,6 +111,12 @@ class Plan:
         return dict(harm_samples=v[0].value, harm_terms=v[1].value, harm_amp_bytes=v[2].value,
                     fft_frames=v[3].value, stft_samples=w[0].value, stft_bytes=w[1].value, stft_flops=w[2].value)
 
+    def table_stats(self):
+        """Wavetable spans of the uploaded plan: (tables, samples, terms)."""
+        v = [C.c_int64() for _ in range(3)]
+        native.check(native.lib().sg_plan_table_stats(self.ptr, *[C.byref(x) for x in v]))
+        return tuple(x.value for x in v)
+
     def conditioning(self):
         """Per call: the planner's fp32 conditioning estimate of its formant filter
         (the largest over its filtered bouts; bouts above the threshold go fp64)."""

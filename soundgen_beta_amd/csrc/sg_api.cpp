@@ -704,6 +704,14 @@ int sg_plan_kernel_stats(const sg_plan* plan, int64_t* harm_samples, int64_t* ha
   return SG_OK;
 }
 
+int sg_plan_table_stats(const sg_plan* plan, int64_t* tables, int64_t* samples, int64_t* terms) {
+  if (!plan || !tables || !samples || !terms) return SG_E_ARG;
+  *tables = plan->D.uploaded ? (int64_t)plan->D.tabjobs_host.size() : 0;
+  *samples = plan->D.uploaded ? plan->D.tab_samples : 0;
+  *terms = plan->D.uploaded ? plan->D.tab_terms : 0;
+  return SG_OK;
+}
+
 int sg_plan_stft_stats(const sg_plan* plan, int64_t* samples, int64_t* alg_bytes, double* flops) {
   if (!plan) return SG_E_ARG;
   *samples = plan->B.stft_samples;

@@ -80,6 +80,30 @@ struct SgWTask {
                        // all zero (rounded up to 4; they add exact zeros); R keeps the class
 };
 static_assert(sizeof(SgWTask) == 128, "SgWTask layout");
+
+// Wavetable path of a long span of constant-amplitude, linear-phase tasks (a static
+// tone: SG_TASK_CONST | SG_TASK_LIN over thousands of samples, e.g. C2's tones).
+// There W(j) = S(x_j) with S(x) = sum_r A_r sin(2 pi r x) a fixed 1-periodic function
+// of the phase x_j in cycles. One workgroup per span (sg_sine_bank_tab) tabulates S
+// and dS/dx at N = 2^b points per cycle into LDS (one fp32 inverse FFT; each
+// interval's cubic Hermite coefficients), then every sample of the span's tasks is
+// one table read and three FMAs at its phase, carried per lane as a 32-bit fixed
+// point fraction of a cycle (one integer add per 64 samples; rounding <= 2^-33
+// cycles per add). The interpolation error is at most
+// (2 pi)^4 sum_r |A_r| r^4 / (384 N^4); the planner takes the smallest N in
+// [2^8, 2^11] that holds it to SG_TAB_TOL sum_r |A_r| for the span's amplitude
+// column (no table if none does), so a rolled-off spectrum gets a small table
+// (tests/test_gpu_parity.py: the table path's error against the oracle stays at or
+// below the fp32 recurrence's). The table is rebuilt every execute, by every
+// workgroup of the span, and a span takes one only with >= 4 N samples.
+struct SgTabJob {    // one workgroup: tasks [t0, t0 + n) (consecutive) on one amplitude column
+  int64_t a_off;     // the column A[0..Rn)
+  int32_t Rn, t0, n, logn;
+};
+constexpr int SG_TAB_LOGN_MIN = 8;
+constexpr int SG_TAB_LOGN_MAX = 11;   // LDS 20 N bytes: 40 KB
+constexpr double SG_TAB_TOL = 1e-7;
+constexpr int SG_TAB_TASKS = 64;      // tasks per workgroup at most (a longer span: more workgroups)
 #ifndef SG_PAIR
 #define SG_PAIR 1  // build knob: short fp32 tasks (<= 64 samples) two per wave in the halves of packed pairs
 #endif

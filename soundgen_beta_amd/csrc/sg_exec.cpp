@@ -1,7 +1,11 @@
 // sg_exec.cpp — HBM arena for a plan and the per-batch launch sequence.
 #include "sg_exec.h"
+#include "sg_amp.h"
 
 #include <algorithm>
+#include <cmath>
+#include <climits>
+#include <atomic>
 #include <map>
 #include <cstdlib>
 #include <cstdio>
@@ -142,6 +146,97 @@ static void split_finalize_tiles(Batch& B) {
   }
 }
 
+// Wavetable spans (SgTabJob, sg_dev.h): runs of consecutive constant-amplitude,
+// linear-phase fp32 tasks of one syllable on one amplitude column whose
+// interpolation-error bound admits a table of N <= 2^SG_TAB_LOGN_MAX points and
+// with >= 4 N samples; each run one job per SG_TAB_TASKS tasks, in task order.
+struct TabSpans {
+  std::vector<SgTabJob> jobs;
+  std::vector<uint8_t> in_tab;
+  int64_t tasks = 0;
+  int64_t samples = 0, terms = 0;
+};
+// the column's amplitudes as sg_amp_build computes them (host restatement)
+struct ColumnReader {
+  const Batch& B;
+  std::vector<std::pair<int64_t, int32_t>> by_off;  // (amp_off, job)
+  std::vector<double> lg;
+  explicit ColumnReader(const Batch& b) : B(b) {
+    for (size_t j = 0; j < B.ampjobs.size(); ++j) by_off.push_back({B.ampjobs[j].amp_off, (int32_t)j});
+    std::sort(by_off.begin(), by_off.end());
+    lg.resize((size_t)B.amp_lg_rows + 2);
+    for (size_t k = 0; k < lg.size(); ++k) lg[k] = std::log2((double)(k + 1));
+  }
+  // smallest log2 N with the bound <= SG_TAB_TOL sum |A_r|, 0 if none <= SG_TAB_LOGN_MAX
+  int logn(int64_t a_off, int32_t Rn) const {
+    auto it = std::upper_bound(by_off.begin(), by_off.end(), std::make_pair(a_off, INT32_MAX));
+    if (it == by_off.begin()) return 0;
+    const SgAmpJob& J = B.ampjobs[(size_t)std::prev(it)->second];
+    const int64_t rel = a_off - J.amp_off;
+    if (J.Rp <= 0 || rel % J.Rp != 0 || rel / J.Rp >= J.G || Rn > J.Rp) return 0;
+    const int g = (int)(rel / J.Rp);
+    double s0 = 0, s4 = 0;
+    for (int r = 0; r < Rn; ++r) {
+      double a = 0;
+      if (r < J.R) a = J.src_off >= 0 ? (double)B.ampsrc[(size_t)(J.src_off + (int64_t)g * J.Rp + r)]
+                                      : (double)(float)amp_value(B.ampcols.data() + J.col0, J, lg.data(), g, r);
+      const double k = r + 1.0;
+      s0 += std::fabs(a);
+      s4 += std::fabs(a) * k * k * k * k;
+    }
+    if (!(s0 > 0)) return 0;
+    const double two_pi4 = 1558.5454565440389;  // (2 pi)^4
+    for (int b = SG_TAB_LOGN_MIN; b <= SG_TAB_LOGN_MAX; ++b) {
+      const double n4 = std::ldexp(1.0, 4 * b);
+      if (two_pi4 * s4 / (384.0 * n4) <= SG_TAB_TOL * s0) return b;
+    }
+    return 0;
+  }
+};
+static TabSpans group_tables(const Batch& B) {
+  TabSpans S;
+  const int64_t ntask = bulk_size(B.tasks_x, B.tasks);
+  S.in_tab.assign((size_t)ntask, 0);
+  auto tab_task = [](const SgWTask& t) {
+    return t.flags == (SG_TASK_CONST | SG_TASK_LIN) && t.R <= SG_ROWS_F32 && t.Rn > 0 && t.len > 64;
+  };
+  const ColumnReader cols(B);
+  std::vector<SgTabJob> jobs;
+  int64_t run0 = -1, run_samples = 0;
+  SgWTask first{};
+  auto close_run = [&](int64_t end) {  // tasks [run0, end)
+    if (run0 < 0) return;
+    const int logn = run_samples >= (int64_t(4) << SG_TAB_LOGN_MIN) ? cols.logn(first.a_off, first.Rn) : 0;
+    if (logn && run_samples >= (int64_t(4) << logn)) {
+      for (int64_t i = run0; i < end; i += SG_TAB_TASKS) {
+        const int32_t n = (int32_t)std::min<int64_t>(SG_TAB_TASKS, end - i);
+        jobs.push_back(SgTabJob{first.a_off, first.Rn, (int32_t)i, n, logn});
+        for (int64_t q = i; q < i + n; ++q) S.in_tab[(size_t)q] = 1;
+      }
+      S.samples += run_samples;
+      S.terms += run_samples * first.Rn;
+    }
+    run0 = -1;
+  };
+  bulk_each(B.tasks_x, B.tasks, [&](int64_t o, const SgWTask* p, int64_t n) {
+    for (int64_t k = 0; k < n; ++k) {
+      const SgWTask& t = p[k];
+      const bool ok = tab_task(t);
+      if (run0 >= 0 && !(ok && t.a_off == first.a_off && t.Rn == first.Rn && t.syl == first.syl)) close_run(o + k);
+      if (ok && run0 < 0) {
+        run0 = o + k;
+        first = t;
+        run_samples = 0;
+      }
+      if (ok) run_samples += t.len;
+    }
+  });
+  close_run(ntask);
+  for (const SgTabJob& j : jobs) S.tasks += j.n;
+  S.jobs = std::move(jobs);
+  return S;
+}
+
 void finalize_plan(Batch& B) {
   split_finalize_tiles(B);
   if (std::getenv("SG_DEBUG_PLAN")) {
@@ -156,6 +251,20 @@ void finalize_plan(Batch& B) {
       }
       std::fprintf(stderr, "sg plan: amplitude bytes: plain epochs %.3g, subharmonic epochs %.3g (%lld of %zu)\n", plain,
                    fry, (long long)nfry, B.epochs.size());
+    }
+    {
+      const TabSpans T = group_tables(B);
+      int64_t cl = 0, cl_samples = 0;
+      bulk_each(B.tasks_x, B.tasks, [&](int64_t, const SgWTask* p, int64_t n) {
+        for (int64_t k = 0; k < n; ++k)
+          if (p[k].flags == (SG_TASK_CONST | SG_TASK_LIN)) { ++cl; cl_samples += p[k].len; }
+      });
+      int64_t hist[13] = {0};
+      for (const SgTabJob& j : T.jobs) ++hist[j.logn];
+      std::fprintf(stderr, "sg plan: wavetable jobs %zu (N = 256/512/1024/2048: %lld %lld %lld %lld; %zu tasks, %lld samples, %.3g terms); CONST|LIN tasks %lld (%lld samples)\n",
+                   T.jobs.size(), (long long)hist[8], (long long)hist[9], (long long)hist[10], (long long)hist[11],
+                   (size_t)T.tasks, (long long)T.samples, (double)T.terms, (long long)cl,
+                   (long long)cl_samples);
     }
     std::vector<SgWTask> tasks;  // the merged task list (debug statistics only)
     bulk_each(B.tasks_x, B.tasks, [&](int64_t, const SgWTask* p, int64_t n) { tasks.insert(tasks.end(), p, p + n); });
@@ -250,12 +359,35 @@ int64_t device_bytes(const Batch& B) { return (int64_t)Layout(B).total; }
 
 void device_free(DevicePlan& D) {
   if (D.arena) (void)hipFree(D.arena);
+  if (D.tabbuf) (void)hipFree(D.tabbuf);
   D.pcm.free();
   for (hipEvent_t e : D.ev_slice) (void)hipEventDestroy(e);
   if (D.ev_fork) (void)hipEventDestroy(D.ev_fork);
   if (D.ev_join) (void)hipEventDestroy(D.ev_join);
   D = DevicePlan{};
 }
+
+// wavetable path for long static spans (sg_sine_bank_tab): on by default;
+// SG_TABLE=0 or sg_set_sine_table(0) turns it off
+static std::atomic<int> g_tab{-1};
+static bool tab_on() {
+  int v = g_tab.load();
+  if (v < 0) {
+    const char* e = std::getenv("SG_TABLE");
+    v = (e && e[0] == '0') ? 0 : 1;
+    int expect = -1;
+    g_tab.compare_exchange_strong(expect, v);
+  }
+  return v != 0;
+}
+
+}  // namespace sg
+extern "C" int sg_set_sine_table(int32_t on) {
+  if (on != 0 && on != 1) return SG_E_ARG;
+  sg::g_tab.store(on);
+  return SG_OK;
+}
+namespace sg {
 
 void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   Layout L(B);
@@ -331,11 +463,31 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   D.tshort_host.clear();
   D.tallp_host.clear();
   D.thp_host.clear();
+  // wavetable spans (SgTabJob, sg_dev.h)
+  TabSpans T;
+  if (tab_on()) T = group_tables(B);
+  D.tabjobs_host.swap(T.jobs);
+  const std::vector<uint8_t>& in_tab = T.in_tab;
+  D.tab_samples = T.samples;
+  D.tab_terms = T.terms;
+  if (!D.tabjobs_host.empty()) {  // one allocation kept across uploads
+    const size_t bj = D.tabjobs_host.size() * sizeof(SgTabJob);
+    if (D.tabbuf && D.tabbuf_bytes < bj) {
+      (void)hipFree(D.tabbuf);
+      D.tabbuf = nullptr;
+    }
+    if (!D.tabbuf) {
+      HIPCHK(hipMalloc(&D.tabbuf, bj));
+      D.tabbuf_bytes = bj;
+    }
+    D.tabjobs = (SgTabJob*)D.tabbuf;
+  }
   bulk_each(B.tasks_x, B.tasks, [&](int64_t o, const SgWTask* p, int64_t n) {
     for (int64_t k = 0; k < n; ++k) {
       const SgWTask& t = p[k];
       const int32_t i = (int32_t)(o + k);
       const bool shrt = t.len <= 64 && !(t.flags & SG_TASK_ENV);
+      if (!in_tab.empty() && in_tab[(size_t)i]) continue;
       if (t.flags & SG_TASK_HP) D.thp_host.push_back(i);
       else if (t.R > SG_ROWS_F32) (SG_TALL_PAIR && shrt ? D.tallp_host : D.tall_host).push_back(i);
       else if (SG_PAIR && t.len <= 64 && !(t.flags & SG_TASK_ENV)) D.tshort_host.push_back(i);
@@ -347,6 +499,7 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   cp(D.tshort, D.tshort_host.data(), D.tshort_host.size() * sizeof(int32_t));
   cp(D.tallp, D.tallp_host.data(), D.tallp_host.size() * sizeof(int32_t));
   cp(D.thp, D.thp_host.data(), D.thp_host.size() * sizeof(int32_t));
+  if (!D.tabjobs_host.empty()) cp(D.tabjobs, D.tabjobs_host.data(), D.tabjobs_host.size() * sizeof(SgTabJob));
   cp(D.fin_tiles_hp, B.fin_tiles_hp.data(), B.fin_tiles_hp.size() * sizeof(SgSylTile));
   cp(D.frames64, B.frames64.data(), B.frames64.size() * sizeof(SgFrame64));
   cp(D.frames64_tab, B.frames64_tab.data(), B.frames64_tab.size() * sizeof(int64_t));
@@ -430,6 +583,14 @@ static void device_execute_harm(const Batch& B, DevicePlan& D, float* d_out, hip
       launch_sine_bank_tall(D, k0, n, h);
       n = range(D.tallp_host, k0);
       launch_sine_bank_tall_pairs(D, k0, n, h);
+      if (!D.tabjobs_host.empty()) {  // the jobs whose first task lies in the slice, one launch
+        const auto& J = D.tabjobs_host;
+        const auto lo = std::partition_point(J.begin(), J.end(), [&](const SgTabJob& j) { return j.t0 < sl.t0; });
+        const auto hi = std::partition_point(lo, J.end(), [&](const SgTabJob& j) { return j.t0 < sl.t1; });
+        int logn = 0;
+        for (auto it = lo; it != hi; ++it) logn = std::max<int>(logn, it->logn);
+        launch_sine_bank_tab(D, logn, lo - J.begin(), hi - lo, h);
+      }
     }
     if (prof) {
       HIPCHK(hipEventRecord(e1, h));

@@ -43,6 +43,13 @@ struct DevicePlan {
   std::vector<int32_t> tallp_host;
   int32_t* thp = nullptr;            // SG_TASK_HP tasks (sg_sine_bank_hp)
   std::vector<int32_t> thp_host;
+  // wavetable path (SgTabJob): tasks of long static-tone spans
+  // (a separate allocation made at upload)
+  char* tabbuf = nullptr;              // the wavetable spans' jobs (sg_sine_bank_tab)
+  size_t tabbuf_bytes = 0;
+  SgTabJob* tabjobs = nullptr;         // in task order
+  std::vector<SgTabJob> tabjobs_host;
+  int64_t tab_samples = 0, tab_terms = 0;  // samples and (sample, row) terms the tables stand in for
   SgSylTile* fin_tiles_hp = nullptr; // finalize tiles of fp64 syllables (sg_harm_finalize_hp)
   double* W64 = nullptr;             // fp64 epoch waveforms of SG_TASK_HP tasks
   double* fh = nullptr;              // fp64 sounds (voiced parts, pre-filter sounds) of fp64 bouts
@@ -120,6 +127,7 @@ void launch_harm_finalize(const DevicePlan& D, int64_t f0, int64_t n_stiles, flo
 void launch_harm_copy(const DevicePlan& D, int64_t c0, int64_t n_ctiles, float* out, hipStream_t s);
 // the fp64 path of ill-conditioned formant-filter calls (SG_TASK_HP, SgSyllable::hp, sg_mix to fh, SgFrame64)
 void launch_sine_bank_hp(const DevicePlan& D, int64_t n, hipStream_t s);
+void launch_sine_bank_tab(const DevicePlan& D, int logn, int64_t j0, int64_t n, hipStream_t s);
 void launch_piece_max_hp(const DevicePlan& D, int64_t p0, int64_t n_ptiles, hipStream_t s);
 void launch_harm_finalize_hp(const DevicePlan& D, int64_t n_stiles, hipStream_t s);
 void launch_mix_hp(const DevicePlan& D, int64_t t0, int64_t n_tiles, hipStream_t s);

@@ -415,12 +415,8 @@ __device__ __forceinline__ void run_pair(const SgWTask& P, const SgWTask& Q, flo
   mq = vq && jq >= Q.dj0 && jq < Q.dj1 ? yq : 0.f;
 }
 
-// Tasks of the fp32 class (listed in idx), one per wave; SG_SB_PERSIST: a grid of
-// resident waves, each walking the list with the grid's stride (no wave launch
-// per task).
-#ifndef SG_SB_PERSIST
-#define SG_SB_PERSIST 0  // build knob
-#endif
+// Tasks of the fp32 class (listed in idx), one per wave. (A grid of resident waves
+// walking the list measured slower: r04f, C2 +14 %, C5 +22 %.)
 extern "C" __global__ __launch_bounds__(256) void sg_sine_bank(
     const int32_t* __restrict__ idx, int64_t n, const SgWTask* __restrict__ tasks, const float* __restrict__ amps,
     const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, float* __restrict__ W,
@@ -428,23 +424,12 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank(
   __shared__ __attribute__((aligned(16))) float rows[4][2][SG_LDS_ROWS];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#if SG_SB_PERSIST
-  const int64_t stride = (int64_t)gridDim.x * 4;
-  for (int64_t k = (int64_t)blockIdx.x * 4 + wave; k < n; k += stride) {
-    const int64_t ti = idx[k];
-    const SgWTask T = tasks[ti];
-    const float wm = wave_max(run_one(T, rows[wave][0], rows[wave][1], amps, syls, cknots, W, lane));
-    if (lane == 0) taskmax[ti] = wm;
-    __builtin_amdgcn_wave_barrier();  // the next task's rows overwrite this one's LDS slot
-  }
-#else
   const int64_t k = (int64_t)blockIdx.x * 4 + wave;
   if (k >= n) return;
   const int64_t ti = idx[k];
   const SgWTask T = tasks[ti];
   const float wm = wave_max(run_one(T, rows[wave][0], rows[wave][1], amps, syls, cknots, W, lane));
   if (lane == 0) taskmax[ti] = wm;
-#endif
 }
 
 // Short fp32 tasks (<= 64 samples, no envelope; listed in idx), two per wave in
@@ -778,6 +763,165 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_hp(
   const SgWTask T = tasks[ti];
   const float wm = wave_max(run_one_hp(T, rows[wave][0], rows[wave][1], amps, syls, cknots, W64, lane));
   if (lane == 0) taskmax[ti] = wm;
+}
+
+// ------------------------------------------- wavetable path (SgTabJob, sg_dev.h)
+// One workgroup per job. Table: S and h dS/dx (h = 1 / N) at the N points as the
+// real and imaginary parts of ONE inverse complex DFT, x_k = sum_m Z_m e^{2 pi i m k / N}
+// with Z = U + i V for the two Hermitian spectra U_{+-r} = -+i A_r / 2 (real part:
+// sum_r A_r sin(2 pi r k / N) = S_k) and V_{+-r} = r A_r pi / N (imaginary part:
+// (2 pi / N) sum_r r A_r cos(2 pi r k / N) = h S'(x_k)); fp32 radix-2 Stockham in LDS
+// (N / 2 log2 N butterflies instead of the 2 N Rn fp64 Clenshaw steps, rounding
+// ~log2 N eps of sum |A_r|), twiddles from sincospif. Then each interval's cubic
+// Hermite coefficients. LDS (bytes from 0): the float4 table [16 N), aliased by the
+// FFT's two float2 buffers during the transform, and the twiddles [16 N, 20 N).
+constexpr int SG_TAB_THREADS = 512;
+#ifndef SG_TAB_DIAG
+#define SG_TAB_DIAG 0
+#endif
+__device__ __forceinline__ void tab_build(float4* __restrict__ lt, const float* __restrict__ la, int Rn, int logn) {
+  const int N = 1 << logn;
+  float2* X = reinterpret_cast<float2*>(lt);
+  float2* Y = X + N;
+  float2* tw = X + 2 * N;
+  const float pin = 3.14159265358979f / (float)N;
+  for (int t = threadIdx.x; t < N / 2; t += SG_TAB_THREADS) {
+    float sv, cv;
+    sincospif(2.f * (float)t / (float)N, &sv, &cv);
+    tw[t] = make_float2(cv, sv);
+  }
+  for (int m = threadIdx.x; m < N; m += SG_TAB_THREADS) {
+    float z = 0.f;
+    if (m >= 1 && m <= Rn) z = la[m - 1] * ((float)m * pin - 0.5f);
+    else if (m >= N - Rn) z = la[N - m - 1] * ((float)(N - m) * pin + 0.5f);
+    X[m] = make_float2(0.f, z);
+  }
+  __syncthreads();
+  for (int st = 0, Ns = 1; st < logn; ++st, Ns <<= 1) {
+    for (int j = threadIdx.x; j < N / 2; j += SG_TAB_THREADS) {
+      const int k = j & (Ns - 1);
+      const float2 w = tw[k << (logn - 1 - st)];
+      const float2 a = X[j], b0 = X[j + N / 2];
+      const float2 b = make_float2(b0.x * w.x - b0.y * w.y, b0.x * w.y + b0.y * w.x);
+      const int o = (j - k) * 2 + k;
+      Y[o] = make_float2(a.x + b.x, a.y + b.y);
+      Y[o + Ns] = make_float2(a.x - b.x, a.y - b.y);
+    }
+    __syncthreads();
+    float2* t = X;
+    X = Y;
+    Y = t;
+  }
+  // X: (S_k, h S'_k). Intervals k = tid + 512 q into registers, then the table over the buffers
+  constexpr int QM = (1 << SG_TAB_LOGN_MAX) / SG_TAB_THREADS;
+  float4 c[QM];
+#pragma unroll
+  for (int q = 0; q < QM; ++q) {
+    const int k = threadIdx.x + q * SG_TAB_THREADS;
+    if (k < N) {
+      const float2 p0 = X[k], p1 = X[(k + 1) & (N - 1)];
+      c[q] = make_float4(p0.x, p0.y, 3.f * (p1.x - p0.x) - 2.f * p0.y - p1.y, 2.f * (p0.x - p1.x) + p0.y + p1.y);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < QM; ++q) {
+    const int k = threadIdx.x + q * SG_TAB_THREADS;
+    if (k < N) lt[k] = c[q];
+  }
+}
+
+// Blocks of 64 samples of a task from the table at lane phases x, x + dx, ...
+// (fixed point), their table reads issued together. FULL: all exist and land 1:1
+// in [dj0, dj1) (no per-lane tests).
+template <int NB, bool FULL>
+__device__ __forceinline__ void tab_blocks(const float4* __restrict__ lt, int logn, const SgWTask& T,
+                                           float* __restrict__ w, uint32_t x, uint32_t dx, int l, float& tmax) {
+  float4 c[NB];
+  uint32_t xs[NB];
+#pragma unroll
+  for (int s = 0; s < NB; ++s) {
+    xs[s] = x + (uint32_t)s * dx;
+#if SG_TAB_DIAG == 3  // diagnostic timing build only: no table reads
+    c[s] = make_float4((float)xs[s], 0.5f, 0.25f, 0.125f);
+#else
+    c[s] = lt[xs[s] >> (32 - logn)];
+#endif
+  }
+#pragma unroll
+  for (int s = 0; s < NB; ++s) {
+    const float f = (float)(xs[s] << logn) * 2.3283064365386963e-10f;  // [0, 1]
+    const float y = fmaf(f, fmaf(f, fmaf(f, c[s].w, c[s].z), c[s].y), c[s].x);
+#if SG_TAB_DIAG == 4  // diagnostic timing build only: no stores
+    tmax = fmaxf(tmax, y);
+    continue;
+#endif
+    if (FULL) {
+      w[64 * s] = y;
+      tmax = fmaxf(tmax, y);
+    } else if (l + 64 * s < T.len) {
+      w[64 * s] = y;
+      const int j = T.j0 + l + 64 * s;
+      tmax = (j >= T.dj0 && j < T.dj1) ? fmaxf(tmax, y) : tmax;
+    }
+  }
+}
+
+// One workgroup per SgTabJob (dynamic LDS: the launch's 2^logn float4 entries).
+// The job's task descriptors are staged in LDS with the amplitude column, before
+// any store: loads and stores share vmcnt, so a descriptor load after a task's
+// stores would wait for all of them to complete.
+extern "C" __global__ __launch_bounds__(SG_TAB_THREADS) void sg_sine_bank_tab(
+    const SgTabJob* __restrict__ jobs, const SgWTask* __restrict__ tasks, const float* __restrict__ amps,
+    float* __restrict__ W, float* __restrict__ taskmax) {
+  extern __shared__ float4 lt[];
+  __shared__ float la[SG_ROWS_F32 + 4];
+  __shared__ SgWTask ts[SG_TAB_TASKS];
+  const SgTabJob J = jobs[blockIdx.x];
+  const int logn = J.logn;
+  for (int r = threadIdx.x; r < J.Rn; r += SG_TAB_THREADS) la[r] = amps[J.a_off + r];
+  {
+    constexpr int W4 = sizeof(SgWTask) / sizeof(float4);
+    const float4* src = reinterpret_cast<const float4*>(tasks + J.t0);
+    float4* dst = reinterpret_cast<float4*>(ts);
+    for (int k = threadIdx.x; k < J.n * W4; k += SG_TAB_THREADS) dst[k] = src[k];
+  }
+  __syncthreads();
+#if SG_TAB_DIAG != 2  // diagnostic timing build: 2 = no table build
+  tab_build(lt, la, J.Rn, logn);
+  __syncthreads();
+#endif
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  constexpr double TWO32 = 4294967296.0;
+#if SG_TAB_DIAG == 1  // diagnostic timing build: no sampling
+  if (J.n >= 0) return;
+#endif
+  for (int q = wave; q < J.n; q += SG_TAB_THREADS / 64) {
+    const int64_t ti = (int64_t)J.t0 + q;
+    const SgWTask T = ts[q];
+    // the lane's phase at its first sample and the advance over 64 samples, in
+    // 2^-32 cycles (the fp64 phase of sample_setup, reduced mod 1)
+    const double P = fma((double)(T.mbase + lane), T.c1, T.c0);
+    uint32_t x = (uint32_t)(uint64_t)((P - floor(P)) * TWO32);
+    const double d64 = 64.0 * T.c1;
+    const uint32_t dx = (uint32_t)(uint64_t)((d64 - floor(d64)) * TWO32 + 0.5);
+    float* __restrict__ wp = W + T.w_off + T.j0 + lane;
+    float tmax = 0.f;
+    int l0 = 0;
+#pragma unroll 1
+    for (; l0 + 256 <= T.len; l0 += 256, x += 4u * dx) {
+      const int jp = T.j0 + l0;
+      if (jp >= T.dj0 && jp + 256 <= T.dj1)
+        tab_blocks<4, true>(lt, logn, T, wp + l0, x, dx, 0, tmax);
+      else
+        tab_blocks<4, false>(lt, logn, T, wp + l0, x, dx, l0 + lane, tmax);
+    }
+#pragma unroll 1
+    for (; l0 < T.len; l0 += 64, x += dx) tab_blocks<1, false>(lt, logn, T, wp + l0, x, dx, l0 + lane, tmax);
+    const float wm = wave_max(tmax);
+    if (lane == 0) taskmax[ti] = wm;
+  }
 }
 
 // per-syllable max over its task slots and crossfade-piece slots
@@ -1237,11 +1381,7 @@ void launch_amp_build(const DevicePlan& D, int64_t n_jobs, hipStream_t s) {
 }
 void launch_sine_bank(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s) {
   if (n <= 0) return;
-#if SG_SB_PERSIST
-  const int64_t nb = std::min<int64_t>((n + 3) / 4, SG_SB_PERSIST * 256);  // SG_SB_PERSIST workgroups per CU
-#else
   const int64_t nb = (n + 3) / 4;
-#endif
   hipLaunchKernelGGL(sg_sine_bank, dim3((unsigned)nb), dim3(256), 0, s, D.tlong + k0, n, D.tasks, D.amps,
                      D.syls, D.cknots, D.W, D.taskmax);
   SG_LAUNCHED("sg_sine_bank");
@@ -1263,6 +1403,13 @@ void launch_sine_bank_tall_pairs(const DevicePlan& D, int64_t k0, int64_t n, hip
   hipLaunchKernelGGL(sg_sine_bank_tall_pairs, dim3((unsigned)((n + 7) / 8)), dim3(256), 0, s, D.tallp + k0, n,
                      D.tasks, D.amps, D.W, D.taskmax);
   SG_LAUNCHED("sg_sine_bank_tall_pairs");
+}
+void launch_sine_bank_tab(const DevicePlan& D, int logn, int64_t j0, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  // the table (16 N bytes, the FFT buffers during the build) and the twiddles (4 N)
+  hipLaunchKernelGGL(sg_sine_bank_tab, dim3((unsigned)n), dim3(SG_TAB_THREADS), (size_t)20 << logn, s,
+                     D.tabjobs + j0, D.tasks, D.amps, D.W, D.taskmax);
+  SG_LAUNCHED("sg_sine_bank_tab");
 }
 void launch_piece_max(const DevicePlan& D, int64_t p0, int64_t n_ptiles, hipStream_t s) {
   if (n_ptiles <= 0) return;

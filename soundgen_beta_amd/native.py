@@ -80,6 +80,8 @@ def lib():
     L.sg_set_fp64_policy.argtypes = [C.c_int32, C.c_double]
     L.sg_set_amp_policy.argtypes = [C.c_int32]
     L.sg_set_uniform_gather.argtypes = [C.c_int32]
+    L.sg_set_sine_table.argtypes = [C.c_int32]
+    L.sg_plan_table_stats.argtypes = [C.c_void_p, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)]
     L.sg_host_cache_trim.argtypes = []
     L.sg_host_cache_trim.restype = i64
     L.sg_get_smooth_contour.argtypes = [_abi.sg_anchors, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_double,

@@ -30,6 +30,41 @@ def test_c2_tones_batch(oracle):
         assert _rms(y, ref) <= TOL
 
 
+def test_sine_table_path_vs_recurrence(oracle):
+    """Static tones (the wavetable path, sg_sine_bank_tab) against the same
+    plan on the row recurrence (sg_set_sine_table(0)) and the oracle, over f0
+    from 55 Hz (many rows) to 1.5 kHz, flat and steep rolloffs, 16 and 44.1 kHz."""
+    from soundgen_beta_amd import batch, native
+    L = native.lib()
+    calls = []
+    for f in (55.0, 80.0, 123.4, 250.0, 399.0, 1500.0):
+        for roll in (-12, -3):
+            prm = dict(C2, rolloff=roll, rolloffOct=0 if roll == -3 else C2["rolloffOct"])
+            calls.append({"kind": "harmonics", "pitch": np.full(3500, f), "params": prm})
+    calls.append({"kind": "harmonics", "pitch": np.full(1500, 190.0), "params": dict(C2, samplingRate=16000)})
+    outs = {}
+    try:
+        for on in (1, 0):
+            assert L.sg_set_sine_table(on) == 0
+            plan = batch.Plan(calls, native.default_context(0))
+            plan.upload()
+            tabs, samples, _ = plan.table_stats()
+            assert (tabs >= 8 and samples > 0.5 * plan.total) if on else tabs == 0  # 55 / 80 Hz at -3 dB: tall rows
+            outs[on] = batch.synthesize(calls)
+    finally:
+        L.sg_set_sine_table(1)
+    rows = []
+    for c, y1, y0 in zip(calls, outs[1], outs[0]):
+        assert len(y1) == len(y0)
+        ref = oracle.generate_harmonics(c["pitch"], **c["params"])
+        e1, e0 = np.asarray(y1, np.float64) - ref, np.asarray(y0, np.float64) - ref
+        rows.append((np.sqrt(np.mean(e1 ** 2)), np.sqrt(np.mean(e0 ** 2)), np.abs(e1).max(), np.abs(e0).max()))
+    for r in rows:
+        print("table rms %.3g max %.3g | recurrence rms %.3g max %.3g" % (r[0], r[2], r[1], r[3]))
+    for r in rows:  # the table within the tolerance, and no worse than the fp32 recurrence by more than 1e-6
+        assert r[0] <= TOL and r[2] <= r[3] + 1e-6, r
+
+
 def test_planner_cases_one_batch(oracle):
     """Every planner case (vibrato, subharmonic epochs + crossfades, jitter,
     shimmer, temperature random walks, 16 kHz, near-ceiling f0) in ONE batch."""
