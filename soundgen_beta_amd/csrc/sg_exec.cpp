@@ -168,6 +168,7 @@ struct ColumnReader {
     for (size_t k = 0; k < lg.size(); ++k) lg[k] = std::log2((double)(k + 1));
   }
   // smallest log2 N with the bound <= SG_TAB_TOL sum |A_r|, 0 if none <= SG_TAB_LOGN_MAX
+  int logn_max = SG_TAB_LOGN_MAX;
   int logn(int64_t a_off, int32_t Rn) const {
     auto it = std::upper_bound(by_off.begin(), by_off.end(), std::make_pair(a_off, INT32_MAX));
     if (it == by_off.begin()) return 0;
@@ -186,7 +187,7 @@ struct ColumnReader {
     }
     if (!(s0 > 0)) return 0;
     const double two_pi4 = 1558.5454565440389;  // (2 pi)^4
-    for (int b = SG_TAB_LOGN_MIN; b <= SG_TAB_LOGN_MAX; ++b) {
+    for (int b = SG_TAB_LOGN_MIN; b <= logn_max; ++b) {
       const double n4 = std::ldexp(1.0, 4 * b);
       if (two_pi4 * s4 / (384.0 * n4) <= SG_TAB_TOL * s0) return b;
     }
@@ -200,7 +201,11 @@ static TabSpans group_tables(const Batch& B) {
   auto tab_task = [](const SgWTask& t) {
     return t.flags == (SG_TASK_CONST | SG_TASK_LIN) && t.R <= SG_ROWS_F32 && t.Rn > 0 && t.len > 64;
   };
-  const ColumnReader cols(B);
+  ColumnReader cols(B);
+  if (const char* e = std::getenv("SG_TAB_LOGN"))  // experiment knob: largest table
+    cols.logn_max = std::min(SG_TAB_LOGN_MAX, std::max(SG_TAB_LOGN_MIN, std::atoi(e)));
+  int per_job = SG_TAB_TASKS;
+  if (const char* e = std::getenv("SG_TAB_TASKS")) per_job = std::min(SG_TAB_TASKS, std::max(1, std::atoi(e)));  // experiment knob
   std::vector<SgTabJob> jobs;
   int64_t run0 = -1, run_samples = 0;
   SgWTask first{};
@@ -208,8 +213,8 @@ static TabSpans group_tables(const Batch& B) {
     if (run0 < 0) return;
     const int logn = run_samples >= (int64_t(4) << SG_TAB_LOGN_MIN) ? cols.logn(first.a_off, first.Rn) : 0;
     if (logn && run_samples >= (int64_t(4) << logn)) {
-      for (int64_t i = run0; i < end; i += SG_TAB_TASKS) {
-        const int32_t n = (int32_t)std::min<int64_t>(SG_TAB_TASKS, end - i);
+      for (int64_t i = run0; i < end; i += per_job) {
+        const int32_t n = (int32_t)std::min<int64_t>(per_job, end - i);
         jobs.push_back(SgTabJob{first.a_off, first.Rn, (int32_t)i, n, logn});
         for (int64_t q = i; q < i + n; ++q) S.in_tab[(size_t)q] = 1;
       }

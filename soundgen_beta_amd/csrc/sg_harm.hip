@@ -770,12 +770,15 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_hp(
 // real and imaginary parts of ONE inverse complex DFT, x_k = sum_m Z_m e^{2 pi i m k / N}
 // with Z = U + i V for the two Hermitian spectra U_{+-r} = -+i A_r / 2 (real part:
 // sum_r A_r sin(2 pi r k / N) = S_k) and V_{+-r} = r A_r pi / N (imaginary part:
-// (2 pi / N) sum_r r A_r cos(2 pi r k / N) = h S'(x_k)); fp32 radix-2 Stockham in LDS
-// (N / 2 log2 N butterflies instead of the 2 N Rn fp64 Clenshaw steps, rounding
+// (2 pi / N) sum_r r A_r cos(2 pi r k / N) = h S'(x_k)); fp32 radix-4 Stockham in LDS
+// (~N / 4 log4 N butterflies instead of the 2 N Rn fp64 Clenshaw steps, rounding
 // ~log2 N eps of sum |A_r|), twiddles from sincospif. Then each interval's cubic
 // Hermite coefficients. LDS (bytes from 0): the float4 table [16 N), aliased by the
-// FFT's two float2 buffers during the transform, and the twiddles [16 N, 20 N).
-constexpr int SG_TAB_THREADS = 512;
+// FFT's two float2 buffers during the transform, and the twiddles [16 N, 18 N).
+#ifndef SG_TAB_THREADS_N
+#define SG_TAB_THREADS_N 512  // build knob: threads per sg_sine_bank_tab workgroup
+#endif
+constexpr int SG_TAB_THREADS = SG_TAB_THREADS_N;
 #ifndef SG_TAB_DIAG
 #define SG_TAB_DIAG 0
 #endif
@@ -785,7 +788,11 @@ __device__ __forceinline__ void tab_build(float4* __restrict__ lt, const float* 
   float2* Y = X + N;
   float2* tw = X + 2 * N;
   const float pin = 3.14159265358979f / (float)N;
-  for (int t = threadIdx.x; t < N / 2; t += SG_TAB_THREADS) {
+#ifndef SG_TAB_SKIP
+#define SG_TAB_SKIP 0  // diagnostic timing builds only: bit 0 no twiddles, 1 no FFT stages, 2 no coefficients
+#endif
+  if (!(SG_TAB_SKIP & 1))
+  for (int t = threadIdx.x; t < N / 4; t += SG_TAB_THREADS) {  // the radix-4 stages' w^1
     float sv, cv;
     sincospif(2.f * (float)t / (float)N, &sv, &cv);
     tw[t] = make_float2(cv, sv);
@@ -797,15 +804,37 @@ __device__ __forceinline__ void tab_build(float4* __restrict__ lt, const float* 
     X[m] = make_float2(0.f, z);
   }
   __syncthreads();
-  for (int st = 0, Ns = 1; st < logn; ++st, Ns <<= 1) {
+  // Stockham autosort: a radix-2 stage first when log2 N is odd, then radix-4
+  // stages; stage with sub-transform size Ns: v_r = X[j + r N / R] w^r,
+  // w = e^{2 pi i k / (R Ns)}, k = j mod Ns, into Y[(j - k) R + k + r Ns]
+  int Ns = 1;
+  if ((logn & 1) && !(SG_TAB_SKIP & 2)) {
     for (int j = threadIdx.x; j < N / 2; j += SG_TAB_THREADS) {
+      const float2 a = X[j], b = X[j + N / 2];
+      Y[2 * j] = make_float2(a.x + b.x, a.y + b.y);
+      Y[2 * j + 1] = make_float2(a.x - b.x, a.y - b.y);
+    }
+    __syncthreads();
+    float2* t = X;
+    X = Y;
+    Y = t;
+    Ns = 2;
+  }
+  auto cmul = [](float2 a, float2 b) { return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); };
+  for (; Ns < ((SG_TAB_SKIP & 2) ? 0 : N); Ns <<= 2) {
+    const int sh = logn - 2 - __builtin_ctz(Ns);  // w = tw[k N / (4 Ns)]
+    for (int j = threadIdx.x; j < N / 4; j += SG_TAB_THREADS) {
       const int k = j & (Ns - 1);
-      const float2 w = tw[k << (logn - 1 - st)];
-      const float2 a = X[j], b0 = X[j + N / 2];
-      const float2 b = make_float2(b0.x * w.x - b0.y * w.y, b0.x * w.y + b0.y * w.x);
-      const int o = (j - k) * 2 + k;
-      Y[o] = make_float2(a.x + b.x, a.y + b.y);
-      Y[o + Ns] = make_float2(a.x - b.x, a.y - b.y);
+      const float2 w1 = tw[k << sh], w2 = cmul(w1, w1), w3 = cmul(w2, w1);
+      const float2 v0 = X[j], v1 = cmul(X[j + N / 4], w1), v2 = cmul(X[j + N / 2], w2),
+                   v3 = cmul(X[j + 3 * N / 4], w3);
+      const float2 s02 = make_float2(v0.x + v2.x, v0.y + v2.y), d02 = make_float2(v0.x - v2.x, v0.y - v2.y);
+      const float2 s13 = make_float2(v1.x + v3.x, v1.y + v3.y), d13 = make_float2(v1.x - v3.x, v1.y - v3.y);
+      const int o = (j - k) * 4 + k;
+      Y[o] = make_float2(s02.x + s13.x, s02.y + s13.y);
+      Y[o + Ns] = make_float2(d02.x - d13.y, d02.y + d13.x);  // v0 + i v1 - v2 - i v3
+      Y[o + 2 * Ns] = make_float2(s02.x - s13.x, s02.y - s13.y);
+      Y[o + 3 * Ns] = make_float2(d02.x + d13.y, d02.y - d13.x);  // v0 - i v1 - v2 + i v3
     }
     __syncthreads();
     float2* t = X;
@@ -814,6 +843,7 @@ __device__ __forceinline__ void tab_build(float4* __restrict__ lt, const float* 
   }
   // X: (S_k, h S'_k). Intervals k = tid + 512 q into registers, then the table over the buffers
   constexpr int QM = (1 << SG_TAB_LOGN_MAX) / SG_TAB_THREADS;
+  if (SG_TAB_SKIP & 4) return;
   float4 c[QM];
 #pragma unroll
   for (int q = 0; q < QM; ++q) {
@@ -834,8 +864,9 @@ __device__ __forceinline__ void tab_build(float4* __restrict__ lt, const float* 
 // Blocks of 64 samples of a task from the table at lane phases x, x + dx, ...
 // (fixed point), their table reads issued together. FULL: all exist and land 1:1
 // in [dj0, dj1) (no per-lane tests).
-template <int NB, bool FULL>
-__device__ __forceinline__ void tab_blocks(const float4* __restrict__ lt, int logn, const SgWTask& T,
+struct TabTask;
+template <int NB, bool FULL, typename TT>
+__device__ __forceinline__ void tab_blocks(const float4* __restrict__ lt, int logn, const TT& T,
                                            float* __restrict__ w, uint32_t x, uint32_t dx, int l, float& tmax) {
   float4 c[NB];
   uint32_t xs[NB];
@@ -867,24 +898,28 @@ __device__ __forceinline__ void tab_blocks(const float4* __restrict__ lt, int lo
   }
 }
 
-// One workgroup per SgTabJob (dynamic LDS: the launch's 2^logn float4 entries).
-// The job's task descriptors are staged in LDS with the amplitude column, before
-// any store: loads and stores share vmcnt, so a descriptor load after a task's
-// stores would wait for all of them to complete.
+// The fields of a task the table path reads (48 B in LDS instead of 128)
+struct TabTask {
+  double c0, c1;
+  int64_t w_off;
+  int32_t mbase, j0, len, dj0, dj1, pad;
+};
+// One workgroup per SgTabJob (dynamic LDS: the table and twiddles, 18 N bytes).
+// The job's task fields are staged in LDS with the amplitude column, before any
+// store: loads and stores share vmcnt, so a descriptor load after a task's stores
+// would wait for all of them to complete. At N = 2048, 4 workgroups fit per CU.
 extern "C" __global__ __launch_bounds__(SG_TAB_THREADS) void sg_sine_bank_tab(
     const SgTabJob* __restrict__ jobs, const SgWTask* __restrict__ tasks, const float* __restrict__ amps,
     float* __restrict__ W, float* __restrict__ taskmax) {
   extern __shared__ float4 lt[];
   __shared__ float la[SG_ROWS_F32 + 4];
-  __shared__ SgWTask ts[SG_TAB_TASKS];
+  __shared__ TabTask ts[SG_TAB_TASKS];
   const SgTabJob J = jobs[blockIdx.x];
   const int logn = J.logn;
   for (int r = threadIdx.x; r < J.Rn; r += SG_TAB_THREADS) la[r] = amps[J.a_off + r];
-  {
-    constexpr int W4 = sizeof(SgWTask) / sizeof(float4);
-    const float4* src = reinterpret_cast<const float4*>(tasks + J.t0);
-    float4* dst = reinterpret_cast<float4*>(ts);
-    for (int k = threadIdx.x; k < J.n * W4; k += SG_TAB_THREADS) dst[k] = src[k];
+  for (int q = threadIdx.x; q < J.n; q += SG_TAB_THREADS) {
+    const SgWTask& T = tasks[J.t0 + q];
+    ts[q] = TabTask{T.c0, T.c1, T.w_off, T.mbase, T.j0, T.len, T.dj0, T.dj1, 0};
   }
   __syncthreads();
 #if SG_TAB_DIAG != 2  // diagnostic timing build: 2 = no table build
@@ -899,7 +934,7 @@ extern "C" __global__ __launch_bounds__(SG_TAB_THREADS) void sg_sine_bank_tab(
 #endif
   for (int q = wave; q < J.n; q += SG_TAB_THREADS / 64) {
     const int64_t ti = (int64_t)J.t0 + q;
-    const SgWTask T = ts[q];
+    const TabTask T = ts[q];
     // the lane's phase at its first sample and the advance over 64 samples, in
     // 2^-32 cycles (the fp64 phase of sample_setup, reduced mod 1)
     const double P = fma((double)(T.mbase + lane), T.c1, T.c0);
@@ -1406,8 +1441,8 @@ void launch_sine_bank_tall_pairs(const DevicePlan& D, int64_t k0, int64_t n, hip
 }
 void launch_sine_bank_tab(const DevicePlan& D, int logn, int64_t j0, int64_t n, hipStream_t s) {
   if (n <= 0) return;
-  // the table (16 N bytes, the FFT buffers during the build) and the twiddles (4 N)
-  hipLaunchKernelGGL(sg_sine_bank_tab, dim3((unsigned)n), dim3(SG_TAB_THREADS), (size_t)20 << logn, s,
+  // the table (16 N bytes, the FFT buffers during the build) and the twiddles (2 N)
+  hipLaunchKernelGGL(sg_sine_bank_tab, dim3((unsigned)n), dim3(SG_TAB_THREADS), (size_t)18 << logn, s,
                      D.tabjobs + j0, D.tasks, D.amps, D.W, D.taskmax);
   SG_LAUNCHED("sg_sine_bank_tab");
 }

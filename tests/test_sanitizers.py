@@ -20,5 +20,9 @@ def test_planner_and_oracle_under_asan_ubsan():
                         "tests/test_loess_cursor.py", "tests/test_api_helpers.py", "tests/test_rrng.py",
                         "tests/test_dist.py", "-m", "not gpu"],
                        cwd=ROOT, capture_output=True, text=True, timeout=1400)
+    if r.returncode != 0:  # keep the whole report (pytest shows only the tail)
+        os.makedirs(os.path.join(ROOT, "tests", "sanitize", "_build"), exist_ok=True)
+        with open(os.path.join(ROOT, "tests", "sanitize", "_build", "last_failure.log"), "w") as f:
+            f.write(r.stdout + "\n----- stderr -----\n" + r.stderr)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
     assert " passed" in r.stdout and "skipped" not in r.stdout.split("\n")[-2], r.stdout[-2000:]
