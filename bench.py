@@ -296,7 +296,7 @@ def pmc_from_profiles(config, kernel):
 
 # waves per SIMD the kernels run at (hipcc -Rpass-analysis=kernel-resource-usage, gfx950)
 WAVES_PER_SIMD = {"sg_stft_ola": 2, "sg_stft_ola_noise": 3, "sg_sine_bank": 7, "sg_sine_bank_pairs": 8,
-                  "sg_sine_bank_tall": 5, "sg_sine_bank_tall_pairs": 8, "sg_sine_bank_tab": 8, "sg_sine_bank_tab4k": 4}
+                  "sg_sine_bank_tall": 5, "sg_sine_bank_tall_pairs": 8, "sg_sine_bank_tab": 8}
 
 
 def roofline(st, prof, steps, config, kern):
@@ -313,12 +313,17 @@ def roofline(st, prof, steps, config, kern):
     if kern == "sg_sine_bank":
         # fp32 epoch waveform write + the amplitude blocks it reads (A and dA columns)
         alg = (4 * st["harm_samples"] + st["harm_amp_bytes"]) / lps
-        valu_ops = 2.0 * st["harm_terms"] / lps  # Clenshaw: 2 lane-ops per (sample, row, chain)
+        # Clenshaw: 2 lane-ops per (sample, row, chain) of the tasks on the row recurrence;
+        # the wavetable spans' samples (one table read + 3 FMAs each) are not priced here
+        valu_ops = 2.0 * (st["harm_terms"] - st.get("tab_terms", 0)) / lps
         vfrac = valu_ops / sec / VALU_PEAK_OPS if sec else 0
         extra = {"valu": {"ops_per_launch": valu_ops, "achieved_ops_s": valu_ops / sec if sec else 0,
-                          "peak_ops_s": VALU_PEAK_OPS, "frac": vfrac}}
+                          "peak_ops_s": VALU_PEAK_OPS, "frac": vfrac,
+                          "wavetable": {"spans": st.get("tab_spans", 0) / lps,
+                                        "samples": st.get("tab_samples", 0) / lps,
+                                        "terms_replaced": st.get("tab_terms", 0) / lps}}}
         kernels = ("sg_sine_bank", "sg_sine_bank_pairs", "sg_sine_bank_tall", "sg_sine_bank_tall_pairs",
-                   "sg_sine_bank_tab", "sg_sine_bank_tab4k")
+                   "sg_sine_bank_tab")
         name = " + ".join(kernels)
     else:
         # source / uniforms + envelope columns read, trimmed output written
@@ -547,6 +552,10 @@ def main():
         for p, _, _ in plans:
             for k, v in p.stats().items():
                 st[k] = st.get(k, 0) + v
+            tabs, tab_samples, tab_terms = p.table_stats()  # wavetable spans (no row recurrence)
+            st["tab_spans"] = st.get("tab_spans", 0) + tabs
+            st["tab_samples"] = st.get("tab_samples", 0) + tab_samples
+            st["tab_terms"] = st.get("tab_terms", 0) + tab_terms
         tot = {k: v[0] * v[1] for k, v in prof.items()}
         dom = max(tot, key=tot.get) if any(tot.values()) else "sg_sine_bank"
         roof = roofline(st, prof, args.steps, args.config, dom)

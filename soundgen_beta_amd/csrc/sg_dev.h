@@ -99,7 +99,9 @@ static_assert(sizeof(SgWTask) == 128, "SgWTask layout");
 struct SgTabJob {    // one workgroup: tasks [t0, t0 + n) (consecutive) on one amplitude column
   int64_t a_off;     // the column A[0..Rn)
   int32_t Rn, t0, n, logn;
+  int32_t syl, flags;
 };
+constexpr int SG_TAB_DIRECT = 1;  // the job is a whole syllable of direct pieces: final samples to the output
 constexpr int SG_TAB_LOGN_MIN = 8;
 constexpr int SG_TAB_LOGN_MAX = 11;   // LDS 20 N bytes: 40 KB
 constexpr double SG_TAB_TOL = 1e-7;

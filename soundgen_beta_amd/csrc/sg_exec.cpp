@@ -146,6 +146,12 @@ static void split_finalize_tiles(Batch& B) {
   }
 }
 
+// direct-output table jobs: on by default; SG_TAB_DIRECT=0 keeps every span on W (experiment knob)
+static bool direct_on() {  // read at each upload
+  const char* e = std::getenv("SG_TAB_DIRECT");
+  return !(e && e[0] == '0');
+}
+
 // Wavetable spans (SgTabJob, sg_dev.h): runs of consecutive constant-amplitude,
 // linear-phase fp32 tasks of one syllable on one amplitude column whose
 // interpolation-error bound admits a table of N <= 2^SG_TAB_LOGN_MAX points and
@@ -153,7 +159,8 @@ static void split_finalize_tiles(Batch& B) {
 struct TabSpans {
   std::vector<SgTabJob> jobs;
   std::vector<uint8_t> in_tab;
-  int64_t tasks = 0;
+  std::vector<uint8_t> direct_syl;  // per syllable: its samples go straight to the output (SG_TAB_DIRECT)
+  int64_t tasks = 0, direct = 0;
   int64_t samples = 0, terms = 0;
 };
 // the column's amplitudes as sg_amp_build computes them (host restatement)
@@ -199,7 +206,19 @@ static TabSpans group_tables(const Batch& B) {
   const int64_t ntask = bulk_size(B.tasks_x, B.tasks);
   S.in_tab.assign((size_t)ntask, 0);
   auto tab_task = [](const SgWTask& t) {
-    return t.flags == (SG_TASK_CONST | SG_TASK_LIN) && t.R <= SG_ROWS_F32 && t.Rn > 0 && t.len > 64;
+    return t.flags == (SG_TASK_CONST | SG_TASK_LIN) && t.R <= SG_ROWS_F32 && t.Rn > 0;
+  };
+  S.direct_syl.assign(B.syls.size(), 0);
+  // a whole syllable of direct (or zero) pieces without envelope or drift: the job
+  // writes its final samples (sg_sine_bank_tab's direct mode)
+  auto direct_ok = [&](const SgWTask& t, int64_t r0, int64_t r1) {
+    if (t.syl < 0 || t.syl >= (int32_t)B.syls.size() || !direct_on()) return false;
+    const SgSyllable& sy = B.syls[(size_t)t.syl];
+    if (sy.hp || sy.env.kind != 0 || sy.drift.nk != 0 || sy.nptile != 0) return false;
+    if (r0 != sy.task0 || r1 != sy.task0 + sy.ntask || r1 - r0 > SG_TAB_TASKS) return false;
+    for (int32_t p = sy.piece0; p < sy.piece0 + sy.npiece; ++p)
+      if (B.pieces[(size_t)p].nterms > 0) return false;
+    return true;
   };
   ColumnReader cols(B);
   if (const char* e = std::getenv("SG_TAB_LOGN"))  // experiment knob: largest table
@@ -213,9 +232,14 @@ static TabSpans group_tables(const Batch& B) {
     if (run0 < 0) return;
     const int logn = run_samples >= (int64_t(4) << SG_TAB_LOGN_MIN) ? cols.logn(first.a_off, first.Rn) : 0;
     if (logn && run_samples >= (int64_t(4) << logn)) {
+      const bool dir = end - run0 <= per_job && direct_ok(first, run0, end);
+      if (dir) {
+        S.direct_syl[(size_t)first.syl] = 1;
+        ++S.direct;
+      }
       for (int64_t i = run0; i < end; i += per_job) {
         const int32_t n = (int32_t)std::min<int64_t>(per_job, end - i);
-        jobs.push_back(SgTabJob{first.a_off, first.Rn, (int32_t)i, n, logn});
+        jobs.push_back(SgTabJob{first.a_off, first.Rn, (int32_t)i, n, logn, first.syl, dir ? SG_TAB_DIRECT : 0});
         for (int64_t q = i; q < i + n; ++q) S.in_tab[(size_t)q] = 1;
       }
       S.samples += run_samples;
@@ -266,8 +290,8 @@ void finalize_plan(Batch& B) {
       });
       int64_t hist[13] = {0};
       for (const SgTabJob& j : T.jobs) ++hist[j.logn];
-      std::fprintf(stderr, "sg plan: wavetable jobs %zu (N = 256/512/1024/2048: %lld %lld %lld %lld; %zu tasks, %lld samples, %.3g terms); CONST|LIN tasks %lld (%lld samples)\n",
-                   T.jobs.size(), (long long)hist[8], (long long)hist[9], (long long)hist[10], (long long)hist[11],
+      std::fprintf(stderr, "sg plan: wavetable jobs %zu, %lld direct syllables (N = 256/512/1024/2048: %lld %lld %lld %lld; %zu tasks, %lld samples, %.3g terms); CONST|LIN tasks %lld (%lld samples)\n",
+                   T.jobs.size(), (long long)T.direct, (long long)hist[8], (long long)hist[9], (long long)hist[10], (long long)hist[11],
                    (size_t)T.tasks, (long long)T.samples, (double)T.terms, (long long)cl,
                    (long long)cl_samples);
     }
@@ -513,7 +537,15 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   cp(D.pieces, B.pieces.data(), B.pieces.size() * sizeof(SgPiece));
   cp(D.syls, B.syls.data(), B.syls.size() * sizeof(SgSyllable));
   cp(D.syl_tiles, B.fin_tiles.data(), B.fin_tiles.size() * sizeof(SgSylTile));
-  cp(D.copy_tiles, B.copy_tiles.data(), B.copy_tiles.size() * sizeof(SgCopyTile));
+  if (T.direct) {  // direct syllables: their W-reading copy tiles become empty (zero pieces stay)
+    std::vector<SgCopyTile> ct(B.copy_tiles);
+    for (SgCopyTile& c : ct)
+      if (T.direct_syl[(size_t)c.syl] && !(c.flags & SG_COPY_ZERO)) c.n = 0;
+    cp(D.copy_tiles, ct.data(), ct.size() * sizeof(SgCopyTile));
+    HIPCHK(hipStreamSynchronize(s));  // ct is a temporary
+  } else {
+    cp(D.copy_tiles, B.copy_tiles.data(), B.copy_tiles.size() * sizeof(SgCopyTile));
+  }
   cp(D.ptiles, B.ptiles.data(), B.ptiles.size() * sizeof(SgSylTile));
   cp(D.cknots, B.cknots.data(), B.cknots.size() * sizeof(double));
   cp(D.geoms, B.geoms.data(), B.geoms.size() * sizeof(SgFftGeom));
@@ -594,7 +626,7 @@ static void device_execute_harm(const Batch& B, DevicePlan& D, float* d_out, hip
         const auto hi = std::partition_point(lo, J.end(), [&](const SgTabJob& j) { return j.t0 < sl.t1; });
         int logn = 0;
         for (auto it = lo; it != hi; ++it) logn = std::max<int>(logn, it->logn);
-        launch_sine_bank_tab(D, logn, lo - J.begin(), hi - lo, h);
+        launch_sine_bank_tab(D, logn, lo - J.begin(), hi - lo, d_out, h);
       }
     }
     if (prof) {

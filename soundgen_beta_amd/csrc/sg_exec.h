@@ -127,7 +127,7 @@ void launch_harm_finalize(const DevicePlan& D, int64_t f0, int64_t n_stiles, flo
 void launch_harm_copy(const DevicePlan& D, int64_t c0, int64_t n_ctiles, float* out, hipStream_t s);
 // the fp64 path of ill-conditioned formant-filter calls (SG_TASK_HP, SgSyllable::hp, sg_mix to fh, SgFrame64)
 void launch_sine_bank_hp(const DevicePlan& D, int64_t n, hipStream_t s);
-void launch_sine_bank_tab(const DevicePlan& D, int logn, int64_t j0, int64_t n, hipStream_t s);
+void launch_sine_bank_tab(const DevicePlan& D, int logn, int64_t j0, int64_t n, float* out, hipStream_t s);
 void launch_piece_max_hp(const DevicePlan& D, int64_t p0, int64_t n_ptiles, hipStream_t s);
 void launch_harm_finalize_hp(const DevicePlan& D, int64_t n_stiles, hipStream_t s);
 void launch_mix_hp(const DevicePlan& D, int64_t t0, int64_t n_tiles, hipStream_t s);

@@ -765,6 +765,17 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_hp(
   if (lane == 0) taskmax[ti] = wm;
 }
 
+// fade(k) of R's fade() on a syllable of L samples, lf-sample ramps (R/source.R:436-467)
+template <typename V = float>
+__device__ __forceinline__ V fade_at(int lf, int64_t L, int64_t k) {
+  V f = 1;
+  const V by = (V)1 / (V)(lf - 1);
+  if (k < lf) f *= (k == lf - 1) ? (V)1 : (V)k * by;
+  const int64_t kb = L - 1 - k;
+  if (kb < lf) f *= (kb == lf - 1) ? (V)1 : (V)kb * by;
+  return f;
+}
+
 // ------------------------------------------- wavetable path (SgTabJob, sg_dev.h)
 // One workgroup per job. Table: S and h dS/dx (h = 1 / N) at the N points as the
 // real and imaginary parts of ONE inverse complex DFT, x_k = sum_m Z_m e^{2 pi i m k / N}
@@ -901,25 +912,97 @@ __device__ __forceinline__ void tab_blocks(const float4* __restrict__ lt, int lo
 // The fields of a task the table path reads (48 B in LDS instead of 128)
 struct TabTask {
   double c0, c1;
-  int64_t w_off;
-  int32_t mbase, j0, len, dj0, dj1, pad;
+  int64_t off;    // W offset of epoch sample 0; direct jobs: output offset of epoch sample 0
+  int32_t mbase, j0, len, dj0, dj1, dk0;
 };
+// A direct job's samples of one task in its window [dj0, dj1): pass 1 (STORE false)
+// the max, pass 2 out[off + j] = y / max * fade(dk0 + j) (sg_harm_copy's arithmetic).
+// Blocks of 4 x 64 samples on the W path's grid; a block inside the window and
+// clear of the fades takes no per-lane tests.
+template <bool STORE, bool CHECK>
+__device__ __forceinline__ void tab_dblocks(const float4* __restrict__ lt, int logn, float* __restrict__ w,
+                                            uint32_t x, uint32_t dx, int l, int ls, int le, float inv, int lf,
+                                            int64_t L, int64_t k, float& tmax) {
+  float4 c[4];
+  uint32_t xs[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    xs[s] = x + (uint32_t)s * dx;
+    c[s] = lt[xs[s] >> (32 - logn)];
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const float f = (float)(xs[s] << logn) * 2.3283064365386963e-10f;
+    const float y = fmaf(f, fmaf(f, fmaf(f, c[s].w, c[s].z), c[s].y), c[s].x);
+    const bool ok = !CHECK || (l + 64 * s >= ls && l + 64 * s < le);
+    if (STORE) {
+      float v = y * inv;
+      if (CHECK && lf >= 2) v *= fade_at(lf, L, k + 64 * s);
+      if (ok) w[64 * s] = v;
+    } else {
+      tmax = ok ? fmaxf(tmax, y) : tmax;
+    }
+  }
+}
+template <bool STORE>
+__device__ __forceinline__ void tab_direct(const float4* __restrict__ lt, int logn, const TabTask& T,
+                                           float* __restrict__ base, int lane, float inv, int lf, int64_t L,
+                                           float& tmax) {
+  const int ls = max(0, T.dj0 - T.j0), le = min(T.len, T.dj1 - T.j0);  // task samples in the window
+  if (le <= ls) return;
+  // the lane phases of the W path (x at sample lane, + dx per 64 samples, mod 2^32):
+  // the same samples bit for bit
+  constexpr double TWO32 = 4294967296.0;
+  const double P = fma((double)(T.mbase + lane), T.c1, T.c0);
+  const double d64 = 64.0 * T.c1;
+  const uint32_t dx = (uint32_t)(uint64_t)((d64 - floor(d64)) * TWO32 + 0.5);
+  const int lb = ls & ~63;
+  uint32_t x = (uint32_t)(uint64_t)((P - floor(P)) * TWO32) + (uint32_t)(lb >> 6) * dx;
+  float* __restrict__ wp = base + T.off + T.j0 + lane;
+  const int64_t kt = (int64_t)T.dk0 + T.j0;  // syllable sample of task sample 0
+#pragma unroll 1
+  for (int l0 = lb; l0 < le; l0 += 256, x += 4u * dx) {
+    const bool ramp = lf >= 2 && (kt + l0 < lf || kt + l0 + 256 > L - lf);
+    if (l0 >= ls && l0 + 256 <= le && !ramp)
+      tab_dblocks<STORE, false>(lt, logn, wp + l0, x, dx, l0 + lane, ls, le, inv, lf, L, kt + l0 + lane, tmax);
+    else
+      tab_dblocks<STORE, true>(lt, logn, wp + l0, x, dx, l0 + lane, ls, le, inv, lf, L, kt + l0 + lane, tmax);
+  }
+}
+
 // One workgroup per SgTabJob (dynamic LDS: the table and twiddles, 18 N bytes).
 // The job's task fields are staged in LDS with the amplitude column, before any
 // store: loads and stores share vmcnt, so a descriptor load after a task's stores
 // would wait for all of them to complete. At N = 2048, 4 workgroups fit per CU.
-extern "C" __global__ __launch_bounds__(SG_TAB_THREADS) void sg_sine_bank_tab(
+// SG_TAB_DIRECT jobs hold a whole syllable without crossfades, envelope or drift:
+// the workgroup takes its max itself (pass 1, every task's in-window samples)
+// and writes the final samples to the output (pass 2) instead of W, where
+// sg_harm_copy would have read them back.
+extern "C" __global__ __launch_bounds__(SG_TAB_THREADS) __attribute__((amdgpu_waves_per_eu(8))) void sg_sine_bank_tab(
     const SgTabJob* __restrict__ jobs, const SgWTask* __restrict__ tasks, const float* __restrict__ amps,
-    float* __restrict__ W, float* __restrict__ taskmax) {
+    const SgSyllable* __restrict__ syls, float* __restrict__ W, float* __restrict__ out_buf,
+    float* __restrict__ fs, float* __restrict__ taskmax) {
   extern __shared__ float4 lt[];
   __shared__ float la[SG_ROWS_F32 + 4];
   __shared__ TabTask ts[SG_TAB_TASKS];
+  __shared__ float red[SG_TAB_THREADS / 64];
   const SgTabJob J = jobs[blockIdx.x];
   const int logn = J.logn;
+  const bool direct = J.flags & SG_TAB_DIRECT;
+  int64_t out0 = 0, L = 0;
+  int lf = 0;
+  float* obase = W;
+  if (direct) {
+    const SgSyllable& sy = syls[J.syl];
+    out0 = sy.out_off;
+    L = sy.L;
+    lf = sy.fade;
+    obase = sy.dst_fs ? fs : out_buf;
+  }
   for (int r = threadIdx.x; r < J.Rn; r += SG_TAB_THREADS) la[r] = amps[J.a_off + r];
   for (int q = threadIdx.x; q < J.n; q += SG_TAB_THREADS) {
     const SgWTask& T = tasks[J.t0 + q];
-    ts[q] = TabTask{T.c0, T.c1, T.w_off, T.mbase, T.j0, T.len, T.dj0, T.dj1, 0};
+    ts[q] = TabTask{T.c0, T.c1, direct ? out0 + T.dk0 : T.w_off, T.mbase, T.j0, T.len, T.dj0, T.dj1, (int32_t)T.dk0};
   }
   __syncthreads();
 #if SG_TAB_DIAG != 2  // diagnostic timing build: 2 = no table build
@@ -932,6 +1015,25 @@ extern "C" __global__ __launch_bounds__(SG_TAB_THREADS) void sg_sine_bank_tab(
 #if SG_TAB_DIAG == 1  // diagnostic timing build: no sampling
   if (J.n >= 0) return;
 #endif
+  if (direct) {
+    float wm = 0.f;
+    for (int q = wave; q < J.n; q += SG_TAB_THREADS / 64) {
+      float tmax = 0.f;
+      tab_direct<false>(lt, logn, ts[q], obase, lane, 0.f, lf, L, tmax);
+      const float m = wave_max(tmax);
+      if (lane == 0) taskmax[(int64_t)J.t0 + q] = m;  // sg_syl_max takes the same max
+      wm = fmaxf(wm, m);
+    }
+    if (lane == 0) red[wave] = wm;
+    __syncthreads();
+    float m = red[0];
+#pragma unroll
+    for (int w = 1; w < SG_TAB_THREADS / 64; ++w) m = fmaxf(m, red[w]);
+    const float inv = 1.f / m;
+    float unused = 0.f;
+    for (int q = wave; q < J.n; q += SG_TAB_THREADS / 64) tab_direct<true>(lt, logn, ts[q], obase, lane, inv, lf, L, unused);
+    return;
+  }
   for (int q = wave; q < J.n; q += SG_TAB_THREADS / 64) {
     const int64_t ti = (int64_t)J.t0 + q;
     const TabTask T = ts[q];
@@ -941,7 +1043,7 @@ extern "C" __global__ __launch_bounds__(SG_TAB_THREADS) void sg_sine_bank_tab(
     uint32_t x = (uint32_t)(uint64_t)((P - floor(P)) * TWO32);
     const double d64 = 64.0 * T.c1;
     const uint32_t dx = (uint32_t)(uint64_t)((d64 - floor(d64)) * TWO32 + 0.5);
-    float* __restrict__ wp = W + T.w_off + T.j0 + lane;
+    float* __restrict__ wp = W + T.off + T.j0 + lane;
     float tmax = 0.f;
     int l0 = 0;
 #pragma unroll 1
@@ -1026,15 +1128,6 @@ extern "C" __global__ __launch_bounds__(256) void sg_piece_max_hp(
 // A tile lying inside one direct piece with a 16-B aligned source and
 // destination moves float4s (4 consecutive samples per thread); otherwise
 // each thread takes samples k0 + 256 e + tid.
-template <typename V = float>
-__device__ __forceinline__ V fade_at(int lf, int64_t L, int64_t k) {
-  V f = 1;
-  const V by = (V)1 / (V)(lf - 1);
-  if (k < lf) f *= (k == lf - 1) ? (V)1 : (V)k * by;
-  const int64_t kb = L - 1 - k;
-  if (kb < lf) f *= (kb == lf - 1) ? (V)1 : (V)kb * by;
-  return f;
-}
 
 #ifndef SG_COPY_NT
 #define SG_COPY_NT 0  // build knob: non-temporal W loads (last use) and output stores
@@ -1439,11 +1532,11 @@ void launch_sine_bank_tall_pairs(const DevicePlan& D, int64_t k0, int64_t n, hip
                      D.tasks, D.amps, D.W, D.taskmax);
   SG_LAUNCHED("sg_sine_bank_tall_pairs");
 }
-void launch_sine_bank_tab(const DevicePlan& D, int logn, int64_t j0, int64_t n, hipStream_t s) {
+void launch_sine_bank_tab(const DevicePlan& D, int logn, int64_t j0, int64_t n, float* out, hipStream_t s) {
   if (n <= 0) return;
   // the table (16 N bytes, the FFT buffers during the build) and the twiddles (2 N)
   hipLaunchKernelGGL(sg_sine_bank_tab, dim3((unsigned)n), dim3(SG_TAB_THREADS), (size_t)18 << logn, s,
-                     D.tabjobs + j0, D.tasks, D.amps, D.W, D.taskmax);
+                     D.tabjobs + j0, D.tasks, D.amps, D.syls, D.W, out, D.fs, D.taskmax);
   SG_LAUNCHED("sg_sine_bank_tab");
 }
 void launch_piece_max(const DevicePlan& D, int64_t p0, int64_t n_ptiles, hipStream_t s) {

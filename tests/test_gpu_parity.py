@@ -65,6 +65,37 @@ def test_sine_table_path_vs_recurrence(oracle):
         assert r[0] <= TOL and r[2] <= r[3] + 1e-6, r
 
 
+def test_sine_table_direct_output_equals_w_path():
+    """Whole-syllable table spans write their final samples themselves
+    (SG_TAB_DIRECT, no W round trip, no sg_harm_copy pass): bit-identical to the
+    same spans through W + sg_syl_max + sg_harm_copy (SG_TAB_DIRECT=0), including
+    attack/release fades and a batch mixing direct and non-direct syllables."""
+    import os
+    import torch
+    from soundgen_beta_amd import batch, native
+    calls = [{"kind": "harmonics", "pitch": np.full(n, f), "params": dict(C2, attackLen=a)}
+             for f, n, a in ((97.0, 3500, 50), (210.0, 1200, 10), (333.3, 5000, 0), (150.0, 800, 300))]
+    calls.append({"kind": "harmonics", "pitch": np.linspace(120, 260, 2000), "params": C2})  # not a static span
+    outs = []
+    for direct in ("1", "0"):
+        os.environ["SG_TAB_DIRECT"] = direct
+        try:
+            plan = batch.Plan(calls, native.default_context(0))
+            plan.upload()
+            assert plan.table_stats()[0] >= 4
+            out = torch.full((plan.total,), float("nan"), dtype=torch.float32, device="cuda")
+            plan.execute(out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            outs.append((out.cpu().numpy(), plan.offsets.copy(), plan.lengths.copy()))
+        finally:
+            os.environ.pop("SG_TAB_DIRECT", None)
+    (a, oa, la), (b, ob, lb) = outs
+    assert np.array_equal(oa, ob) and np.array_equal(la, lb)
+    for o, n in zip(oa, la):
+        assert np.array_equal(a[o:o + n], b[o:o + n]), o
+        assert np.isfinite(a[o:o + n]).all()
+
+
 def test_planner_cases_one_batch(oracle):
     """Every planner case (vibrato, subharmonic epochs + crossfades, jitter,
     shimmer, temperature random walks, 16 kHz, near-ceiling f0) in ONE batch."""
