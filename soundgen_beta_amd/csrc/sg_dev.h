@@ -372,7 +372,10 @@ struct SgMix {
   float am_dep, pad;
   SgContour mult;     // amplAnchorsGlobal envelope (kind 0: none)
 };
-constexpr int SG_MIX_TILE = 8192;  // samples per sg_mix workgroup (chunks of 1024: descriptors loaded once)
+#ifndef SG_MIX_TILE_N
+#define SG_MIX_TILE_N 8192  // build knob
+#endif
+constexpr int SG_MIX_TILE = SG_MIX_TILE_N;  // samples per sg_mix workgroup (chunks of 2048: descriptors loaded once)
 struct SgMixTile {
   int32_t mix, pad;
   int64_t k0;
