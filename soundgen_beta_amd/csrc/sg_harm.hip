@@ -353,38 +353,7 @@ __device__ __forceinline__ float run_one(const SgWTask& T, float* __restrict__ l
 // task. Their rows interleave in LDS (la[2r] = A_P[r], la[2r + 1] = A_Q[r],
 // zero above a task's R; the dA rows likewise, zero for a CONST task), and one
 // broadcast ds_read_b128 yields rows r, r + 1 of both.
-// a pair's rows r = lane, lane + 64 (R <= SG_ROWS_F32 <= 128) in registers
-static_assert(SG_ROWS_F32 <= 128, "PairRows holds two rows per lane");
-struct PairRows {
-  float ap[2], aq[2], dp[2], dq[2];
-};
 template <bool TWO>
-__device__ __forceinline__ PairRows load_pair_rows(int64_t pa, int64_t pd, int pn, bool pc, int64_t qa, int64_t qd,
-                                                   int qn, bool qc, const float* __restrict__ amps, int lane) {
-  PairRows x;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int r = lane + 64 * i;
-    x.ap[i] = r < pn ? amps[pa + r] : 0.f;
-    x.aq[i] = r < qn ? amps[qa + r] : 0.f;
-    x.dp[i] = TWO && r < pn && !pc ? amps[pd + r] : 0.f;
-    x.dq[i] = TWO && r < qn && !qc ? amps[qd + r] : 0.f;
-  }
-  return x;
-}
-template <bool TWO>
-__device__ __forceinline__ void stage_pair_rows(const PairRows& x, int R, float* __restrict__ la, float* __restrict__ ld,
-                                                int lane) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int r = lane + 64 * i;
-    if (r < R) {
-      *reinterpret_cast<float2*>(la + 2 * r) = make_float2(x.ap[i], x.aq[i]);
-      if (TWO) *reinterpret_cast<float2*>(ld + 2 * r) = make_float2(x.dp[i], x.dq[i]);
-    }
-  }
-}
-template <bool TWO, bool STAGED = false>
 __device__ __forceinline__ void run_pair(const SgWTask& P, const SgWTask& Q, float* __restrict__ la,
                                          float* __restrict__ ld, const float* __restrict__ amps,
                                          float* __restrict__ W, int lane, float& mp, float& mq) {
@@ -393,7 +362,6 @@ __device__ __forceinline__ void run_pair(const SgWTask& P, const SgWTask& Q, flo
 #else
   const int R = P.Rn > Q.Rn ? P.Rn : Q.Rn;  // multiples of 16
 #endif
-  if (!STAGED)  // else the caller staged them (sg_sine_bank_pairs' prefetch loop)
   for (int r = lane; r < R; r += 64) {
     *reinterpret_cast<float2*>(la + 2 * r) = make_float2(r < P.Rn ? amps[P.a_off + r] : 0.f, r < Q.Rn ? amps[Q.a_off + r] : 0.f);
     if (TWO)
@@ -467,86 +435,14 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank(
 // Short fp32 tasks (<= 64 samples, no envelope; listed in idx), two per wave in
 // the halves of packed pairs (run_pair). The arithmetic of a task does not
 // depend on its partner (the last odd one pairs with itself).
-#ifndef SG_PAIRS_PERSIST
-#define SG_PAIRS_PERSIST 0  // build knob: > 0: pair kernels launch SG_PAIRS_PERSIST workgroups per CU, grid-stride
-#endif
-#ifndef SG_PAIRS_PF
-#define SG_PAIRS_PF 0  // build knob (with SG_PAIRS_PERSIST): the next pair's rows loaded before this pair's stores
-#endif
-#if SG_PAIRS_PF
-// Grid-stride over pairs; the next pair's amplitude rows are loaded into registers
-// before this pair's W stores (loads and stores share vmcnt: a load issued after the
-// stores would wait for them), its descriptors are scalar loads (lgkmcnt).
 extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_pairs(
     const int32_t* __restrict__ idx, int64_t n, const SgWTask* __restrict__ tasks, const float* __restrict__ amps,
     float* __restrict__ W, float* __restrict__ taskmax) {
   __shared__ __attribute__((aligned(16))) float rows[4][2][SG_LDS_ROWS];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t stride = (int64_t)gridDim.x * 8;
-  int64_t k = ((int64_t)blockIdx.x * 4 + wave) * 2;
-  if (k >= n) return;
-  int64_t tp = idx[k], tq = k + 1 < n ? idx[k + 1] : tp;
-  auto rows_of = [&](int64_t a, int64_t b) {
-    const SgWTask& A = tasks[a];
-    const SgWTask& B = tasks[b];
-    const bool two = !((A.flags & B.flags) & SG_TASK_CONST);
-    return two ? load_pair_rows<true>(A.a_off, A.d_off, A.Rn, A.flags & SG_TASK_CONST, B.a_off, B.d_off, B.Rn,
-                                      B.flags & SG_TASK_CONST, amps, lane)
-               : load_pair_rows<false>(A.a_off, A.d_off, A.Rn, true, B.a_off, B.d_off, B.Rn, true, amps, lane);
-  };
-  PairRows cur = rows_of(tp, tq);
-#pragma unroll 1
-  for (;;) {
-    const SgWTask P = tasks[tp];
-    const SgWTask Q = tasks[tq];
-    const bool has_q = k + 1 < n;
-    const int64_t kn = k + stride;
-    int64_t tpn = tp, tqn = tq;
-    PairRows nxt = cur;
-    if (kn < n) {  // wave-uniform
-      tpn = idx[kn];
-      tqn = kn + 1 < n ? idx[kn + 1] : tpn;
-      nxt = rows_of(tpn, tqn);
-    }
-    const int R = P.Rn > Q.Rn ? P.Rn : Q.Rn;
-    float mp, mq;
-    if ((P.flags & Q.flags) & SG_TASK_CONST) {
-      stage_pair_rows<false>(cur, R, rows[wave][0], rows[wave][1], lane);
-      run_pair<false, true>(P, Q, rows[wave][0], rows[wave][1], amps, W, lane, mp, mq);
-    } else {
-      stage_pair_rows<true>(cur, R, rows[wave][0], rows[wave][1], lane);
-      run_pair<true, true>(P, Q, rows[wave][0], rows[wave][1], amps, W, lane, mp, mq);
-    }
-    mp = wave_max(mp);
-    mq = wave_max(mq);
-    if (lane == 0) {
-      taskmax[tp] = mp;
-      if (has_q) taskmax[tq] = mq;
-    }
-    if (kn >= n) break;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next pair overwrites the wave's rows
-    __builtin_amdgcn_wave_barrier();
-    k = kn;
-    tp = tpn;
-    tq = tqn;
-    cur = nxt;
-  }
-}
-#else
-extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_pairs(
-    const int32_t* __restrict__ idx, int64_t n, const SgWTask* __restrict__ tasks, const float* __restrict__ amps,
-    float* __restrict__ W, float* __restrict__ taskmax) {
-  __shared__ __attribute__((aligned(16))) float rows[4][2][SG_LDS_ROWS];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#if SG_PAIRS_PERSIST
-  for (int64_t k = ((int64_t)blockIdx.x * 4 + wave) * 2; k < n; k += (int64_t)gridDim.x * 8) {
-#else
-  {
   const int64_t k = ((int64_t)blockIdx.x * 4 + wave) * 2;
   if (k >= n) return;
-#endif
   const int64_t tp = idx[k];
   const bool has_q = k + 1 < n;
   const int64_t tq = has_q ? idx[k + 1] : tp;
@@ -561,13 +457,7 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_pairs(
     taskmax[tp] = mp;
     if (has_q) taskmax[tq] = mq;
   }
-#if SG_PAIRS_PERSIST
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next pair overwrites the wave's rows
-  __builtin_amdgcn_wave_barrier();
-#endif
-  }
 }
-#endif  // SG_PAIRS_PF
 
 // ---------------------------------------------- tall tasks, fp32 Reinsch
 // Plain Clenshaw in fp32 loses ~R^2 eps when cos(theta) is near +-1 (a sideband
@@ -822,13 +712,8 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_tall_pairs(
   __shared__ __attribute__((aligned(16))) float rows[4][2][SG_LDS_ROWS];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#if SG_PAIRS_PERSIST
-  for (int64_t k = ((int64_t)blockIdx.x * 4 + wave) * 2; k < n; k += (int64_t)gridDim.x * 8) {
-#else
-  {
   const int64_t k = ((int64_t)blockIdx.x * 4 + wave) * 2;
   if (k >= n) return;
-#endif
   const int64_t tp = idx[k];
   const bool has_q = k + 1 < n;
   const int64_t tq = has_q ? idx[k + 1] : tp;
@@ -842,11 +727,6 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_tall_pairs(
   if (lane == 0) {
     taskmax[tp] = mp;
     if (has_q) taskmax[tq] = mq;
-  }
-#if SG_PAIRS_PERSIST
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next pair overwrites the wave's rows
-  __builtin_amdgcn_wave_barrier();
-#endif
   }
 }
 
@@ -1140,15 +1020,15 @@ extern "C" __global__ __launch_bounds__(SG_TAB_THREADS) __attribute__((amdgpu_wa
     for (int q = wave; q < J.n; q += SG_TAB_THREADS / 64) {
       float tmax = 0.f;
       tab_direct<false>(lt, logn, ts[q], obase, lane, 0.f, lf, L, tmax);
-      const float m = wave_max(tmax);
-      if (lane == 0) taskmax[(int64_t)J.t0 + q] = m;  // sg_syl_max takes the same max
-      wm = fmaxf(wm, m);
+      wm = fmaxf(wm, wave_max(tmax));
     }
     if (lane == 0) red[wave] = wm;
     __syncthreads();
     float m = red[0];
 #pragma unroll
     for (int w = 1; w < SG_TAB_THREADS / 64; ++w) m = fmaxf(m, red[w]);
+    // every task slot of the syllable holds the syllable max: sg_syl_max takes the same value
+    for (int q = threadIdx.x; q < J.n; q += SG_TAB_THREADS) taskmax[(int64_t)J.t0 + q] = m;
     const float inv = 1.f / m;
     float unused = 0.f;
     for (int q = wave; q < J.n; q += SG_TAB_THREADS / 64) tab_direct<true>(lt, logn, ts[q], obase, lane, inv, lf, L, unused);
@@ -1636,8 +1516,7 @@ void launch_sine_bank(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s)
 }
 void launch_sine_bank_pairs(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s) {
   if (n <= 0) return;
-  const int64_t blocks = SG_PAIRS_PERSIST ? std::min<int64_t>((n + 7) / 8, 256 * SG_PAIRS_PERSIST) : (n + 7) / 8;
-  hipLaunchKernelGGL(sg_sine_bank_pairs, dim3((unsigned)blocks), dim3(256), 0, s, D.tshort + k0, n, D.tasks,
+  hipLaunchKernelGGL(sg_sine_bank_pairs, dim3((unsigned)((n + 7) / 8)), dim3(256), 0, s, D.tshort + k0, n, D.tasks,
                      D.amps, D.W, D.taskmax);
   SG_LAUNCHED("sg_sine_bank_pairs");
 }
@@ -1649,8 +1528,7 @@ void launch_sine_bank_tall(const DevicePlan& D, int64_t k0, int64_t n, hipStream
 }
 void launch_sine_bank_tall_pairs(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s) {
   if (n <= 0) return;
-  const int64_t blocks = SG_PAIRS_PERSIST ? std::min<int64_t>((n + 7) / 8, 256 * SG_PAIRS_PERSIST) : (n + 7) / 8;
-  hipLaunchKernelGGL(sg_sine_bank_tall_pairs, dim3((unsigned)blocks), dim3(256), 0, s, D.tallp + k0, n,
+  hipLaunchKernelGGL(sg_sine_bank_tall_pairs, dim3((unsigned)((n + 7) / 8)), dim3(256), 0, s, D.tallp + k0, n,
                      D.tasks, D.amps, D.W, D.taskmax);
   SG_LAUNCHED("sg_sine_bank_tall_pairs");
 }

@@ -67,14 +67,18 @@ def test_sine_table_path_vs_recurrence(oracle):
 
 def test_sine_table_direct_output_equals_w_path():
     """Whole-syllable table spans write their final samples themselves
-    (SG_TAB_DIRECT, no W round trip, no sg_harm_copy pass): bit-identical to the
-    same spans through W + sg_syl_max + sg_harm_copy (SG_TAB_DIRECT=0), including
-    attack/release fades and a batch mixing direct and non-direct syllables."""
+    (SG_TAB_DIRECT, no W round trip, no sg_harm_copy pass; the max from the
+    candidate samples, or the full pass): bit-identical to the same spans through
+    W + sg_syl_max + sg_harm_copy (SG_TAB_DIRECT=0), including attack/release
+    fades and a batch mixing direct and non-direct syllables."""
     import os
     import torch
     from soundgen_beta_amd import batch, native
+    # 441 Hz and 2205 Hz: phase grids of 100 and 20 points per cycle (f0 / fs = 1 / 100, 1 / 20),
+    # coarser than the table, so the candidate search may fall back to the full pass
     calls = [{"kind": "harmonics", "pitch": np.full(n, f), "params": dict(C2, attackLen=a)}
-             for f, n, a in ((97.0, 3500, 50), (210.0, 1200, 10), (333.3, 5000, 0), (150.0, 800, 300))]
+             for f, n, a in ((97.0, 3500, 50), (210.0, 1200, 10), (333.3, 5000, 0), (150.0, 800, 300),
+                             (441.0, 2000, 50), (2205.0, 2000, 50), (1000.0, 3000, 20))]
     calls.append({"kind": "harmonics", "pitch": np.linspace(120, 260, 2000), "params": C2})  # not a static span
     outs = []
     for direct in ("1", "0"):
