@@ -42,6 +42,8 @@ def test_sine_table_path_vs_recurrence(oracle):
             prm = dict(C2, rolloff=roll, rolloffOct=0 if roll == -3 else C2["rolloffOct"])
             calls.append({"kind": "harmonics", "pitch": np.full(3500, f), "params": prm})
     calls.append({"kind": "harmonics", "pitch": np.full(1500, 190.0), "params": dict(C2, samplingRate=16000)})
+    # 2 s: 88 tasks, more than one table job (SG_TAB_TASKS), so the span goes through W
+    calls.append({"kind": "harmonics", "pitch": np.full(7000, 201.0), "params": C2})
     outs = {}
     try:
         for on in (1, 0):
@@ -78,7 +80,7 @@ def test_sine_table_direct_output_equals_w_path():
     # coarser than the table, so the candidate search may fall back to the full pass
     calls = [{"kind": "harmonics", "pitch": np.full(n, f), "params": dict(C2, attackLen=a)}
              for f, n, a in ((97.0, 3500, 50), (210.0, 1200, 10), (333.3, 5000, 0), (150.0, 800, 300),
-                             (441.0, 2000, 50), (2205.0, 2000, 50), (1000.0, 3000, 20))]
+                             (441.0, 2000, 50), (2205.0, 2000, 50), (1000.0, 3000, 20), (201.0, 7000, 50))]
     calls.append({"kind": "harmonics", "pitch": np.linspace(120, 260, 2000), "params": C2})  # not a static span
     outs = []
     for direct in ("1", "0"):
