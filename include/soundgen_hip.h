@@ -253,6 +253,10 @@ int sg_plan_precision(const sg_plan* plan, int32_t* call_fp64, int64_t* fp64_fra
  * (the largest over the call's filtered bouts; 0 when none was estimated):
  * bouts above the fp64 policy's threshold take the fp64 filter path. */
 int sg_plan_conditioning(const sg_plan* plan, double* rho);
+/* The same estimate for the pre-filter noise of each call's filtered bouts
+ * (its fp32 inverse STFT's round-off against the formant envelope); above the
+ * noise threshold those noise frames take the fp64 kernel. */
+int sg_plan_noise_conditioning(const sg_plan* plan, double* rho);
 /* Per-call device work the plan emits (ABI 2): sine-bank (sample, row) terms and
  * nominal FFT flops (5 wl log2 wl per transform), for load balancing across
  * GPUs (soundgen_beta_amd/dist.py). Either pointer may be NULL. */

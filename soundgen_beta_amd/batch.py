@@ -117,6 +117,14 @@ class Plan:
         native.check(native.lib().sg_plan_table_stats(self.ptr, *[C.byref(x) for x in v]))
         return tuple(x.value for x in v)
 
+    def noise_conditioning(self):
+        """Per call: the planner's fp32 conditioning estimate of its pre-filter noise
+        (the largest over its filtered bouts; above the threshold the noise frames
+        take the fp64 kernel)."""
+        v = np.zeros(self.n, dtype=np.float64)
+        native.check(native.lib().sg_plan_noise_conditioning(self.ptr, v.ctypes.data_as(C.POINTER(C.c_double))))
+        return v
+
     def conditioning(self):
         """Per call: the planner's fp32 conditioning estimate of its formant filter
         (the largest over its filtered bouts; bouts above the threshold go fp64)."""

@@ -166,6 +166,7 @@ void plan_range(sg::Batch& B, const sg_call_desc* calls, int64_t c0, int64_t c1)
   B.call_status.assign(n, 0);
   B.call_fp64.assign(n, 0);
   B.call_rho.assign(n, 0.0);
+  B.call_rho_noise.assign(n, 0.0);
   B.call_rows.assign(n, 0.0);
   B.call_flops.assign(n, 0.0);
   B.call_msg.assign(n, "");
@@ -177,6 +178,7 @@ void plan_range(sg::Batch& B, const sg_call_desc* calls, int64_t c0, int64_t c1)
     const int64_t hp0 = B.hp_bouts, rows0 = B.harm_terms;
     const double fl0 = B.fft_flops;
     B.rho_cur = 0;
+    B.rho_noise_cur = 0;
     try {
       sg::Rng R;
       R.s = &d.random;
@@ -201,6 +203,7 @@ void plan_range(sg::Batch& B, const sg_call_desc* calls, int64_t c0, int64_t c1)
       B.call_len[i] = L;
       B.call_fp64[i] = (int32_t)(B.hp_bouts - hp0);
       B.call_rho[i] = B.rho_cur;
+      B.call_rho_noise[i] = B.rho_noise_cur;
       B.call_rows[i] = (double)(B.harm_terms - rows0);
       B.call_flops[i] = B.fft_flops - fl0;
       off += (L + 63) / 64 * 64;  // 256-B aligned call slots
@@ -289,7 +292,7 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
   D.fu_total = c.fu; D.ugath.resize(c.ug);
   D.ecols.resize(c.col); D.envjobs.resize(c.job);
   D.call_len.resize(c.call); D.call_off.resize(c.call); D.call_status.resize(c.call); D.call_msg.resize(c.call);
-  D.call_fp64.resize(c.call); D.call_rho.resize(c.call); D.call_rows.resize(c.call); D.call_flops.resize(c.call);
+  D.call_fp64.resize(c.call); D.call_rho.resize(c.call); D.call_rho_noise.resize(c.call); D.call_rows.resize(c.call); D.call_flops.resize(c.call);
   D.epochs.resize(c.epoch); D.knots.resize(c.knot); D.pieces.resize(c.piece);
   D.amp_total = c.amp; D.ampsrc.resize(c.asrc); D.ampcols.resize(c.acol); D.ampjobs.resize(c.ajob); D.syls.resize(c.syl); D.syl_tiles.resize(c.st);
   D.cknots.resize(c.ck); D.items.resize(c.item);
@@ -316,6 +319,7 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
       D.call_status[b.call + i] = S.call_status[i];
       D.call_fp64[b.call + i] = S.call_fp64[i];
       D.call_rho[b.call + i] = S.call_rho[i];
+      D.call_rho_noise[b.call + i] = S.call_rho_noise[i];
       D.call_rows[b.call + i] = S.call_rows[i];
       D.call_flops[b.call + i] = S.call_flops[i];
       D.call_msg[b.call + i] = std::move(S.call_msg[i]);
@@ -747,6 +751,13 @@ int sg_plan_conditioning(const sg_plan* plan, double* rho) {
   if (!plan || !rho) return SG_E_ARG;
   const sg::Batch& B = plan->B;
   std::memcpy(rho, B.call_rho.data(), B.call_rho.size() * sizeof(double));
+  return SG_OK;
+}
+
+int sg_plan_noise_conditioning(const sg_plan* plan, double* rho) {
+  if (!plan || !rho) return SG_E_ARG;
+  const sg::Batch& B = plan->B;
+  std::memcpy(rho, B.call_rho_noise.data(), B.call_rho_noise.size() * sizeof(double));
   return SG_OK;
 }
 

@@ -1283,7 +1283,10 @@ __device__ __forceinline__ float fade_in_out(int lf, int64_t L, int64_t k) {  //
 // 29), R = 2, 4: one item per butterfly. (Grouping several outputs per item so each
 // input pair is read once measured no better: r04d, +2 % at 3, +21 % at 2 per item.) Roots of unity W_N^t from an fp64 table
 // in global memory, one per window length (sg_roots64), L2-resident.
-constexpr int SG_F64_THREADS = 256;
+#ifndef SG_F64_THREADS_N
+#define SG_F64_THREADS_N 256  // build knob: threads per fp64 frame
+#endif
+constexpr int SG_F64_THREADS = SG_F64_THREADS_N;
 namespace {
 __device__ __forceinline__ double2 cmul64(double2 a, double2 b) {
   return make_double2(fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x));
@@ -1599,7 +1602,15 @@ __device__ __forceinline__ void mix_body(const SgMixTile* __restrict__ tiles, co
   }
 }
 
-extern "C" __global__ __launch_bounds__(256) void sg_mix(const SgMixTile* __restrict__ tiles,
+#ifndef SG_MIX_WPE
+#define SG_MIX_WPE 0  // build knob: > 0 caps sg_mix's registers for that many waves per SIMD
+#endif
+#if SG_MIX_WPE
+#define SG_MIX_ATTR __attribute__((amdgpu_waves_per_eu(SG_MIX_WPE)))
+#else
+#define SG_MIX_ATTR
+#endif
+extern "C" __global__ __launch_bounds__(256) SG_MIX_ATTR void sg_mix(const SgMixTile* __restrict__ tiles,
                                                          const SgMix* __restrict__ mixes,
                                                          const SgNoiseItem* __restrict__ items,
                                                          const float* __restrict__ olamax,

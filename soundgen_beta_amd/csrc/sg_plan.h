@@ -185,6 +185,8 @@ struct Batch {
   std::vector<int32_t> call_fp64;   // bouts of the call on the fp64 filter path
   std::vector<double> call_rho;     // the largest conditioning estimate over the call's filtered bouts
   double rho_cur = 0;               // (the call being planned)
+  std::vector<double> call_rho_noise;  // the same for the pre-filter noise of its filtered bouts
+  double rho_noise_cur = 0;
   std::vector<std::string> call_msg;
   int64_t total_out = 0;
   // ---- stats ----

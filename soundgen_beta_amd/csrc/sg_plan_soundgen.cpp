@@ -632,10 +632,11 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
       std::vector<int> nolas;
       for (const SgNoiseItem& it : noises)
         if (it.ola >= 0 && !(it.flags & SG_ITEM_ZERO)) nolas.push_back(it.ola);
-      if (!nolas.empty() &&
-          (hp_mode() == 2 || noise_conditioning(*grid, A.rolloffNoise, B.olas[0][nolas[0]].wl, wl) > hp_rho_noise()) &&
-          noise_to_fp64(B, nolas))
-        ++B.hp_noise_bouts;
+      if (!nolas.empty()) {
+        const double rn = noise_conditioning(*grid, A.rolloffNoise, B.olas[0][nolas[0]].wl, wl);
+        B.rho_noise_cur = std::max(B.rho_noise_cur, rn);
+        if ((hp_mode() == 2 || rn > hp_rho_noise()) && noise_to_fp64(B, nolas)) ++B.hp_noise_bouts;
+      }
     }
     if (hp) {  // voiced syllables to the fp64 path; their items read fh
       ++B.hp_bouts;

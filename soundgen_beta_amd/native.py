@@ -76,6 +76,7 @@ def lib():
     L.sg_profile_read_kernel.argtypes = [vp, C.c_int, dp, i64p]
     L.sg_plan_stft_stats.argtypes = [vp, i64p, i64p, dp]
     L.sg_plan_conditioning.argtypes = [vp, dp]
+    L.sg_plan_noise_conditioning.argtypes = [vp, dp]
     L.sg_plan_precision.argtypes = [vp, C.POINTER(C.c_int32), i64p, i64p]
     L.sg_set_fp64_policy.argtypes = [C.c_int32, C.c_double]
     L.sg_set_amp_policy.argtypes = [C.c_int32]
