@@ -367,10 +367,14 @@ int hp_mode() {
   }
   return m;
 }
+// the pre-filter noise's fp64 threshold: measured with every noise in fp32
+// (tools/noise_selector_study.py, profiles/r04x_noise_selector_study.json): the
+// smallest noise estimate of a call over 1e-5 was 255 (1,280 C3 + C5 calls; every
+// call at <= 200 within 6.2e-6), so 150 (round 3: 30, unmeasured)
 double hp_rho_noise() {
   static const double r = [] {
     const char* e = std::getenv("SG_HP_RHO_NOISE");
-    return e ? std::atof(e) : 30.0;
+    return e ? std::atof(e) : 150.0;
   }();
   return r;
 }
