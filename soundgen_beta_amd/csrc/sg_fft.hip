@@ -1500,7 +1500,7 @@ __device__ __forceinline__ void mix_body(const SgMixTile* __restrict__ tiles, co
   if constexpr (HP) dst = fh;
   else dst = X.to_fs ? fs : out;
 #ifndef SG_MIX_E
-#define SG_MIX_E 8  // build knob: samples per thread and chunk (8: 2.94 -> 2.75 ms per C5 16k-call launch)
+#define SG_MIX_E 4  // build knob: samples per thread and chunk (r02: 8 over 4 at 5 waves per SIMD; r04: 4 at 8 waves, 1.83 -> 1.74 ms per C5 launch)
 #endif
   constexpr int E = SG_MIX_E;  // samples per thread and chunk
   const int64_t kend = T.k0 + SG_MIX_TILE < X.len ? T.k0 + SG_MIX_TILE : X.len;
@@ -1603,7 +1603,7 @@ __device__ __forceinline__ void mix_body(const SgMixTile* __restrict__ tiles, co
 }
 
 #ifndef SG_MIX_WPE
-#define SG_MIX_WPE 0  // build knob: > 0 caps sg_mix's registers for that many waves per SIMD
+#define SG_MIX_WPE 8  // build knob: > 0 caps sg_mix's registers for that many waves per SIMD (0: none)
 #endif
 #if SG_MIX_WPE
 #define SG_MIX_ATTR __attribute__((amdgpu_waves_per_eu(SG_MIX_WPE)))
