@@ -127,3 +127,27 @@ def test_extreme_calls_meet_tolerance_with_default_policy(oracle):
         worst = max(worst, err)
         assert err <= TOL, (i, err, rho[i], hp[i])
     assert worst > 0
+
+
+@pytest.mark.gpu
+def test_noise_threshold_meets_tolerance(oracle):
+    """The pre-filter noise's fp64 threshold (150, measured: tools/noise_selector_study.py,
+    profiles/r04x_noise_selector_study.json). M1$Sigh calls, whose noise estimates
+    (~200-400) straddle it, and C3 calls (31-65, now on the fp32 kernels) all meet 1e-5
+    with the default policy; a plan holding calls above the threshold runs fp64 noise frames."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    sigh = [c for c in bench.c5_calls(4096) if c.get("preset") == "M1$Sigh"][:16]
+    calls = sigh + bench.c3_calls(16)
+    plan = batch.Plan(calls, None)
+    rho_n = plan.noise_conditioning()
+    assert (rho_n[:len(sigh)] > 150).any() and (rho_n[len(sigh):] < 150).all(), rho_n
+    assert plan.precision()[1] > 0  # fp64 frames: the noise of the calls above the threshold
+    outs = batch.synthesize(calls)
+    for i, (c, y) in enumerate(zip(calls, outs)):
+        ref = bench.oracle_call(oracle, c)
+        assert len(y) == len(ref), i
+        err = float(np.sqrt(np.mean((np.asarray(y, np.float64) - ref) ** 2)))
+        assert err <= TOL, (i, c.get("preset"), rho_n[i], err)
