@@ -417,7 +417,10 @@ __device__ __forceinline__ void run_pair(const SgWTask& P, const SgWTask& Q, flo
 
 // Tasks of the fp32 class (listed in idx), one per wave. (A grid of resident waves
 // walking the list measured slower: r04f, C2 +14 %, C5 +22 %.)
-extern "C" __global__ __launch_bounds__(256) void sg_sine_bank(
+#ifndef SG_SB_WPE
+#define SG_SB_WPE 0  // build knob: > 0 caps sg_sine_bank's registers for that many waves per SIMD
+#endif
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SG_SB_WPE > 0 ? SG_SB_WPE : 1))) void sg_sine_bank(
     const int32_t* __restrict__ idx, int64_t n, const SgWTask* __restrict__ tasks, const float* __restrict__ amps,
     const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, float* __restrict__ W,
     float* __restrict__ taskmax) {
@@ -689,7 +692,10 @@ __device__ __forceinline__ float run_one_tall(const SgWTask& T, float* __restric
 // fp32 Reinsch chains (SG_TALL_F32), else fp64 sincospi and fp64 Clenshaw chains.
 // Tall tasks (listed in idx): SG_TALL_PAIR lists the short ones (<= 64 samples, no
 // envelope) separately for sg_sine_bank_tall_pairs; these run one per wave.
-extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_tall(
+#ifndef SG_TALL_WPE
+#define SG_TALL_WPE 0  // build knob: > 0 caps sg_sine_bank_tall's registers for that many waves per SIMD
+#endif
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SG_TALL_WPE > 0 ? SG_TALL_WPE : 1))) void sg_sine_bank_tall(
     const int32_t* __restrict__ idx, int64_t n, const SgWTask* __restrict__ tasks, const float* __restrict__ amps,
     const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, float* __restrict__ W,
     float* __restrict__ taskmax) {
@@ -750,7 +756,10 @@ __device__ __forceinline__ float run_one_hp(const SgWTask& T, float* __restrict_
            : run_task<true, false, false, double, double>(T, la, ld, amps, syls, cknots, W, lane);
 }
 
-extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_hp(
+#ifndef SG_HP_WPE
+#define SG_HP_WPE 0  // build knob: > 0 caps sg_sine_bank_hp's registers for that many waves per SIMD
+#endif
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SG_HP_WPE > 0 ? SG_HP_WPE : 1))) void sg_sine_bank_hp(
     const int32_t* __restrict__ idx, int64_t n, const SgWTask* __restrict__ tasks, const float* __restrict__ amps,
     const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, double* __restrict__ W64,
     float* __restrict__ taskmax) {
