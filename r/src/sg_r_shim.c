@@ -200,7 +200,9 @@ SEXP C_sg_soundgen(SEXP args) {
  * call order, each call's draws in the reference's order, so the result equals
  * lapply(calls, function(a) do.call(soundgen, a)) after the same set.seed().
  * A call R would stop() on stops the batch with that call's message, as the
- * loop would (its draws and those of the calls before it are consumed). */
+ * loop would: its draws and those of the calls before it are consumed, and the
+ * planner plans no later call once a callback-drawing call has failed
+ * (plan_range in sg_api.cpp), so .Random.seed ends where the R loop leaves it. */
 SEXP C_sg_soundgen_batch(SEXP calls) {
   if (!Rf_isNewList(calls)) Rf_error("soundgen_hip: calls must be a list of argument lists");
   const R_xlen_t n = Rf_xlength(calls);

@@ -171,8 +171,22 @@ void plan_range(sg::Batch& B, const sg_call_desc* calls, int64_t c0, int64_t c1)
   B.call_flops.assign(n, 0.0);
   B.call_msg.assign(n, "");
   int64_t off = 0;
+  // A call drawing from callbacks (R's RNG through the shim) that fails ends the
+  // callback stream there: lapply(calls, soundgen) stops at that call's stop(),
+  // so no later call may consume draws (.Random.seed stays where R leaves it).
+  // Callback batches plan in one range on the calling thread (sg_plan_batch).
+  int64_t cb_failed = -1;
   for (int64_t i = 0; i < n; ++i) {
     const sg_call_desc& d = calls[c0 + i];
+    const bool cb = d.random.norm_cb || d.random.unif_cb || d.random.gamma_cb;
+    if (cb && cb_failed >= 0) {
+      B.call_status[i] = SG_E_ARG;
+      B.call_msg[i] = "not planned: call " + std::to_string(c0 + cb_failed + 1) +
+                      " of the batch failed first (the RNG callback stream stops there)";
+      B.call_off[i] = off;
+      B.call_len[i] = 0;
+      continue;
+    }
     Checkpoint cp(B);
     const int first_syl = (int)B.syls.size();
     const int64_t hp0 = B.hp_bouts, rows0 = B.harm_terms;
@@ -214,6 +228,7 @@ void plan_range(sg::Batch& B, const sg_call_desc* calls, int64_t c0, int64_t c1)
       B.call_msg[i] = e.what();
       B.call_off[i] = off;
       B.call_len[i] = 0;
+      if (cb && cb_failed < 0) cb_failed = i;
     }
   }
   B.total_out = off;

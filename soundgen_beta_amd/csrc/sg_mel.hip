@@ -313,8 +313,14 @@ double mel2hz(double z) {
 }
 
 // Device buffers of one compareSounds / getMelSpec launch sequence
+// Device buffers of one mel run, and the host copies their uploads read: an
+// async H2D copy from pageable memory may still be pending when the caller's
+// vector goes away, so upload() stages the bytes in memory this object owns.
+// The destructor frees the device buffers first (hipFree waits for the device),
+// then the staged host bytes.
 struct DevBuf {
   std::vector<void*> p;
+  std::vector<std::vector<char>> host;
   template <class T>
   T* get(size_t n) {
     void* q = nullptr;
@@ -330,7 +336,11 @@ struct DevBuf {
 template <class T>
 T* upload(DevBuf& db, const std::vector<T>& v, hipStream_t s) {
   T* d = db.get<T>(v.size());
-  if (!v.empty()) MELCHK(hipMemcpyAsync(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
+  if (!v.empty()) {
+    const char* src = reinterpret_cast<const char*>(v.data());
+    db.host.emplace_back(src, src + v.size() * sizeof(T));
+    MELCHK(hipMemcpyAsync(d, db.host.back().data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
+  }
   return d;
 }
 

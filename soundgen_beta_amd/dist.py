@@ -249,7 +249,11 @@ def gather_timed(data, offsets, lengths, calls, rank, world, root=0):
     shard outputs (`data`, shard call i at offsets[i], lengths[i] samples, -1
     failed; shard order as shard() lists it) gathered to the root in call order
     by gather_packed, bracketed by barriers. Returns (root: the per-call list,
-    else None; wall ms of the exchange, the same on every rank's clock span)."""
+    else None; wall ms of the exchange, the same on every rank's clock span).
+    A rank whose part of the exchange raises still reaches the closing
+    agreement: every rank all-reduces a failure flag before the barrier, and all
+    of them raise if any rank failed (the caller's 'reported, not fatal' holds
+    on every rank, not only on the one that raised)."""
     import time
 
     import torch
@@ -259,8 +263,18 @@ def gather_timed(data, offsets, lengths, calls, rank, world, root=0):
     dist.barrier()
     sync()
     t = time.perf_counter()
-    got = gather_packed(data, offsets, lengths, owner, rank, world, root)
-    sync()
+    got, err = None, None
+    try:
+        got = gather_packed(data, offsets, lengths, owner, rank, world, root)
+        sync()
+    except Exception as e:  # noqa: BLE001 -- agreed on below, then re-raised on every rank
+        err = e
+    flag = torch.tensor([1 if err is not None else 0], dtype=torch.int32,
+                        device=data.device if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX)
     dist.barrier()
+    if int(flag.item()):
+        raise RuntimeError("gather_timed: the exchange failed on %s" %
+                           ("this rank: %r" % (err,) if err is not None else "another rank"))
     return got, (time.perf_counter() - t) * 1e3
 

@@ -69,10 +69,10 @@ def test_sine_table_path_vs_recurrence(oracle):
 
 def test_sine_table_direct_output_equals_w_path():
     """Whole-syllable table spans write their final samples themselves
-    (SG_TAB_DIRECT, no W round trip, no sg_harm_copy pass; the max from the
-    candidate samples, or the full pass): bit-identical to the same spans through
-    W + sg_syl_max + sg_harm_copy (SG_TAB_DIRECT=0), including attack/release
-    fades and a batch mixing direct and non-direct syllables."""
+    (SG_TAB_DIRECT, no W round trip, no sg_harm_copy pass; the max from a full
+    evaluation pass): bit-identical to the same spans through W + sg_syl_max +
+    sg_harm_copy (SG_TAB_DIRECT=0), including attack/release fades and a batch
+    mixing direct and non-direct syllables."""
     import os
     import torch
     from soundgen_beta_amd import batch, native
@@ -100,6 +100,45 @@ def test_sine_table_direct_output_equals_w_path():
     for o, n in zip(oa, la):
         assert np.array_equal(a[o:o + n], b[o:o + n]), o
         assert np.isfinite(a[o:o + n]).all()
+
+
+def test_sine_table_direct_into_filtered_bout(oracle):
+    """A direct table syllable of a FILTERED bout writes into the pre-filter
+    scratch fs (obase = fs), on the harmonic stream, before the noise copies and
+    the join: soundgen() calls with a static pitch, temperature 0 and formants,
+    some with breathing noise in the same bout. Byte-equal with SG_TAB_DIRECT=1
+    and =0, and within the tolerance of the oracle."""
+    import os
+    import torch
+    from soundgen_beta_amd import batch, native
+    from test_spectral_cpu import N, U
+    base = dict(samplingRate=44100, temperature=0, addSilence=0, formants="a", attackLen=30)
+    cases = [dict(base, sylLen=300, pitchAnchors=[180, 180], noiseAnchors=None),
+             dict(base, sylLen=450, pitchAnchors=[123.4, 123.4], noiseAnchors=None, formants="o"),
+             dict(base, sylLen=350, pitchAnchors=[220, 220],
+                  noiseAnchors={"time": [0, 350], "value": [-25, -25]}),
+             dict(base, sylLen=250, pitchAnchors=[150, 150], noiseAnchors=None, repeatBout=2, pauseLen=40)]
+    calls = [{"kind": "soundgen", "args": a, "normals": N, "uniforms": U} for a in cases]
+    outs = []
+    for direct in ("1", "0"):
+        os.environ["SG_TAB_DIRECT"] = direct
+        try:
+            plan = batch.Plan(calls, native.default_context(0))
+            plan.upload()
+            assert plan.table_stats()[0] >= len(cases)
+            out = torch.full((plan.total,), float("nan"), dtype=torch.float32, device="cuda")
+            plan.execute(out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            outs.append((out.cpu().numpy(), plan.offsets.copy(), plan.lengths.copy()))
+        finally:
+            os.environ.pop("SG_TAB_DIRECT", None)
+    (a, oa, la), (b, ob, lb) = outs
+    assert np.array_equal(oa, ob) and np.array_equal(la, lb)
+    for args, o, n in zip(cases, oa, la):
+        assert np.array_equal(a[o:o + n], b[o:o + n]), args
+        ref = oracle.soundgen(normals=N, uniforms=U, **args)
+        assert n == len(ref)
+        assert _rms(a[o:o + n], ref) <= TOL, args
 
 
 def test_planner_cases_one_batch(oracle):

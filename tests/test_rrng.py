@@ -95,3 +95,20 @@ def test_seeded_soundgen_plan_matches_oracle(oracle):
     assert plan.status[0] == 0, plan.message(0)
     ref = oracle.soundgen(rng=RRng(3), **args)
     assert int(plan.lengths[0]) == len(ref)
+
+
+def test_callback_batch_stops_at_first_failing_call():
+    """A batch drawing from one R stream stops where lapply(calls, soundgen)
+    stops: the failing call reports its error, no later call is planned, and the
+    stream is left where the calls before the failure left it."""
+    a = dict(sylLen=300, temperature=0.2, samplingRate=16000, addSilence=0)
+    bad = dict(a, samplingRate=-5, invalidArgAction="abort")
+    g = RRng(5)
+    plan = batch.Plan([{"kind": "soundgen", "args": a, "rng": g}, {"kind": "soundgen", "args": bad, "rng": g},
+                       {"kind": "soundgen", "args": a, "rng": g}], None)
+    assert plan.status[0] == 0
+    assert plan.status[1] != 0 and "samplingRate" in plan.message(1)
+    assert plan.status[2] != 0 and "not planned" in plan.message(2)
+    ref = RRng(5)
+    batch.Plan([{"kind": "soundgen", "args": a, "rng": ref}], None)
+    assert g.random() == ref.random()
