@@ -407,7 +407,9 @@ double sg_noise_threshold(int32_t which, double nonlinBalance);
 /* Test hook, no reference counterpart: the wavefront FFT stages used inside
  * the fused STFT/ISTFT kernel, on nframes frames of wl/2 complex points
  * (interleaved re, im, in place semantics: out = DFT(in), unscaled; inverse
- * uses exp(+2 pi i nk / M)). SG_E_UNSUPPORTED if wl is not on that path. */
+ * bit 0 uses exp(+2 pi i nk / M); bit 1, for wl = 2204 only, runs the radix-29
+ * stage on the VALU as sg_stft_ola_noise does instead of on the matrix pipe).
+ * SG_E_UNSUPPORTED if wl is not on that path. */
 int sg_debug_wave_fft(sg_ctx* ctx, int32_t wl, int32_t inverse, int32_t nframes,
                       const float* in, float* out);
 

@@ -21,39 +21,6 @@
 #include <type_traits>
 
 #include "sg_dev.h"
-#ifndef SG_FFT_WPE
-#define SG_FFT_WPE 2  // build knob: waves per SIMD for sg_stft_ola
-#endif
-#ifndef SG_FFT_WPE_NOISE
-#define SG_FFT_WPE_NOISE (SG_FFT_WAVES_NOISE_N > 8 ? 3 : 2)  // waves per SIMD for sg_stft_ola_noise
-#endif
-#ifndef SG_PF_AHEAD
-#define SG_PF_AHEAD 0  // build knob (filter kernel): 1 the next frame's inputs before this frame's inverse FFT;
-                       // 2 the next frame's sound after it, this frame's envelope before the forward FFT;
-                       // 3 the next frame's envelope right after this frame's untangle; 4: 3 and the next
-                       // frame's sound after this frame's inverse FFT
-#endif
-#ifndef SG_PF_AHEAD_NOISE
-#define SG_PF_AHEAD_NOISE 0  // the same for sg_stft_ola_noise (2: the next frame's input after the inverse FFT)
-#endif
-#ifndef SG_UNT_HOIST
-#define SG_UNT_HOIST 0  // build knob: the untangle reads all its LDS pairs before its first write (r03i A/B: neutral)
-#endif
-#ifndef SG_UNT_PACK
-#define SG_UNT_PACK 1  // build knob: the filter untangle + inverse packing in packed (re, im) arithmetic
-#endif
-#ifndef SG_NOISE_PACK
-#define SG_NOISE_PACK 1  // build knob: the noise spectrum's inverse packing from the real products directly
-#endif
-#ifndef SG_HAN_SCALED
-#define SG_HAN_SCALED 1  // build knob: the LDS hanning table pre-scaled by 1 / wl (one packed FMA per windowed pair)
-#endif
-#ifndef SG_OUT_REG
-#define SG_OUT_REG 0  // build knob: interior frames' final samples stored from the windowing registers (r03n A/B: 2 % slower, off)
-#endif
-#ifndef SG_OUT_BATCH
-#define SG_OUT_BATCH 1  // build knob: output samples and the next carry read from LDS in batches (no per-sample waits)
-#endif
 #include "sg_devfn.h"
 #include "sg_roots.h"
 
@@ -402,7 +369,7 @@ __device__ __forceinline__ void stage_w(float2* X, int M_, int Ns_, const float2
 // sg_stft_ola frame loop, accumulated per wave with s_memtime and summed into a
 // buffer that nothing else reads (sg_debug_stft_stamps).
 #ifdef SG_STFT_STAMPS
-__device__ unsigned long long sg_stft_st[16];
+__device__ unsigned long long sg_stft_st[32];  // [0, 16): filter frames, [16, 32): noise frames
 #define SG_ST(i)                                          \
   do {                                                    \
     if (st_acc) {                                         \
@@ -442,23 +409,130 @@ __device__ __forceinline__ void fft_w(float2* X, const SgFftGeom& g, const float
   }
 }
 
-// The dominant geometry (C5: 94 % of frames are wl = 2204, M = 1102 = 2 x 19 x 29)
-// with every size and stride a compile-time constant
-template <bool INV, int CM, int R0, int R1, int R2>
-__device__ __forceinline__ void fft_wc(float2* X, const float2* twS, int lane SG_ST_PARAMS) {
-  stage_w<R0, INV, CM, 1>(X, CM, 1, twS, 0u, lane);
+// ------------------------------------------- radix-29 stage on the matrix pipe
+// The first stage (Ns = 1: no twiddles) of the M = 1102 = 29 x 19 x 2 frame:
+// 38 butterflies of 29 points, y_k = sum_m x_m W_29^{mk}, in the symmetric form
+//   P_k = x_0 + sum_{m=1..14} (x_m + x_{29-m}) cos(2 pi mk / 29)     k = 0..14
+//   Q_k =       sum_{m=1..14} (x_m - x_{29-m}) sin(2 pi mk / 29)     k = 1..14
+//   forward y_k = P_k - i Q_k, y_{29-k} = P_k + i Q_k (inverse: the signs swap)
+// as two real products [16 x 16] x [16 x 80] on v_mfma_f32_16x16x4_f32 (exact
+// fp32: a k-ordered fmaf chain, like the VALU form). Rows: k; the cos matrix's
+// column m = 0 is 1 (x_0 enters P), row 15 / column 15 are zero padding.
+// Columns: n < 38 the real parts of butterfly j = n, 38 <= n < 76 the imaginary
+// parts of j = n - 38, 76..79 padding. Q's operand carries the OTHER component
+// of the same column, so one lane holds P_k.c and (Q_k).c' for its column c and
+// finishes y_k.c, y_{29-k}.c alone: y.re = P.re +- Q.im, y.im = P.im -+ Q.re.
+// Per lane: 40 two-point LDS reads, 40 MFMAs (1,280 matrix-pipe cycles per
+// wave), 40 single-float writes and ~80 VALU, instead of ~520 VALU with 38 of 64
+// lanes busy (stage_w<29>). Reference: the DFT of seewave's stft/istft,
+// seewave.r:7782-7819, :3447-3486 (R's fft).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+// The A fragments live in a 2 KB LDS table shared by the workgroup (lane l:
+// cos fragments of k-steps 0..3 at tab[l], sin fragments at tab[64 + l]) and
+// are read where the stage starts, so they hold no registers across the frame.
+constexpr int SG_MAT29_BYTES = 128 * 16;
+// Fills the table from the global twN[t] = W_2204^t = (cos, -sin)(2 pi t / 2204),
+// t < 1102: W_29^t = W_2204^{76 t}, and W_2204^{t + 1102} = -W_2204^t. Threads
+// 0..63 of the workgroup; the caller's barrier publishes it. LDS: after the
+// workgroup's frame slices (planner: SG_MAT29_BYTES more for M = 1102).
+__device__ __forceinline__ void mat29_fill(float4* tab, const float2* twN, int t) {
+  if (t >= 64) return;
+  const int k = t & 15;
+  float p[4], q[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int m = 4 * ks + (t >> 4);
+    const int idx = 76 * ((m * k) % 29);
+    const float2 w = idx < 1102 ? twN[idx] : make_float2(-twN[idx - 1102].x, -twN[idx - 1102].y);
+    p[ks] = (k <= 14 && m <= 14) ? w.x : 0.f;
+    q[ks] = (k >= 1 && k <= 14 && m >= 1 && m <= 14) ? -w.y : 0.f;
+  }
+  tab[t] = make_float4(p[0], p[1], p[2], p[3]);
+  tab[64 + t] = make_float4(q[0], q[1], q[2], q[3]);
+}
+
+template <bool INV>
+__device__ __forceinline__ void stage29_mfma(float2* X, const float4* tab, int lane) {
+  constexpr int MR = 38, NT = 5;
+  const int col = lane & 15, mg = lane >> 4;
+  const float4 ap = tab[lane], aq = tab[64 + lane];
+  const float Ap[4] = {ap.x, ap.y, ap.z, ap.w}, Aq[4] = {aq.x, aq.y, aq.z, aq.w};
+  // column group nt: lane column n = 16 nt + col is the real (n < 38) or the
+  // imaginary (38 <= n < 76) part of butterfly j; k-step ks: row m = 4 ks + mg
+  auto load = [&](int nt, float2 (&la)[4], float2 (&lb)[4]) {
+    const int n = 16 * nt + col;
+    const int j = n < 2 * MR ? (n >= MR ? n - MR : n) : 0;  // padding columns read butterfly 0 (finite, discarded)
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int m = 4 * ks + mg;        // 0..15
+      const int ma = m <= 14 ? m : 14;  // column 15: any finite value (A's column is zero)
+      const int mb = ma == 0 ? 0 : 29 - ma;
+      la[ks] = X[j + MR * ma];
+      lb[ks] = X[j + MR * mb];
+    }
+  };
+  f32x4 P[NT], Q[NT];
+  float2 la[2][4], lb[2][4];
+  load(0, la[0], lb[0]);
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    // the next group's operands are in flight while this group's MFMAs issue
+    if (nt + 1 < NT) load(nt + 1, la[(nt + 1) & 1], lb[(nt + 1) & 1]);
+    const int c = 16 * nt + col >= MR ? 1 : 0;
+    P[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    Q[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const float2 a = la[nt & 1][ks], b = lb[nt & 1][ks];
+      const bool m0 = ks == 0 && mg == 0;
+      const float bp = c ? (m0 ? a.y : a.y + b.y) : (m0 ? a.x : a.x + b.x);
+      const float bq = c ? a.x - b.x : a.y - b.y;  // the other component (m = 0: A's column is zero)
+      P[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ap[ks], bp, P[nt], 0, 0, 0);
+      Q[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Aq[ks], bq, Q[nt], 0, 0, 0);
+    }
+    // at most two column groups' operands live (all 20 k-step groups at once
+    // would take 80 VGPRs on top of the 40 accumulators)
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  sg_wave_fence();  // every read above precedes the in-place writes below
+  float* Yf = reinterpret_cast<float*>(X);
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int n = 16 * nt + col;
+    if (n >= 2 * MR) continue;
+    const int c = n >= MR ? 1 : 0;
+    const int j = n - c * MR;
+    const float sg = (c == 0) != INV ? 1.f : -1.f;
+    float* y = Yf + 2 * 29 * j + c;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = 4 * mg + r;  // D layout: column = lane & 15, row = 4 (lane / 16) + r
+      if (k > 14) continue;
+      const float p = P[nt][r], q = sg * Q[nt][r];
+      y[2 * k] = p + q;  // k = 0: Q_0 = 0
+      if (k > 0) y[2 * (29 - k)] = p - q;
+    }
+  }
+  sg_wave_fence();
+}
+
+// The dominant geometry (C5: 94 % of frames are wl = 2204, M = 1102 = 29 x 19 x 2)
+// with every size and stride a compile-time constant. MFMA: the radix-29 first
+// stage on the matrix pipe (A29: its fragment table in LDS). Measured per C5
+// launch (r05a, profiles/r05a_stft_ab.txt): the filter kernel 9.46 ms (stage
+// order 2, 19, 29) -> 9.15 (29 first, VALU) -> 8.88 (29 first, MFMA); the noise
+// kernel 2.53 -> 2.44 -> 2.56 (3 waves per SIMD: the MFMA stage's accumulators
+// push it into spills), so the noise kernel keeps the VALU stage.
+template <bool INV, int CM, int R0, int R1, int R2, bool MFMA = true>
+__device__ __forceinline__ void fft_wc(float2* X, const float2* twS, const float4* A29, int lane SG_ST_PARAMS) {
+  if constexpr (MFMA && CM == 1102 && R0 == 29) stage29_mfma<INV>(X, A29, lane);
+  else stage_w<R0, INV, CM, 1>(X, CM, 1, twS, 0u, lane);
   SG_ST(INV ? 5 : 1);
   stage_w<R1, INV, CM, R0>(X, CM, R0, twS, 0u, lane);
   SG_ST(INV ? 6 : 2);
   stage_w<R2, INV, CM, R0 * R1>(X, CM, R0 * R1, twS, 0u, lane);
   SG_ST(INV ? 7 : 3);
 }
-#ifndef SG_STFT_CP13
-#define SG_STFT_CP13 0  // build knob: the M = 1102 path with 13 carry pairs when the OLA's tail fits (hop >= 540)
-#endif
-#ifndef SG_STFT_SPEC
-#define SG_STFT_SPEC 1  // build knob: compile-time specialisation of sg_stft_ola for M = 1102 = 2 x 19 x 29
-#endif
 
 // Complex n-point DFT of X (LDS, n points, in place) by the workgroup (sg_fft_frames):
 // the Stockham FFT of size n, or Bluestein's chirp-z form through two L-point
@@ -673,8 +747,9 @@ extern "C" __global__ __launch_bounds__(SG_FFT_THREADS) void sg_fft_frames(
 }
 
 // ------------------------------------------------ fused frame pipeline
-// Inputs of one frame, prefetched into registers one frame ahead (their HBM
-// latency overlaps the previous frame's inverse FFT and overlap-add):
+// Inputs of one frame, loaded into registers at the top of the frame (their HBM
+// latency overlaps the other wave's work on the SIMD; loading a frame ahead
+// measured neutral or slower, r03i/r03l):
 //   FILTER: s[i] = sound (y[2n], y[2n+1]), n = 64 i + lane; a[i] = envelope
 //           (env[k], env[M - k]) with k = 64 i + lane (k = 0: env[0], env[M-1]); xh = env[half]
 //   NOISE:  a[i] = uniforms (u[k], u[M - k]), b[i] = filter (f[k], f[M - k]) (k = 0: M - 1); xh, xh2 at half
@@ -689,31 +764,24 @@ struct FramePf {
   __device__ __forceinline__ const float2& b(int i) const { return s[i]; }
 };
 
-// PART: 0 everything; 1 what the frame front consumes first (FILTER: the sound;
-// NOISE: everything); 2 the rest (FILTER: the envelope, consumed after the forward FFT)
-template <int PART = 0>
 __device__ __forceinline__ void frame_prefetch(FramePf& P, const SgFrame& F, int mode, int M,
                                                const float* __restrict__ fl, const float* __restrict__ fs, int lane) {
   const int half = M / 2;
   if (mode == SG_FRAME_FILTER) {
     const float* src = fs + F.src;
     const float* env = fl + F.env;
-    if (PART != 2) {
 #pragma unroll
-      for (int i = 0; i < SG_PF_SRC; ++i) {
-        const int n = 64 * i + lane;
-        if (n < M) P.s[i] = make_float2(src[2 * n], src[2 * n + 1]);
-      }
+    for (int i = 0; i < SG_PF_SRC; ++i) {
+      const int n = 64 * i + lane;
+      if (n < M) P.s[i] = make_float2(src[2 * n], src[2 * n + 1]);
     }
-    if (PART != 1) {
 #pragma unroll
-      for (int i = 0; i < SG_PF_PAIR; ++i) {
-        const int k = 64 * i + lane;
-        if (k <= half) P.a[i] = make_float2(env[k], env[k == 0 ? M - 1 : M - k]);
-      }
-      P.xh = env[half];
+    for (int i = 0; i < SG_PF_PAIR; ++i) {
+      const int k = 64 * i + lane;
+      if (k <= half) P.a[i] = make_float2(env[k], env[k == 0 ? M - 1 : M - k]);
     }
-  } else if (PART != 2) {
+    P.xh = env[half];
+  } else {
     const float* u = fl + F.src;
     const float* flt = fl + F.env;
 #pragma unroll
@@ -735,7 +803,8 @@ __device__ __forceinline__ void frame_prefetch(FramePf& P, const SgFrame& F, int
 // mirror; NOISE: uniforms x filter). Tables in LDS: ham (wl floats), twN (M pairs).
 template <int CM, int R0, int R1, int R2>
 __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mode, const SgFftGeom& g,
-                                            const float2* twS, const float2* twN, const float* ham, int lane SG_ST_PARAMS) {
+                                            const float2* twS, const float2* twN, const float* ham,
+                                            const float4* A29, int lane SG_ST_PARAMS) {
   int M = CM ? CM : g.M, N = CM ? 2 * CM : g.wl;
   if (!CM) __asm__ __volatile__("" : "+s"(M), "+s"(N));  // opaque: no hoisting across the caller's frame loop
   const float invN = 1.f / (float)N;
@@ -748,29 +817,11 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
     }
     sg_wave_fence();
     SG_ST(0);
-    if constexpr (CM != 0) fft_wc<false, CM, R0, R1, R2>(A, twS, lane SG_ST_ARGS);
+    if constexpr (CM != 0) fft_wc<false, CM, R0, R1, R2>(A, twS, A29, lane SG_ST_ARGS);  // filter frames only
     else fft_w<false>(A, g, twS, lane SG_ST_ARGS);
     // untangle X[k] = E + W_N^k O (E, O from Z_k, conj Z_{M-k}), Y = X / wl x env,
     // pack for the inverse; pair k owns slots k and M - k, the k = 0 lane also
-    // reads slots 1, M - 1 and half. SG_UNT_HOIST: every read of every pair
-    // before the first write (the slots of different pairs are disjoint, so the
-    // LDS latency is paid once per frame, not once per 64 pairs); else every read
-    // of an iteration precedes its writes
-#if SG_UNT_HOIST
-    float2 zav[SG_PF_PAIR], zbv[SG_PF_PAIR];
-#pragma unroll
-    for (int i = 0; i < SG_PF_PAIR; ++i) {
-      const int k0 = 64 * i;
-      if (k0 > half) break;
-      const int k = k0 + lane;
-      const bool act = k <= half && (k == 0 || k < M - k);
-      const int kk = act ? k : 0;
-      zav[i] = A[kk];
-      zbv[i] = A[kk == 0 ? 0 : M - kk];
-    }
-    const float2 z1h = A[1], zM1h = A[M - 1], zhh = A[half];
-    sg_wave_fence();
-#endif
+    // reads slots 1, M - 1 and half; every read of an iteration precedes its writes
 #pragma unroll
     for (int i = 0; i < SG_PF_PAIR; ++i) {
       const int k0 = 64 * i;
@@ -779,10 +830,6 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
       const bool act = k <= half && (k == 0 || k < M - k);
       const int kk = act ? k : 0;
       const int km = kk == 0 ? 0 : M - kk;
-#if SG_UNT_HOIST
-      const float2 za = zav[i], zb = zbv[i];
-      const float2 z1 = z1h, zM1 = zM1h, zh = zhh;
-#else
       const float2 za = A[kk], zb = A[km];
       float2 z1 = za, zM1 = za, zh = za;
       if (i == 0) {
@@ -794,7 +841,6 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
       // thread the compiler may sink them into the k = 0 branch, which the
       // SIMT code runs after the other branch
       sg_wave_fence();
-#endif
       if (!act) continue;
       auto X_at = [&](float2 a, float2 b, int t) -> float2 {
         const float2 e = make_float2(0.5f * (a.x + b.x), 0.5f * (a.y - b.y));
@@ -817,7 +863,6 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
           A[half] = a;
         }
       } else {
-#if SG_UNT_PACK
         // packed form (v_pk_* on (re, im)): with s = Z_k + conj Z_{M-k}, d = Z_k - conj Z_{M-k},
         // p = d W_N^k: 2 X_k = s - i p and 2 X_{M-k} = conj(s + i p) (W_N^{M-k} = -conj W_N^k:
         // no second twiddle read); the inverse packing Z'_k = e + i q, Z'_{M-k} = conj(e - i q)
@@ -833,15 +878,6 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
         const v2 zk = add_piq(e, q), zm = add_miq(e, q);
         A[kk] = F(zk);
         A[km] = make_float2(zm.x, -zm.y);
-#else
-        const float2 xk = X_at(za, zb, kk), xm = X_at(zb, za, km);
-        const float2 yk = make_float2(xk.x * ek, xk.y * ek);
-        const float2 ym = make_float2(xm.x * em, xm.y * em);
-        float2 a, b;
-        pack_pair(yk, ym, twN[kk], a, b);
-        A[kk] = a;
-        A[km] = b;
-#endif
       }
     }
   } else {  // SG_FRAME_NOISE: real spectrum u x filter, packed
@@ -859,7 +895,6 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
           A[half] = a;
         }
       } else if (k < M - k) {
-#if SG_NOISE_PACK
         // pack_pair of the real Y_k = a, Y_{M-k} = b: with e = a + b, r = a - b,
         // Z'_k = (e + r Im W, r Re W), Z'_{M-k} = (e - r Im W, r Re W)
         const float a = P.a[i].x * P.b(i).x, b = P.a[i].y * P.b(i).y;
@@ -867,13 +902,6 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
         const float e = a + b, r = a - b, im = r * w.x;
         A[k] = make_float2(fmaf(r, w.y, e), im);
         A[M - k] = make_float2(fmaf(-r, w.y, e), im);
-#else
-        const float2 yk = make_float2(P.a[i].x * P.b(i).x, 0.f), ym = make_float2(P.a[i].y * P.b(i).y, 0.f);
-        float2 a, b;
-        pack_pair(yk, ym, twN[k], a, b);
-        A[k] = a;
-        A[M - k] = b;
-#endif
       }
     }
   }
@@ -888,9 +916,8 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
 // which live in registers (pair layout: lane l, register r <-> samples
 // 2(64r + l), +1 of the frame). The samples before the next frame's start are
 // final (scaled, trimmed, written, max-reduced); the rest, shifted by the
-// hop, is the next carry. The next frame's inputs are prefetched into
-// registers while this frame's inverse FFT runs. Frames never leave LDS;
-// summation is in frame order, so results are deterministic.
+// hop, is the next carry. Frames never leave LDS; summation is in frame
+// order, so results are deterministic.
 // LDS: twS (M pairs), twN (M pairs), ham + han (M pairs each), SG_FFT_WAVES slices (M pairs each).
 // One segment of sg_stft_ola (CM > 0: the M = CM geometry with radices R0 x R1 x R2, sizes folded)
 template <int CM, int R0, int R1, int R2, int MODE, int CP = SG_CARRY_PAIRS>
@@ -904,7 +931,6 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
   const SgOla& O = olas[S.ola];
   float2* A = twS + M * (4 + w);
   const float* Af = reinterpret_cast<const float*>(A);
-  [[maybe_unused]] const float invN = 1.f / (float)N;  // the windowing without SG_HAN_SCALED
   const int hi = O.hi;
   const double h = O.h;
   auto bstart = [&](int f) -> int { return hi > 0 ? f * hi : (int)floor((double)f * h); };
@@ -916,6 +942,8 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
 #pragma unroll
   for (int r = 0; r < CP; ++r) C[r] = make_float2(0.f, 0.f);
   FramePf P;
+  constexpr int W = MODE == SG_FRAME_NOISE ? SG_FFT_WAVES_NOISE : SG_FFT_WAVES;
+  const float4* A29 = reinterpret_cast<const float4*>(twS + M * (4 + W));  // radix-29 fragments (M = 1102)
 #ifdef SG_STFT_STAMPS
   uint64_t st_accv[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t st_lastv = __builtin_amdgcn_s_memtime();
@@ -923,108 +951,36 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
   uint64_t* st_last = &st_lastv;
 #endif
   int bf = bstart(S.f0);
-  constexpr int PFA = MODE == SG_FRAME_NOISE ? SG_PF_AHEAD_NOISE : SG_PF_AHEAD;
-  if constexpr (PFA != 0) {
-    int Mk = M;
-    if (!CM) __asm__ __volatile__("" : "+s"(Mk));
-    frame_prefetch<PFA == 2 ? 1 : (PFA == 3 ? 2 : 0)>(P, frames[S.fdev], mode, Mk, fl, fs, lane);  // 4: both
-  }
   for (int k = 0; k < S.nf; ++k) {
-    if constexpr (PFA == 3) {  // this frame's sound; its envelope is in flight since the previous untangle
-      int Mk = M;
-      if (!CM) __asm__ __volatile__("" : "+s"(Mk));
-      frame_prefetch<1>(P, frames[S.fdev + k], mode, Mk, fl, fs, lane);
-    } else if constexpr (PFA == 0) {
+    {
       int Mk = M;
       if (!CM) __asm__ __volatile__("" : "+s"(Mk));
       frame_prefetch(P, frames[S.fdev + k], mode, Mk, fl, fs, lane);
-    } else if constexpr (PFA == 2) {  // the envelope: in flight during the forward FFT
-      int Mk = M;
-      if (!CM) __asm__ __volatile__("" : "+s"(Mk));
-      frame_prefetch<2>(P, frames[S.fdev + k], mode, Mk, fl, fs, lane);
     }
-    frame_front<CM, R0, R1, R2>(A, P, mode, g, twS, twN, ham, lane SG_ST_ARGS);
-    if constexpr (PFA == 3 || PFA == 4) {
-      // the next frame's envelope: in flight during this frame's inverse FFT, overlap-add
-      // and the next forward FFT (its registers take the place the forward FFT's env held)
-      if (k + 1 < S.nf) {
-        int Mk = M;
-        if (!CM) __asm__ __volatile__("" : "+s"(Mk));
-        frame_prefetch<2>(P, frames[S.fdev + k + 1], mode, Mk, fl, fs, lane);
-      }
-    }
-    if constexpr (PFA == 1) {
-      // the next frame's inputs are in flight during this frame's inverse FFT and overlap-add
-      if (k + 1 < S.nf) {
-        int Mk = M;
-        if (!CM) __asm__ __volatile__("" : "+s"(Mk));
-        frame_prefetch(P, frames[S.fdev + k + 1], mode, Mk, fl, fs, lane);
-      }
-    }
+    frame_front<CM, R0, R1, R2>(A, P, mode, g, twS, twN, ham, A29, lane SG_ST_ARGS);
     SG_ST(4);
-    if constexpr (CM != 0) fft_wc<true, CM, R0, R1, R2>(A, twS, lane SG_ST_ARGS);
+    if constexpr (CM != 0) fft_wc<true, CM, R0, R1, R2, MODE == SG_FRAME_FILTER>(A, twS, A29, lane SG_ST_ARGS);
     else fft_w<true>(A, g, twS, lane SG_ST_ARGS);
     int Mk = M, Nk = N;
     if (!CM) __asm__ __volatile__("" : "+s"(Mk), "+s"(Nk));
-    if constexpr (PFA == 2 || PFA == 4) {
-      // the next frame's sound (noise: its whole input): in flight during the
-      // overlap-add, the output and the carry reload (the FFT state is dead here)
-      if (k + 1 < S.nf) frame_prefetch<1>(P, frames[S.fdev + k + 1], mode, Mk, fl, fs, lane);
-    }
-    // window (/wl x hanning) and add the carry (pairs n = 64 r + lane)
-#if SG_HAN_SCALED
-    // han holds hanning / wl: one packed FMA per pair
+    // window (han holds hanning / wl: one packed FMA per pair) and add the carry
+    // (pairs n = 64 r + lane)
     const float2* han2 = reinterpret_cast<const float2*>(han);
 #pragma unroll
     for (int r = 0; r < CP; ++r) {
       const int n = 64 * r + lane;
-      if (n < Mk) {
-        C[r] = F(pfma(V(A[n]), V(han2[n]), V(C[r])));  // C[r] now holds the windowed pair (SG_OUT_REG)
-        A[n] = C[r];
-      }
+      if (n < Mk) A[n] = F(pfma(V(A[n]), V(han2[n]), V(C[r])));
     }
     for (int n = 64 * CP + lane; n < Mk; n += 64) A[n] = F(V(A[n]) * V(han2[n]));
-#else
-#pragma unroll
-    for (int r = 0; r < CP; ++r) {
-      const int n = 64 * r + lane;
-      if (n < Mk) {
-        const float2 v = A[n];
-        A[n] = make_float2(fmaf(v.x * invN, han[2 * n], C[r].x), fmaf(v.y * invN, han[2 * n + 1], C[r].y));
-      }
-    }
-    for (int n = 64 * CP + lane; n < Mk; n += 64) {
-      const float2 v = A[n];
-      A[n] = make_float2(v.x * invN * han[2 * n], v.y * invN * han[2 * n + 1]);
-    }
-#endif
     sg_wave_fence();
     SG_ST(8);
     const bool lastf = k == S.nf - 1;
     const int bn = lastf ? S.pb : bstart(S.f0 + k + 1);
     const int D = bn - bf;  // samples [bf, bn) are final
-    if (SG_OUT_REG && SG_HAN_SCALED && MODE == SG_FRAME_FILTER && bf >= S.pa && bf - first >= 0 && bn - first <= len && D <= 128 * CP) {
-      // interior frame whose final samples all lie in the carried pairs: written from
-      // the registers the windowing left them in (pair n = 64 r + lane: samples 2n, 2n + 1)
-      float* __restrict__ o = out + (bf - first);
-#pragma unroll
-      for (int r = 0; r < CP; ++r) {
-        const int i = 2 * (64 * r + lane);
-        const float vx = C[r].x * scale, vy = C[r].y * scale;
-        if (i < D) {
-          o[i] = vx;
-          m = fmaxf(m, vx);
-        }
-        if (i + 1 < D) {
-          o[i + 1] = vy;
-          m = fmaxf(m, vy);
-        }
-      }
-    } else if (bf >= S.pa && bf - first >= 0 && bn - first <= len && D <= Nk) {
+    if (bf >= S.pa && bf - first >= 0 && bn - first <= len && D <= Nk) {
       // interior frame (wave-uniform): every final sample is owned, inside the trim and the frame
       float* __restrict__ o = out + (bf - first);
       int i = lane;
-#if SG_OUT_BATCH
       for (; i + 192 < D; i += 256) {  // four LDS reads in flight per lane before the stores
         float v[4];
 #pragma unroll
@@ -1035,7 +991,6 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
           m = fmaxf(m, v[e]);
         }
       }
-#endif
       for (; i < D; i += 64) {
         const float v = Af[i] * scale;
         o[i] = v;
@@ -1053,28 +1008,14 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
       }
     }
     if (!lastf) {
-      const int tail = Nk - D;  // carried samples (pairs beyond it are zero)
-#if SG_OUT_BATCH
-      // every read unconditional (index clamped into the slice): all in flight at once;
-      // i0 >= Nk exactly when the pair lies past the tail
-      (void)tail;
+      // the next carry: every read unconditional (index clamped into the slice), all
+      // in flight at once; i0 >= Nk exactly when the pair lies past the carried tail
 #pragma unroll
       for (int r = 0; r < CP; ++r) {
         const int i0 = 2 * (64 * r + lane) + D;
         const float a = Af[min(i0, Nk - 1)], b = Af[min(i0 + 1, Nk - 1)];
         C[r] = make_float2(i0 < Nk ? a : 0.f, i0 + 1 < Nk ? b : 0.f);
       }
-#else
-#pragma unroll
-      for (int r = 0; r < CP; ++r) {
-        if (128 * r < tail) {  // wave-uniform
-          const int i0 = 2 * (64 * r + lane) + D;
-          C[r] = make_float2(i0 < Nk ? Af[i0] : 0.f, i0 + 1 < Nk ? Af[i0 + 1] : 0.f);
-        } else {
-          C[r] = make_float2(0.f, 0.f);
-        }
-      }
-#endif
     }
     sg_wave_fence();  // the next frame overwrites the slice
     bf = bn;
@@ -1082,9 +1023,10 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
   }
 #ifdef SG_STFT_STAMPS
   if (lane == 0) {
-    for (int i = 0; i < 10; ++i) atomicAdd(&sg_stft_st[i], (unsigned long long)st_acc[i]);
-    atomicAdd(&sg_stft_st[10], (unsigned long long)S.nf);
-    atomicAdd(&sg_stft_st[11], 1ull);
+    unsigned long long* st = sg_stft_st + (MODE == SG_FRAME_NOISE ? 16 : 0);
+    for (int i = 0; i < 10; ++i) atomicAdd(&st[i], (unsigned long long)st_acc[i]);
+    atomicAdd(&st[10], (unsigned long long)S.nf);
+    atomicAdd(&st[11], 1ull);
   }
 #endif
   // matchLengths padding (zeros) outside the istft output
@@ -1100,6 +1042,11 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
     }
   m = sgd::wave_max(m);
   if (lane == 0) slotmax[S.slot] = m;
+}
+
+// the specialised geometry: M = 1102 in the planner's stage order 29, 19, 2
+__device__ __forceinline__ bool geom_1102(const SgFftGeom& g) {
+  return g.M == 1102 && g.nstages == 3 && g.radix[0] == 29 && g.radix[1] == 19 && g.radix[2] == 2;
 }
 
 template <int MODE>
@@ -1124,28 +1071,22 @@ __device__ __forceinline__ void stft_ola_body(
       if (t < M - 1) twS[t] = tsg[t];
       twN[t] = tng[t];
     }
-    // hamming, then hanning (SG_HAN_SCALED: times 1 / wl, the inverse transform's scale)
-    const float hs = SG_HAN_SCALED ? 1.f / (float)N : 1.f;
+    // hamming, then hanning times 1 / wl (the inverse transform's scale)
+    const float hs = 1.f / (float)N;
     for (int t = threadIdx.x; t < 2 * N; t += NT) ham[t] = t < N ? wg[t] : wg[t] * hs;
+    if (MODE == SG_FRAME_FILTER && geom_1102(g)) mat29_fill(reinterpret_cast<float4*>(twS + M * (4 + W)), tng, threadIdx.x);
   }
   __syncthreads();
   const SgSegment S = segs[blockIdx.x * W + w];
   if (S.nf <= 0) return;  // padding segment
-#if SG_STFT_SPEC
-  if (M == 1102 && g.nstages == 3 && g.radix[0] == 2 && g.radix[1] == 19 && g.radix[2] == 29)
-    if (SG_STFT_CP13 && 2204 - (olas[S.ola].hi > 0 ? olas[S.ola].hi : (int)floor(olas[S.ola].h)) <= 128 * 13)
-      stft_segment<1102, 2, 19, 29, MODE, 13>(S, olas, frames, g, fl, fs, slotmax, twS, twN, ham, han, w, lane);
-    else
-      stft_segment<1102, 2, 19, 29, MODE>(S, olas, frames, g, fl, fs, slotmax, twS, twN, ham, han, w, lane);
+  if (geom_1102(g))
+    stft_segment<1102, 29, 19, 2, MODE>(S, olas, frames, g, fl, fs, slotmax, twS, twN, ham, han, w, lane);
   else
-#endif
-#ifndef SG_STFT_ONLY_SPEC  // diagnostic: the specialised path alone (register budget)
     stft_segment<0, 0, 0, 0, MODE>(S, olas, frames, g, fl, fs, slotmax, twS, twN, ham, han, w, lane);
-#else
-    ;
-#endif
 }
 
+constexpr int SG_FFT_WPE = 2;  // waves per SIMD of sg_stft_ola (241 VGPRs)
+constexpr int SG_FFT_WPE_NOISE = SG_FFT_WAVES_NOISE > 8 ? 3 : 2;
 extern "C" __global__ __launch_bounds__(SG_FFT_WAVES * 64) __attribute__((amdgpu_waves_per_eu(SG_FFT_WPE))) void sg_stft_ola(
     const SgSegment* __restrict__ segs, const SgOla* __restrict__ olas, const SgFrame* __restrict__ frames,
     const SgFftGeom* __restrict__ geoms, const float* __restrict__ fl, float* __restrict__ fs,
@@ -1161,7 +1102,9 @@ extern "C" __global__ __launch_bounds__(SG_FFT_WAVES_NOISE * 64) __attribute__((
 }
 
 // Test probe: wavefront w transforms frame w (M complex points, in place) with
-// the stage kernel of sg_stft_ola; inverse = conjugate twiddles, no scaling.
+// the stage kernels of sg_stft_ola (the specialised M = 1102 path, radix-29 stage
+// on the matrix pipe, when the geometry is that one); inverse = conjugate
+// twiddles, no scaling. LDS: twS, twN (M pairs each), the frame, the radix-29 table.
 extern "C" __global__ __launch_bounds__(64) void sg_fft_probe(const SgFftGeom* __restrict__ geom,
                                                               const float* __restrict__ fl, float2* __restrict__ data,
                                                               int inverse) {
@@ -1169,16 +1112,29 @@ extern "C" __global__ __launch_bounds__(64) void sg_fft_probe(const SgFftGeom* _
   const SgFftGeom& g = geom[0];
   const int M = g.M, lane = threadIdx.x;
   float2* twS = reinterpret_cast<float2*>(lds4);
-  float2* A = twS + M;
+  float2* twN = twS + M;
+  float2* A = twN + M;
+  float4* A29 = reinterpret_cast<float4*>(A + M);
   const float2* tsg = reinterpret_cast<const float2*>(fl + g.tws);
+  const float2* tng = reinterpret_cast<const float2*>(fl + g.tw) + M;
   float2* d = data + (int64_t)blockIdx.x * M;
   for (int t = lane; t < M; t += 64) {
     if (t < M - 1) twS[t] = tsg[t];
+    twN[t] = tng[t];
     A[t] = d[t];
   }
+  if (geom_1102(g)) mat29_fill(A29, tng, lane);
   sg_wave_fence();
-  if (inverse) fft_w<true>(A, g, twS, lane);
-  else fft_w<false>(A, g, twS, lane);
+  if (geom_1102(g)) {  // inverse bit 1: the VALU radix-29 stage (sg_stft_ola_noise's)
+    if (inverse == 1) fft_wc<true, 1102, 29, 19, 2>(A, twS, A29, lane);
+    else if (inverse == 3) fft_wc<true, 1102, 29, 19, 2, false>(A, twS, A29, lane);
+    else if (inverse == 2) fft_wc<false, 1102, 29, 19, 2, false>(A, twS, A29, lane);
+    else fft_wc<false, 1102, 29, 19, 2>(A, twS, A29, lane);
+  } else if (inverse & 1) {
+    fft_w<true>(A, g, twS, lane);
+  } else {
+    fft_w<false>(A, g, twS, lane);
+  }
   for (int t = lane; t < M; t += 64) d[t] = A[t];
 }
 
@@ -1251,9 +1207,6 @@ __device__ __forceinline__ float sigmoid_at(const float* __restrict__ tab, int l
   return r < lo ? tab[r] : tab[2 * lo - 1 - r];
 }
 
-#ifndef SG_MIX_LDS_SPLINE
-#define SG_MIX_LDS_SPLINE 1  // build knob: sg_mix evaluates spline contours from LDS-staged knots
-#endif
 [[maybe_unused]] constexpr int SG_MIX_KMAX = 32;  // knots of an LDS-staged contour
 __device__ __forceinline__ float fade_in_out(int lf, int64_t L, int64_t k) {  // fadeInOut(), R/utilities_soundgen.R:440-459
   float f = 1.f;
@@ -1283,10 +1236,7 @@ __device__ __forceinline__ float fade_in_out(int lf, int64_t L, int64_t k) {  //
 // 29), R = 2, 4: one item per butterfly. (Grouping several outputs per item so each
 // input pair is read once measured no better: r04d, +2 % at 3, +21 % at 2 per item.) Roots of unity W_N^t from an fp64 table
 // in global memory, one per window length (sg_roots64), L2-resident.
-#ifndef SG_F64_THREADS_N
-#define SG_F64_THREADS_N 256  // build knob: threads per fp64 frame
-#endif
-constexpr int SG_F64_THREADS = SG_F64_THREADS_N;
+constexpr int SG_F64_THREADS = 256;  // threads per fp64 frame (r04: 128 / 512 / 1,024 slower)
 namespace {
 __device__ __forceinline__ double2 cmul64(double2 a, double2 b) {
   return make_double2(fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x));
@@ -1499,10 +1449,8 @@ __device__ __forceinline__ void mix_body(const SgMixTile* __restrict__ tiles, co
   V* __restrict__ dst;
   if constexpr (HP) dst = fh;
   else dst = X.to_fs ? fs : out;
-#ifndef SG_MIX_E
-#define SG_MIX_E 4  // build knob: samples per thread and chunk (r02: 8 over 4 at 5 waves per SIMD; r04: 4 at 8 waves, 1.83 -> 1.74 ms per C5 launch)
-#endif
-  constexpr int E = SG_MIX_E;  // samples per thread and chunk
+  // samples per thread and chunk (r04: 4 at 8 waves per SIMD, 1.83 -> 1.74 ms per C5 launch over 8 at 5)
+  constexpr int E = 4;
   const int64_t kend = T.k0 + SG_MIX_TILE < X.len ? T.k0 + SG_MIX_TILE : X.len;
   // per-tile constants, hoisted out of the sample loops (one scalar-load burst)
   const float base_scale = X.base_kind == SG_BASE_NORM ? 1.f / olamax[X.base_ola] : 1.f;
@@ -1513,7 +1461,6 @@ __device__ __forceinline__ void mix_body(const SgMixTile* __restrict__ tiles, co
   __shared__ int curs[NC][256];
   for (int i = 0; i < NC && i < X.nitems; ++i) curs[i][threadIdx.x] = -1;
   int mcur = -1;
-#if SG_MIX_LDS_SPLINE
   // spline contours (kind 3, <= SG_MIX_KMAX knots) of the mult envelope (slot NC) and
   // the first NC items staged in LDS: the per-sample interval walk and the five
   // coefficient loads then hit LDS instead of a dependent chain of global loads
@@ -1527,7 +1474,6 @@ __device__ __forceinline__ void mix_body(const SgMixTile* __restrict__ tiles, co
     for (int j = threadIdx.x; j < 5 * c.nk; j += 256) cks[i][j] = src[j];
   }
   __syncthreads();
-#endif
 #pragma unroll 1
   for (int64_t kc = T.k0; kc < kend; kc += E * 256) {
     V v[E];
@@ -1565,13 +1511,11 @@ __device__ __forceinline__ void mix_body(const SgMixTile* __restrict__ tiles, co
         V nv = raw[e] * (V)nscale;
         if (flat) nv *= (V)sflat;
         else if (it.strength.kind != 0) {
-#if SG_MIX_LDS_SPLINE
           if (i < NC && lds_ok(it.strength)) {
             SgContour cl = it.strength;
             cl.k_off = 0;
             nv = (V)((double)nv * sgd::contour_at_cursor(cl, &cks[i][0], it.len, j, cur));
           } else
-#endif
             nv = (V)((double)nv * sgd::contour_at_cursor(it.strength, cknots, it.len, j, cur));
         }
         nv *= (V)fade_in_out(it.fade, it.len, j);
@@ -1583,13 +1527,11 @@ __device__ __forceinline__ void mix_body(const SgMixTile* __restrict__ tiles, co
     for (int e = 0; e < E; ++e) {
       const int64_t k = kc + e * 256 + threadIdx.x;
       if (X.mult.kind != 0 && k < kend) {
-#if SG_MIX_LDS_SPLINE
         if (lds_ok(X.mult)) {
           SgContour cl = X.mult;
           cl.k_off = 0;
           v[e] = (V)((double)v[e] * sgd::contour_at_cursor(cl, &cks[NC][0], X.len, k, mcur));
         } else
-#endif
           v[e] = (V)((double)v[e] * sgd::contour_at_cursor(X.mult, cknots, X.len, k, mcur));
       }
       if (X.am_lo > 0) v[e] *= (V)(1.f - sigmoid_at(fl + X.am_tab, X.am_lo, k) * X.am_dep / 100.f);
@@ -1602,14 +1544,8 @@ __device__ __forceinline__ void mix_body(const SgMixTile* __restrict__ tiles, co
   }
 }
 
-#ifndef SG_MIX_WPE
-#define SG_MIX_WPE 8  // build knob: > 0 caps sg_mix's registers for that many waves per SIMD (0: none)
-#endif
-#if SG_MIX_WPE
-#define SG_MIX_ATTR __attribute__((amdgpu_waves_per_eu(SG_MIX_WPE)))
-#else
-#define SG_MIX_ATTR
-#endif
+// sg_mix's registers capped for 8 waves per SIMD (r04: 94 VGPRs = 5 waves uncapped)
+#define SG_MIX_ATTR __attribute__((amdgpu_waves_per_eu(8)))
 extern "C" __global__ __launch_bounds__(256) SG_MIX_ATTR void sg_mix(const SgMixTile* __restrict__ tiles,
                                                          const SgMix* __restrict__ mixes,
                                                          const SgNoiseItem* __restrict__ items,
@@ -1678,7 +1614,7 @@ void launch_stft_ola(const DevicePlan& D, int phase, int64_t s0, int64_t n_segs,
 }
 void launch_fft_probe(const SgFftGeom* geom, const float* fl, float* data, int M, int nframes, int inverse,
                       hipStream_t s) {
-  hipLaunchKernelGGL(sg_fft_probe, dim3((unsigned)nframes), dim3(64), 2 * M * 8, s, geom, fl,
+  hipLaunchKernelGGL(sg_fft_probe, dim3((unsigned)nframes), dim3(64), 3 * M * 8 + SG_MAT29_BYTES, s, geom, fl,
                      reinterpret_cast<float2*>(data), inverse);
   SG_LAUNCHED("sg_fft_probe");
 }
@@ -1734,8 +1670,8 @@ void launch_ugather(const SgUJob* jobs, int64_t n_jobs, const float* us, float* 
 
 #ifdef SG_STFT_STAMPS
 extern "C" int sg_debug_stft_stamps(unsigned long long* out) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(sg_stft_st), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
-  unsigned long long z[16] = {};
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(sg_stft_st), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
+  unsigned long long z[32] = {};
   return hipMemcpyToSymbol(HIP_SYMBOL(sg_stft_st), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif

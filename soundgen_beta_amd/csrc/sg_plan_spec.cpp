@@ -22,7 +22,12 @@
 namespace sg {
 
 namespace {
-constexpr int kRadices[] = {4, 2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31};
+// Stage order of a transform: the largest odd primes first, then 4s and a 2. The
+// first Stockham stage (Ns = 1) needs no twiddles, and it saves the most twiddle
+// products on the largest radix ((R - 1) M / R of them); for M = 1102 = 29 x 19 x 2
+// it makes the radix-29 stage the first, where sg_stft_ola runs it on the matrix
+// pipe (sg_fft.hip stage29_mfma).
+constexpr int kRadices[] = {31, 29, 23, 19, 17, 13, 11, 7, 5, 3, 4, 2};
 
 // The fp64 trig tables of a transform depend on its length alone: each is
 // computed once per process (every batch part plans its own geometries, so
@@ -870,7 +875,8 @@ void finalize_spec(Batch& B) {
       const int gi = fg[i];
       const SgFftGeom& g = B.geoms[gi];
       if (g.kind == SG_FFT_WAVE) {  // transformed inside sg_stft_ola
-        B.fgroup_lds[ph][0] = std::max(B.fgroup_lds[ph][0], (sg_fft_waves(ph) + 4) * g.M * 8);
+        // + the radix-29 fragment table of the specialised M = 1102 path (sg_fft.hip SG_MAT29_BYTES)
+        B.fgroup_lds[ph][0] = std::max(B.fgroup_lds[ph][0], (sg_fft_waves(ph) + 4) * g.M * 8 + (g.M == 1102 ? 2048 : 0));
         ++i;
         continue;
       }

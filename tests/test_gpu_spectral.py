@@ -16,7 +16,9 @@ def _rms(a, b):
 
 @pytest.mark.parametrize("wl", [8, 64, 440, 800, 1000, 1764, 2048, 2204, 2400])
 def test_wave_fft_vs_numpy(wl):
-    """The wavefront FFT stages (radices 2, 4, odd primes) against numpy, both directions."""
+    """The wavefront FFT stages (radices 2, 4, odd primes) against numpy, both
+    directions; wl = 2204 also with its radix-29 stage on the VALU (the noise
+    kernel's) as well as on the matrix pipe (the filter kernel's)."""
     import ctypes as C
     from soundgen_beta_amd import native
     M, nf = wl // 2, 3
@@ -24,7 +26,7 @@ def test_wave_fft_vs_numpy(wl):
     x = (rng.normal(size=(nf, M)) + 1j * rng.normal(size=(nf, M))).astype(np.complex64)
     ctx = native.Context(0)
     try:
-        for inv in (0, 1):
+        for inv in ((0, 1, 2, 3) if wl == 2204 else (0, 1)):
             src = np.ascontiguousarray(x).view(np.float32).ravel()
             dst = np.zeros_like(src)
             fp = C.POINTER(C.c_float)
@@ -33,7 +35,7 @@ def test_wave_fft_vs_numpy(wl):
                 pytest.skip("wl %d runs the workgroup FFT" % wl)
             native.check(rc, ctx.ptr)
             got = dst.view(np.complex64).reshape(nf, M)
-            want = np.fft.ifft(x, axis=1) * M if inv else np.fft.fft(x, axis=1)
+            want = np.fft.ifft(x, axis=1) * M if inv & 1 else np.fft.fft(x, axis=1)
             err = np.abs(got - want).max() / np.abs(want).max()
             assert err < 2e-6 * np.log2(M) + 1e-6, (wl, inv, err)
     finally:

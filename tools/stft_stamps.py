@@ -1,10 +1,12 @@
 """Diagnostic: cycles per section of sg_stft_ola's frame loop, from a library
 built with -DSG_STFT_STAMPS (tools/build_variant.sh stamps -DSG_STFT_STAMPS,
 SRC=sg_fft.hip).  SG_HIP_LIB=.../exp_stamps.so python tools/stft_stamps.py c3 [calls]
-Sections (per wave, summed over frames): 0 descriptor + input loads + hamming
-store (filter frames), 1-3 forward FFT stages (filter frames; stage 3 = all
-stages after the second), 4 untangle x envelope (filter) or the noise spectrum,
-5-7 inverse FFT stages, 8 hanning + carry add, 9 output + next carry.
+Sections (per wave, summed over frames), reported separately for the filter
+kernel (sg_stft_ola) and the noise kernel (sg_stft_ola_noise): 0 descriptor +
+input loads + hamming store (filter frames), 1-3 forward FFT stages (filter
+frames; stage 3 = all stages after the second), 4 untangle x envelope (filter)
+or input loads + the noise spectrum (noise), 5-7 inverse FFT stages, 8 hanning
++ carry add, 9 output + next carry.
 """
 import ctypes as C
 import json
@@ -28,7 +30,7 @@ out = torch.empty((p.total + 63) // 64 * 64, dtype=torch.float32, device="cuda:0
 L = native.lib()
 f = L.sg_debug_stft_stamps
 f.argtypes = [C.POINTER(C.c_ulonglong)]
-buf = (C.c_ulonglong * 16)()
+buf = (C.c_ulonglong * 32)()
 p.execute(out.data_ptr(), torch.cuda.current_stream().cuda_stream)
 torch.cuda.synchronize()
 f(buf)  # drop the warmup
@@ -37,12 +39,14 @@ for _ in range(reps):
     p.execute(out.data_ptr(), torch.cuda.current_stream().cuda_stream)
 torch.cuda.synchronize()
 f(buf)
-v = list(buf)
-frames, waves = v[10], v[11]
 names = ["loads+ham", "fwd_s1", "fwd_s2", "fwd_s3+", "untangle", "inv_s1", "inv_s2", "inv_s3+", "han+carry",
          "out+carry"]
-tot = sum(v[:10])
-res = {"config": cfg, "calls": n, "frames": frames, "waves": waves,
-       "cycles_per_frame": {k: v[i] / max(frames, 1) for i, k in enumerate(names)},
-       "share": {k: v[i] / max(tot, 1) for i, k in enumerate(names)}}
+res = {"config": cfg, "calls": n}
+for kern, base in (("sg_stft_ola", 0), ("sg_stft_ola_noise", 16)):
+    v = list(buf)[base:base + 16]
+    frames, waves = v[10], v[11]
+    tot = sum(v[:10])
+    res[kern] = {"frames": frames, "waves": waves, "cycles_per_frame_total": tot / max(frames, 1),
+                 "cycles_per_frame": {k: v[i] / max(frames, 1) for i, k in enumerate(names)},
+                 "share": {k: v[i] / max(tot, 1) for i, k in enumerate(names)}}
 print(json.dumps(res, indent=1))
