@@ -245,7 +245,7 @@ int sg_plan_stft_stats(const sg_plan* plan, int64_t* samples, int64_t* alg_bytes
 /* Precision path of the plan (ABI 2): per call, the number of its bouts whose
  * formant filter runs in fp64 (source, pre-filter mix and forward STFT; the
  * planner's conditioning estimate of the fp32 round-off through the envelope
- * exceeded its threshold, env SG_HP_RHO, default 100; SG_HP=0 never, 2 always);
+ * exceeded its threshold, env SG_HP_RHO, default 100; sg_set_fp64_policy: 0 never, 2 always);
  * totals of fp64 filter frames and sine-bank tasks. Any pointer may be NULL.
  * No reference counterpart: the R path is fp64 throughout. */
 int sg_plan_precision(const sg_plan* plan, int32_t* call_fp64, int64_t* fp64_frames, int64_t* fp64_tasks);
@@ -317,8 +317,7 @@ int sg_set_uniform_gather(int32_t on);
  * later (sg_plan_upload, or the first sg_execute of a plan): 1 (default)
  * long runs of constant-amplitude, linear-phase tasks (static tones) sample a
  * per-span table of the harmonic sum by cubic Hermite interpolation
- * (sg_sine_bank_tab); 0 every task runs the row recurrence. SG_TABLE=0 in the
- * environment sets the default off. */
+ * (sg_sine_bank_tab); 0 every task runs the row recurrence. */
 int sg_set_sine_table(int32_t on);
 /* Release the planner's process-wide cache of freed host blocks (kept for the
  * next plan, capped by SG_HOST_CACHE_MB or 8 GB / LOCAL_WORLD_SIZE). Returns

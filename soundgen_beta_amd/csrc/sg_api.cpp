@@ -494,10 +494,7 @@ int sg_plan_batch(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, sg_pl
       plan_range(B, calls, 0, n_calls);
       g_growth.record(B, n_calls);
     } else {
-      static const int per_thread = [] {  // parts per thread (SG_PLAN_PARTS: experiments)
-        const char* e = std::getenv("SG_PLAN_PARTS");
-        return e ? std::max(1, std::atoi(e)) : 8;
-      }();
+      constexpr int per_thread = 8;  // parts per thread (dynamic balance over uneven calls)
       const int64_t nchunk = std::min<int64_t>(n_calls, (int64_t)threads * per_thread);
       std::vector<sg::Batch> parts((size_t)nchunk);
       std::vector<std::exception_ptr> errs((size_t)nchunk);

@@ -53,10 +53,7 @@ constexpr int SG_TASK_CONST = 1;  // columns equal over the task: A chain only
 constexpr int SG_TASK_ENV = 4;    // the syllable has an amplitude envelope (max taken after it)
 // tasks with more rows than this (subharmonic sidebands) run in sg_sine_bank_tall:
 // fp64 angle and recurrence (parity on the C5 presets with subFreq << f0)
-#ifndef SG_ROWS_F32_N
-#define SG_ROWS_F32_N 96  // build knob
-#endif
-constexpr int SG_ROWS_F32 = SG_ROWS_F32_N;
+constexpr int SG_ROWS_F32 = 96;
 constexpr int SG_TASK_LIN = 2;    // phase segment linear (c2 = c3 = c4 = 0): one fp64 FMA per sample
 // fp64 source of an ill-conditioned formant-filter call (planner: filter_conditioning,
 // sg_plan_soundgen.cpp): fp64 angle and recurrence, w_off indexes the fp64 epoch scratch W64
@@ -106,15 +103,6 @@ constexpr int SG_TAB_LOGN_MIN = 8;
 constexpr int SG_TAB_LOGN_MAX = 11;   // LDS 20 N bytes: 40 KB
 constexpr double SG_TAB_TOL = 1e-7;
 constexpr int SG_TAB_TASKS = 64;      // tasks per workgroup at most (a longer span: more workgroups)
-#ifndef SG_PAIR
-#define SG_PAIR 1  // build knob: short fp32 tasks (<= 64 samples) two per wave in the halves of packed pairs
-#endif
-#ifndef SG_TALL_PAIR
-#define SG_TALL_PAIR 1  // build knob: short tall tasks two per wave, fp32 Reinsch in packed halves
-#endif
-#ifndef SG_TASKS_PER_BLOCK
-#define SG_TASKS_PER_BLOCK 4  // 4 waves x 1 task (build knob; measured better than 2 per wave)
-#endif
 // batch slices of the sine-bank / finalize pipeline; measured on MI355X (C2): 4 slices
 // on two streams ran 0.41 ms/step against 0.32 for one (both kernels slowed when
 // co-resident), so the default is a single slice
@@ -253,16 +241,11 @@ constexpr int SG_FFT_DFT = 2;   // M with a prime factor > 31: Bluestein (SgCdft
 // wl-point and 2M-point DFTs (cd[0], cd[1]), one frame per sg_fft_frames workgroup
 constexpr int SG_FFT_ODD = 3;
 constexpr int SG_WAVE_STATE = 24;  // complex butterfly points a lane holds per stage in sg_stft_ola
-#ifndef SG_FFT_WAVES_N
-#define SG_FFT_WAVES_N 8  // build knob
-#endif
-constexpr int SG_FFT_WAVES = SG_FFT_WAVES_N;    // wavefronts (segments) per sg_stft_ola workgroup: one workgroup per CU
-#ifndef SG_FFT_WAVES_NOISE_N
-#define SG_FFT_WAVES_NOISE_N 12  // build knob
-#endif
+constexpr int SG_FFT_WAVES = 8;    // wavefronts (segments) per sg_stft_ola workgroup: one workgroup per CU
+
 // sg_stft_ola_noise (no forward FFT: its specialised path fits 168 VGPRs, 3 waves per
 // SIMD, and (12 + 4) M pairs of LDS fit 160 KB for every M <= 64 SG_PF_SRC)
-constexpr int SG_FFT_WAVES_NOISE = SG_FFT_WAVES_NOISE_N;
+constexpr int SG_FFT_WAVES_NOISE = 12;
 constexpr int sg_fft_waves(int phase) { return phase == 0 ? SG_FFT_WAVES_NOISE : SG_FFT_WAVES; }
 constexpr int SG_PF_SRC = 20;      // sg_stft_ola register prefetch: sound pairs per lane (M <= 1280)
 constexpr int SG_PF_PAIR = 10;     // bin pairs per lane (M / 2 + 1 <= 640)
@@ -372,10 +355,7 @@ struct SgMix {
   float am_dep, pad;
   SgContour mult;     // amplAnchorsGlobal envelope (kind 0: none)
 };
-#ifndef SG_MIX_TILE_N
-#define SG_MIX_TILE_N 8192  // build knob
-#endif
-constexpr int SG_MIX_TILE = SG_MIX_TILE_N;  // samples per sg_mix workgroup (chunks of 2048: descriptors loaded once)
+constexpr int SG_MIX_TILE = 8192;  // samples per sg_mix workgroup (chunks of 2048: descriptors loaded once)
 struct SgMixTile {
   int32_t mix, pad;
   int64_t k0;

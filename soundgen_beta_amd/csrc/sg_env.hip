@@ -22,19 +22,7 @@
 
 #include "sg_dev.h"
 
-#ifndef SG_ENV_SMEM
-#define SG_ENV_SMEM 1  // build knob: a selected track's parameters by scalar loads (0: v_readlane broadcasts)
-#endif
-
-__device__ __forceinline__ double bcast(double v, int lane) {
-  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
-  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
-  return __hiloint2double(hi, lo);
-}
-
-#ifndef SG_ENV_LG_LDS
-#define SG_ENV_LG_LDS 2048  // build knob: log2(k) table entries staged in LDS per workgroup (0: read from HBM)
-#endif
+constexpr int SG_ENV_LG_LDS = 2048;  // log2(k) table entries staged in LDS per workgroup (r02: 4.9 -> 3.8 ms)
 
 // One column of a job: per 64-bin chunk, the tracks whose bands reach it (ballot),
 // their parameters by scalar loads; LG: log2(k) from the LDS copy.
@@ -44,7 +32,6 @@ __device__ __forceinline__ void env_column(const SgEnvJob& J, int c, const SgEnv
                                            float* __restrict__ fe, int lane) {
   const float thrf = -SG_ENV_CUT;  // log2 units
   // lane t: term t (group 0) and term 64 + t (group 1); absent terms get an empty range
-  double A[2], Rr[2], Lm[2];
   float amp[2];
   int klo[2], khi[2];
 #pragma unroll
@@ -52,9 +39,6 @@ __device__ __forceinline__ void env_column(const SgEnvJob& J, int c, const SgEnv
     const int t = g * 64 + lane;
     const bool in = t < J.ntr;
     const SgEnvTerm& e = tm[in ? t : 0];
-    if (!SG_ENV_SMEM) {
-      A[g] = e.A; Rr[g] = e.Rr; Lm[g] = e.Lm;
-    }
     amp[g] = (float)e.amp;
     klo[g] = in ? e.klo : 1 << 30;
     khi[g] = in ? e.khi : -1;
@@ -72,12 +56,8 @@ __device__ __forceinline__ void env_column(const SgEnvJob& J, int c, const SgEnv
       while (m) {
         const int t = __builtin_ctzll(m);
         m &= m - 1;
-#if SG_ENV_SMEM
         const SgEnvTerm* __restrict__ e = tm + g * 64 + t;  // wave-uniform: scalar loads into SGPRs
         const double a = e->A, r = e->Rr, l = e->Lm;
-#else
-        const double a = bcast(A[g], t), r = bcast(Rr[g], t), l = bcast(Lm[g], t);
-#endif
         const float am = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amp[g]), t));
         const double d = fma(a, lx, fma(-r, x, -l));
         // d > thr >= -126: the raw v_exp_f32 is exact enough and never denormal
@@ -101,7 +81,6 @@ extern "C" __global__ __launch_bounds__(256) void sg_spec_env(const SgEnvTask* _
   const int lane = threadIdx.x & 63;
   const SgEnvTask T = tasks[w < ntask ? w : ntask - 1];
   const SgEnvJob J = jobs[T.job];
-#if SG_ENV_LG_LDS
   // the log2(k) table is common to every job: one LDS copy per workgroup, as far
   // as the workgroup's longest column reaches (whole 64-bin chunks)
   __shared__ double lgs[SG_ENV_LG_LDS];
@@ -115,10 +94,6 @@ extern "C" __global__ __launch_bounds__(256) void sg_spec_env(const SgEnvTask* _
   const int nst = need < cap ? need : cap;
   for (int i = threadIdx.x; i < nst; i += 256) lgs[i] = lg2[i];
   __syncthreads();
-#else
-  const double* lgs = nullptr;
-  const int nst = 0;
-#endif
   if (w >= ntask) return;
   const int c1 = T.c0 + SG_ENV_COLS < J.nc ? T.c0 + SG_ENV_COLS : J.nc;
   const bool lds = (J.nr + 63) / 64 * 64 <= nst;  // every chunk's k inside the staged table

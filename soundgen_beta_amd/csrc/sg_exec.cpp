@@ -98,8 +98,7 @@ struct Layout {
 // touching a crossfade (multi-term) piece, and every tile of a syllable with an
 // envelope or drift, keep the general kernel.
 static void split_finalize_tiles(Batch& B) {
-  int64_t copy_tile = SG_COPY_TILE;
-  if (const char* e = std::getenv("SG_COPY_TILE")) copy_tile = std::min<int64_t>(SG_COPY_TILE_MAX, std::max(1024, std::atoi(e)));
+  const int64_t copy_tile = SG_COPY_TILE;
   B.fin_tiles.clear();
   B.fin_tiles_hp.clear();
   B.copy_tiles.clear();
@@ -221,10 +220,7 @@ static TabSpans group_tables(const Batch& B) {
     return true;
   };
   ColumnReader cols(B);
-  if (const char* e = std::getenv("SG_TAB_LOGN"))  // experiment knob: largest table
-    cols.logn_max = std::min(SG_TAB_LOGN_MAX, std::max(SG_TAB_LOGN_MIN, std::atoi(e)));
-  int per_job = SG_TAB_TASKS;
-  if (const char* e = std::getenv("SG_TAB_TASKS")) per_job = std::min(SG_TAB_TASKS, std::max(1, std::atoi(e)));  // experiment knob
+  const int per_job = SG_TAB_TASKS;
   std::vector<SgTabJob> jobs;
   int64_t run0 = -1, run_samples = 0;
   SgWTask first{};
@@ -358,7 +354,6 @@ void finalize_plan(Batch& B) {
   int64_t total = 0;
   for (const SgSyllable& sy : B.syls) total += sy.L;
   int slices = SG_SLICES;
-  if (const char* e = std::getenv("SG_SLICES")) slices = std::max(1, std::atoi(e));  // experiment knob
   if (any_hp) slices = 1;  // the fp64 syllables' tiles are listed after every fp32 one
   const int K = (int)std::min<int64_t>(slices, nsyl);
   int64_t acc = 0, ft = 0, ct = 0;
@@ -397,13 +392,12 @@ void device_free(DevicePlan& D) {
 }
 
 // wavetable path for long static spans (sg_sine_bank_tab): on by default;
-// SG_TABLE=0 or sg_set_sine_table(0) turns it off
+// sg_set_sine_table(0) turns it off
 static std::atomic<int> g_tab{-1};
 static bool tab_on() {
   int v = g_tab.load();
   if (v < 0) {
-    const char* e = std::getenv("SG_TABLE");
-    v = (e && e[0] == '0') ? 0 : 1;
+    v = 1;  // sg_set_sine_table(0) turns the wavetable path off (tests)
     int expect = -1;
     g_tab.compare_exchange_strong(expect, v);
   }
@@ -518,8 +512,8 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
       const bool shrt = t.len <= 64 && !(t.flags & SG_TASK_ENV);
       if (!in_tab.empty() && in_tab[(size_t)i]) continue;
       if (t.flags & SG_TASK_HP) D.thp_host.push_back(i);
-      else if (t.R > SG_ROWS_F32) (SG_TALL_PAIR && shrt ? D.tallp_host : D.tall_host).push_back(i);
-      else if (SG_PAIR && t.len <= 64 && !(t.flags & SG_TASK_ENV)) D.tshort_host.push_back(i);
+      else if (t.R > SG_ROWS_F32) (shrt ? D.tallp_host : D.tall_host).push_back(i);
+      else if (t.len <= 64 && !(t.flags & SG_TASK_ENV)) D.tshort_host.push_back(i);
       else D.tlong_host.push_back(i);
     }
   });

@@ -32,21 +32,11 @@ using sgd::wave_max;
 // v_sub measured 4.5 lane-instructions per (sample, row) on gfx950, VGPR/SGPR
 // operands 2.7 — tools/ubench/clenshaw_ubench.hip.)
 constexpr int SG_LDS_ROWS = 256;
-#ifndef SG_NS8_TWO
-#define SG_NS8_TWO 0  // build knob: 8-slot passes also with the dA chain
-#endif
 
-#ifndef SG_NS_MAX
-#define SG_NS_MAX 8  // build knob: largest slot pass (8 or 4)
-#endif
-// Interpolated amplitudes (the dA chain). SG_FAMP 1: ONE chain over the per-sample
-// amplitude a_r(t) = A_r + t dA_r (fma, then the recurrence: 3 VALU ops per row
-// instead of 2 x 2 for the A and dA chains; Reinsch 4 instead of 6), so
-// W = (sum_r a_r(t) sin r theta) by linearity. SG_FAMP 0: the two chains,
-// W = (b_1 + t e_1) sin theta.
-#ifndef SG_FAMP
-#define SG_FAMP 1
-#endif
+// Interpolated amplitudes (the dA rows): ONE chain over the per-sample amplitude
+// a_r(t) = A_r + t dA_r (fma, then the recurrence: 3 VALU ops per row instead of
+// 2 x 2 for separate A and dA chains; Reinsch 4 instead of 6), so
+// W = (sum_r a_r(t) sin r theta) by linearity (r04: the sine-bank classes -13 %).
 
 
 template <bool TWO>
@@ -58,47 +48,27 @@ __device__ __forceinline__ void stage_rows(float* __restrict__ la, float* __rest
   }
 }
 
-#ifndef SG_PK
-#define SG_PK 1  // build knob: slot pairs as packed fp32 (v_pk_fma_f32 / v_pk_add_f32)
-#endif
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float vfma(float a, float b, float c) { return fmaf(a, b, c); }
 __device__ __forceinline__ double vfma(double a, double b, double c) { return fma(a, b, c); }
 __device__ __forceinline__ f2 vfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
-// Clenshaw over staged rows n-1 .. 0 (n a multiple of 4), continuing b (and e)
+// Clenshaw over staged rows n-1 .. 0 (n a multiple of 4), continuing b
 #define SG_ROW(a, d)                                                  \
   {                                                                   \
     _Pragma("unroll") for (int s = 0; s < NS; ++s) {                  \
-      if (TWO && SG_FAMP) {                                           \
-        const Acc av = vfma(tt[s], (Acc)(d), (Acc)(a));               \
-        const Acc b = vfma(al[s], b1[s], av - b2[s]);                 \
-        b2[s] = b1[s];                                                \
-        b1[s] = b;                                                    \
-      } else {                                                        \
-        const Acc b = vfma(al[s], b1[s], (Acc)(a) - b2[s]);           \
-        b2[s] = b1[s];                                                \
-        b1[s] = b;                                                    \
-        if (TWO) {                                                    \
-          const Acc e = vfma(al[s], e1[s], (Acc)(d) - e2[s]);         \
-          e2[s] = e1[s];                                              \
-          e1[s] = e;                                                  \
-        }                                                             \
-      }                                                               \
+      const Acc av = TWO ? vfma(tt[s], (Acc)(d), (Acc)(a)) : (Acc)(a); \
+      const Acc b = vfma(al[s], b1[s], av - b2[s]);                   \
+      b2[s] = b1[s];                                                  \
+      b1[s] = b;                                                      \
     }                                                                 \
   }
-#ifndef SG_ROWS_IT
-#define SG_ROWS_IT 8  // rows per loop iteration (build knob: 4 or 8)
-#endif
+constexpr int SG_ROWS_IT = 8;  // rows per loop iteration (r01: 8 over 4)
 template <int NS, bool TWO, typename Acc>
 __device__ __forceinline__ void clenshaw_lds(const float* __restrict__ la, const float* __restrict__ ld, int n,
-                                             const Acc (&al)[NS], const Acc (&tt)[NS], Acc (&b1)[NS], Acc (&b2)[NS],
-                                             Acc (&e1)[NS], Acc (&e2)[NS]) {
+                                             const Acc (&al)[NS], const Acc (&tt)[NS], Acc (&b1)[NS], Acc (&b2)[NS]) {
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-#ifdef SG_DIAG_NOROWS  // diagnostic timing build only: no row work
-  n = 0;
-#endif
-  if (SG_ROWS_IT == 8 && (n & 4)) {  // odd group of 4 on top
+  if (n & 4) {  // odd group of 4 on top
     const float4 A4 = *reinterpret_cast<const float4*>(la + n - 4);
     const float4 D4 = TWO ? *reinterpret_cast<const float4*>(ld + n - 4) : z4;
     SG_ROW(A4.w, D4.w)
@@ -109,23 +79,18 @@ __device__ __forceinline__ void clenshaw_lds(const float* __restrict__ la, const
   }
 #pragma unroll 1
   for (int r = n - SG_ROWS_IT; r >= 0; r -= SG_ROWS_IT) {
-    const float4 A4 = *reinterpret_cast<const float4*>(la + r + SG_ROWS_IT - 4);
-    const float4 D4 = TWO ? *reinterpret_cast<const float4*>(ld + r + SG_ROWS_IT - 4) : z4;
-    float4 A0 = z4, D0 = z4;
-    if (SG_ROWS_IT == 8) {
-      A0 = *reinterpret_cast<const float4*>(la + r);
-      if (TWO) D0 = *reinterpret_cast<const float4*>(ld + r);
-    }
+    const float4 A4 = *reinterpret_cast<const float4*>(la + r + 4);
+    const float4 D4 = TWO ? *reinterpret_cast<const float4*>(ld + r + 4) : z4;
+    const float4 A0 = *reinterpret_cast<const float4*>(la + r);
+    const float4 D0 = TWO ? *reinterpret_cast<const float4*>(ld + r) : z4;
     SG_ROW(A4.w, D4.w)
     SG_ROW(A4.z, D4.z)
     SG_ROW(A4.y, D4.y)
     SG_ROW(A4.x, D4.x)
-    if (SG_ROWS_IT == 8) {
-      SG_ROW(A0.w, D0.w)
-      SG_ROW(A0.z, D0.z)
-      SG_ROW(A0.y, D0.y)
-      SG_ROW(A0.x, D0.x)
-    }
+    SG_ROW(A0.w, D0.w)
+    SG_ROW(A0.z, D0.z)
+    SG_ROW(A0.y, D0.y)
+    SG_ROW(A0.x, D0.x)
   }
 }
 
@@ -148,35 +113,30 @@ __device__ __forceinline__ void sample_setup(const SgWTask& T, int l, float& t, 
 template <int NS, bool TWO>
 __device__ __forceinline__ void clenshaw_pk(const float* __restrict__ la, const float* __restrict__ ld, int n,
                                             const float (&al)[NS], const float (&tt)[NS], float (&b1)[NS],
-                                            float (&b2)[NS], float (&e1)[NS], float (&e2)[NS]) {
+                                            float (&b2)[NS]) {
   constexpr int NP = NS / 2;
-  f2 al2[NP], t2[NP], p1[NP], p2[NP], q1[NP], q2[NP];
+  f2 al2[NP], t2[NP], p1[NP], p2[NP];
 #pragma unroll
   for (int i = 0; i < NP; ++i) {
     al2[i] = f2{al[2 * i], al[2 * i + 1]};
     t2[i] = f2{tt[2 * i], tt[2 * i + 1]};
     p1[i] = f2{b1[2 * i], b1[2 * i + 1]};
     p2[i] = f2{b2[2 * i], b2[2 * i + 1]};
-    q1[i] = f2{e1[2 * i], e1[2 * i + 1]};
-    q2[i] = f2{e2[2 * i], e2[2 * i + 1]};
   }
-  clenshaw_lds<NP, TWO, f2>(la, ld, n, al2, t2, p1, p2, q1, q2);
+  clenshaw_lds<NP, TWO, f2>(la, ld, n, al2, t2, p1, p2);
 #pragma unroll
   for (int i = 0; i < NP; ++i) {
     b1[2 * i] = p1[i].x; b1[2 * i + 1] = p1[i].y;
     b2[2 * i] = p2[i].x; b2[2 * i + 1] = p2[i].y;
-    e1[2 * i] = q1[i].x; e1[2 * i + 1] = q1[i].y;
-    e2[2 * i] = q2[i].x; e2[2 * i + 1] = q2[i].y;
   }
 }
 template <int NS, bool TWO, typename Acc>
 __device__ __forceinline__ void clenshaw_any(const float* __restrict__ la, const float* __restrict__ ld, int n,
-                                             const Acc (&al)[NS], const Acc (&tt)[NS], Acc (&b1)[NS], Acc (&b2)[NS],
-                                             Acc (&e1)[NS], Acc (&e2)[NS]) {
-  if constexpr (SG_PK && sizeof(Acc) == 4 && NS % 2 == 0)
-    clenshaw_pk<NS, TWO>(la, ld, n, al, tt, b1, b2, e1, e2);
+                                             const Acc (&al)[NS], const Acc (&tt)[NS], Acc (&b1)[NS], Acc (&b2)[NS]) {
+  if constexpr (sizeof(Acc) == 4 && NS % 2 == 0)  // fp32 slot pairs as packed fp32 (v_pk_fma_f32 / v_pk_add_f32)
+    clenshaw_pk<NS, TWO>(la, ld, n, al, tt, b1, b2);
   else
-    clenshaw_lds<NS, TWO, Acc>(la, ld, n, al, tt, b1, b2, e1, e2);
+    clenshaw_lds<NS, TWO, Acc>(la, ld, n, al, tt, b1, b2);
 }
 
 // fp64 variant for tall tasks (T.R > SG_ROWS_F32, subharmonic sidebands): the
@@ -192,24 +152,22 @@ __device__ __forceinline__ void sample_setup(const SgWTask& T, int l, float& t, 
   al = 2.0 * cs;
 }
 
-#ifndef SG_ROT
-#define SG_ROT 1  // build knob: linear-phase slots 1..7 by rotation of slot 0 (no per-slot fp64 / v_sin / v_cos)
-#endif
 template <int NS, bool TWO, bool ENV, bool LIN, typename Acc, typename WT = float>
 __device__ __forceinline__ void run_slots(const SgWTask& T, bool staged, float* __restrict__ la, float* __restrict__ ld,
                                           const float* __restrict__ amps, const SgSyllable* __restrict__ syls,
                                           const double* __restrict__ cknots, WT* __restrict__ W, int l0, int lane,
                                           float& tmax, const float (&rc)[8], const float (&rs)[8]) {
-  constexpr bool ROT = SG_ROT && LIN && sizeof(Acc) == 4 && NS > 1;
+  // linear-phase slots 1..7 by rotation of slot 0 (no per-slot fp64 / v_sin / v_cos)
+  constexpr bool ROT = LIN && sizeof(Acc) == 4 && NS > 1;
   float t[NS];
-  Acc al[NS], sn[NS], b1[NS], b2[NS], e1[NS], e2[NS];
+  Acc al[NS], sn[NS], b1[NS], b2[NS];
   int l[NS];
   bool valid[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     l[s] = l0 + 64 * s + lane;
     valid[s] = l[s] < T.len;
-    b1[s] = b2[s] = e1[s] = e2[s] = (Acc)0;
+    b1[s] = b2[s] = (Acc)0;
     if (ROT && s > 0) {  // slot s = slot 0 rotated by 64 s samples of a linear phase
       t[s] = TWO ? fmaf((float)l[s], T.xby, T.tc0) * T.rdx : 0.f;
       const float h = 0.5f * (float)al[0], s2 = 2.f * (float)sn[0];
@@ -223,25 +181,22 @@ __device__ __forceinline__ void run_slots(const SgWTask& T, bool staged, float* 
 #pragma unroll
   for (int s = 0; s < NS; ++s) tt[s] = (Acc)t[s];
   if (staged) {
-    clenshaw_any<NS, TWO, Acc>(la, ld, T.Rn, al, tt, b1, b2, e1, e2);
+    clenshaw_any<NS, TWO, Acc>(la, ld, T.Rn, al, tt, b1, b2);
   } else {  // rare (subharmonic epochs with many rows): 256-row chunks, top first
     for (int r0 = (T.Rn - 1) / SG_LDS_ROWS * SG_LDS_ROWS; r0 >= 0; r0 -= SG_LDS_ROWS) {
       const int n = T.Rn - r0 < SG_LDS_ROWS ? T.Rn - r0 : SG_LDS_ROWS;
       stage_rows<TWO>(la, ld, amps + T.a_off, amps + T.d_off, r0, n, lane);
-      clenshaw_any<NS, TWO, Acc>(la, ld, n, al, tt, b1, b2, e1, e2);
+      clenshaw_any<NS, TWO, Acc>(la, ld, n, al, tt, b1, b2);
     }
   }
   // a pass whose samples all exist and all land 1:1 in the syllable (most of a long
   // task's passes): no per-lane range tests in the epilogue
-#ifndef SG_FAST_EPI
-#define SG_FAST_EPI 1  // build knob
-#endif
   const int jp0 = T.j0 + l0;
-  if (SG_FAST_EPI && !ENV && l0 + 64 * NS <= T.len && jp0 >= T.dj0 && jp0 + 64 * NS <= T.dj1) {
+  if (!ENV && l0 + 64 * NS <= T.len && jp0 >= T.dj0 && jp0 + 64 * NS <= T.dj1) {
     WT* __restrict__ wp = W + T.w_off + jp0 + lane;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      const Acc yv = (TWO && !SG_FAMP ? fma((Acc)t[s], e1[s], b1[s]) : b1[s]) * sn[s];
+      const Acc yv = b1[s] * sn[s];
       wp[64 * s] = (WT)yv;
       tmax = fmaxf(tmax, (float)yv);
     }
@@ -249,7 +204,7 @@ __device__ __forceinline__ void run_slots(const SgWTask& T, bool staged, float* 
   }
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    const Acc yv = (TWO && !SG_FAMP ? fma((Acc)t[s], e1[s], b1[s]) : b1[s]) * sn[s];
+    const Acc yv = b1[s] * sn[s];
     const float y = (float)yv;
     const int j = T.j0 + l[s];
     if (valid[s]) W[T.w_off + j] = (WT)yv;
@@ -277,7 +232,7 @@ __device__ __forceinline__ float run_task(const SgWTask& T, float* __restrict__ 
   constexpr bool F32 = sizeof(Acc) == 4;
   // cos / sin of the linear phase advance over 64 k samples, k = 0..7 (wave-uniform)
   float rc[8], rs[8];
-  if (SG_ROT && LIN && F32) {
+  if (LIN && F32) {
     const double x = (double)(64 * (lane & 7)) * T.c1;
     const float f = (float)(x - rint(x));
     const int c = __builtin_bit_cast(int, __builtin_amdgcn_cosf(f)), sv = __builtin_bit_cast(int, __builtin_amdgcn_sinf(f));
@@ -290,10 +245,7 @@ __device__ __forceinline__ float run_task(const SgWTask& T, float* __restrict__ 
 #pragma unroll
     for (int k = 0; k < 8; ++k) rc[k] = rs[k] = 0.f;
   }
-#ifndef SG_F64_NS_MAX
-#define SG_F64_NS_MAX 2  // build knob: widest fp64 slot pass (tall tasks; fewer VGPRs, higher occupancy)
-#endif
-  if constexpr (!F32 && SG_F64_NS_MAX < 4) {
+  if constexpr (!F32) {  // fp64 passes of at most 2 slots (fewer VGPRs, higher occupancy; r02)
 #pragma unroll 1
     for (; T.len - l0 > 64; l0 += 128)
       run_slots<2, TWO, ENV, LIN, Acc, WT>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax, rc, rs);
@@ -301,7 +253,7 @@ __device__ __forceinline__ float run_task(const SgWTask& T, float* __restrict__ 
       run_slots<1, TWO, ENV, LIN, Acc, WT>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax, rc, rs);
     return tmax;
   }
-  if (F32 && (!TWO || SG_NS8_TWO) && SG_NS_MAX >= 8) {
+  if (F32 && !TWO) {
 #pragma unroll 1
     for (; T.len - l0 > 448; l0 += 512)
       run_slots<8, TWO, ENV, LIN, Acc, WT>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax, rc, rs);
@@ -318,28 +270,13 @@ __device__ __forceinline__ float run_task(const SgWTask& T, float* __restrict__ 
   return tmax;
 }
 
-#ifndef SG_ENV_NOINLINE
-#define SG_ENV_NOINLINE 0  // build knob: amplitude-envelope tasks (rare) out of line, a smaller hot kernel
-#endif
-#if SG_ENV_NOINLINE
-__device__ __noinline__ float run_env(const SgWTask& T, float* __restrict__ la, float* __restrict__ ld,
-                                      const float* __restrict__ amps, const SgSyllable* __restrict__ syls,
-                                      const double* __restrict__ cknots, float* __restrict__ W, int lane) {
-  return (T.flags & SG_TASK_CONST) ? run_task<false, true, false>(T, la, ld, amps, syls, cknots, W, lane)
-                                   : run_task<true, true, false>(T, la, ld, amps, syls, cknots, W, lane);
-}
-#endif
 // One task on its own wave pass (any length, envelope, linear or general phase)
 __device__ __forceinline__ float run_one(const SgWTask& T, float* __restrict__ la, float* __restrict__ ld,
                                          const float* __restrict__ amps, const SgSyllable* __restrict__ syls,
                                          const double* __restrict__ cknots, float* __restrict__ W, int lane) {
-#if SG_ENV_NOINLINE
-  if (T.flags & SG_TASK_ENV) return run_env(T, la, ld, amps, syls, cknots, W, lane);
-#else
   if (T.flags & SG_TASK_ENV)  // amplAnchors envelope: rare, kept out of the hot variants
     return (T.flags & SG_TASK_CONST) ? run_task<false, true, false>(T, la, ld, amps, syls, cknots, W, lane)
                                      : run_task<true, true, false>(T, la, ld, amps, syls, cknots, W, lane);
-#endif
   if (T.flags & SG_TASK_LIN)  // constant pitch over the phase segment
     return (T.flags & SG_TASK_CONST) ? run_task<false, false, true>(T, la, ld, amps, syls, cknots, W, lane)
                                      : run_task<true, false, true>(T, la, ld, amps, syls, cknots, W, lane);
@@ -357,11 +294,7 @@ template <bool TWO>
 __device__ __forceinline__ void run_pair(const SgWTask& P, const SgWTask& Q, float* __restrict__ la,
                                          float* __restrict__ ld, const float* __restrict__ amps,
                                          float* __restrict__ W, int lane, float& mp, float& mq) {
-#ifdef SG_DIAG_NOROWS
-  const int R = 0;
-#else
   const int R = P.Rn > Q.Rn ? P.Rn : Q.Rn;  // multiples of 16
-#endif
   for (int r = lane; r < R; r += 64) {
     *reinterpret_cast<float2*>(la + 2 * r) = make_float2(r < P.Rn ? amps[P.a_off + r] : 0.f, r < Q.Rn ? amps[Q.a_off + r] : 0.f);
     if (TWO)
@@ -374,24 +307,13 @@ __device__ __forceinline__ void run_pair(const SgWTask& P, const SgWTask& Q, flo
   sample_setup<TWO, false>(P, vp ? lane : 0, tp, alp, snp);
   sample_setup<TWO, false>(Q, vq ? lane : 0, tq, alq, snq);
   const f2 al{alp, alq}, tpq{tp, tq};
-  f2 b1{0.f, 0.f}, b2{0.f, 0.f}, e1{0.f, 0.f}, e2{0.f, 0.f};
-#define SG_PROW(a, d)                          \
-  {                                            \
-    if (TWO && SG_FAMP) {                      \
-      const f2 av = vfma(tpq, (d), (a));       \
-      const f2 b = vfma(al, b1, av - b2);      \
-      b2 = b1;                                 \
-      b1 = b;                                  \
-    } else {                                   \
-      const f2 b = vfma(al, b1, (a) - b2);     \
-      b2 = b1;                                 \
-      b1 = b;                                  \
-      if (TWO) {                               \
-        const f2 e = vfma(al, e1, (d) - e2);   \
-        e2 = e1;                               \
-        e1 = e;                                \
-      }                                        \
-    }                                          \
+  f2 b1{0.f, 0.f}, b2{0.f, 0.f};
+#define SG_PROW(a, d)                                   \
+  {                                                     \
+    const f2 av = TWO ? vfma(tpq, (d), (a)) : (a);      \
+    const f2 b = vfma(al, b1, av - b2);                 \
+    b2 = b1;                                            \
+    b1 = b;                                             \
   }
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll 1
@@ -406,8 +328,8 @@ __device__ __forceinline__ void run_pair(const SgWTask& P, const SgWTask& Q, flo
     SG_PROW((f2{A0.x, A0.y}), (f2{D0.x, D0.y}))
   }
 #undef SG_PROW
-  const float yp = (TWO && !SG_FAMP ? fmaf(tp, e1.x, b1.x) : b1.x) * snp;
-  const float yq = (TWO && !SG_FAMP ? fmaf(tq, e1.y, b1.y) : b1.y) * snq;
+  const float yp = b1.x * snp;
+  const float yq = b1.y * snq;
   const int jp = P.j0 + lane, jq = Q.j0 + lane;
   if (vp) W[P.w_off + jp] = yp;
   if (vq) W[Q.w_off + jq] = yq;
@@ -417,11 +339,8 @@ __device__ __forceinline__ void run_pair(const SgWTask& P, const SgWTask& Q, flo
 
 // Tasks of the fp32 class (listed in idx), one per wave. (A grid of resident waves
 // walking the list measured slower: r04f, C2 +14 %, C5 +22 %.)
-#ifndef SG_SB_WPE
-#define SG_SB_WPE 8  // build knob: > 0 caps sg_sine_bank's registers for that many waves per SIMD (8: 70 ->
-                     // 63 VGPRs, no spill; r04occ C5 1.964 -> 1.798 ms per launch, same RMS)
-#endif
-extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SG_SB_WPE > 0 ? SG_SB_WPE : 1))) void sg_sine_bank(
+// Registers capped for 8 waves per SIMD (70 -> 63 VGPRs, no spill; r04occ C5 1.964 -> 1.798 ms per launch).
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void sg_sine_bank(
     const int32_t* __restrict__ idx, int64_t n, const SgWTask* __restrict__ tasks, const float* __restrict__ amps,
     const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, float* __restrict__ W,
     float* __restrict__ taskmax) {
@@ -474,9 +393,6 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_pairs(
 // (3 FMAs per row and chain; samples in packed pairs). sin/cos of the half angle
 // come from fp32 Taylor polynomials on [-pi/2, pi/2] (relative error < 1e-9 before
 // rounding), not from v_sin / v_cos, whose error is absolute.
-#ifndef SG_TALL_F32
-#define SG_TALL_F32 0  // build knob: 1 = fp32 Reinsch chains (measured equal time on C5: the tall kernel is latency-bound)
-#endif
 
 __device__ __forceinline__ void rs_setup(const SgWTask& T, int l, bool two, float& t, float& u, float& sg, float& sn) {
   t = two ? fmaf((float)l, T.xby, T.tc0) * T.rdx : 0.f;
@@ -504,109 +420,6 @@ __device__ __forceinline__ void rs_setup(const SgWTask& T, int l, bool two, floa
   u = pos ? -4.f * s * s : 4.f * c * c;
 }
 
-#define SG_RROW(a, dd)                                             \
-  {                                                                \
-    _Pragma("unroll") for (int p = 0; p < NP; ++p) {               \
-      const f2 av = (TWO && SG_FAMP) ? vfma(tt[p], f2{(dd), (dd)}, f2{(a), (a)}) : f2{(a), (a)}; \
-      f2 q = vfma(sg[p], d[p], av);                                \
-      q = vfma(u[p], b[p], q);                                     \
-      b[p] = vfma(sg[p], b[p], q);                                 \
-      d[p] = q;                                                    \
-      if (TWO && !SG_FAMP) {                                       \
-        f2 r = vfma(sg[p], g[p], f2{(dd), (dd)});                  \
-        r = vfma(u[p], e[p], r);                                   \
-        e[p] = vfma(sg[p], e[p], r);                               \
-        g[p] = r;                                                  \
-      }                                                            \
-    }                                                              \
-  }
-// rows n-1 .. 0 (n a multiple of 4) of the staged chunk, continuing (b, d) and (e, g)
-template <int NP, bool TWO>
-__device__ __forceinline__ void reinsch_lds(const float* __restrict__ la, const float* __restrict__ ld, int n,
-                                            const f2 (&u)[NP], const f2 (&sg)[NP], const f2 (&tt)[NP], f2 (&b)[NP],
-                                            f2 (&d)[NP], f2 (&e)[NP], f2 (&g)[NP]) {
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll 1
-  for (int r = n - 4; r >= 0; r -= 4) {
-    const float4 A4 = *reinterpret_cast<const float4*>(la + r);
-    const float4 D4 = TWO ? *reinterpret_cast<const float4*>(ld + r) : z4;
-    SG_RROW(A4.w, D4.w)
-    SG_RROW(A4.z, D4.z)
-    SG_RROW(A4.y, D4.y)
-    SG_RROW(A4.x, D4.x)
-  }
-}
-#undef SG_RROW
-
-// NP packed pairs per lane: pair p holds samples l0 + 128 p + lane and l0 + 128 p + 64 + lane
-template <int NP, bool TWO, bool ENV>
-__device__ __forceinline__ void run_pairs_rs(const SgWTask& T, bool staged, float* __restrict__ la,
-                                             float* __restrict__ ld, const float* __restrict__ amps,
-                                             const SgSyllable* __restrict__ syls, const double* __restrict__ cknots,
-                                             float* __restrict__ W, int l0, int lane, float& tmax) {
-  constexpr int NS = 2 * NP;
-  float t[NS], uu[NS], ss[NS], sn[NS];
-  int l[NS];
-  bool valid[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    l[s] = l0 + 64 * s + lane;
-    valid[s] = l[s] < T.len;
-    rs_setup(T, valid[s] ? l[s] : 0, TWO, t[s], uu[s], ss[s], sn[s]);
-  }
-  f2 u[NP], sg[NP], t2[NP], b[NP], d[NP], e[NP], g[NP];
-#pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    u[p] = f2{uu[2 * p], uu[2 * p + 1]};
-    sg[p] = f2{ss[2 * p], ss[2 * p + 1]};
-    t2[p] = f2{t[2 * p], t[2 * p + 1]};
-    b[p] = d[p] = e[p] = g[p] = f2{0.f, 0.f};
-  }
-  if (staged) {
-    reinsch_lds<NP, TWO>(la, ld, T.Rn, u, sg, t2, b, d, e, g);
-  } else {  // more than SG_LDS_ROWS rows: 256-row chunks, top first
-    for (int r0 = (T.Rn - 1) / SG_LDS_ROWS * SG_LDS_ROWS; r0 >= 0; r0 -= SG_LDS_ROWS) {
-      const int n = T.Rn - r0 < SG_LDS_ROWS ? T.Rn - r0 : SG_LDS_ROWS;
-      stage_rows<TWO>(la, ld, amps + T.a_off, amps + T.d_off, r0, n, lane);
-      reinsch_lds<NP, TWO>(la, ld, n, u, sg, t2, b, d, e, g);
-    }
-  }
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const float bs = (s & 1) ? b[s >> 1].y : b[s >> 1].x;
-    const float es = (s & 1) ? e[s >> 1].y : e[s >> 1].x;
-    const float y = (TWO && !SG_FAMP ? fmaf(t[s], es, bs) : bs) * sn[s];
-    const int j = T.j0 + l[s];
-    if (valid[s]) W[T.w_off + j] = y;
-    const bool in = valid[s] && j >= T.dj0 && j < T.dj1;
-    if (!ENV) {
-      tmax = in ? fmaxf(tmax, y) : tmax;
-    } else if (in) {
-      const SgSyllable& sy = syls[T.syl];
-      tmax = fmaxf(tmax, (float)((double)y * contour_at(sy.env, cknots, sy.L, T.dk0 + j)));
-    }
-  }
-}
-
-template <bool TWO, bool ENV>
-__device__ __forceinline__ float run_task_rs(const SgWTask& T, float* __restrict__ la, float* __restrict__ ld,
-                                             const float* __restrict__ amps, const SgSyllable* __restrict__ syls,
-                                             const double* __restrict__ cknots, float* __restrict__ W, int lane) {
-  const bool staged = T.Rn <= SG_LDS_ROWS;
-  if (staged) stage_rows<TWO>(la, ld, amps + T.a_off, amps + T.d_off, 0, T.Rn, lane);
-  float tmax = 0.f;
-  int l0 = 0;
-#pragma unroll 1
-  for (; T.len - l0 > 256; l0 += 512)
-    run_pairs_rs<4, TWO, ENV>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax);
-  if (T.len - l0 > 128) {
-    run_pairs_rs<2, TWO, ENV>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax);
-    l0 += 256;
-  }
-  if (l0 < T.len) run_pairs_rs<1, TWO, ENV>(T, staged, la, ld, amps, syls, cknots, W, l0, lane, tmax);
-  return tmax;
-}
-
 // Two tall tasks of <= 64 samples in one wave (as run_pair: task P in the low,
 // Q in the high half of packed pairs), Reinsch chains, rows staged interleaved
 // in 128-row chunks from the top.
@@ -620,20 +433,14 @@ __device__ __forceinline__ void run_pair_rs(const SgWTask& P, const SgWTask& Q, 
   rs_setup(P, vp ? lane : 0, TWO, tp, up, sgp, snp);
   rs_setup(Q, vq ? lane : 0, TWO, tq, uq, sgq, snq);
   const f2 u{up, uq}, sg{sgp, sgq}, tpq{tp, tq};
-  f2 b{0.f, 0.f}, d{0.f, 0.f}, e{0.f, 0.f}, g{0.f, 0.f};
-#define SG_RPROW(a, dd)                                           \
-  {                                                               \
-    const f2 av = (TWO && SG_FAMP) ? vfma(tpq, (dd), (a)) : (a);  \
-    f2 q = vfma(sg, d, av);                                       \
-    q = vfma(u, b, q);                                            \
-    b = vfma(sg, b, q);                                           \
-    d = q;                                                        \
-    if (TWO && !SG_FAMP) {                                        \
-      f2 w = vfma(sg, g, (dd));                                   \
-      w = vfma(u, e, w);                                          \
-      e = vfma(sg, e, w);                                         \
-      g = w;                                                      \
-    }                                                             \
+  f2 b{0.f, 0.f}, d{0.f, 0.f};
+#define SG_RPROW(a, dd)                                  \
+  {                                                      \
+    const f2 av = TWO ? vfma(tpq, (dd), (a)) : (a);      \
+    f2 q = vfma(sg, d, av);                              \
+    q = vfma(u, b, q);                                   \
+    b = vfma(sg, b, q);                                  \
+    d = q;                                               \
   }
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   constexpr int CH = SG_LDS_ROWS / 2;  // rows per interleaved chunk
@@ -662,8 +469,8 @@ __device__ __forceinline__ void run_pair_rs(const SgWTask& P, const SgWTask& Q, 
     }
   }
 #undef SG_RPROW
-  const float yp = (TWO && !SG_FAMP ? fmaf(tp, e.x, b.x) : b.x) * snp;
-  const float yq = (TWO && !SG_FAMP ? fmaf(tq, e.y, b.y) : b.y) * snq;
+  const float yp = b.x * snp;
+  const float yq = b.y * snq;
   const int jp = P.j0 + lane, jq = Q.j0 + lane;
   if (vp) W[P.w_off + jp] = yp;
   if (vq) W[Q.w_off + jq] = yq;
@@ -674,29 +481,18 @@ __device__ __forceinline__ void run_pair_rs(const SgWTask& P, const SgWTask& Q, 
 __device__ __forceinline__ float run_one_tall(const SgWTask& T, float* __restrict__ la, float* __restrict__ ld,
                                               const float* __restrict__ amps, const SgSyllable* __restrict__ syls,
                                               const double* __restrict__ cknots, float* __restrict__ W, int lane) {
-#if SG_TALL_F32
-  if (T.flags & SG_TASK_ENV)
-    return (T.flags & SG_TASK_CONST) ? run_task_rs<false, true>(T, la, ld, amps, syls, cknots, W, lane)
-                                     : run_task_rs<true, true>(T, la, ld, amps, syls, cknots, W, lane);
-  return (T.flags & SG_TASK_CONST) ? run_task_rs<false, false>(T, la, ld, amps, syls, cknots, W, lane)
-                                   : run_task_rs<true, false>(T, la, ld, amps, syls, cknots, W, lane);
-#else
   if (T.flags & SG_TASK_ENV)
     return (T.flags & SG_TASK_CONST) ? run_task<false, true, false, double>(T, la, ld, amps, syls, cknots, W, lane)
                                      : run_task<true, true, false, double>(T, la, ld, amps, syls, cknots, W, lane);
   return (T.flags & SG_TASK_CONST) ? run_task<false, false, false, double>(T, la, ld, amps, syls, cknots, W, lane)
                                    : run_task<true, false, false, double>(T, la, ld, amps, syls, cknots, W, lane);
-#endif
 }
 
 // The tasks with more than SG_ROWS_F32 rows (listed in idx), one task per wave:
-// fp32 Reinsch chains (SG_TALL_F32), else fp64 sincospi and fp64 Clenshaw chains.
-// Tall tasks (listed in idx): SG_TALL_PAIR lists the short ones (<= 64 samples, no
-// envelope) separately for sg_sine_bank_tall_pairs; these run one per wave.
-#ifndef SG_TALL_WPE
-#define SG_TALL_WPE 0  // build knob: > 0 caps sg_sine_bank_tall's registers for that many waves per SIMD
-#endif
-extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SG_TALL_WPE > 0 ? SG_TALL_WPE : 1))) void sg_sine_bank_tall(
+// fp64 sincospi and fp64 Clenshaw chains (fp32 Reinsch chains measured equal time
+// on C5: the kernel is latency-bound). The short ones (<= 64 samples, no envelope)
+// are listed separately for sg_sine_bank_tall_pairs.
+extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_tall(
     const int32_t* __restrict__ idx, int64_t n, const SgWTask* __restrict__ tasks, const float* __restrict__ amps,
     const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, float* __restrict__ W,
     float* __restrict__ taskmax) {
@@ -757,10 +553,7 @@ __device__ __forceinline__ float run_one_hp(const SgWTask& T, float* __restrict_
            : run_task<true, false, false, double, double>(T, la, ld, amps, syls, cknots, W, lane);
 }
 
-#ifndef SG_HP_WPE
-#define SG_HP_WPE 0  // build knob: > 0 caps sg_sine_bank_hp's registers for that many waves per SIMD
-#endif
-extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SG_HP_WPE > 0 ? SG_HP_WPE : 1))) void sg_sine_bank_hp(
+extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_hp(
     const int32_t* __restrict__ idx, int64_t n, const SgWTask* __restrict__ tasks, const float* __restrict__ amps,
     const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, double* __restrict__ W64,
     float* __restrict__ taskmax) {
@@ -796,23 +589,13 @@ __device__ __forceinline__ V fade_at(int lf, int64_t L, int64_t k) {
 // ~log2 N eps of sum |A_r|), twiddles from sincospif. Then each interval's cubic
 // Hermite coefficients. LDS (bytes from 0): the float4 table [16 N), aliased by the
 // FFT's two float2 buffers during the transform, and the twiddles [16 N, 18 N).
-#ifndef SG_TAB_THREADS_N
-#define SG_TAB_THREADS_N 512  // build knob: threads per sg_sine_bank_tab workgroup
-#endif
-constexpr int SG_TAB_THREADS = SG_TAB_THREADS_N;
-#ifndef SG_TAB_DIAG
-#define SG_TAB_DIAG 0
-#endif
+constexpr int SG_TAB_THREADS = 512;  // threads per sg_sine_bank_tab workgroup
 __device__ __forceinline__ void tab_build(float4* __restrict__ lt, const float* __restrict__ la, int Rn, int logn) {
   const int N = 1 << logn;
   float2* X = reinterpret_cast<float2*>(lt);
   float2* Y = X + N;
   float2* tw = X + 2 * N;
   const float pin = 3.14159265358979f / (float)N;
-#ifndef SG_TAB_SKIP
-#define SG_TAB_SKIP 0  // diagnostic timing builds only: bit 0 no twiddles, 1 no FFT stages, 2 no coefficients
-#endif
-  if (!(SG_TAB_SKIP & 1))
   for (int t = threadIdx.x; t < N / 4; t += SG_TAB_THREADS) {  // the radix-4 stages' w^1
     float sv, cv;
     sincospif(2.f * (float)t / (float)N, &sv, &cv);
@@ -829,7 +612,7 @@ __device__ __forceinline__ void tab_build(float4* __restrict__ lt, const float* 
   // stages; stage with sub-transform size Ns: v_r = X[j + r N / R] w^r,
   // w = e^{2 pi i k / (R Ns)}, k = j mod Ns, into Y[(j - k) R + k + r Ns]
   int Ns = 1;
-  if ((logn & 1) && !(SG_TAB_SKIP & 2)) {
+  if (logn & 1) {
     for (int j = threadIdx.x; j < N / 2; j += SG_TAB_THREADS) {
       const float2 a = X[j], b = X[j + N / 2];
       Y[2 * j] = make_float2(a.x + b.x, a.y + b.y);
@@ -842,7 +625,7 @@ __device__ __forceinline__ void tab_build(float4* __restrict__ lt, const float* 
     Ns = 2;
   }
   auto cmul = [](float2 a, float2 b) { return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); };
-  for (; Ns < ((SG_TAB_SKIP & 2) ? 0 : N); Ns <<= 2) {
+  for (; Ns < N; Ns <<= 2) {
     const int sh = logn - 2 - __builtin_ctz(Ns);  // w = tw[k N / (4 Ns)]
     for (int j = threadIdx.x; j < N / 4; j += SG_TAB_THREADS) {
       const int k = j & (Ns - 1);
@@ -864,7 +647,6 @@ __device__ __forceinline__ void tab_build(float4* __restrict__ lt, const float* 
   }
   // X: (S_k, h S'_k). Intervals k = tid + 512 q into registers, then the table over the buffers
   constexpr int QM = (1 << SG_TAB_LOGN_MAX) / SG_TAB_THREADS;
-  if (SG_TAB_SKIP & 4) return;
   float4 c[QM];
 #pragma unroll
   for (int q = 0; q < QM; ++q) {
@@ -894,20 +676,12 @@ __device__ __forceinline__ void tab_blocks(const float4* __restrict__ lt, int lo
 #pragma unroll
   for (int s = 0; s < NB; ++s) {
     xs[s] = x + (uint32_t)s * dx;
-#if SG_TAB_DIAG == 3  // diagnostic timing build only: no table reads
-    c[s] = make_float4((float)xs[s], 0.5f, 0.25f, 0.125f);
-#else
     c[s] = lt[xs[s] >> (32 - logn)];
-#endif
   }
 #pragma unroll
   for (int s = 0; s < NB; ++s) {
     const float f = (float)(xs[s] << logn) * 2.3283064365386963e-10f;  // [0, 1]
     const float y = fmaf(f, fmaf(f, fmaf(f, c[s].w, c[s].z), c[s].y), c[s].x);
-#if SG_TAB_DIAG == 4  // diagnostic timing build only: no stores
-    tmax = fmaxf(tmax, y);
-    continue;
-#endif
     if (FULL) {
       w[64 * s] = y;
       tmax = fmaxf(tmax, y);
@@ -1015,16 +789,11 @@ extern "C" __global__ __launch_bounds__(SG_TAB_THREADS) __attribute__((amdgpu_wa
     ts[q] = TabTask{T.c0, T.c1, direct ? out0 + T.dk0 : T.w_off, T.mbase, T.j0, T.len, T.dj0, T.dj1, (int32_t)T.dk0};
   }
   __syncthreads();
-#if SG_TAB_DIAG != 2  // diagnostic timing build: 2 = no table build
   tab_build(lt, la, J.Rn, logn);
   __syncthreads();
-#endif
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   constexpr double TWO32 = 4294967296.0;
-#if SG_TAB_DIAG == 1  // diagnostic timing build: no sampling
-  if (J.n >= 0) return;
-#endif
   if (direct) {
     float wm = 0.f;
     for (int q = wave; q < J.n; q += SG_TAB_THREADS / 64) {
@@ -1139,27 +908,6 @@ extern "C" __global__ __launch_bounds__(256) void sg_piece_max_hp(
 // destination moves float4s (4 consecutive samples per thread); otherwise
 // each thread takes samples k0 + 256 e + tid.
 
-#ifndef SG_COPY_NT
-#define SG_COPY_NT 0  // build knob: non-temporal W loads (last use) and output stores
-#endif
-__device__ __forceinline__ float4 ld_last(const float4* p) {
-#if SG_COPY_NT
-  typedef float v4 __attribute__((ext_vector_type(4)));
-  const v4 r = __builtin_nontemporal_load(reinterpret_cast<const v4*>(p));
-  return make_float4(r.x, r.y, r.z, r.w);
-#else
-  return *p;
-#endif
-}
-__device__ __forceinline__ void st_stream(float4* p, float4 v) {
-#if SG_COPY_NT
-  typedef float v4 __attribute__((ext_vector_type(4)));
-  __builtin_nontemporal_store(v4{v.x, v.y, v.z, v.w}, reinterpret_cast<v4*>(p));
-#else
-  *p = v;
-#endif
-}
-
 // Fast path of the finalize (tiles from the planner's split, SgCopyTile):
 // one wavefront per tile of <= SG_COPY_TILE_MAX samples; aligned tiles keep up to
 // sixteen float4 loads per lane in flight before any store; one dependent descriptor level
@@ -1180,7 +928,7 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_copy(const SgCopyTile*
     float4 v[E];
 #pragma unroll
     for (int e = 0; e < E; ++e)
-      if (256 * e + 4 * lane < T.n) v[e] = ld_last(reinterpret_cast<const float4*>(src + 256 * e + 4 * lane));
+      if (256 * e + 4 * lane < T.n) v[e] = *reinterpret_cast<const float4*>(src + 256 * e + 4 * lane);
     const bool ramp = T.fade >= 2 && (T.k0 < T.fade || T.k0 + T.n > T.L - T.fade);
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -1191,7 +939,7 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_copy(const SgCopyTile*
         v[e].x *= fade_at(T.fade, T.L, k); v[e].y *= fade_at(T.fade, T.L, k + 1);
         v[e].z *= fade_at(T.fade, T.L, k + 2); v[e].w *= fade_at(T.fade, T.L, k + 3);
       }
-      st_stream(reinterpret_cast<float4*>(dst + 256 * e + 4 * lane), v[e]);
+      *reinterpret_cast<float4*>(dst + 256 * e + 4 * lane) = v[e];
     }
   } else {  // misaligned or short runs, zero pieces
     const bool zero = T.flags & SG_COPY_ZERO;
@@ -1205,49 +953,14 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_copy(const SgCopyTile*
 
 // General path: the tiles the planner did not give to sg_harm_copy (crossfade
 // pieces, amplitude envelope, drift, misaligned slots).
-#ifndef SG_FIN_LDS_ENV
-#define SG_FIN_LDS_ENV 2  // build knob: envelope spline by interval cursors (2), also from LDS-staged knots (1; the
-                          // per-tile barriers cost more than they save: 5.98 -> 6.27 ms on C5), bisection per sample (0)
-#endif
-#ifndef SG_FIN_WAVE_TILE
-#define SG_FIN_WAVE_TILE 0  // build knob: one wave per 1024-sample tile (its 4 quarters in turn)
-#endif
-#ifndef SG_FIN_DIRECT
-#define SG_FIN_DIRECT 0  // build knob: whole-tile path for tiles inside one direct piece (16 samples per lane;
-                         // measured 5.93 -> 7.82 ms on C5: 108 VGPRs and per-sample fp64 drift division)
-#endif
-static_assert(!((SG_FIN_WAVE_TILE || SG_FIN_DIRECT) && SG_FIN_LDS_ENV == 1), "LDS envelope staging needs all waves on one tile");
-#ifndef SG_FIN_DRIFT_LDS
-#define SG_FIN_DRIFT_LDS 1  // build knob: drift interval by index from per-wave LDS (x, y, slope) rows
-#endif
-constexpr int SG_FIN_KMAX = 32;  // knots of an LDS-staged envelope
 // V = double: an fp64 syllable (W64 -> fh; out_buf is fh, fs unused)
 template <typename V = float>
 __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece* __restrict__ pieces,
                                               const SgSyllable* __restrict__ syls, const double* __restrict__ cknots,
                                               const V* __restrict__ W, const float* __restrict__ maxes,
-                                              V* __restrict__ out_buf, V* __restrict__ fs, double* lenv,
+                                              V* __restrict__ out_buf, V* __restrict__ fs,
                                               int wv, double* lkw) {
   const SgSyllable& sy = syls[tl.syl];
-#if SG_FIN_LDS_ENV == 1
-  // the syllable's envelope knots (x, y, b, c, d) in LDS for this tile (all waves
-  // of the workgroup work on the same tile: sync before overwriting, sync after)
-  const bool envl = sy.env.kind == 3 && sy.env.nk <= SG_FIN_KMAX;
-  __syncthreads();
-  if (envl)
-    for (int j = threadIdx.x; j < 5 * sy.env.nk; j += 256) lenv[j] = cknots[sy.env.k_off + j];
-  __syncthreads();
-#elif SG_FIN_LDS_ENV == 3
-  // the same per wave (its own copy, no workgroup barrier)
-  const bool envl = sy.env.kind == 3 && sy.env.nk <= SG_FIN_KMAX;
-  if (envl) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // earlier reads of the slot come first
-    __builtin_amdgcn_wave_barrier();
-    for (int j = threadIdx.x & 63; j < 5 * sy.env.nk; j += 64) lenv[j] = cknots[sy.env.k_off + j];
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
-#endif
   int ecur = -1;  // a lane's samples increase: the envelope interval is found by stepping
   constexpr bool F64 = sizeof(V) == 8;
   V* __restrict__ out = (!F64 && sy.dst_fs) ? fs : out_buf;
@@ -1287,7 +1000,6 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
     }
     // every sample of the chunk lies in intervals d0 .. d0 + KW - 2
     local_knots = d0 + KW - 1 >= dr.nk - 1 || u_at(c1 - 1) < xs[KW - 1];
-#if SG_FIN_DRIFT_LDS
     // per interval (x_t, y_t, slope_t) in the wave's LDS slot: a lane then reads its
     // interval by index instead of selecting four doubles through KW - 2 compares,
     // and multiplies by the slope instead of dividing (a few fp64 ulps from approx()'s
@@ -1304,7 +1016,6 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#endif
   }
   int p = pu, di = d0;
   V res[4];  // every load of the chunk before its stores
@@ -1323,18 +1034,7 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
       x = pc.nterms == 0 ? (V)0 : piece_value(pc, W, k - pc.start);
     }
     if (sy.env.kind != 0) {
-#if SG_FIN_LDS_ENV == 1 || SG_FIN_LDS_ENV == 3
-      if (envl) {
-        SgContour cl = sy.env;
-        cl.k_off = 0;
-        x = (V)((double)x * sgd::contour_at_cursor(cl, lenv, sy.L, k, ecur));
-      } else
-        x = (V)((double)x * sgd::contour_at_cursor(sy.env, cknots, sy.L, k, ecur));
-#elif SG_FIN_LDS_ENV == 2
       x = (V)((double)x * sgd::contour_at_cursor(sy.env, cknots, sy.L, k, ecur));
-#else
-      x = (V)((double)x * contour_at(sy.env, cknots, sy.L, k));
-#endif
     }
     x *= inv_max;
     if (sy.fade >= 2) x *= fade_at<V>(sy.fade, sy.L, k);
@@ -1342,19 +1042,11 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
       double dm;
       if (local_knots) {  // linear_at's interval and arithmetic, knots from registers
         const double u = u_at(k);
-#if SG_FIN_DRIFT_LDS
         int t = 0;  // the conditions hold for a prefix of t: their count is the interval
 #pragma unroll
         for (int q = 1; q < KW - 1; ++q) t += (d0 + q <= dr.nk - 2 && xs[q] <= u) ? 1 : 0;
         const double xi = lkw[3 * t], yi = lkw[3 * t + 1], sl = lkw[3 * t + 2];
         dm = u == xi ? yi : fma(sl, u - xi, yi);
-#else
-        double xi = xs[0], xj = xs[1], yi = ys[0], yj = ys[1];
-#pragma unroll
-        for (int t = 1; t < KW - 1; ++t)
-          if (d0 + t <= dr.nk - 2 && xs[t] <= u) { xi = xs[t]; xj = xs[t + 1]; yi = ys[t]; yj = ys[t + 1]; }
-        dm = u == xj ? yj : (u == xi ? yi : yi + (yj - yi) * ((u - xi) / (xj - xi)));
-#endif
       } else {
         dm = sgd::linear_at_cursor(dr, cknots, sy.L, k, di);
       }
@@ -1373,105 +1065,23 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
 
 // SG_FIN_TILES consecutive 1024-sample tiles per workgroup: the descriptor
 // chain (tile -> syllable -> piece, drift knots) of a syllable's next tile hits cache
-#ifndef SG_FIN_TILES_N
-#define SG_FIN_TILES_N 4  // build knob
-#endif
-constexpr int SG_FIN_TILES = SG_FIN_TILES_N;
-// A tile lying inside ONE direct piece (the epoch waveform itself, no crossfade
-// terms), taken by one wave: lane l loads samples k0 + 256 j + 4 l + e (j, e < 4),
-// all sixteen before any store (the general path keeps four per lane in flight
-// and is memory-latency-bound), then envelope, 1/max, fades and drift per
-// sample in the general path's order (drift by the cursor form of approx()).
-// Returns false (nothing written) when the tile is not of that kind.
-__device__ __forceinline__ bool finalize_tile_direct(const SgSylTile& tl, const SgPiece* __restrict__ pieces,
-                                                     const SgSyllable* __restrict__ syls,
-                                                     const double* __restrict__ cknots, const float* __restrict__ W,
-                                                     const float* __restrict__ maxes, float* __restrict__ out_buf,
-                                                     float* __restrict__ fs) {
-  const SgSyllable& sy = syls[tl.syl];
-  const int64_t tile_end = tl.k0 + 1024 < sy.L ? tl.k0 + 1024 : sy.L;
-  const int pu = tl.wpiece[0];
-  const int pend = sy.piece0 + sy.npiece;
-  const SgPiece& pc = pieces[pu];
-  if (pc.nterms >= 0 || pc.start > tl.k0 || (pu + 1 < pend && pieces[pu + 1].start < tile_end)) return false;
-  const int lane = threadIdx.x & 63;
-  const float* __restrict__ src = W + (pc.t[0].src - pc.start);  // sample k -> src[k]
-  float* __restrict__ out = (sy.dst_fs ? fs : out_buf) + sy.out_off;
-  float x[16];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int64_t k = tl.k0 + 256 * j + 4 * lane + e;
-      x[4 * j + e] = src[k < tile_end ? k : tl.k0];
-    }
-  const float inv_max = 1.f / maxes[sy.max_slot];
-  const SgLinear dr = sy.drift;
-  int ecur = -1, di = tl.wdrift[0];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int64_t k = tl.k0 + 256 * j + 4 * lane + e;
-      float v = x[4 * j + e];
-      if (sy.env.kind != 0) v = (float)((double)v * sgd::contour_at_cursor(sy.env, cknots, sy.L, k, ecur));
-      v *= inv_max;
-      if (sy.fade >= 2) v *= fade_at(sy.fade, sy.L, k);
-      if (dr.nk > 1) v = (float)((double)v * sgd::linear_at_cursor(dr, cknots, sy.L, k, di));
-      else if (dr.nk == 1) v = (float)((double)v * cknots[dr.k_off + 1]);
-      x[4 * j + e] = v;
-    }
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int64_t k = tl.k0 + 256 * j + 4 * lane + e;
-      if (k < tile_end) out[k] = x[4 * j + e];
-    }
-  return true;
-}
-
-#ifndef SG_FIN_WPE
-#define SG_FIN_WPE 8  // build knob: > 0 caps sg_harm_finalize's registers for that many waves per SIMD (8: SGPRs
-                      // 106 -> 78, 7 -> 8 waves; measured 3.75 -> 3.40 ms per C5 launch, same RMS; 0: none)
-#endif
-#if SG_FIN_WPE
-#define SG_FIN_ATTR __attribute__((amdgpu_waves_per_eu(SG_FIN_WPE)))
-#else
-#define SG_FIN_ATTR
-#endif
-extern "C" __global__ __launch_bounds__(256) SG_FIN_ATTR void sg_harm_finalize(
+constexpr int SG_FIN_TILES = 4;  // r02: 2 / 8 neutral; r04: 1 / 2 neutral
+// Registers capped for 8 waves per SIMD (SGPRs 106 -> 78, 7 -> 8 waves; r04: 3.75 -> 3.40 ms per C5 launch).
+// (A whole-tile path for tiles inside one direct piece measured 5.93 -> 7.82 ms on C5;
+// one wave per tile, LDS-staged envelope knots: no better.)
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void sg_harm_finalize(
     const SgSylTile* __restrict__ stiles, int64_t ntiles, const SgPiece* __restrict__ pieces,
     const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, const float* __restrict__ W,
     const float* __restrict__ maxes, float* __restrict__ out_buf, float* __restrict__ fs) {
-#if SG_FIN_LDS_ENV == 3
-  __shared__ double lenv_w[4][5 * SG_FIN_KMAX];  // per wave
-  double* lenv = lenv_w[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
-#else
-  __shared__ double lenv[5 * SG_FIN_KMAX];
-#endif
   __shared__ double lk[4][3 * 8];  // per wave: drift intervals (x, y, slope)
   double* lkw = lk[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
-#if SG_FIN_WAVE_TILE || SG_FIN_DIRECT
-  // wave w takes tile 4 b + w whole: the direct path, else its quarters in turn
-  const int64_t t = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (t >= ntiles) return;
-  const SgSylTile tl = stiles[t];
-  if (SG_FIN_DIRECT && finalize_tile_direct(tl, pieces, syls, cknots, W, maxes, out_buf, fs)) return;
-#pragma unroll 1
-  for (int q = 0; q < 4; ++q) finalize_tile(tl, pieces, syls, cknots, W, maxes, out_buf, fs, lenv, q, lkw);
-#else
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#ifndef SG_FIN_UNROLL
-#define SG_FIN_UNROLL 1  // build knob: tiles of a workgroup unrolled (their descriptor chains may overlap)
-#endif
-#pragma unroll SG_FIN_UNROLL
+#pragma unroll 1
   for (int i = 0; i < SG_FIN_TILES; ++i) {
     const int64_t t = (int64_t)blockIdx.x * SG_FIN_TILES + i;
     if (t >= ntiles) break;
-    finalize_tile(stiles[t], pieces, syls, cknots, W, maxes, out_buf, fs, lenv, wv, lkw);
+    finalize_tile(stiles[t], pieces, syls, cknots, W, maxes, out_buf, fs, wv, lkw);
   }
-#endif
 }
 
 // fp64 syllables (SgSyllable::hp): W64 -> fh, the general path in fp64
@@ -1479,12 +1089,11 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize_hp(
     const SgSylTile* __restrict__ stiles, int64_t ntiles, const SgPiece* __restrict__ pieces,
     const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, const double* __restrict__ W64,
     const float* __restrict__ maxes, double* __restrict__ fh) {
-  __shared__ double lenv[5 * SG_FIN_KMAX];
   __shared__ double lk[4][3 * 8];
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t t = blockIdx.x;
   if (t >= ntiles) return;
-  finalize_tile<double>(stiles[t], pieces, syls, cknots, W64, maxes, fh, fh, lenv, wv, lk[wv]);
+  finalize_tile<double>(stiles[t], pieces, syls, cknots, W64, maxes, fh, fh, wv, lk[wv]);
 }
 
 // ---------------------------------------------------------------- launchers
@@ -1596,7 +1205,7 @@ void launch_harm_finalize_hp(const DevicePlan& D, int64_t n_stiles, hipStream_t 
 }
 void launch_harm_finalize(const DevicePlan& D, int64_t f0, int64_t n_stiles, float* out, hipStream_t s) {
   if (n_stiles <= 0) return;
-  const int64_t per_block = (SG_FIN_WAVE_TILE || SG_FIN_DIRECT) ? 4 : SG_FIN_TILES;
+  const int64_t per_block = SG_FIN_TILES;
   hipLaunchKernelGGL(sg_harm_finalize, dim3((unsigned)((n_stiles + per_block - 1) / per_block)), dim3(256), 0, s,
                      D.syl_tiles + f0, n_stiles, D.pieces, D.syls,
                      D.cknots, D.W, D.maxes, out, D.fs);

@@ -660,12 +660,12 @@ static bool fry_spec(const AmpSpec& S, int64_t H, int64_t g0, int64_t g1, int64_
 }
 
 // 1: every call takes the host-built path (tests compare the two); default
-// from SG_AMP_HOST, changed by sg_set_amp_policy
+// 0, changed by sg_set_amp_policy
 static std::atomic<int> g_amp_host{-1};
 static bool amp_device_enabled() {
   int h = g_amp_host.load();
   if (h < 0) {
-    h = std::getenv("SG_AMP_HOST") != nullptr ? 1 : 0;
+    h = 0;  // sg_set_amp_policy(1) forces the host-built matrices (tests)
     g_amp_host.store(h);
   }
   return h == 0;
@@ -965,15 +965,8 @@ static void cross_fade(Chain& A, const HostEpoch& W, int64_t e, double sr, doubl
 }
 
 // ----------------------------------------------------------- planner
-// samples per sine-bank task (SG_TASK_MAX; SG_TASK_MAX env override for experiments)
-static int64_t task_max() {
-  static const int64_t v = [] {
-    const char* e = std::getenv("SG_TASK_MAX");
-    const long x = e ? std::atol(e) : 0;
-    return (int64_t)(x >= 64 ? x : SG_TASK_MAX);
-  }();
-  return v;
-}
+// samples per sine-bank task
+static constexpr int64_t task_max() { return SG_TASK_MAX; }
 
 // segment b continues segment a's line: both linear, same slope, and b's
 // offset equals a's line at b's start (to rounding)

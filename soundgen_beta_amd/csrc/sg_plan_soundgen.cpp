@@ -361,8 +361,7 @@ std::atomic<double> g_hp_rho{-1.0};
 int hp_mode() {
   int m = g_hp_mode.load();
   if (m < 0) {
-    const char* e = std::getenv("SG_HP");
-    m = e ? std::atoi(e) : 1;
+    m = 1;  // sg_set_fp64_policy changes it
     g_hp_mode.store(m);
   }
   return m;

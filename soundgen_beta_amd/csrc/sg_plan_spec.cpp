@@ -51,14 +51,13 @@ std::shared_ptr<const vec> trig_table(int kind, int n, Make&& make) {
 constexpr int kFftSlots = 8192;  // complex points per FFT workgroup (sg_fft.hip SG_FFT_SLOTS)
 }  // namespace
 // 0: noise uniforms copied into fl per item by the planner (the pre-round-3
-// path); 1 (default; SG_UGATHER=0 in the environment turns it off) gathered on
+// path); 1 (default) gathered on
 // the device at upload. sg_set_uniform_gather changes it (tests compare the two).
 std::atomic<int> g_ugather{-1};
 bool ugather_on() {
   int v = g_ugather.load();
   if (v < 0) {
-    const char* e = std::getenv("SG_UGATHER");
-    v = (e && std::atoi(e) == 0) ? 0 : 1;
+    v = 1;
     g_ugather.store(v);
   }
   return v == 1;

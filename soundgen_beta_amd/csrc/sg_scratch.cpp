@@ -149,8 +149,7 @@ void* bulk_alloc(size_t bytes) {
   }
   void* q = std::aligned_alloc(HUGE_PAGE, sz);
   if (!q) throw std::bad_alloc();
-  static const bool no_thp = std::getenv("SG_NO_THP") != nullptr;  // experiment knob
-  if (!no_thp) (void)madvise(q, sz, MADV_HUGEPAGE);  // advisory: 4 KB pages when THP is off
+  (void)madvise(q, sz, MADV_HUGEPAGE);  // advisory: 4 KB pages when THP is off
   return q;
 }
 
