@@ -249,20 +249,20 @@ def rms_check(plans, out, calls, n_check):
             "tolerance": 1e-5, "within_tolerance": int(sum(e <= 1e-5 for e in errs))}
 
 
-def traffic_from_profiles(config, kernel, launches_per_step):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of
-    this workload (profiles/rNN_<config>_traffic.json by tools/gpu_traffic.sh:
-    separate FETCH_SIZE / WRITE_SIZE passes, gfx950 FETCH_SIZE doubled): the sum
-    over the kernel's launches of one execute, per launch."""
+def traffic_from_profiles(config, kernels, launches_per_step):
+    """HBM bytes per launch of the kernel group `kernels` (one launch of each per
+    plan) from the committed rocprofv3 PMC summary of this workload
+    (profiles/rNN_<config>_traffic.json by tools/gpu_traffic.sh: separate
+    FETCH_SIZE / WRITE_SIZE passes, gfx950 FETCH_SIZE doubled): the sum over the
+    group's launches of one execute, per launch of the group."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_%s_traffic.json" % config)))
     if not files:
         return None, None
     d = json.load(open(files[-1]))
     ex = d.get("executes")
-    names = (kernel, kernel + "_noise")  # sg_stft_ola: the filter and the noise (phase 0) kernels
     hits = [(v["hbm_bytes"], v.get("launches")) for k, v in d.get("kernels", {}).items()
-            if k.split(" ")[0] in names and "hbm_bytes" in v]
+            if k.split(" ")[0] in kernels and "hbm_bytes" in v]
     if not hits or not ex or any(n is None for _, n in hits):
         return None, None
     per_step = sum(b * n for b, n in hits) / ex
@@ -271,10 +271,19 @@ def traffic_from_profiles(config, kernel, launches_per_step):
 
 def pmc_from_profiles(config, kernel):
     """Issue profile of `kernel` from the newest committed rocprofv3 SQ-counter
-    summary of this workload (profiles/rNN_<config>_pmc.json, tools/pmc_summary.py):
-    the fraction of its waves' cycles with a VALU / LDS instruction issued and
-    parked on s_waitcnt, averaged over its launches (each counter from its own
-    pass)."""
+    summary of this workload (profiles/rNN_<config>_pmc.json, tools/pmc_summary.py),
+    averaged over its launches:
+      valu/lds_issue_per_wave  SQ_ACTIVE_INST_VALU / _LDS over SQ_WAVE_CYCLES (both
+                               quad-cycles): the share of a wave's life issuing them
+      waitcnt_per_wave         SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES
+      waves_per_simd           ACHIEVED occupancy: SQ_WAVE_CYCLES (quad-cycles summed
+                               over waves) / SQ_BUSY_CU_CYCLES (cycles summed over CUs)
+                               = mean waves resident per SIMD while the CUs are busy
+      valu_busy_per_simd       SQ_ACTIVE_INST_VALU / SQ_BUSY_CU_CYCLES: the share of a
+                               SIMD's cycles issuing VALU (waves x issue share)
+      mfma_busy_per_simd       SQ_VALU_MFMA_BUSY_CYCLES / (4 SQ_BUSY_CU_CYCLES)
+    The last three need SQ_BUSY_CU_CYCLES in the summary (tools/gpu_pmc_head.sh since
+    round 5)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_%s_pmc.json" % config)))
     if not files:
@@ -287,16 +296,20 @@ def pmc_from_profiles(config, kernel):
         for c in ("SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS", "SQ_WAIT_INST_ANY"):
             if c in v:
                 acc.setdefault(c, []).append(v[c] / v["SQ_WAVE_CYCLES"])
+        busy = v.get("SQ_BUSY_CU_CYCLES")
+        if busy:
+            acc.setdefault("waves", []).append(v["SQ_WAVE_CYCLES"] / busy)
+            if "SQ_ACTIVE_INST_VALU" in v:
+                acc.setdefault("valu_busy", []).append(v["SQ_ACTIVE_INST_VALU"] / busy)
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in v:
+                acc.setdefault("mfma_busy", []).append(v["SQ_VALU_MFMA_BUSY_CYCLES"] / (4 * busy))
     if not acc:
         return None
     m = {c: float(np.mean(x)) for c, x in acc.items()}
     return {"valu_issue_per_wave": m.get("SQ_ACTIVE_INST_VALU"), "lds_issue_per_wave": m.get("SQ_ACTIVE_INST_LDS"),
-            "waitcnt_per_wave": m.get("SQ_WAIT_INST_ANY"), "source": os.path.relpath(files[-1], ROOT)}
-
-
-# waves per SIMD the kernels run at (hipcc -Rpass-analysis=kernel-resource-usage, gfx950)
-WAVES_PER_SIMD = {"sg_stft_ola": 2, "sg_stft_ola_noise": 3, "sg_sine_bank": 7, "sg_sine_bank_pairs": 8,
-                  "sg_sine_bank_tall": 5, "sg_sine_bank_tall_pairs": 8, "sg_sine_bank_tab": 8}
+            "waitcnt_per_wave": m.get("SQ_WAIT_INST_ANY"), "waves_per_simd": m.get("waves"),
+            "valu_busy_per_simd": m.get("valu_busy"), "mfma_busy_per_simd": m.get("mfma_busy"),
+            "source": os.path.relpath(files[-1], ROOT)}
 
 
 def roofline(st, prof, steps, config, kern):
@@ -336,7 +349,7 @@ def roofline(st, prof, steps, config, kern):
         name = "sg_stft_ola + sg_stft_ola_noise"
     achieved = alg / sec / 1e9 if sec > 0 else 0.0
     hfrac = achieved / HBM_PEAK_GBS
-    traffic, src = traffic_from_profiles(config, kern, lps)
+    traffic, src = traffic_from_profiles(config, kernels, lps)
     r = {"bound": "valu" if vfrac > hfrac else "hbm", "kernel": name, "achieved": achieved, "peak": HBM_PEAK_GBS,
          "unit": "GB/s", "frac": hfrac, "traffic": traffic, "alg_bytes_per_launch": alg, "avg_launch_ms": ms,
          "launches_timed": n,
@@ -348,12 +361,12 @@ def roofline(st, prof, steps, config, kern):
         r["traffic_source"] = src
     r.update(extra)
     issue = {k: pmc_from_profiles(config, k) for k in kernels}
-    issue = {k: dict(v, waves_per_simd=WAVES_PER_SIMD.get(k)) for k, v in issue.items() if v}
+    issue = {k: v for k, v in issue.items() if v}
     if issue:
         r["issue"] = issue
     if kern == "sg_stft_ola":
-        r["binding"] = ("VALU issue and latency at 2 waves/SIMD (241 VGPRs): the odd-prime radix-19/29 "
-                        "butterflies of M = 1102 = 2 x 19 x 29 are ~64 % of the VALU per frame")
+        r["binding"] = ("latency at 2 waves/SIMD (241 VGPRs): per wave ~37 % issuing, ~35 % parked on s_waitcnt; "
+                        "radix-29 stage on the matrix pipe (MFMA), radix 19 and 2 on the VALU; see issue")
     return r
 
 

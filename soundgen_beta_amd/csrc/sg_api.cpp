@@ -340,7 +340,7 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
       D.call_msg[b.call + i] = std::move(S.call_msg[i]);
     }
     for (auto& e : S.epochs) {
-      e.w_off += b.w; e.amp_off += b.amp; e.da_off += b.amp; e.knot_off += b.knot;
+      e.w_off += b.w; e.amp_off += b.amp; e.knot_off += b.knot;
       e.seg_off += (int32_t)b.seg; e.syl += (int32_t)b.syl;
     }
     for (auto& t : S.tasks) {
@@ -405,7 +405,7 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
       x.base[k] = at;
     };
     for (auto& j : S.ampjobs) {
-      j.amp_off += b.amp; j.da_off += b.amp;
+      j.amp_off += b.amp;
       if (j.src_off >= 0) j.src_off += b.asrc;
       if (j.col0 >= 0) j.col0 += b.acol;
     }
@@ -744,18 +744,14 @@ int sg_plan_debug_amps(const sg_plan* plan, float* out, int64_t n) {
   std::vector<double> lg((size_t)B.amp_lg_rows + 1);
   for (size_t k = 0; k < lg.size(); ++k) lg[k] = std::log2((double)(k + 1));
   for (const SgAmpJob& J : B.ampjobs)  // sg_amp_build, one job after the other
-    for (int32_t r = 0; r < J.Rp; ++r) {
-      float prev = 0.f;
+    for (int32_t r = 0; r < J.Rp; ++r)
       for (int32_t g = 0; g < J.G; ++g) {
         float a;
         if (r >= J.R) a = 0.f;
         else if (J.src_off >= 0) a = B.ampsrc[J.src_off + (int64_t)g * J.Rp + r];
         else a = (float)sg::amp_value(B.ampcols.data() + J.col0, J, lg.data(), g, r);
         out[J.amp_off + (int64_t)g * J.Rp + r] = a;
-        if (g > 0) out[J.da_off + (int64_t)(g - 1) * J.Rp + r] = a - prev;
-        prev = a;
       }
-    }
   return SG_OK;
 }
 

@@ -21,7 +21,6 @@ struct SgSeg {
 struct SgEpoch {
   int64_t w_off;     // scratch offset of W[0]
   int64_t amp_off;   // float offset of the [G][R] amplitude block
-  int64_t da_off;    // float offset of the [G-1][R] block dA[i] = A[i+1] - A[i]
   int64_t knot_off;  // double offset of the G knots
   int32_t seg_off;   // first SgSeg of the syllable
   int32_t nseg;
@@ -62,7 +61,7 @@ constexpr int SG_TASK_MAX = 1024;  // samples per task (16 slots of 64 lanes)
 struct SgWTask {
   int64_t w_off;       // W offset of epoch sample 0
   int64_t a_off;       // float offset of A[i][0..R)
-  int64_t d_off;       // float offset of dA[i][0..R) = A[i+1] - A[i]
+  int64_t d_off;       // float offset of A[i+1][0..R): dA[i] = A[i+1] - A[i] is formed where the rows are staged
   int64_t dk0;         // syllable sample (0-based) of epoch sample 0
   double c0, c1, c2, c3, c4;  // phase segment (see SgSeg) times invD
   double invD;         // 1 / (nSubharm + 1)
@@ -433,8 +432,8 @@ struct SgAmpCol {     // one glottal cycle
   double pa, pb, pc;  // parabola a k^2 + b k + c over harmonics k <= rph
   double sbw;         // subharmonic bandwidth subDep (Hz; vocal-fry epochs)
 };
-struct SgAmpJob {     // one epoch's [G][Rp] block A and [G-1][Rp] block dA = A[g+1] - A[g]
-  int64_t amp_off, da_off;  // destinations in the device amplitude array
+struct SgAmpJob {     // one epoch's [G][Rp] amplitude block A
+  int64_t amp_off;          // destination in the device amplitude array
   int64_t src_off;          // >= 0: copy [G][Rp] floats from the uploaded source (host-built fallback)
   int64_t col0;             // SgAmpCol of the syllable's glottal cycle 0
   int32_t g0, G;            // the epoch's cycles [g0, g0 + G) of the syllable

@@ -39,12 +39,15 @@ constexpr int SG_LDS_ROWS = 256;
 // W = (sum_r a_r(t) sin r theta) by linearity (r04: the sine-bank classes -13 %).
 
 
+// A: the task's column A[i], A1: the next column A[i + 1]; ld gets dA = A1 - A
+// (fp32, as the column differences were stored before round 5: bit for bit)
 template <bool TWO>
 __device__ __forceinline__ void stage_rows(float* __restrict__ la, float* __restrict__ ld, const float* __restrict__ A,
-                                           const float* __restrict__ D, int r0, int n, int lane) {
+                                           const float* __restrict__ A1, int r0, int n, int lane) {
   for (int r = lane; r < n; r += 64) {
-    la[r] = A[r0 + r];
-    if (TWO) ld[r] = D[r0 + r];
+    const float a = A[r0 + r];
+    la[r] = a;
+    if (TWO) ld[r] = A1[r0 + r] - a;
   }
 }
 
@@ -296,11 +299,12 @@ __device__ __forceinline__ void run_pair(const SgWTask& P, const SgWTask& Q, flo
                                          float* __restrict__ W, int lane, float& mp, float& mq) {
   const int R = P.Rn > Q.Rn ? P.Rn : Q.Rn;  // multiples of 16
   for (int r = lane; r < R; r += 64) {
-    *reinterpret_cast<float2*>(la + 2 * r) = make_float2(r < P.Rn ? amps[P.a_off + r] : 0.f, r < Q.Rn ? amps[Q.a_off + r] : 0.f);
+    const float ap = r < P.Rn ? amps[P.a_off + r] : 0.f, aq = r < Q.Rn ? amps[Q.a_off + r] : 0.f;
+    *reinterpret_cast<float2*>(la + 2 * r) = make_float2(ap, aq);
     if (TWO)
       *reinterpret_cast<float2*>(ld + 2 * r) =
-          make_float2(r < P.Rn && !(P.flags & SG_TASK_CONST) ? amps[P.d_off + r] : 0.f,
-                      r < Q.Rn && !(Q.flags & SG_TASK_CONST) ? amps[Q.d_off + r] : 0.f);
+          make_float2(r < P.Rn && !(P.flags & SG_TASK_CONST) ? amps[P.d_off + r] - ap : 0.f,
+                      r < Q.Rn && !(Q.flags & SG_TASK_CONST) ? amps[Q.d_off + r] - aq : 0.f);
   }
   const bool vp = lane < P.len, vq = lane < Q.len;
   float tp, alp, snp, tq, alq, snq;
@@ -449,12 +453,12 @@ __device__ __forceinline__ void run_pair_rs(const SgWTask& P, const SgWTask& Q, 
     const int n = R - r0 < CH ? R - r0 : CH;  // multiple of 16
     for (int r = lane; r < n; r += 64) {
       const int rr = r0 + r;
-      *reinterpret_cast<float2*>(la + 2 * r) =
-          make_float2(rr < P.Rn ? amps[P.a_off + rr] : 0.f, rr < Q.Rn ? amps[Q.a_off + rr] : 0.f);
+      const float ap = rr < P.Rn ? amps[P.a_off + rr] : 0.f, aq = rr < Q.Rn ? amps[Q.a_off + rr] : 0.f;
+      *reinterpret_cast<float2*>(la + 2 * r) = make_float2(ap, aq);
       if (TWO)
         *reinterpret_cast<float2*>(ld + 2 * r) =
-            make_float2(rr < P.Rn && !(P.flags & SG_TASK_CONST) ? amps[P.d_off + rr] : 0.f,
-                        rr < Q.Rn && !(Q.flags & SG_TASK_CONST) ? amps[Q.d_off + rr] : 0.f);
+            make_float2(rr < P.Rn && !(P.flags & SG_TASK_CONST) ? amps[P.d_off + rr] - ap : 0.f,
+                        rr < Q.Rn && !(Q.flags & SG_TASK_CONST) ? amps[Q.d_off + rr] - aq : 0.f);
     }
 #pragma unroll 1
     for (int r = n - 4; r >= 0; r -= 4) {
@@ -1099,26 +1103,22 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize_hp(
 // ---------------------------------------------------------------- launchers
 // ------------------------------------------------- amplitude blocks (K3)
 // One workgroup per epoch job (run once, at upload): thread r owns row r of
-// every glottal cycle, walks the cycles in order and writes A[g][r] and
-// dA[g - 1][r] = A[g][r] - A[g - 1][r] in fp32, as the sine banks read them.
+// every glottal cycle and writes A[g][r] in fp32 (the sine banks form the column
+// differences dA[g] = A[g + 1] - A[g] in fp32 where they stage the rows).
 // The values come from the shared formula (sg_amp.h) or, for the host-built
 // fallback, from the uploaded blocks.
 __global__ __launch_bounds__(256) void sg_amp_build(const SgAmpJob* __restrict__ jobs,
                                                     const SgAmpCol* __restrict__ cols, const float* __restrict__ src,
                                                     const double* __restrict__ lg, float* __restrict__ amps) {
   const SgAmpJob J = jobs[blockIdx.x];
-  for (int r = threadIdx.x; r < J.Rp; r += blockDim.x) {
-    float prev = 0.f;
+  for (int r = threadIdx.x; r < J.Rp; r += blockDim.x)
     for (int g = 0; g < J.G; ++g) {
       float a;
       if (r >= J.R) a = 0.f;
       else if (J.src_off >= 0) a = src[J.src_off + (int64_t)g * J.Rp + r];
       else a = (float)sg::amp_value(cols + J.col0, J, lg, g, r);
       amps[J.amp_off + (int64_t)g * J.Rp + r] = a;
-      if (g > 0) amps[J.da_off + (int64_t)(g - 1) * J.Rp + r] = a - prev;
-      prev = a;
     }
-  }
 }
 
 #include "sg_exec.h"

@@ -1257,15 +1257,13 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
     d.invD = 1.0 / (double)m.D;
     d.knot_off = (int64_t)B.knots.size();
     B.knots.insert(B.knots.end(), he.knots.begin(), he.knots.end());
-    // [G][R] amplitudes then [G-1][R] column differences (device array, built by
-    // sg_amp_build at upload from the job: formula, or the host-built values)
+    // [G][R] amplitudes (device array, built by sg_amp_build at upload from the
+    // job: formula, or the host-built values); a task reads its two columns
     d.amp_off = B.amp_total;
-    d.da_off = d.amp_off + (int64_t)d.G * d.R;
-    B.amp_total += (int64_t)(2 * d.G - 1) * d.R;
+    B.amp_total += (int64_t)d.G * d.R;
     {
       SgAmpJob j = dev_amps ? m.job : SgAmpJob{};
       j.amp_off = d.amp_off;
-      j.da_off = d.da_off;
       j.G = d.G;
       j.R = (int32_t)m.R;
       j.Rp = d.R;
@@ -1292,7 +1290,7 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
     B.epochs.push_back(d);
     B.harm_samples += he.n;
     B.harm_terms += he.n * (int64_t)d.R;
-    B.harm_amp_bytes += (int64_t)(2 * d.G - 1) * d.R * 4;
+    B.harm_amp_bytes += (int64_t)d.G * d.R * 4;
   }
   // pieces; the single full-weight piece of each epoch becomes its direct window
   sy.piece0 = (int32_t)B.pieces.size();
@@ -1377,7 +1375,7 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
         SgWTask T{};
         T.w_off = ep.w_off;
         T.a_off = ep.amp_off + i * ep.R;
-        T.d_off = ep.da_off + i * ep.R;
+        T.d_off = ep.amp_off + (i + 1) * ep.R;  // A[i + 1]
         T.dk0 = ep.dk0;
         // phase in cycles of the epoch's lowest multiplier: integr / D folded into the
         // coefficients (the device evaluates the polynomial only)
