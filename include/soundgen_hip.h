@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SG_ABI_VERSION 2
+#define SG_ABI_VERSION 3
 
 enum {
   SG_OK = 0,
@@ -167,6 +167,47 @@ int sg_abi_version(void);
 /* Fill the defaults of generateHarmonics()/soundgen() formals. */
 void sg_default_harm_params(sg_harm_params* p);
 void sg_default_soundgen_args(sg_soundgen_args* a);
+
+/* ---- whole-node batch path: one process, several devices (ABI 3) --------
+ * Replaces the single-device loop behind the R batch callers that north_star
+ * keeps: soundgen_batch(), morph() (R/morph.R:200-208) and matchPars()
+ * (R/matchPars.R:168-202), each a list of independent soundgen() calls.
+ * A node is a list of device ordinals (a device may appear more than once;
+ * NULL: 0 .. n - 1, and n <= 0 with NULL: every visible device). Planning needs
+ * no device; each device's context is created on first execution. */
+typedef struct sg_node sg_node;
+typedef struct sg_node_plan sg_node_plan;
+int sg_device_count(void);
+int sg_node_create(const int32_t* devices, int32_t n, sg_node** out);
+void sg_node_destroy(sg_node* node);
+int32_t sg_node_size(const sg_node* node);
+const char* sg_node_last_error(const sg_node* node);
+/* Calls are assigned to the node's devices by LPT over an analytic cost per
+ * call (samples x kept harmonic rows, STFT frames, per-sample assembly); each
+ * device's shard is planned as one sg_plan. Lengths, offsets, statuses and
+ * messages are those of the WHOLE batch in call order with sg_plan_batch's
+ * layout, and every call's samples equal what sg_plan_batch of the whole batch
+ * produces (a call's arithmetic does not depend on the batch around it). With
+ * draw callbacks (R's RNG) the calls are first planned in call order recording
+ * each call's draws -- R's stream, R's order; a failing call ends it as
+ * lapply() would -- and the shards are then planned from the recorded draws. */
+int sg_node_plan_batch(sg_node* node, const sg_call_desc* calls, int64_t n_calls, sg_node_plan** out);
+void sg_node_plan_destroy(sg_node_plan* plan);
+int64_t sg_node_plan_n_calls(const sg_node_plan* plan);
+int64_t sg_node_plan_total_samples(const sg_node_plan* plan);
+int sg_node_plan_lengths(const sg_node_plan* plan, int64_t* out_len, int64_t* out_off);
+int sg_node_plan_status(const sg_node_plan* plan, int32_t* out_status);
+const char* sg_node_plan_call_message(const sg_node_plan* plan, int64_t i);
+/* the node device index (0 .. size - 1) each call was assigned to */
+int sg_node_plan_owner(const sg_node_plan* plan, int32_t* owner);
+/* the analytic cost per call the assignment used (ns of one MI355X) */
+int sg_node_plan_costs(const sg_node_plan* plan, double* cost);
+int64_t sg_node_plan_shard_samples(const sg_node_plan* plan, int32_t k);
+/* Synchronous: every device uploads, synthesizes its shard on its own stream
+ * and copies it over its own link; each call's samples land in out_host at its
+ * whole-batch offset (sg_node_plan_total_samples values in all). */
+int sg_node_execute_to_host(sg_node* node, sg_node_plan* plan, double* out_host);
+int sg_node_execute_to_host_f32(sg_node* node, sg_node_plan* plan, float* out_host);
 
 /* ---- batch path (planned on host, executed on device) ------------------ */
 /* All integer/length bookkeeping happens here, bit-exact with R. */

@@ -37,6 +37,35 @@ static sg_ctx* ctx(void) {
   return g_ctx;
 }
 
+/* The node of soundgen_batch: the devices of the last call's `devices`
+ * (getOption("soundgen_hip.devices"); NULL = every visible device), kept across
+ * calls while they stay the same. */
+static sg_node* g_node = NULL;
+static int32_t g_node_dev[64];
+static int32_t g_node_n = -1;
+
+static sg_node* node(SEXP devices) {
+  int32_t dv[64];
+  int32_t n = 0;
+  if (!Rf_isNull(devices)) {
+    const R_xlen_t m = Rf_xlength(devices);
+    if (TYPEOF(devices) != INTSXP || m < 1 || m > 64)
+      Rf_error("soundgen_hip: devices must be an integer vector of 1 to 64 device ordinals");
+    for (R_xlen_t i = 0; i < m; ++i) {
+      const int v = INTEGER(devices)[i];
+      if (v == NA_INTEGER || v < 0) Rf_error("soundgen_hip: device ordinals must be >= 0");
+      dv[n++] = (int32_t)v;
+    }
+  }
+  if (g_node && n == g_node_n && (n == 0 || !memcmp(dv, g_node_dev, (size_t)n * sizeof(int32_t)))) return g_node;
+  if (g_node) sg_node_destroy(g_node);
+  g_node = NULL;
+  if (sg_node_create(n ? dv : NULL, n, &g_node) != SG_OK) Rf_error("soundgen_hip: no usable MI355X (sg_node_create failed)");
+  memcpy(g_node_dev, dv, (size_t)n * sizeof(int32_t));
+  g_node_n = n;
+  return g_node;
+}
+
 static double cb_norm(void* u) { (void)u; return norm_rand(); }
 static double cb_unif(void* u) { (void)u; return unif_rand(); }
 static double cb_gamma(void* u, double shape, double rate) { (void)u; return rgamma(shape, 1.0 / rate); }
@@ -196,14 +225,16 @@ SEXP C_sg_soundgen(SEXP args) {
 
 /* soundgen_batch(calls): a list of resolved soundgen() argument lists (as
  * .sg_soundgen_args builds each) planned as ONE sg_plan_batch and executed in
- * one pass; returns the list of waveforms in call order. R's RNG is drawn in
+ * one pass over the node's devices (sg_node: LPT shards, each device on its own
+ * stream and link; `devices` NULL = every visible device); returns the list of
+ * waveforms in call order. R's RNG is drawn in
  * call order, each call's draws in the reference's order, so the result equals
  * lapply(calls, function(a) do.call(soundgen, a)) after the same set.seed().
  * A call R would stop() on stops the batch with that call's message, as the
  * loop would: its draws and those of the calls before it are consumed, and the
  * planner plans no later call once a callback-drawing call has failed
  * (plan_range in sg_api.cpp), so .Random.seed ends where the R loop leaves it. */
-SEXP C_sg_soundgen_batch(SEXP calls) {
+SEXP C_sg_soundgen_batch(SEXP calls, SEXP devices) {
   if (!Rf_isNewList(calls)) Rf_error("soundgen_hip: calls must be a list of argument lists");
   const R_xlen_t n = Rf_xlength(calls);
   SEXP res = PROTECT(Rf_allocVector(VECSXP, n));
@@ -220,28 +251,29 @@ SEXP C_sg_soundgen_batch(SEXP calls) {
     d[i].args = &a[i];
     d[i].random = r_rng();
   }
-  sg_plan* plan = NULL;
+  sg_node* nd = node(devices);
+  sg_node_plan* plan = NULL;
   GetRNGstate();
-  int rc = sg_plan_batch(ctx(), d, (int64_t)n, &plan);
+  int rc = sg_node_plan_batch(nd, d, (int64_t)n, &plan);
   PutRNGstate();
-  check(rc);
+  if (rc) Rf_error("soundgen_hip: %s", sg_node_last_error(nd));
   int32_t* st = (int32_t*)R_alloc((size_t)n, sizeof(int32_t));
   int64_t* len = (int64_t*)R_alloc((size_t)n, sizeof(int64_t));
   int64_t* off = (int64_t*)R_alloc((size_t)n, sizeof(int64_t));
-  sg_plan_status(plan, st);
-  sg_plan_lengths(plan, len, off);
+  sg_node_plan_status(plan, st);
+  sg_node_plan_lengths(plan, len, off);
   for (R_xlen_t i = 0; i < n; ++i)
     if (st[i]) {
       char msg[512];
-      snprintf(msg, sizeof msg, "call %ld: %s", (long)(i + 1), sg_plan_call_message(plan, (int64_t)i));
-      sg_plan_destroy(plan);
+      snprintf(msg, sizeof msg, "call %ld: %s", (long)(i + 1), sg_node_plan_call_message(plan, (int64_t)i));
+      sg_node_plan_destroy(plan);
       Rf_error("soundgen_hip: %s", msg);
     }
-  const int64_t tot = sg_plan_total_samples(plan);
+  const int64_t tot = sg_node_plan_total_samples(plan);
   SEXP all = PROTECT(Rf_allocVector(REALSXP, tot > 0 ? tot : 1));
-  rc = sg_execute_to_host(ctx(), plan, REAL(all));
-  sg_plan_destroy(plan);
-  check(rc);
+  rc = sg_node_execute_to_host(nd, plan, REAL(all));
+  sg_node_plan_destroy(plan);
+  if (rc) Rf_error("soundgen_hip: %s", sg_node_last_error(nd));
   for (R_xlen_t i = 0; i < n; ++i) {
     SEXP y = Rf_allocVector(REALSXP, len[i]);
     SET_VECTOR_ELT(res, i, y);
@@ -323,7 +355,7 @@ static const R_CallMethodDef CALLS[] = {
     {"C_sg_generate_noise", (DL_FUNC)&C_sg_generate_noise, 4},
     {"C_sg_spectral_envelope", (DL_FUNC)&C_sg_spectral_envelope, 5},
     {"C_sg_formant_filter", (DL_FUNC)&C_sg_formant_filter, 4},
-    {"C_sg_soundgen_batch", (DL_FUNC)&C_sg_soundgen_batch, 1},
+    {"C_sg_soundgen_batch", (DL_FUNC)&C_sg_soundgen_batch, 2},
     {NULL, NULL, 0}};
 
 void R_init_soundgen(DllInfo* dll) {
@@ -335,4 +367,7 @@ void R_unload_soundgen(DllInfo* dll) {
   (void)dll;
   if (g_ctx) sg_ctx_destroy(g_ctx);
   g_ctx = NULL;
+  if (g_node) sg_node_destroy(g_node);
+  g_node = NULL;
+  g_node_n = -1;
 }

@@ -76,6 +76,83 @@ def _desc_view():
 _DESC_VIEW = _desc_view()
 
 
+class NodePlan:
+    """A batch planned over a native.Node (sg_node_plan_batch): whole-batch
+    lengths, offsets and statuses in call order (sg_plan_batch's layout), the
+    device each call went to, and synchronous execution into host memory."""
+
+    def __init__(self, calls, node):
+        self.node = node
+        m = Marshalled(calls)
+        self._m = m
+        n = self.n = m.n
+        L = native.lib()
+        self.ptr = C.c_void_p()
+        node.check(L.sg_node_plan_batch(node.ptr, m.descs, n, C.byref(self.ptr)))
+        i64p = C.POINTER(C.c_int64)
+        self.lengths = np.zeros(n, dtype=np.int64)
+        self.offsets = np.zeros(n, dtype=np.int64)
+        L.sg_node_plan_lengths(self.ptr, self.lengths.ctypes.data_as(i64p), self.offsets.ctypes.data_as(i64p))
+        self.status = np.zeros(n, dtype=np.int32)
+        L.sg_node_plan_status(self.ptr, self.status.ctypes.data_as(C.POINTER(C.c_int32)))
+        self.owner = np.zeros(n, dtype=np.int32)
+        L.sg_node_plan_owner(self.ptr, self.owner.ctypes.data_as(C.POINTER(C.c_int32)))
+        self.cost = np.zeros(n, dtype=np.float64)
+        L.sg_node_plan_costs(self.ptr, self.cost.ctypes.data_as(C.POINTER(C.c_double)))
+        self.total = int(L.sg_node_plan_total_samples(self.ptr))
+
+    def message(self, i):
+        return native.lib().sg_node_plan_call_message(self.ptr, i).decode()
+
+    def shard_samples(self, k):
+        return int(native.lib().sg_node_plan_shard_samples(self.ptr, k))
+
+    def execute_to_host(self, dtype=np.float64):
+        """The packed batch (sg_node_plan_total_samples values, call i at offsets[i])."""
+        out = np.zeros(max(self.total, 1), dtype=dtype)
+        L = native.lib()
+        if dtype == np.float32:
+            self.node.check(L.sg_node_execute_to_host_f32(self.node.ptr, self.ptr,
+                                                          out.ctypes.data_as(C.POINTER(C.c_float))))
+        else:
+            self.node.check(L.sg_node_execute_to_host(self.node.ptr, self.ptr,
+                                                      out.ctypes.data_as(C.POINTER(C.c_double))))
+        return out[:self.total]
+
+    def close(self):
+        if self.ptr:
+            native.lib().sg_node_plan_destroy(self.ptr)
+            self.ptr = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def synthesize_node(calls, devices=None, node=None):
+    """soundgen_batch over several devices of this process (sg_node): the list of
+    per-call float64 waveforms (an exception object for a call that failed)."""
+    from . import native as _n
+    own = node is None
+    node = node or _n.Node(devices)
+    try:
+        p = NodePlan(calls, node)
+        y = p.execute_to_host()
+        out = []
+        for i in range(p.n):
+            if p.status[i]:
+                out.append(_n.SoundgenError(int(p.status[i]), p.message(i)))
+            else:
+                out.append(y[p.offsets[i]:p.offsets[i] + p.lengths[i]].copy())
+        p.close()
+        return out
+    finally:
+        if own:
+            node.close()
+
+
 class Plan:
     def __init__(self, calls, ctx=None, marshalled=None):
         """Plan `calls` (or the already marshalled ones). ctx may be None: planning

@@ -159,7 +159,10 @@ struct GrowthEstimate {
 
 GrowthEstimate g_growth;
 
-void plan_range(sg::Batch& B, const sg_call_desc* calls, int64_t c0, int64_t c1) {
+// stream_stop: the calls' draw callbacks are one sequential stream (R's RNG), so a
+// failing call ends the planning of later callback calls; false when every call's
+// callbacks replay its own recorded draws (sg_node's second pass)
+void plan_range(sg::Batch& B, const sg_call_desc* calls, int64_t c0, int64_t c1, bool stream_stop = true) {
   const int64_t n = c1 - c0;
   B.call_len.assign(n, 0);
   B.call_off.assign(n, 0);
@@ -179,7 +182,7 @@ void plan_range(sg::Batch& B, const sg_call_desc* calls, int64_t c0, int64_t c1)
   for (int64_t i = 0; i < n; ++i) {
     const sg_call_desc& d = calls[c0 + i];
     const bool cb = d.random.norm_cb || d.random.unif_cb || d.random.gamma_cb;
-    if (cb && cb_failed >= 0) {
+    if (cb && stream_stop && cb_failed >= 0) {
       B.call_status[i] = SG_E_ARG;
       B.call_msg[i] = "not planned: call " + std::to_string(c0 + cb_failed + 1) +
                       " of the batch failed first (the RNG callback stream stops there)";
@@ -476,6 +479,12 @@ void sg_ctx_destroy(sg_ctx* ctx) {
 const char* sg_last_error(const sg_ctx* ctx) { return ctx ? ctx->err.c_str() : ""; }
 
 int sg_plan_batch(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, sg_plan** out) {
+  return sg::plan_batch_ex(ctx, calls, n_calls, false, out);
+}
+}  // extern "C"
+
+namespace sg {
+int plan_batch_ex(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, bool independent_draws, sg_plan** out) {
   return guarded(ctx, [&]() {
     auto P = std::make_unique<sg_plan>();
     sg::Batch& B = P->B;
@@ -483,15 +492,17 @@ int sg_plan_batch(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, sg_pl
     // calls are planned on host threads into private batches and concatenated in
     // call order (the result equals serial planning). Draw callbacks (R's RNG
     // through the shim, or one generator shared by the batch) are a single
-    // sequential stream: such batches plan on the calling thread.
+    // sequential stream: such batches plan on the calling thread, unless every
+    // call's callbacks replay its own recorded draws (independent_draws).
     bool callbacks = false;
     for (int64_t c = 0; c < n_calls && !callbacks; ++c)
       callbacks = calls[c].random.norm_cb || calls[c].random.unif_cb || calls[c].random.gamma_cb;
-    const int threads = callbacks ? 1 : plan_threads(n_calls);
+    const bool serial = callbacks && !independent_draws;
+    const int threads = serial ? 1 : plan_threads(n_calls);
     g_growth.decay();
     if (threads <= 1) {
       g_growth.reserve(B, n_calls);
-      plan_range(B, calls, 0, n_calls);
+      plan_range(B, calls, 0, n_calls, !independent_draws);
       g_growth.record(B, n_calls);
     } else {
       constexpr int per_thread = 8;  // parts per thread (dynamic balance over uneven calls)
@@ -504,7 +515,7 @@ int sg_plan_batch(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, sg_pl
           try {
             const int64_t c0 = k * n_calls / nchunk, c1 = (k + 1) * n_calls / nchunk;
             g_growth.reserve(parts[k], c1 - c0);
-            plan_range(parts[k], calls, c0, c1);
+            plan_range(parts[k], calls, c0, c1, !independent_draws);
             g_growth.record(parts[k], c1 - c0);
           } catch (...) {
             errs[k] = std::current_exception();
@@ -557,6 +568,9 @@ int sg_plan_batch(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, sg_pl
     return SG_OK;
   });
 }
+}  // namespace sg
+
+extern "C" {
 
 void sg_plan_destroy(sg_plan* plan) {
   if (!plan) return;

@@ -126,5 +126,17 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// XCD-aware workgroup order: the dispatcher deals workgroups round-robin over
+// the 8 XCDs (b and b + 8 share one, each XCD has its own L2), so consecutive
+// workgroups -- which read neighbouring data, e.g. a glottal cycle's amplitude
+// column A[i + 1] is also the next cycle's A[i] -- would fetch it from HBM on two
+// L2s. This bijection of [0, n) gives each XCD a contiguous run of logical
+// indices instead (cdna_hip_programming.md §5.5 T1, bijective for any n). Speed
+// only: nothing depends on where a workgroup runs.
+__device__ __forceinline__ uint32_t xcd_swizzle(uint32_t b, uint32_t n) {
+  const uint32_t x = b & 7u, i = b >> 3, q = n >> 3, r = n & 7u;
+  return x * q + (x < r ? x : r) + i;
+}
+
 }  // namespace sgd
 

@@ -351,7 +351,7 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
   __shared__ __attribute__((aligned(16))) float rows[4][2][SG_LDS_ROWS];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t k = (int64_t)blockIdx.x * 4 + wave;
+  const int64_t k = (int64_t)sgd::xcd_swizzle(blockIdx.x, gridDim.x) * 4 + wave;
   if (k >= n) return;
   const int64_t ti = idx[k];
   const SgWTask T = tasks[ti];
@@ -368,7 +368,7 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_pairs(
   __shared__ __attribute__((aligned(16))) float rows[4][2][SG_LDS_ROWS];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t k = ((int64_t)blockIdx.x * 4 + wave) * 2;
+  const int64_t k = ((int64_t)sgd::xcd_swizzle(blockIdx.x, gridDim.x) * 4 + wave) * 2;
   if (k >= n) return;
   const int64_t tp = idx[k];
   const bool has_q = k + 1 < n;
@@ -503,7 +503,7 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_tall(
   __shared__ __attribute__((aligned(16))) float rows[4][2][SG_LDS_ROWS];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t k = (int64_t)blockIdx.x * 4 + wave;
+  const int64_t k = (int64_t)sgd::xcd_swizzle(blockIdx.x, gridDim.x) * 4 + wave;
   if (k >= n) return;
   const int64_t ti = idx[k];
   const SgWTask T = tasks[ti];
@@ -519,7 +519,7 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_tall_pairs(
   __shared__ __attribute__((aligned(16))) float rows[4][2][SG_LDS_ROWS];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t k = ((int64_t)blockIdx.x * 4 + wave) * 2;
+  const int64_t k = ((int64_t)sgd::xcd_swizzle(blockIdx.x, gridDim.x) * 4 + wave) * 2;
   if (k >= n) return;
   const int64_t tp = idx[k];
   const bool has_q = k + 1 < n;
@@ -564,7 +564,7 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_hp(
   __shared__ __attribute__((aligned(16))) float rows[4][2][SG_LDS_ROWS];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t k = (int64_t)blockIdx.x * 4 + wave;
+  const int64_t k = (int64_t)sgd::xcd_swizzle(blockIdx.x, gridDim.x) * 4 + wave;
   if (k >= n) return;
   const int64_t ti = idx[k];
   const SgWTask T = tasks[ti];

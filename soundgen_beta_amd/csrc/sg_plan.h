@@ -285,3 +285,10 @@ void clumper(vec& s, const vec& minLen);
 double noise_threshold(int which, double nonlinBalance);
 
 }  // namespace sg
+
+namespace sg {
+// sg_plan_batch with the draw-independence of the calls stated by the caller:
+// independent_draws = every call's callbacks replay that call's own recorded
+// draws (sg_node.cpp), so the batch may plan on host threads like injected draws
+int plan_batch_ex(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, bool independent_draws, sg_plan** out);
+}  // namespace sg

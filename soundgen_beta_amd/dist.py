@@ -38,14 +38,6 @@ W_FLOP = 0.00004   # per nominal FFT flop of sg_stft_ola
 W_SAMPLE = 0.05    # per output sample: finalize, mixes
 
 
-def _anchors_len(a):
-    if a is None:
-        return 0
-    if isinstance(a, dict):
-        return len(np.atleast_1d(a.get("value", a.get("time", []))))
-    return len(np.atleast_1d(a))
-
-
 def _is_na(v):
     return v is None or (isinstance(v, str) and v.upper() == "NA")
 
@@ -125,7 +117,11 @@ def call_cost(call):
     wl = max(4.0, 2 * math.floor(float(a.get("windowLength", 50)) * sr / 1000 / 2))
     hop = wl * (1 - float(a.get("overlap", 75)) / 100)
     frames = n / max(hop, 1.0)
-    noise = 1.0 + (_anchors_len(a.get("noiseAnchors")) > 0)
+    # a noise phase exists when some noise anchor is above throwaway (R's default
+    # noiseAnchors are -120 dB: no breathing)
+    na = a.get("noiseAnchors")
+    nv = _finite(na.get("value", []) if isinstance(na, dict) else na)
+    noise = 1.0 + bool((nv > float(a.get("throwaway", -120))).any())
     fft = 2 * 5 * wl * math.log2(wl) * frames * noise
     return n * (rows * W_ROW + W_SAMPLE) + fft * W_FLOP
 

@@ -130,6 +130,30 @@ def lib():
     L.sg_noise_threshold.argtypes = [C.c_int32, C.c_double]
     L.sg_noise_threshold.restype = C.c_double
     L.sg_abi_version.restype = C.c_int
+    # whole-node batch path (sg_node.cpp)
+    L.sg_device_count.restype = C.c_int
+    L.sg_node_create.argtypes = [C.POINTER(C.c_int32), C.c_int32, C.POINTER(vp)]
+    L.sg_node_destroy.argtypes = [vp]
+    L.sg_node_size.argtypes = [vp]
+    L.sg_node_size.restype = C.c_int32
+    L.sg_node_last_error.argtypes = [vp]
+    L.sg_node_last_error.restype = C.c_char_p
+    L.sg_node_plan_batch.argtypes = [vp, vp, i64, C.POINTER(vp)]
+    L.sg_node_plan_destroy.argtypes = [vp]
+    L.sg_node_plan_n_calls.argtypes = [vp]
+    L.sg_node_plan_n_calls.restype = i64
+    L.sg_node_plan_total_samples.argtypes = [vp]
+    L.sg_node_plan_total_samples.restype = i64
+    L.sg_node_plan_lengths.argtypes = [vp, i64p, i64p]
+    L.sg_node_plan_status.argtypes = [vp, C.POINTER(C.c_int32)]
+    L.sg_node_plan_call_message.argtypes = [vp, i64]
+    L.sg_node_plan_call_message.restype = C.c_char_p
+    L.sg_node_plan_owner.argtypes = [vp, C.POINTER(C.c_int32)]
+    L.sg_node_plan_costs.argtypes = [vp, dp]
+    L.sg_node_plan_shard_samples.argtypes = [vp, C.c_int32]
+    L.sg_node_plan_shard_samples.restype = i64
+    L.sg_node_execute_to_host.argtypes = [vp, vp, dp]
+    L.sg_node_execute_to_host_f32.argtypes = [vp, vp, C.POINTER(C.c_float)]
     _lib = L
     return L
 
@@ -154,6 +178,41 @@ class Context:
     def close(self):
         if self.ptr:
             lib().sg_ctx_destroy(self.ptr)
+            self.ptr = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Node:
+    """Several devices driven from this process (sg_node_*): a batch is sharded
+    over them by calls (LPT), each device synthesizes its shard and copies it over
+    its own link. devices: ordinals (repeats allowed: a 2-way node on one GPU), or
+    None for every visible device. Planning works without a GPU."""
+
+    def __init__(self, devices=None):
+        L = lib()
+        self.ptr = C.c_void_p()
+        if devices is None:
+            rc = L.sg_node_create(None, 0, C.byref(self.ptr))
+        else:
+            d = (C.c_int32 * len(devices))(*devices)
+            rc = L.sg_node_create(d, len(devices), C.byref(self.ptr))
+        if rc < 0:
+            raise SoundgenError(rc, "sg_node_create failed (no usable GPU?)")
+        self.size = int(L.sg_node_size(self.ptr))
+
+    def check(self, rc):
+        if rc < 0:
+            raise SoundgenError(rc, lib().sg_node_last_error(self.ptr).decode())
+        return rc
+
+    def close(self):
+        if self.ptr:
+            lib().sg_node_destroy(self.ptr)
             self.ptr = C.c_void_p()
 
     def __del__(self):

@@ -14,7 +14,7 @@ rm -f "$HERE"/_build/report.*
 ASAN_LIB=$(gcc -print-file-name=libasan.so)
 CXX_LIB=$(gcc -print-file-name=libstdc++.so.6)
 [ $# -gt 0 ] || set -- tests/test_planner.py tests/test_amp_build.py tests/test_oracle.py tests/test_loess_cursor.py \
-  tests/test_api_helpers.py tests/test_rrng.py tests/test_dist.py -m "not gpu"
+  tests/test_api_helpers.py tests/test_rrng.py tests/test_dist.py tests/test_node.py -m "not gpu"
 cd "$ROOT"
 rc=0
 env LD_PRELOAD="$ASAN_LIB $CXX_LIB" \

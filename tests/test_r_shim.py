@@ -27,7 +27,7 @@ MOCK = os.path.join(ROOT, "tests", "rmock")
 TOL = 1e-5
 
 ROUTINES = {"C_sg_generate_harmonics": 3, "C_sg_soundgen": 1, "C_sg_generate_noise": 4,
-            "C_sg_spectral_envelope": 5, "C_sg_formant_filter": 4, "C_sg_soundgen_batch": 1}
+            "C_sg_spectral_envelope": 5, "C_sg_formant_filter": 4, "C_sg_soundgen_batch": 2}
 REALSXP, INTSXP, VECSXP = 14, 13, 19
 
 
@@ -223,8 +223,10 @@ def sg_soundgen_args(R, call):
     return R.list(items)
 
 
-def r_soundgen_batch(R, calls):
-    out = R.call("C_sg_soundgen_batch", R.list([sg_soundgen_args(R, c) for c in calls], named=False))
+def r_soundgen_batch(R, calls, devices=None):
+    """soundgen_batch(calls, devices): the node of `devices` (NULL: every visible device)."""
+    dev = R.null() if devices is None else R.int_(devices)
+    out = R.call("C_sg_soundgen_batch", R.list([sg_soundgen_args(R, c) for c in calls], named=False), dev)
     assert R.L.rm_type(out) == VECSXP and R.L.rm_length(out) == len(calls)
     return [R.as_array(R.L.rm_elt(out, i)) for i in range(len(calls))]
 
@@ -260,13 +262,15 @@ def test_shim_argument_errors_unwind_like_stop(shim):
     with pytest.raises(RError, match="len must be"):
         R.call("C_sg_generate_noise", R.real(-1), R.null(), R.list([]), R.null())
     with pytest.raises(RError, match="list of argument lists"):
-        R.call("C_sg_soundgen_batch", R.real(1))
+        R.call("C_sg_soundgen_batch", R.real(1), R.null())
+    with pytest.raises(RError, match="integer vector of 1 to 64"):
+        R.call("C_sg_soundgen_batch", R.list([sg_soundgen_args(R, dict(sylLen=100))], named=False), R.real(0))
     with pytest.raises(RError, match="anchors must be numeric"):
         R.call("C_sg_soundgen", R.list([("pitchAnchors", R.list([("time", R.int_([0, 1])),
                                                                   ("value", R.int_([1, 2]))]))]))
     assert R.L.rm_protect_depth() == 0
     # an empty batch returns list() without touching the device
-    out = R.call("C_sg_soundgen_batch", R.list([], named=False))
+    out = R.call("C_sg_soundgen_batch", R.list([], named=False), R.null())
     assert R.L.rm_type(out) == VECSXP and R.L.rm_length(out) == 0
 
 
@@ -371,10 +375,19 @@ def test_shim_soundgen_and_batch_vs_oracle(shim, oracle):
     shim.L.rm_set_seed(11)
     batched = r_soundgen_batch(shim, SHIM_CALLS)
     _same_stream_position(shim, rr)
-    for i, (s, b, w) in enumerate(zip(single, batched, want)):
-        assert len(s) == len(b) == len(w), i
+    # the same batch over a 2-way node on device 0 (two shards, two streams): R's
+    # stream recorded in call order, the shards planned from it
+    shim.L.rm_set_seed(11)
+    node2 = r_soundgen_batch(shim, SHIM_CALLS, devices=[0, 0])
+    u_node = shim.L.rm_unif()
+    shim.L.rm_set_seed(11)
+    r_soundgen_batch(shim, SHIM_CALLS)
+    assert shim.L.rm_unif() == u_node  # both leave R's stream at one position
+    for i, (s, b, b2, w) in enumerate(zip(single, batched, node2, want)):
+        assert len(s) == len(b) == len(b2) == len(w), i
         assert _rms(s, w) <= TOL, i
         np.testing.assert_array_equal(s, b)
+        np.testing.assert_array_equal(b, b2)
 
 
 @pytest.mark.gpu
