@@ -51,7 +51,8 @@ def test_node_r_stream_equals_single_plan():
     args = [dict(sylLen=150 + 40 * i, temperature=0.15, samplingRate=22050, addSilence=0, formants="i",
                  noiseAnchors={"time": [0, 150], "value": [-30, -20]},
                  pitchAnchors={"time": [0, 1], "value": [140 + 15 * i, 110]}) for i in range(8)]
-    p1, y1 = _single([{"kind": "soundgen", "args": a, "rng": RRng(21)} for a in args])
+    g1 = RRng(21)  # one stream for the whole batch, as R's
+    p1, y1 = _single([{"kind": "soundgen", "args": a, "rng": g1} for a in args])
     node = native.Node([0, 0])
     g = RRng(21)
     p2 = batch.NodePlan([{"kind": "soundgen", "args": a, "rng": g} for a in args], node)
