@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SG_ABI_VERSION 4
+#define SG_ABI_VERSION 3
 
 enum {
   SG_OK = 0,
@@ -283,9 +283,6 @@ int sg_plan_table_stats(const sg_plan* plan, int64_t* tables, int64_t* samples, 
  * output samples, algorithmic HBM bytes (source/uniforms + envelope columns +
  * output) and nominal flops (5 wl log2 wl per transform). */
 int sg_plan_stft_stats(const sg_plan* plan, int64_t* samples, int64_t* alg_bytes, double* flops);
-/* Spectral-envelope columns of the plan (R/sourceSpectrum.R:507-541) evaluated
- * inside sg_stft_ola frames, and materialised by sg_spec_env (sg_set_envelope_fusion). ABI 4. */
-int sg_plan_env_stats(const sg_plan* plan, int64_t* cols_evaluated, int64_t* cols_materialised);
 /* Precision path of the plan (ABI 2): per call, the number of its bouts whose
  * formant filter runs in fp64 (source, pre-filter mix and forward STFT; the
  * planner's conditioning estimate of the fp32 round-off through the envelope
@@ -357,13 +354,6 @@ int sg_set_amp_policy(int32_t host_built);
  * copied into the plan (the same values either way; tests compare the two).
  * The arrays are read during sg_plan_batch only. */
 int sg_set_uniform_gather(int32_t on);
-/* Process-wide handling of spectral-envelope columns for later sg_plan_batch
- * calls, a bit mask: bit 0 formant-filter columns, bit 1 noise-filter columns.
- * A set bit (default 3) evaluates a column read only by sg_stft_ola frames in
- * the frame that uses it (not written to HBM and read back); a clear bit
- * materialises the columns by sg_spec_env first. The same bits either way
- * (tests compare them). SG_E_ARG outside 0..3. ABI 4. */
-int sg_set_envelope_fusion(int32_t on);
 /* Process-wide switch of the sine bank's wavetable path, for plans uploaded
  * later (sg_plan_upload, or the first sg_execute of a plan): 1 (default)
  * long runs of constant-amplitude, linear-phase tasks (static tones) sample a

@@ -188,12 +188,6 @@ class Plan:
         return dict(harm_samples=v[0].value, harm_terms=v[1].value, harm_amp_bytes=v[2].value,
                     fft_frames=v[3].value, stft_samples=w[0].value, stft_bytes=w[1].value, stft_flops=w[2].value)
 
-    def env_stats(self):
-        """Spectral-envelope columns (evaluated inside sg_stft_ola, materialised by sg_spec_env)."""
-        ev, mat = C.c_int64(), C.c_int64()
-        native.check(native.lib().sg_plan_env_stats(self.ptr, C.byref(ev), C.byref(mat)))
-        return ev.value, mat.value
-
     def table_stats(self):
         """Wavetable spans of the uploaded plan: (tables, samples, terms)."""
         v = [C.c_int64() for _ in range(3)]

@@ -750,13 +750,6 @@ int sg_plan_stft_stats(const sg_plan* plan, int64_t* samples, int64_t* alg_bytes
   return SG_OK;
 }
 
-int sg_plan_env_stats(const sg_plan* plan, int64_t* cols_evaluated, int64_t* cols_materialised) {
-  if (!plan || !cols_evaluated || !cols_materialised) return SG_E_ARG;
-  *cols_evaluated = plan->B.env_cols_fused;
-  *cols_materialised = plan->B.env_cols_mat;
-  return SG_OK;
-}
-
 int64_t sg_plan_amp_count(const sg_plan* plan) { return plan && !plan->host_released ? plan->B.amp_total : 0; }
 
 int sg_plan_debug_amps(const sg_plan* plan, float* out, int64_t n) {

@@ -253,21 +253,9 @@ constexpr int SG_FRAME_FILTER = 0;  // fs sound -> hamming -> FFT/wl -> x env ->
 constexpr int SG_FRAME_NOISE = 1;   // fl uniforms x fl filter (real spectrum)  -> ISTFT/wl -> x hann
 struct SgFrame {
   int64_t src;  // FILTER: fs offset of the frame's first sound sample; NOISE: fl offset of nr uniforms
-  int64_t env;  // fl offset of the nr envelope (FILTER) / filter (NOISE) values (ejob < 0)
+  int64_t env;  // fl offset of the nr envelope (FILTER) / filter (NOISE) values
   int64_t dst;  // fs offset of the wl windowed ISTFT outputs
-  // ejob >= 0: the envelope is column ecol of SgEnvJob ejob, evaluated by sg_stft_ola
-  // where the frame uses it (sgd::env_bin) instead of read from the envelope area
-  int32_t ejob, ecol;
 };
-// Dynamic LDS of a sg_stft_ola launch (sg_fft.hip stft_ola_body): twiddles, windows and
-// the waves' frame slices; for M = 1102 the radix-29 fragment table; the log2(k) table
-// (fp64, M entries) when the launch evaluates envelope columns; and for the filter's
-// M = 1102 path the table's slot plus each wave's envelope pairs (M / 2 + 1 float2)
-constexpr int sg_stft_lds(int phase, int M, bool env) {
-  const bool spec_filter = phase == 1 && M == 1102;
-  return (sg_fft_waves(phase) + 4) * M * 8 + (M == 1102 ? 2048 : 0) + (env || spec_filter ? M * 8 : 0) +
-         (spec_filter ? sg_fft_waves(phase) * (M / 2 + 1) * 8 : 0);
-}
 // A formant-filter frame of an ill-conditioned call (sg_fft_frames64): the fp64
 // sound fh[src .. src + wl) -> hamming -> fp64 DFT / wl -> x env (fp32 envelope
 // area / fl) -> fp64 inverse DFT / 2M -> x hann -> fs[dst .. dst + wl) (fp32, for sg_ola)
@@ -396,8 +384,7 @@ struct SgEnvCol {
   float lip, boost;
 };
 struct SgEnvJob {
-  int64_t out;     // offset of the nr x nc output in the envelope area (fl + fe_base on the device);
-                   // -1 after finalize_spec when every reader is a sg_stft_ola frame (not materialised)
+  int64_t out;     // offset of the nr x nc output in the envelope area (fl + fe_base on the device)
   int64_t term0;   // SgEnvTerm of column c, track t: term0 + c * ntr + t
   int64_t col0;    // SgEnvCol of column c: col0 + c
   int32_t nr, nc, ntr;

@@ -21,24 +21,53 @@
 #include <hip/hip_runtime.h>
 
 #include "sg_dev.h"
-#include "sg_envfn.h"
 
 constexpr int SG_ENV_LG_LDS = 2048;  // log2(k) table entries staged in LDS per workgroup (r02: 4.9 -> 3.8 ms)
 
 // One column of a job: per 64-bin chunk, the tracks whose bands reach it (ballot),
-// their parameters by scalar loads (sgd::env_bin); LG: log2(k) from the LDS copy.
+// their parameters by scalar loads; LG: log2(k) from the LDS copy.
 template <bool LG>
 __device__ __forceinline__ void env_column(const SgEnvJob& J, int c, const SgEnvTerm* __restrict__ tm,
                                            const SgEnvCol& C, const double* __restrict__ lg2, const double* lgs,
                                            float* __restrict__ fe, int lane) {
-  const sgd::EnvLane<2> L = sgd::env_lane<2>(tm, J.ntr, lane);
+  const float thrf = -SG_ENV_CUT;  // log2 units
+  // lane t: term t (group 0) and term 64 + t (group 1); absent terms get an empty range
+  float amp[2];
+  int klo[2], khi[2];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int t = g * 64 + lane;
+    const bool in = t < J.ntr;
+    const SgEnvTerm& e = tm[in ? t : 0];
+    amp[g] = (float)e.amp;
+    klo[g] = in ? e.klo : 1 << 30;
+    khi[g] = in ? e.khi : -1;
+  }
   float* __restrict__ dst = fe + J.out + (int64_t)c * J.nr;
 #pragma unroll 1
   for (int k0 = 0; k0 < J.nr; k0 += 64) {
     const int k = k0 + lane;
+    const double x = (double)(k + 1);
     const double lx = LG ? lgs[k] : lg2[k];
-    const float v = sgd::env_bin(L, tm, C.lip, C.boost, J.slope, k, lx, k0 + 1, k0 + 64);
-    if (k < J.nr) dst[k] = v;
+    float acc = 0.f;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      uint64_t m = __ballot(klo[g] <= k0 + 64 && khi[g] >= k0 + 1);
+      while (m) {
+        const int t = __builtin_ctzll(m);
+        m &= m - 1;
+        const SgEnvTerm* __restrict__ e = tm + g * 64 + t;  // wave-uniform: scalar loads into SGPRs
+        const double a = e->A, r = e->Rr, l = e->Lm;
+        const float am = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amp[g]), t));
+        const double d = fma(a, lx, fma(-r, x, -l));
+        // d > thr >= -126: the raw v_exp_f32 is exact enough and never denormal
+        const float df = (float)d;
+        if (df > thrf) acc = fmaf(am, __builtin_amdgcn_exp2f(df), acc);
+      }
+    }
+    const float lxf = (float)lx;
+    const float v = fmaf(fmaf(C.lip, lxf, acc), C.boost, J.slope * lxf);
+    if (k < J.nr) dst[k] = exp2f(v * 0.1f);
   }
 }
 

@@ -697,7 +697,7 @@ void device_execute_spec(const Batch& B, const DevicePlan& D, float* d_out, hipS
       HIPCHK(hipEventCreate(&e1));
       HIPCHK(hipEventRecord(e0, s));
     }
-    launch_stft_ola(D, ph, B.seg_range[ph][0], nseg, B.fgroup_lds[ph][0], B.env_fused[ph], s);
+    launch_stft_ola(D, ph, B.seg_range[ph][0], nseg, B.fgroup_lds[ph][0], s);
     if (prof && nseg > 0) {
       HIPCHK(hipEventRecord(e1, s));
       prof->push_back({SG_PROF_STFT_OLA, e0, e1});

@@ -134,8 +134,7 @@ void launch_mix_hp(const DevicePlan& D, int64_t t0, int64_t n_tiles, hipStream_t
 void launch_fft_frames64(const DevicePlan& D, const Batch& B, int ph, hipStream_t s);
 // sg_fft.hip
 void launch_fft_frames(const DevicePlan& D, int64_t g0, int64_t n_groups, int lds_bytes, hipStream_t s);
-void launch_stft_ola(const DevicePlan& D, int phase, int64_t s0, int64_t n_segs, int lds_bytes, bool env,
-                     hipStream_t s);
+void launch_stft_ola(const DevicePlan& D, int phase, int64_t s0, int64_t n_segs, int lds_bytes, hipStream_t s);
 void launch_ola(const DevicePlan& D, int64_t t0, int64_t n_tiles, hipStream_t s);
 void launch_ola_max(const DevicePlan& D, int64_t o0, int64_t n_olas, hipStream_t s);
 void launch_fft_probe(const SgFftGeom* geom, const float* fl, float* data, int M, int nframes, int inverse,

@@ -22,7 +22,6 @@
 
 #include "sg_dev.h"
 #include "sg_devfn.h"
-#include "sg_envfn.h"
 #include "sg_roots.h"
 
 namespace {
@@ -765,136 +764,37 @@ struct FramePf {
   __device__ __forceinline__ const float2& b(int i) const { return s[i]; }
 };
 
-// Envelope columns evaluated in the frame (SgFrame::ejob >= 0): the job tables and the
-// workgroup's LDS copy of log2(k), k = 1..M
-struct EnvSrc {
-  const SgEnvJob* __restrict__ jobs;
-  const SgEnvTerm* __restrict__ terms;
-  const SgEnvCol* __restrict__ cols;
-  const double* lgs;
-};
-
-// Column F.ecol of job F.ejob, evaluated pair by pair where frame_front uses it (its
-// temporaries never meet the transform's registers)
-struct EnvCol {
-  const SgEnvTerm* __restrict__ tm;
-  const double* lgs;
-  float lip, boost, slope;
-  sgd::EnvLane<1, true> L;  // the planner evaluates columns of <= 64 tracks only
-};
-__device__ __forceinline__ EnvCol env_col(const SgFrame& F, const EnvSrc& E, int lane) {
-  const SgEnvJob J = E.jobs[F.ejob];
-  EnvCol c;
-  c.tm = E.terms + J.term0 + (int64_t)F.ecol * J.ntr;
-  c.lgs = E.lgs;
-  const SgEnvCol C = E.cols[J.col0 + F.ecol];
-  c.lip = C.lip;
-  c.boost = C.boost;
-  c.slope = J.slope;
-  c.L = sgd::env_lane<1, true>(c.tm, J.ntr, lane);
-  return c;
-}
-// Pair i of the prefetch layout: (env[k], env[M - k]), k = 64 i + lane (k = 0: env[0],
-// env[M - 1]); lanes past half evaluate bin half. The wave evaluates two 64-bin ranges,
-// [64 i, 64 i + 63] and its mirror, each summing only the tracks whose bands reach it
-// (sgd::env_bin: the same bits as sg_spec_env). Every lane must call it.
-__device__ __forceinline__ float2 env_pair(const EnvCol& c, int i, int M, int lane) {
-  const int half = M / 2;
-  const int k = min(64 * i + lane, half);
-  const int km = k == 0 ? M - 1 : M - k;
-  const float x = sgd::env_bin(c.L, c.tm, c.lip, c.boost, c.slope, k, c.lgs[k], 64 * i + 1, 64 * i + 64);
-  const int mlo = i == 0 ? M - 62 : M - 64 * i - 62, mhi = i == 0 ? M : M - 64 * i + 1;  // 1-based
-  const float y = sgd::env_bin(c.L, c.tm, c.lip, c.boost, c.slope, km, c.lgs[km], mlo, mhi);
-  return make_float2(x, y);
-}
-__device__ __forceinline__ float lane_value(float v, int l) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
-}
-// The frame's envelope pairs (env[k], env[M - k]), k <= half (k = 0: env[0], env[M - 1]).
-// Specialised path (CM > 0): staged in LDS at EV[k] before the frame's loads -- the
-// filter's in the wave's envelope area (read by the untangle after the forward FFT,
-// so no registers are held across the transform), the noise's in the frame slice
-// (read by the packing) -- evaluated (F.ejob >= 0) or copied from the materialised
-// column. Generic path: the materialised column into the P.a / P.b registers (the
-// planner evaluates columns only for the specialised geometry).
-template <int CM>
 __device__ __forceinline__ void frame_prefetch(FramePf& P, const SgFrame& F, int mode, int M,
-                                               const float* __restrict__ fl, const float* __restrict__ fs,
-                                               const EnvSrc& E, float2* EV, int lane) {
+                                               const float* __restrict__ fl, const float* __restrict__ fs, int lane) {
   const int half = M / 2;
-  if (CM != 0 && mode == SG_FRAME_NOISE) {  // the uniforms' loads in flight while the filter pairs are staged
-    const float* u = fl + F.src;
-#pragma unroll
-    for (int i = 0; i < SG_PF_PAIR; ++i) {
-      const int k = 64 * i + lane;
-      if (k <= half) P.a[i] = make_float2(u[k], u[k == 0 ? M - 1 : M - k]);
-    }
-    P.xh = u[half];
-  }
-  if (CM != 0 && mode == SG_FRAME_FILTER) {  // the sound's loads in flight while the envelope pairs are staged
+  if (mode == SG_FRAME_FILTER) {
     const float* src = fs + F.src;
+    const float* env = fl + F.env;
 #pragma unroll
     for (int i = 0; i < SG_PF_SRC; ++i) {
       const int n = 64 * i + lane;
       if (n < M) P.s[i] = make_float2(src[2 * n], src[2 * n + 1]);
     }
-  }
-  if constexpr (CM != 0) {
-    if (F.ejob >= 0) {
-      // the lane index made opaque per frame: the bins' LDS addresses are recomputed here
-      // instead of hoisted out of the frame loop into registers held across it
-      int ln = lane;
-      __asm__ __volatile__("" : "+v"(ln));
-      const EnvCol c = env_col(F, E, ln);
 #pragma unroll
-      for (int i = 0; i < SG_PF_PAIR; ++i) {
-        if (64 * i > half) continue;
-        const float2 pr = env_pair(c, i, M, ln);
-        if (64 * i + ln <= half) EV[64 * i + ln] = pr;
-      }
-    } else {
-      const float* env = fl + F.env;
-#pragma unroll
-      for (int i = 0; i < SG_PF_PAIR; ++i) {
-        const int k = 64 * i + lane;
-        if (k <= half) EV[k] = make_float2(env[k], env[k == 0 ? M - 1 : M - k]);
-      }
+    for (int i = 0; i < SG_PF_PAIR; ++i) {
+      const int k = 64 * i + lane;
+      if (k <= half) P.a[i] = make_float2(env[k], env[k == 0 ? M - 1 : M - k]);
     }
-    sg_wave_fence();  // lane 0 reads EV[half]
-  }
-  if (mode == SG_FRAME_FILTER) {
-    if constexpr (CM == 0) {
-      const float* env = fl + F.env;
-#pragma unroll
-      for (int i = 0; i < SG_PF_PAIR; ++i) {
-        const int k = 64 * i + lane;
-        if (k <= half) P.a[i] = make_float2(env[k], env[k == 0 ? M - 1 : M - k]);
-      }
-      P.xh = env[half];
-      const float* src = fs + F.src;
-#pragma unroll
-      for (int i = 0; i < SG_PF_SRC; ++i) {
-        const int n = 64 * i + lane;
-        if (n < M) P.s[i] = make_float2(src[2 * n], src[2 * n + 1]);
-      }
-    }
+    P.xh = env[half];
   } else {
-    if constexpr (CM == 0) {
-      const float* flt = fl + F.env;
+    const float* u = fl + F.src;
+    const float* flt = fl + F.env;
 #pragma unroll
-      for (int i = 0; i < SG_PF_PAIR; ++i) {
-        const int k = 64 * i + lane;
-        if (k <= half) P.b(i) = make_float2(flt[k], flt[k == 0 ? M - 1 : M - k]);
+    for (int i = 0; i < SG_PF_PAIR; ++i) {
+      const int k = 64 * i + lane;
+      if (k <= half) {
+        const int km = k == 0 ? M - 1 : M - k;
+        P.a[i] = make_float2(u[k], u[km]);
+        P.b(i) = make_float2(flt[k], flt[km]);
       }
-      P.xh2 = flt[half];
-      const float* u = fl + F.src;
-#pragma unroll
-      for (int i = 0; i < SG_PF_PAIR; ++i) {
-        const int k = 64 * i + lane;
-        if (k <= half) P.a[i] = make_float2(u[k], u[k == 0 ? M - 1 : M - k]);
-      }
-      P.xh = u[half];
     }
+    P.xh = u[half];
+    P.xh2 = flt[half];
   }
 }
 
@@ -904,7 +804,7 @@ __device__ __forceinline__ void frame_prefetch(FramePf& P, const SgFrame& F, int
 template <int CM, int R0, int R1, int R2>
 __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mode, const SgFftGeom& g,
                                             const float2* twS, const float2* twN, const float* ham,
-                                            const float4* A29, const float2* EV, int lane SG_ST_PARAMS) {
+                                            const float4* A29, int lane SG_ST_PARAMS) {
   int M = CM ? CM : g.M, N = CM ? 2 * CM : g.wl;
   if (!CM) __asm__ __volatile__("" : "+s"(M), "+s"(N));  // opaque: no hoisting across the caller's frame loop
   const float invN = 1.f / (float)N;
@@ -948,8 +848,7 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
         const float2 o = make_float2(0.5f * dd.y, -0.5f * dd.x);
         return cadd(e, cmul(o, twN[t]));
       };
-      const float2 ep = CM ? EV[kk] : P.a[i];  // (env[k], env[M - k]); k = 0: env[0], env[M - 1]
-      const float ek = ep.x * invN, em = ep.y * invN;
+      const float ek = P.a[i].x * invN, em = P.a[i].y * invN;  // k = 0: env[0], env[M - 1]
       if (kk == 0) {
         const float2 x0 = X_at(za, za, 0), xl = X_at(zM1, z1, M - 1);
         const float y0 = x0.x * ek;
@@ -957,7 +856,7 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
         A[0] = make_float2(y0 + nyq, y0 - nyq);
         if (M % 2 == 0) {
           const float2 xk = X_at(zh, zh, half);
-          const float eh = (CM ? EV[half].x : P.xh) * invN;
+          const float eh = P.xh * invN;
           const float2 yk = make_float2(xk.x * eh, xk.y * eh);
           float2 a, b;
           pack_pair(yk, yk, twN[half], a, b);
@@ -982,19 +881,15 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
       }
     }
   } else {  // SG_FRAME_NOISE: real spectrum u x filter, packed
-    // CM: the filter pairs are in the slice (EV == A); a lane's writes go to its own pair
-    // slot k and to slot M - k > half, which holds no pair; lane 0 reads f[half] first
-    const float fh = CM ? EV[half].x : P.xh2;
 #pragma unroll
     for (int i = 0; i < SG_PF_PAIR; ++i) {
       const int k = 64 * i + lane;
       if (k > half) continue;
-      const float2 fp = CM ? EV[k] : P.b(i);  // (f[k], f[M - k])
       if (k == 0) {
-        const float y0 = P.a[i].x * fp.x, nyq = P.a[i].y * fp.y;
+        const float y0 = P.a[i].x * P.b(i).x, nyq = P.a[i].y * P.b(i).y;
         A[0] = make_float2(y0 + nyq, y0 - nyq);
         if (M % 2 == 0) {
-          const float2 yk = make_float2(P.xh * fh, 0.f);
+          const float2 yk = make_float2(P.xh * P.xh2, 0.f);
           float2 a, b;
           pack_pair(yk, yk, twN[half], a, b);
           A[half] = a;
@@ -1002,7 +897,7 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
       } else if (k < M - k) {
         // pack_pair of the real Y_k = a, Y_{M-k} = b: with e = a + b, r = a - b,
         // Z'_k = (e + r Im W, r Re W), Z'_{M-k} = (e - r Im W, r Re W)
-        const float a = P.a[i].x * fp.x, b = P.a[i].y * fp.y;
+        const float a = P.a[i].x * P.b(i).x, b = P.a[i].y * P.b(i).y;
         const float2 w = twN[k];
         const float e = a + b, r = a - b, im = r * w.x;
         A[k] = make_float2(fmaf(r, w.y, e), im);
@@ -1030,7 +925,7 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
                                              const SgFrame* __restrict__ frames, const SgFftGeom& g,
                                              const float* __restrict__ fl, float* __restrict__ fs,
                                              float* __restrict__ slotmax, float2* twS, const float2* twN,
-                                             const float* ham, const float* han, const EnvSrc& E, int w, int lane) {
+                                             const float* ham, const float* han, int w, int lane) {
   const int M = CM ? CM : g.M, N = CM ? 2 * CM : g.wl;
   const int mode = MODE;  // the launch's phase fixes it (noise: phase 0, filter: phase 1)
   const SgOla& O = olas[S.ola];
@@ -1049,9 +944,6 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
   FramePf P;
   constexpr int W = MODE == SG_FRAME_NOISE ? SG_FFT_WAVES_NOISE : SG_FFT_WAVES;
   const float4* A29 = reinterpret_cast<const float4*>(twS + M * (4 + W));  // radix-29 fragments (M = 1102)
-  // the envelope pairs of the specialised path (frame_prefetch): the filter's in the
-  // wave's area after the log2 table (sg_stft_lds), the noise's in the frame slice
-  float2* EV = MODE == SG_FRAME_FILTER ? reinterpret_cast<float2*>(const_cast<double*>(E.lgs) + M) + w * (M / 2 + 1) : A;
 #ifdef SG_STFT_STAMPS
   uint64_t st_accv[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t st_lastv = __builtin_amdgcn_s_memtime();
@@ -1063,9 +955,9 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
     {
       int Mk = M;
       if (!CM) __asm__ __volatile__("" : "+s"(Mk));
-      frame_prefetch<CM>(P, frames[S.fdev + k], mode, Mk, fl, fs, E, EV, lane);
+      frame_prefetch(P, frames[S.fdev + k], mode, Mk, fl, fs, lane);
     }
-    frame_front<CM, R0, R1, R2>(A, P, mode, g, twS, twN, ham, A29, EV, lane SG_ST_ARGS);
+    frame_front<CM, R0, R1, R2>(A, P, mode, g, twS, twN, ham, A29, lane SG_ST_ARGS);
     SG_ST(4);
     if constexpr (CM != 0) fft_wc<true, CM, R0, R1, R2, MODE == SG_FRAME_FILTER>(A, twS, A29, lane SG_ST_ARGS);
     else fft_w<true>(A, g, twS, lane SG_ST_ARGS);
@@ -1161,7 +1053,7 @@ template <int MODE>
 __device__ __forceinline__ void stft_ola_body(
     const SgSegment* __restrict__ segs, const SgOla* __restrict__ olas, const SgFrame* __restrict__ frames,
     const SgFftGeom* __restrict__ geoms, const float* __restrict__ fl, float* __restrict__ fs,
-    float* __restrict__ slotmax, EnvSrc E, const double* __restrict__ elog2) {
+    float* __restrict__ slotmax) {
   constexpr int W = MODE == SG_FRAME_NOISE ? SG_FFT_WAVES_NOISE : SG_FFT_WAVES, NT = W * 64;
   extern __shared__ float4 lds4[];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // w wave-uniform
@@ -1183,20 +1075,14 @@ __device__ __forceinline__ void stft_ola_body(
     const float hs = 1.f / (float)N;
     for (int t = threadIdx.x; t < 2 * N; t += NT) ham[t] = t < N ? wg[t] : wg[t] * hs;
     if (MODE == SG_FRAME_FILTER && geom_1102(g)) mat29_fill(reinterpret_cast<float4*>(twS + M * (4 + W)), tng, threadIdx.x);
-    // log2(k), k = 1..M, after the frame slices and the radix-29 table (sg_stft_lds),
-    // when the launch evaluates envelope columns (elog2 non-null)
-    double* lgs = reinterpret_cast<double*>(twS + M * (4 + W) + (MODE == SG_FRAME_FILTER && M == 1102 ? SG_MAT29_BYTES / 8 : 0));
-    if (elog2)
-      for (int t = threadIdx.x; t < M; t += NT) lgs[t] = elog2[t];
-    E.lgs = lgs;
   }
   __syncthreads();
   const SgSegment S = segs[blockIdx.x * W + w];
   if (S.nf <= 0) return;  // padding segment
   if (geom_1102(g))
-    stft_segment<1102, 29, 19, 2, MODE>(S, olas, frames, g, fl, fs, slotmax, twS, twN, ham, han, E, w, lane);
+    stft_segment<1102, 29, 19, 2, MODE>(S, olas, frames, g, fl, fs, slotmax, twS, twN, ham, han, w, lane);
   else
-    stft_segment<0, 0, 0, 0, MODE>(S, olas, frames, g, fl, fs, slotmax, twS, twN, ham, han, E, w, lane);
+    stft_segment<0, 0, 0, 0, MODE>(S, olas, frames, g, fl, fs, slotmax, twS, twN, ham, han, w, lane);
 }
 
 constexpr int SG_FFT_WPE = 2;  // waves per SIMD of sg_stft_ola (241 VGPRs)
@@ -1204,15 +1090,15 @@ constexpr int SG_FFT_WPE_NOISE = SG_FFT_WAVES_NOISE > 8 ? 3 : 2;
 extern "C" __global__ __launch_bounds__(SG_FFT_WAVES * 64) __attribute__((amdgpu_waves_per_eu(SG_FFT_WPE))) void sg_stft_ola(
     const SgSegment* __restrict__ segs, const SgOla* __restrict__ olas, const SgFrame* __restrict__ frames,
     const SgFftGeom* __restrict__ geoms, const float* __restrict__ fl, float* __restrict__ fs,
-    float* __restrict__ slotmax, EnvSrc env, const double* __restrict__ elog2) {
-  stft_ola_body<SG_FRAME_FILTER>(segs, olas, frames, geoms, fl, fs, slotmax, env, elog2);
+    float* __restrict__ slotmax) {
+  stft_ola_body<SG_FRAME_FILTER>(segs, olas, frames, geoms, fl, fs, slotmax);
 }
 // generateNoise()'s istft (phase 0): the noise mode only
 extern "C" __global__ __launch_bounds__(SG_FFT_WAVES_NOISE * 64) __attribute__((amdgpu_waves_per_eu(SG_FFT_WPE_NOISE))) void sg_stft_ola_noise(
     const SgSegment* __restrict__ segs, const SgOla* __restrict__ olas, const SgFrame* __restrict__ frames,
     const SgFftGeom* __restrict__ geoms, const float* __restrict__ fl, float* __restrict__ fs,
-    float* __restrict__ slotmax, EnvSrc env, const double* __restrict__ elog2) {
-  stft_ola_body<SG_FRAME_NOISE>(segs, olas, frames, geoms, fl, fs, slotmax, env, elog2);
+    float* __restrict__ slotmax) {
+  stft_ola_body<SG_FRAME_NOISE>(segs, olas, frames, geoms, fl, fs, slotmax);
 }
 
 // Test probe: wavefront w transforms frame w (M complex points, in place) with
@@ -1715,8 +1601,7 @@ void launch_fft_frames(const DevicePlan& D, int64_t g0, int64_t n_groups, int ld
                      D.geoms, D.fl, D.fs);
   SG_LAUNCHED("sg_fft_frames");
 }
-void launch_stft_ola(const DevicePlan& D, int phase, int64_t s0, int64_t n_segs, int lds_bytes, bool env,
-                     hipStream_t s) {
+void launch_stft_ola(const DevicePlan& D, int phase, int64_t s0, int64_t n_segs, int lds_bytes, hipStream_t s) {
   if (n_segs <= 0) return;
   auto* k = phase == 0 ? &sg_stft_ola_noise : &sg_stft_ola;
   lds_opt_in(reinterpret_cast<const void*>(k), lds_bytes, phase == 0 ? "sg_stft_ola_noise" : "sg_stft_ola");
@@ -1724,8 +1609,7 @@ void launch_stft_ola(const DevicePlan& D, int phase, int64_t s0, int64_t n_segs,
   if (n_segs % W) throw SgError(SG_E_DEVICE, "sg_stft_ola: segment count not a multiple of the workgroup's waves");
   hipLaunchKernelGGL(k, dim3((unsigned)(n_segs / W)), dim3(W * 64), lds_bytes, s,
                      D.olasegs + s0,
-                     D.olas, D.frames, D.geoms, D.fl, D.fs, D.olatilemax, EnvSrc{D.envjobs, D.eterms, D.ecols, nullptr},
-                     env ? D.elog2 : nullptr);
+                     D.olas, D.frames, D.geoms, D.fl, D.fs, D.olatilemax);
   SG_LAUNCHED("sg_stft_ola");
 }
 void launch_fft_probe(const SgFftGeom* geom, const float* fl, float* data, int M, int nframes, int inverse,

@@ -134,10 +134,6 @@ struct Batch {
   // geometries run fused in sg_stft_ola, fgroup_lds[ph][0] = its dynamic LDS)
   int64_t fgroup_range[2][3] = {{0, 0, 0}, {0, 0, 0}};
   int fgroup_lds[2][2] = {{0, 0}, {0, 0}};  // max dynamic LDS per phase and kernel
-  // sg_stft_ola evaluates envelope columns in the frame (SgFrame::ejob) in this phase;
-  // env_cols_fused / env_cols_mat: columns evaluated there / materialised by sg_spec_env
-  bool env_fused[2] = {false, false};
-  int64_t env_cols_fused = 0, env_cols_mat = 0;
   std::vector<SgOla> olas_dev;
   std::vector<SgOlaTile> olatiles;
   int64_t olatile_split = 0, ola_split = 0;

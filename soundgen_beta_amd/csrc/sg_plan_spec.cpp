@@ -769,112 +769,9 @@ int64_t plan_envelope(Batch& B, Rng& R, double nrd, int64_t nc, const sg_formant
 }
 
 // ------------------------------------------------------------ finalize
-// Envelope columns read only by sg_stft_ola frames are evaluated there, in the frame
-// that uses them (SgFrame::ejob, sgd::env_bin: the same bits as sg_spec_env), instead
-// of written to the envelope area by sg_spec_env and read back (C5: ~56 GB of HBM
-// traffic per step). Jobs with another reader (sg_fft_frames, the fp64 frames, or
-// none: sg_spectral_envelope copies its job to the host) stay materialised, and the
-// envelope area is repacked over them. sg_set_envelope_fusion(0) materialises every
-// job (the A/B and byte-equality tests); 1 / 2 evaluate the filter / noise columns only.
-std::atomic<int> g_env_fusion{3};
-
-static void plan_env_fusion(Batch& B) {
-  const size_t nj = B.envjobs.size();
-  B.env_fused[0] = B.env_fused[1] = false;
-  B.env_cols_fused = B.env_cols_mat = 0;
-  std::vector<int64_t> ord(nj);
-  for (size_t j = 0; j < nj; ++j) ord[j] = (int64_t)j;
-  std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) { return B.envjobs[a].out < B.envjobs[b].out; });
-  auto job_of = [&](int64_t enc, int64_t& col) -> int64_t {  // encoded frame offset -(off + 1)
-    const int64_t off = -enc - 1;
-    auto it = std::upper_bound(ord.begin(), ord.end(), off,
-                               [&](int64_t v, int64_t j) { return v < B.envjobs[j].out; });
-    if (it == ord.begin()) throw SgError(SG_E_DEVICE, "envelope offset before every job (planner bug)");
-    const int64_t j = *(it - 1);
-    const SgEnvJob& J = B.envjobs[j];
-    const int64_t rel = off - J.out;
-    if (rel % J.nr || rel / J.nr >= J.nc) throw SgError(SG_E_DEVICE, "envelope offset not a job column (planner bug)");
-    col = rel / J.nr;
-    return j;
-  };
-  // a phase evaluates columns only if every sg_stft_ola geometry of it has LDS for the log2 table
-  bool fits[2] = {true, true};
-  for (int ph = 0; ph < 2; ++ph)
-    for (int gi : B.frame_geom[ph]) {
-      const SgFftGeom& g = B.geoms[gi];
-      if (g.kind == SG_FFT_WAVE && sg_stft_lds(ph, g.M, true) > 160 * 1024) fits[ph] = false;
-    }
-  const int mask = g_env_fusion.load();  // bit 0: formant-filter frames, bit 1: noise frames
-  std::vector<uint8_t> use(nj, 0);  // bit 0: a sg_stft_ola frame reads the job; bit 1: another reader
-  std::vector<int64_t> nread(nj, 0);
-  std::vector<int64_t> fj[2], fc[2];
-  for (int ph = 0; ph < 2; ++ph) {
-    fj[ph].assign(B.frames[ph].size(), -1);
-    fc[ph].assign(B.frames[ph].size(), 0);
-    for (size_t i = 0; i < B.frames[ph].size(); ++i) {
-      const SgFrame& f = B.frames[ph][i];
-      if (f.env >= 0) continue;
-      const int64_t j = job_of(f.env, fc[ph][i]);
-      fj[ph][i] = j;
-      const SgFftGeom& g = B.geoms[B.frame_geom[ph][i]];
-      // sg_stft_ola's specialised M = 1102 path (radices 29, 19, 2: sg_fft.hip geom_1102)
-      const bool spec = g.kind == SG_FFT_WAVE && g.M == 1102 && g.nstages == 3 && g.radix[0] == 29 &&
-                        g.radix[1] == 19 && g.radix[2] == 2;
-      const bool on = mask & (ph == 1 ? 1 : 2);
-      const bool wave = on && fits[ph] && spec && B.envjobs[j].nr == g.M && B.envjobs[j].ntr <= 64;
-      use[j] |= wave ? 1 : 2;
-      ++nread[j];
-    }
-  }
-  // a column shared by many frames (static formants: one column for the whole bout)
-  // is cheaper read from L2 than evaluated per frame
-  for (size_t j = 0; j < nj; ++j)
-    if (use[j] == 1 && nread[j] > 2 * (int64_t)B.envjobs[j].nc) use[j] = 3;
-  std::vector<int64_t> gj(B.frames64.size(), -1), gc(B.frames64.size(), 0);
-  for (size_t i = 0; i < B.frames64.size(); ++i)
-    if (B.frames64[i].env < 0) {
-      gj[i] = job_of(B.frames64[i].env, gc[i]);
-      use[gj[i]] |= 2;
-    }
-  // the materialised jobs, repacked in their order
-  std::vector<int64_t> nout(nj, -1);
-  int64_t tot = 0;
-  for (int64_t j : ord) {
-    const SgEnvJob& J = B.envjobs[j];
-    if (use[j] == 1) {
-      B.env_cols_fused += J.nc;
-      continue;
-    }
-    nout[j] = tot;
-    tot += ((int64_t)J.nr * J.nc + 63) / 64 * 64;
-    B.env_cols_mat += J.nc;
-  }
-  for (int ph = 0; ph < 2; ++ph)
-    for (size_t i = 0; i < B.frames[ph].size(); ++i) {
-      SgFrame& f = B.frames[ph][i];
-      f.ejob = -1;
-      f.ecol = 0;
-      const int64_t j = fj[ph][i];
-      if (j < 0) continue;
-      if (use[j] == 1) {
-        f.ejob = (int32_t)j;
-        f.ecol = (int32_t)fc[ph][i];
-        f.env = 0;
-        B.env_fused[ph] = true;
-      } else {
-        f.env = -(nout[j] + fc[ph][i] * B.envjobs[j].nr + 1);  // encoded, decoded below
-      }
-    }
-  for (size_t i = 0; i < B.frames64.size(); ++i)
-    if (gj[i] >= 0) B.frames64[i].env = -(nout[gj[i]] + gc[i] * B.envjobs[gj[i]].nr + 1);
-  for (size_t j = 0; j < nj; ++j) B.envjobs[j].out = nout[j];
-  B.fe_total = tot;
-}
-
 void finalize_spec(Batch& B) {
-  plan_env_fusion(B);
   // envelope area after the uploaded floats: decode frame envelope offsets;
-  // sg_spec_env wave tasks of SG_ENV_COLS columns (materialised jobs only)
+  // sg_spec_env wave tasks of SG_ENV_COLS columns
   B.fe_base = (bulk_size(B.fl_x, B.fl) + 63) / 64 * 64;
   B.fu_base = B.fe_base + (B.fe_total + 63) / 64 * 64;
   for (int ph = 0; ph < 2; ++ph)
@@ -947,8 +844,7 @@ void finalize_spec(Batch& B) {
   for (size_t k = 0; k < B.elog2.size(); ++k) B.elog2[k] = std::log2((double)(k + 1));
   B.envtasks.clear();
   for (size_t j = 0; j < B.envjobs.size(); ++j)
-    if (B.envjobs[j].out >= 0)
-      for (int32_t c0 = 0; c0 < B.envjobs[j].nc; c0 += SG_ENV_COLS) B.envtasks.push_back(SgEnvTask{(int32_t)j, c0});
+    for (int32_t c0 = 0; c0 < B.envjobs[j].nc; c0 += SG_ENV_COLS) B.envtasks.push_back(SgEnvTask{(int32_t)j, c0});
   // frames: per phase, sorted by (kernel, geometry), stable so that the
   // frames of one OLA stay consecutive; groups for the workgroup kernel only
   B.fgroups.clear();
@@ -978,9 +874,8 @@ void finalize_spec(Batch& B) {
       const int gi = fg[i];
       const SgFftGeom& g = B.geoms[gi];
       if (g.kind == SG_FFT_WAVE) {  // transformed inside sg_stft_ola
-        // + the radix-29 fragment table of the specialised M = 1102 path (sg_fft.hip SG_MAT29_BYTES),
-        // + the log2 table when the phase evaluates envelope columns
-        B.fgroup_lds[ph][0] = std::max(B.fgroup_lds[ph][0], sg_stft_lds(ph, g.M, B.env_fused[ph]));
+        // + the radix-29 fragment table of the specialised M = 1102 path (sg_fft.hip SG_MAT29_BYTES)
+        B.fgroup_lds[ph][0] = std::max(B.fgroup_lds[ph][0], (sg_fft_waves(ph) + 4) * g.M * 8 + (g.M == 1102 ? 2048 : 0));
         ++i;
         continue;
       }
@@ -1078,26 +973,19 @@ void finalize_spec(Batch& B) {
       const int64_t n = o.nframes;
       const int64_t nseg = std::max<int64_t>(1, (n + seg_frames - 1) / seg_frames);
       {  // algorithmic bytes / flops of this OLA in sg_stft_ola (bench roofline)
-        // envelope: a materialised column's nr floats once per run of frames reading it; an
-        // evaluated column's track terms and column factors once per frame
         const int64_t nr = o.wl / 2;
-        int64_t ncol = 0, prev = -1, ebytes = 0;
+        int64_t ncol = 0, prev = -1;
         for (int64_t f = 0; f < n; ++f) {
-          const SgFrame& fr = B.frames[ph][o.fidx - fbase + f];
-          if (fr.ejob >= 0) {
-            ebytes += (int64_t)sizeof(SgEnvTerm) * B.envjobs[fr.ejob].ntr + (int64_t)sizeof(SgEnvCol);
-            continue;
-          }
-          if (fr.env != prev) ++ncol;
-          prev = fr.env;
+          const int64_t e = B.frames[ph][o.fidx - fbase + f].env;
+          if (e != prev) ++ncol;
+          prev = e;
         }
-        ebytes += 4 * nr * ncol;
         const double fft = 5.0 * o.wl * std::log2((double)o.wl);
         if (ph == 0) {  // noise: uniforms nr per frame + filter columns + trimmed output
-          B.stft_bytes += 4 * (nr * n + o.len) + ebytes;
+          B.stft_bytes += 4 * (nr * n + nr * ncol + o.len);
           B.stft_flops += fft * n;
         } else {  // filter: the sound under the frames + envelope columns + trimmed output
-          B.stft_bytes += 4 * (std::min<int64_t>(o.xlen, o.wl + (int64_t)std::ceil((n - 1) * o.h)) + o.len) + ebytes;
+          B.stft_bytes += 4 * (std::min<int64_t>(o.xlen, o.wl + (int64_t)std::ceil((n - 1) * o.h)) + nr * ncol + o.len);
           B.stft_flops += 2 * fft * n;
         }
         B.stft_samples += o.len;
@@ -1197,11 +1085,5 @@ void finalize_spec(Batch& B) {
 extern "C" int sg_set_uniform_gather(int32_t on) {
   if (on < 0 || on > 1) return SG_E_ARG;
   sg::g_ugather.store(on);
-  return SG_OK;
-}
-
-extern "C" int sg_set_envelope_fusion(int32_t on) {
-  if (on < 0 || on > 3) return SG_E_ARG;
-  sg::g_env_fusion.store(on);
   return SG_OK;
 }

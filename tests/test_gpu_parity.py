@@ -378,37 +378,3 @@ def test_gathered_noise_uniforms_byte_equal():
             L.sg_set_uniform_gather(1)
     for a, b in zip(*outs):
         assert a.tobytes() == b.tobytes()
-
-
-def test_evaluated_envelope_columns_byte_equal():
-    """Spectral-envelope columns evaluated inside sg_stft_ola's frames
-    (sg_set_envelope_fusion(3), the default; sg_envfn.h env_bin) synthesize the
-    same bytes as the columns materialised by sg_spec_env and read back (0):
-    C5 calls (formant filters and noise filters at M = 1102, fp64-path calls
-    whose columns stay materialised), C3 vowels, and 16 kHz calls whose window
-    takes the generic geometry (materialised)."""
-    import bench
-    from soundgen_beta_amd import batch, native
-    from soundgen_beta_amd.rrng import RRng
-    def calls():  # R-stream generators are consumed by planning: fresh ones per plan
-        c = bench.c5_calls(300)[::3] + bench.c3_calls(8)
-        return c + [{"kind": "soundgen", "args": {"sylLen": 250, "samplingRate": 16000, "addSilence": 0,
-                                                  "formants": "a", "noiseAnchors": {"time": [0, 250], "value": [-25, -15]}},
-                     "rng": RRng(40 + i)} for i in range(3)]
-    L = native.lib()
-    outs, stats = [], []
-    for on in (0, 3):
-        assert L.sg_set_envelope_fusion(on) == 0
-        try:
-            p = batch.Plan(calls())
-            stats.append(p.env_stats())
-            p.close()
-            outs.append(batch.synthesize(calls()))
-        finally:
-            L.sg_set_envelope_fusion(3)
-    assert stats[0][0] == 0 and stats[0][1] > 0
-    assert stats[1][0] > 0 and stats[1][1] > 0  # the fp64-path and 16 kHz calls stay materialised
-    assert sum(stats[0]) == sum(stats[1])
-    for a, b in zip(*outs):
-        assert a.tobytes() == b.tobytes()
-    assert L.sg_set_envelope_fusion(4) != 0

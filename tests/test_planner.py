@@ -268,46 +268,6 @@ def test_uniform_gather_plans_the_same_calls():
     assert L.sg_set_uniform_gather(2) != 0
 
 
-def test_envelope_fusion_plans_the_same_calls():
-    """sg_set_envelope_fusion(3) (the default) marks the envelope columns that only
-    sg_stft_ola's M = 1102 frames read as evaluated there; the plan's calls, lengths
-    and frames equal the all-materialised plan's (0), the STFT's algorithmic bytes
-    drop by the columns' floats, and the envelope area shrinks to the rest (the GPU
-    test compares the synthesized bytes)."""
-    import bench
-    from soundgen_beta_amd import native
-    L = native.lib()
-    calls = bench.c5_calls(240) + bench.c3_calls(6)
-    res = []
-    for on in (0, 3):
-        assert L.sg_set_envelope_fusion(on) == 0
-        try:
-            p = batch.Plan(calls, None)
-            res.append((p.lengths.copy(), p.offsets.copy(), p.status.copy(), p.stats(), p.env_stats(),
-                        p.device_bytes()))
-            p.close()
-        finally:
-            L.sg_set_envelope_fusion(3)
-    (l0, o0, s0, st0, e0, d0), (l1, o1, s1, st1, e1, d1) = res
-    assert np.array_equal(l0, l1) and np.array_equal(o0, o1) and np.array_equal(s0, s1)
-    assert e0[0] == 0 and e0[1] > 0
-    assert e1[0] > 0.8 * e0[1] and sum(e1) == e0[1]
-    assert st1["fft_frames"] == st0["fft_frames"] and st1["stft_samples"] == st0["stft_samples"]
-    assert st1["stft_bytes"] < st0["stft_bytes"]
-    assert d1 < d0  # the evaluated columns take no envelope area
-    parts = []
-    for on in (1, 2):  # filter columns only, noise columns only
-        assert L.sg_set_envelope_fusion(on) == 0
-        try:
-            p = batch.Plan(calls, None)
-            parts.append(p.env_stats()[0])
-            p.close()
-        finally:
-            L.sg_set_envelope_fusion(3)
-    assert parts[0] > 0 and parts[1] > 0 and sum(parts) == e1[0]
-    assert L.sg_set_envelope_fusion(4) != 0
-
-
 def test_host_cache_trim_between_plans():
     """sg_host_cache_trim releases the planner's cached host blocks; the next plan
     refills the cache and plans the same batch."""
