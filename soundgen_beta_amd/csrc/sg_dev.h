@@ -268,6 +268,7 @@ struct SgFrame64 {
   int32_t wl;
   int32_t mode;  // SG_F64_FILTER, SG_F64_NOISE
 };
+constexpr int SG_F64W_M_HOST = 1102;  // sg_fft_frames64w's frame size (sg_fft.hip SG_F64W_M)
 constexpr int32_t SG_F64_FILTER = 0;
 constexpr int32_t SG_F64_NOISE = 1;
 struct SgFrameGroup {  // frames of one workgroup: same geometry and mode

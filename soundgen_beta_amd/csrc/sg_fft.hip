@@ -1428,6 +1428,192 @@ extern "C" __global__ __launch_bounds__(SG_F64_THREADS) void sg_fft_frames64(
   }
 }
 
+// ---- fp64 frames of the dominant geometry (wl = 2204, M = 1102 = 29 x 19 x 2), one frame
+// per wavefront (round 5). sg_fft_frames64 spreads a frame over a 256-thread workgroup
+// with a barrier per stage and one work item per odd-prime output pair, which reads all
+// R inputs of its butterfly from LDS (O(R^2) LDS reads per butterfly): LDS-bound at
+// ~17k CU-cycles per frame. Here a lane holds its butterfly's inputs in registers (R
+// reads, R writes), the stages are wave-synchronous (no barrier), and the work is the
+// fp64 FMAs. The arithmetic is sg_fft_frames64's (the same symmetric odd-prime form,
+// roots and twiddles from the sg_roots64 table); the stage order is 29, 19, 2 so that
+// the heaviest stage needs no twiddles and the radix-2 stage works in place.
+constexpr int SG_F64W_WAVES = 8;  // frames per workgroup: 8 x 17.6 KB of LDS, 2 waves per SIMD
+constexpr int SG_F64W_M = SG_F64W_M_HOST;
+namespace {
+// radix-R (odd) butterfly of the R inputs x[] -> y_k at dst[k * ys] (in registers until
+// written); c[t], s[t] = cos, sin (2 pi t / R), t <= H: wave-uniform (scalar registers),
+// the index (m k) mod R folds at compile time (a root t > H is t' = R - t with the sine
+// negated); inv: inverse (outputs k and R - k swapped)
+template <int R>
+__device__ __forceinline__ void bfly64_store(double2 (&x)[R], double2* dst, int ys, const double (&c)[(R - 1) / 2 + 1],
+                                             const double (&s)[(R - 1) / 2 + 1], bool inv) {
+  constexpr int H = (R - 1) / 2;
+  double2 y0 = x[0];
+#pragma unroll
+  for (int m = 1; m <= H; ++m) {  // A_m = x_m + x_{R-m} in x[m], B_m = x_m - x_{R-m} in x[R - m]
+    const double2 u = x[m], v = x[R - m];
+    x[m] = make_double2(u.x + v.x, u.y + v.y);
+    x[R - m] = make_double2(u.x - v.x, u.y - v.y);
+    y0.x += x[m].x;
+    y0.y += x[m].y;
+  }
+  dst[0] = y0;
+#pragma unroll
+  for (int k = 1; k <= H; ++k) {
+    double2 P = make_double2(0.0, 0.0), Q = make_double2(0.0, 0.0);
+#pragma unroll
+    for (int m = 1; m <= H; ++m) {
+      const int t = (m * k) % R;
+      const double wc = t <= H ? c[t] : c[R - t];
+      const double ws = t <= H ? s[t] : -s[R - t];  // sin (2 pi t / R)
+      P.x = fma(x[m].x, wc, P.x);
+      P.y = fma(x[m].y, wc, P.y);
+      Q.x = fma(x[R - m].x, ws, Q.x);
+      Q.y = fma(x[R - m].y, ws, Q.y);
+    }
+    const double2 x0 = x[0];
+    const double2 ya = make_double2(x0.x + P.x + Q.y, x0.y + P.y - Q.x);
+    const double2 yb = make_double2(x0.x + P.x - Q.y, x0.y + P.y + Q.x);
+    dst[k * ys] = inv ? yb : ya;
+    dst[(R - k) * ys] = inv ? ya : yb;
+  }
+}
+// the roots of a radix-R stage from the frame's W_N table (wave-uniform loads): W_R^t = W_N^(t N / R) = (cos, -sin)
+template <int R>
+__device__ __forceinline__ void roots64(const double2* __restrict__ TN, int N, double (&c)[(R - 1) / 2 + 1],
+                                        double (&s)[(R - 1) / 2 + 1]) {
+#pragma unroll
+  for (int t = 0; t <= (R - 1) / 2; ++t) {
+    const double2 w = TN[t * (N / R)];
+    c[t] = w.x;
+    s[t] = -w.y;
+  }
+}
+
+// the M = 1102 transform of frame A (in place, LDS), forward or inverse; TN = W_N^t, t < N
+__device__ __forceinline__ void fft64w_1102(double2* A, const double2* __restrict__ TN, bool inv, int lane) {
+  constexpr int N = 2 * SG_F64W_M;
+  // radix 29 (Ns = 1, 38 butterflies): inputs j + 38 r, outputs 29 j + k
+  {
+    double c[15], sn[15];
+    roots64<29>(TN, N, c, sn);
+    double2 x[29];
+    const int j = lane < 38 ? lane : 0;
+#pragma unroll
+    for (int r = 0; r < 29; ++r) x[r] = A[j + 38 * r];
+    sg_wave_fence();  // every read of the stage before the first write
+    if (lane < 38) bfly64_store<29>(x, A + 29 * j, 1, c, sn, inv);
+    sg_wave_fence();
+  }
+  // radix 19 (Ns = 29, 58 butterflies): inputs j + 58 r times W_551^(r jm), outputs
+  // 19 (j - jm) + jm + 29 k, jm = j mod 29
+  {
+    double c[10], sn[10];
+    roots64<19>(TN, N, c, sn);
+    double2 x[19];
+    const int j = lane < 58 ? lane : 0, jm = j < 29 ? j : j - 29;
+#pragma unroll
+    for (int r = 0; r < 19; ++r) {
+      const double2 v = A[j + 58 * r];
+      x[r] = r == 0 || jm == 0 ? v : cmul64(v, conj_if(TN[4 * r * jm], inv));  // W_551^e = W_2204^(4 e)
+    }
+    sg_wave_fence();
+    if (lane < 58) bfly64_store<19>(x, A + 19 * (j - jm) + jm, 29, c, sn, inv);
+    sg_wave_fence();
+  }
+  // radix 2 (Ns = 551, 551 butterflies): j and j + 551, the second times W_1102^j; in place
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int j = 64 * i + lane;
+    if (j < 551) {
+      const double2 u = A[j], v = cmul64(A[j + 551], conj_if(TN[2 * j], inv));
+      A[j] = make_double2(u.x + v.x, u.y + v.y);
+      A[j + 551] = make_double2(u.x - v.x, u.y - v.y);
+    }
+  }
+  sg_wave_fence();
+}
+}  // namespace
+
+extern "C" __global__ __launch_bounds__(SG_F64W_WAVES * 64) void sg_fft_frames64w(
+    const SgFrame64* __restrict__ frames, int64_t nframes, const int64_t* __restrict__ frame_tab,
+    const double2* __restrict__ tabs, const float* __restrict__ fl, const double* __restrict__ fh,
+    float* __restrict__ fs) {
+  constexpr int M = SG_F64W_M, N = 2 * M, half = M / 2;
+  extern __shared__ double2 lds64w[];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  double2* A = lds64w + (int64_t)w * M;
+  const int64_t f = (int64_t)blockIdx.x * SG_F64W_WAVES + w;
+  if (f >= nframes) return;  // no workgroup barrier below
+  const SgFrame64 F = frames[f];
+  const double2* __restrict__ TN = tabs + frame_tab[f];
+  const double2* __restrict__ ham = TN + N;
+  const double2* __restrict__ han = ham + M;
+  const bool noise = F.mode == SG_F64_NOISE;
+  const double invN = 1.0 / (double)N;
+  const float* env = fl + F.env;
+  if (!noise) {
+    const double* x = fh + F.src;
+#pragma unroll 6
+    for (int n = lane; n < M; n += 64) {  // hamming (seewave ftwindow), packed pairs
+      const double2 h = ham[n];
+      A[n] = make_double2(x[2 * n] * h.x, x[2 * n + 1] * h.y);
+    }
+    sg_wave_fence();
+    fft64w_1102(A, TN, false, lane);
+  }
+  // FILTER: untangle, / N, x env; NOISE: uniforms x filter (real). Then seewave's
+  // Hermitian extension packed for the inverse: slot k <- Y_k and conj Y_{M-k} (k = 0:
+  // Re Y_{M-1}). Lane pair k owns slots k and M - k; the k = 0 lane also reads slots 1
+  // and M - 1 (pair 1's), before any write of the round.
+  const float* uni = fl + F.src;
+  auto Yat = [&](int kk, double2 p, double2 q) -> double2 {  // Y_kk from Z_kk = p, Z_{M-kk} = q
+    if (noise) return make_double2((double)uni[kk] * (double)env[kk], 0.0);
+    const double2 wk = TN[kk];
+    const double2 e = make_double2(0.5 * (p.x + q.x), 0.5 * (p.y - q.y));
+    const double2 o = make_double2(0.5 * (p.y + q.y), -0.5 * (p.x - q.x));
+    const double2 xk = make_double2(e.x + (o.x * wk.x - o.y * wk.y), e.y + (o.x * wk.y + o.y * wk.x));
+    const double sc = invN * (double)env[kk];
+    return make_double2(xk.x * sc, xk.y * sc);
+  };
+  auto pack = [&](int k, double2 yk, double2 yh) -> double2 {  // yh = X'_{k+M}
+    const double2 sm = make_double2(yk.x + yh.x, yk.y + yh.y), df = make_double2(yk.x - yh.x, yk.y - yh.y);
+    const double2 t = cmul64(df, conj_if(TN[k], true));  // W_N^-k (X'_k - X'_{k+M})
+    return make_double2(sm.x - t.y, sm.y + t.x);
+  };
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int k = 64 * i + lane;
+    const bool act = k <= half;
+    const int kk = act ? k : 0, km = kk == 0 ? 0 : M - kk;
+    const double2 p = A[kk], q = A[km];
+    double2 p1 = p, pM1 = p;
+    if (i == 0) {
+      p1 = A[1];
+      pM1 = A[M - 1];
+    }
+    sg_wave_fence();
+    if (!act) continue;
+    if (kk == 0) {
+      const double2 y0 = Yat(0, p, p), yl = Yat(M - 1, pM1, p1);
+      A[0] = pack(0, y0, make_double2(yl.x, 0.0));
+    } else {
+      const double2 yk = Yat(kk, p, q), ym = Yat(km, q, p);
+      A[kk] = pack(kk, yk, make_double2(ym.x, -ym.y));
+      if (km != kk) A[km] = pack(km, ym, make_double2(yk.x, -yk.y));
+    }
+  }
+  sg_wave_fence();
+  fft64w_1102(A, TN, true, lane);
+  float* out = fs + F.dst;
+#pragma unroll 6
+  for (int n = lane; n < M; n += 64) {
+    const double2 h = han[n], c = A[n];
+    out[2 * n] = (float)(c.x * invN * h.x);
+    out[2 * n + 1] = (float)(c.y * invN * h.y);
+  }
+}
+
 // Gathered noise uniforms (upload time): one workgroup per noise item copies its
 // draws from the union of the injected ranges into the uniform area, zero-padded
 extern "C" __global__ __launch_bounds__(256) void sg_ugather(const SgUJob* __restrict__ jobs,
@@ -1629,10 +1815,21 @@ void launch_fft_frames64(const DevicePlan& D, const Batch& B, int ph, hipStream_
                        D.roots64_off, reinterpret_cast<double2*>(D.roots64));
     SG_LAUNCHED("sg_roots64");
   }
+  // the leading wl = 2204 frames of the phase: one per wavefront
+  const int64_t nw = B.frames64_w[ph];
+  if (nw > 0) {
+    const int lds = SG_F64W_WAVES * SG_F64W_M * (int)sizeof(double2);  // a frame per wave
+    lds_opt_in(reinterpret_cast<const void*>(&sg_fft_frames64w), lds, "sg_fft_frames64w");
+    hipLaunchKernelGGL(sg_fft_frames64w, dim3((unsigned)((nw + SG_F64W_WAVES - 1) / SG_F64W_WAVES)),
+                       dim3(SG_F64W_WAVES * 64), lds, s, D.frames64 + f0, nw, D.frames64_tab + f0,
+                       reinterpret_cast<const double2*>(D.roots64), D.fl, D.fh, D.fs);
+    SG_LAUNCHED("sg_fft_frames64w");
+  }
+  if (nf - nw <= 0) return;
   const int lds = (B.frames64_maxwl + 32) * (int)sizeof(double2);  // two M-point buffers + radix roots
   lds_opt_in(reinterpret_cast<const void*>(&sg_fft_frames64), lds, "sg_fft_frames64");
-  hipLaunchKernelGGL(sg_fft_frames64, dim3((unsigned)nf), dim3(SG_F64_THREADS), lds, s, D.frames64 + f0,
-                     D.frames64_tab + f0, reinterpret_cast<const double2*>(D.roots64), D.fl, D.fh, D.fs);
+  hipLaunchKernelGGL(sg_fft_frames64, dim3((unsigned)(nf - nw)), dim3(SG_F64_THREADS), lds, s, D.frames64 + f0 + nw,
+                     D.frames64_tab + f0 + nw, reinterpret_cast<const double2*>(D.roots64), D.fl, D.fh, D.fs);
   SG_LAUNCHED("sg_fft_frames64");
 }
 void launch_mix_hp(const DevicePlan& D, int64_t t0, int64_t n_tiles, hipStream_t s) {

@@ -124,6 +124,8 @@ struct Batch {
   int64_t roots64_total = 0;
   int32_t frames64_maxwl = 0;
   int64_t frames64_noise = 0;  // finalize_spec: frames64 holds the noise frames first
+  // per phase: its leading frames of wl = 2204, one per wavefront in sg_fft_frames64w (the rest: sg_fft_frames64)
+  int64_t frames64_w[2] = {0, 0};
   std::vector<SgNoiseItem> items;        // items[].ola indexes the device OLA table
   std::vector<SgMix> mixes[2];           // [0] pre-filter sounds (fs), [1] final output
   struct Copy { int64_t fl_off, fs_off, n; };

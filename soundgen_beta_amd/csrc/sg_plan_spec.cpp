@@ -820,6 +820,13 @@ void finalize_spec(Batch& B) {
   B.frames64_noise = std::stable_partition(B.frames64.begin(), B.frames64.end(),
                                            [](const SgFrame64& f) { return f.mode == SG_F64_NOISE; }) -
                      B.frames64.begin();
+  // within each phase, the wl = 2204 frames first (sg_fft_frames64w, a frame per wavefront)
+  {
+    auto w = [](const SgFrame64& f) { return f.wl == 2 * SG_F64W_M_HOST; };
+    const auto mid = B.frames64.begin() + B.frames64_noise;
+    B.frames64_w[0] = std::stable_partition(B.frames64.begin(), mid, w) - B.frames64.begin();
+    B.frames64_w[1] = std::stable_partition(mid, B.frames64.end(), w) - mid;
+  }
   for (SgFrame64& f : B.frames64) {
     if (f.env < 0) f.env = B.fe_base + (-f.env - 1);
     if (f.mode == SG_F64_NOISE && f.src < 0) f.src = B.fu_base + (-f.src - 1);
