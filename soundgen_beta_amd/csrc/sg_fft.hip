@@ -1490,9 +1490,16 @@ __device__ __forceinline__ void roots64(const double2* __restrict__ TN, int N, d
   }
 }
 
-// the M = 1102 transform of frame A (in place, LDS), forward or inverse; TN = W_N^t, t < N
+// the M = 1102 transform of frame A (in place, LDS), forward or inverse; TN = W_N^t, t < N.
+// Each stage's twiddles are loaded one stage ahead (their latency under the previous
+// stage's arithmetic).
 __device__ __forceinline__ void fft64w_1102(double2* A, const double2* __restrict__ TN, bool inv, int lane) {
   constexpr int N = 2 * SG_F64W_M;
+  // radix 19's twiddles W_551^(r jm) = W_2204^(4 r jm), jm = j mod 29 (j = lane < 58)
+  const int j19 = lane < 58 ? lane : 0, jm19 = j19 < 29 ? j19 : j19 - 29;
+  double2 tw19[19];
+#pragma unroll
+  for (int r = 1; r < 19; ++r) tw19[r] = TN[4 * r * jm19];
   // radix 29 (Ns = 1, 38 butterflies): inputs j + 38 r, outputs 29 j + k
   {
     double c[15], sn[15];
@@ -1505,20 +1512,23 @@ __device__ __forceinline__ void fft64w_1102(double2* A, const double2* __restric
     if (lane < 38) bfly64_store<29>(x, A + 29 * j, 1, c, sn, inv);
     sg_wave_fence();
   }
+  // radix 2's twiddles W_1102^j = W_2204^(2 j), j = 64 i + lane
+  double2 tw2[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) tw2[i] = TN[2 * min(64 * i + lane, 550)];
   // radix 19 (Ns = 29, 58 butterflies): inputs j + 58 r times W_551^(r jm), outputs
-  // 19 (j - jm) + jm + 29 k, jm = j mod 29
+  // 19 (j - jm) + jm + 29 k
   {
     double c[10], sn[10];
     roots64<19>(TN, N, c, sn);
     double2 x[19];
-    const int j = lane < 58 ? lane : 0, jm = j < 29 ? j : j - 29;
 #pragma unroll
     for (int r = 0; r < 19; ++r) {
-      const double2 v = A[j + 58 * r];
-      x[r] = r == 0 || jm == 0 ? v : cmul64(v, conj_if(TN[4 * r * jm], inv));  // W_551^e = W_2204^(4 e)
+      const double2 v = A[j19 + 58 * r];
+      x[r] = r == 0 || jm19 == 0 ? v : cmul64(v, conj_if(tw19[r], inv));
     }
     sg_wave_fence();
-    if (lane < 58) bfly64_store<19>(x, A + 19 * (j - jm) + jm, 29, c, sn, inv);
+    if (lane < 58) bfly64_store<19>(x, A + 19 * (j19 - jm19) + jm19, 29, c, sn, inv);
     sg_wave_fence();
   }
   // radix 2 (Ns = 551, 551 butterflies): j and j + 551, the second times W_1102^j; in place
@@ -1526,7 +1536,7 @@ __device__ __forceinline__ void fft64w_1102(double2* A, const double2* __restric
   for (int i = 0; i < 9; ++i) {
     const int j = 64 * i + lane;
     if (j < 551) {
-      const double2 u = A[j], v = cmul64(A[j + 551], conj_if(TN[2 * j], inv));
+      const double2 u = A[j], v = cmul64(A[j + 551], conj_if(tw2[i], inv));
       A[j] = make_double2(u.x + v.x, u.y + v.y);
       A[j + 551] = make_double2(u.x - v.x, u.y - v.y);
     }
