@@ -857,13 +857,23 @@ void finalize_spec(Batch& B) {
   B.fgroups.clear();
   std::vector<int64_t> pos[2];
   for (int ph = 0; ph < 2; ++ph) {
-    auto key = [&](int64_t i) {
-      const int gi = B.frame_geom[ph][i];
-      return (int64_t)(B.geoms[gi].kind == SG_FFT_WAVE ? 0 : 1) * (1 << 20) + gi;
-    };
+    // a stable counting sort over the geometries (few keys; 2.8 M frames per 16,384 C5
+    // calls: a comparison sort was 90 % of finalize_spec)
+    const size_t ng = B.geoms.size();
+    std::vector<int64_t> rank(ng), start(ng + 1, 0);
+    {
+      std::vector<int32_t> og(ng);
+      for (size_t g = 0; g < ng; ++g) og[g] = (int32_t)g;
+      std::stable_sort(og.begin(), og.end(), [&](int32_t a, int32_t b) {
+        const int ka = B.geoms[a].kind == SG_FFT_WAVE ? 0 : 1, kb = B.geoms[b].kind == SG_FFT_WAVE ? 0 : 1;
+        return ka != kb ? ka < kb : a < b;
+      });
+      for (size_t r = 0; r < ng; ++r) rank[og[r]] = (int64_t)r;
+    }
+    for (int32_t gi : B.frame_geom[ph]) ++start[rank[gi] + 1];
+    for (size_t r = 0; r < ng; ++r) start[r + 1] += start[r];
     std::vector<int64_t> idx(B.frames[ph].size());
-    for (size_t i = 0; i < idx.size(); ++i) idx[i] = (int64_t)i;
-    std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return key(a) < key(b); });
+    for (size_t i = 0; i < idx.size(); ++i) idx[start[rank[B.frame_geom[ph][i]]]++] = (int64_t)i;
     std::vector<SgFrame> fr(idx.size());
     std::vector<int32_t> fg(idx.size());
     pos[ph].assign(idx.size(), 0);
