@@ -312,6 +312,9 @@ def pmc_from_profiles(config, kernel):
             "source": os.path.relpath(files[-1], ROOT)}
 
 
+SG_WTASK_BYTES = 128  # sizeof(SgWTask), sg_dev.h
+
+
 def roofline(st, prof, steps, config, kern):
     """Roofline of one profiled kernel group: achieved = algorithmic bytes per launch
     (SURVEY.md §8d per-unit bytes) / average launch duration (HIP events
@@ -323,9 +326,13 @@ def roofline(st, prof, steps, config, kern):
     ms, n = prof[kern]
     lps = max(1, n // steps)  # launches per step
     sec = ms / 1e3
+    desc = 0.0
     if kern == "sg_sine_bank":
-        # fp32 epoch waveform write + the amplitude blocks it reads (A and dA columns)
-        alg = (4 * st["harm_samples"] + st["harm_amp_bytes"]) / lps
+        # fp32 epoch waveform write + the amplitude columns it reads (each once) + the 128-B
+        # task descriptors of the fp32 class kernels (each read once, by scalar loads)
+        desc = SG_WTASK_BYTES * sum(st.get(k, 0) for k in ("tasks_long", "tasks_short", "tasks_tall",
+                                                             "tasks_tallp")) / lps
+        alg = (4 * st["harm_samples"] + st["harm_amp_bytes"]) / lps + desc
         # Clenshaw: 2 lane-ops per (sample, row, chain) of the tasks on the row recurrence;
         # the wavetable spans' samples (one table read + 3 FMAs each) are not priced here
         valu_ops = 2.0 * (st["harm_terms"] - st.get("tab_terms", 0)) / lps
@@ -350,6 +357,12 @@ def roofline(st, prof, steps, config, kern):
     achieved = alg / sec / 1e9 if sec > 0 else 0.0
     hfrac = achieved / HBM_PEAK_GBS
     traffic, src = traffic_from_profiles(config, kernels, lps)
+    if traffic is not None and desc:
+        # FETCH_SIZE counts a 128-B scalar (s_load) descriptor read at its true size, where the
+        # gfx950 doubling applies only to vector reads (tools/calib/fetch_calib.hip,
+        # profiles/r05o_fetch_calib.json: factor 1.00 for desc128, 0.50 for 4-B and 16-B lanes):
+        # the doubled total holds the descriptors twice
+        traffic -= desc
     r = {"bound": "valu" if vfrac > hfrac else "hbm", "kernel": name, "achieved": achieved, "peak": HBM_PEAK_GBS,
          "unit": "GB/s", "frac": hfrac, "traffic": traffic, "alg_bytes_per_launch": alg, "avg_launch_ms": ms,
          "launches_timed": n,
@@ -359,6 +372,9 @@ def roofline(st, prof, steps, config, kern):
                            + " in the SG_OVERLAP=0 kernel-stats summary")}
     if src:
         r["traffic_source"] = src
+    if desc:
+        r["traffic_correction"] = ("- %.0f B per launch: the task descriptors, which FETCH_SIZE counts once "
+                                   "(scalar loads; tools/calib/fetch_calib.hip)" % desc)
     r.update(extra)
     issue = {k: pmc_from_profiles(config, k) for k in kernels}
     issue = {k: v for k, v in issue.items() if v}
@@ -564,6 +580,9 @@ def main():
         st = {}
         for p, _, _ in plans:
             for k, v in p.stats().items():
+                st[k] = st.get(k, 0) + v
+            # task descriptors per class (128 B each, read once by their class kernel)
+            for k, v in zip(("tasks_long", "tasks_short", "tasks_tall", "tasks_tallp", "tasks_hp"), p.sine_tasks()):
                 st[k] = st.get(k, 0) + v
             tabs, tab_samples, tab_terms = p.table_stats()  # wavetable spans (no row recurrence)
             st["tab_spans"] = st.get("tab_spans", 0) + tabs

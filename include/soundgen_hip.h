@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SG_ABI_VERSION 3
+#define SG_ABI_VERSION 4
 
 enum {
   SG_OK = 0,
@@ -283,6 +283,11 @@ int sg_plan_table_stats(const sg_plan* plan, int64_t* tables, int64_t* samples, 
  * output samples, algorithmic HBM bytes (source/uniforms + envelope columns +
  * output) and nominal flops (5 wl log2 wl per transform). */
 int sg_plan_stft_stats(const sg_plan* plan, int64_t* samples, int64_t* alg_bytes, double* flops);
+/* Sine-bank wave tasks of an uploaded plan by class (128-B descriptors, SgWTask):
+ * counts[0] sg_sine_bank, [1] sg_sine_bank_pairs, [2] sg_sine_bank_tall,
+ * [3] sg_sine_bank_tall_pairs, [4] sg_sine_bank_hp (zeros before upload). The
+ * bench adds the descriptors to the kernels' algorithmic bytes. ABI 4. */
+int sg_plan_sine_tasks(const sg_plan* plan, int64_t* counts);
 /* Precision path of the plan (ABI 2): per call, the number of its bouts whose
  * formant filter runs in fp64 (source, pre-filter mix and forward STFT; the
  * planner's conditioning estimate of the fp32 round-off through the envelope

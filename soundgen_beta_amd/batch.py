@@ -188,6 +188,13 @@ class Plan:
         return dict(harm_samples=v[0].value, harm_terms=v[1].value, harm_amp_bytes=v[2].value,
                     fft_frames=v[3].value, stft_samples=w[0].value, stft_bytes=w[1].value, stft_flops=w[2].value)
 
+    def sine_tasks(self):
+        """Sine-bank tasks of the uploaded plan by class: (sg_sine_bank, _pairs, _tall,
+        _tall_pairs, _hp)."""
+        v = (C.c_int64 * 5)()
+        native.check(native.lib().sg_plan_sine_tasks(self.ptr, v))
+        return tuple(int(x) for x in v)
+
     def table_stats(self):
         """Wavetable spans of the uploaded plan: (tables, samples, terms)."""
         v = [C.c_int64() for _ in range(3)]

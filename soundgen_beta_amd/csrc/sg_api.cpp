@@ -750,6 +750,17 @@ int sg_plan_stft_stats(const sg_plan* plan, int64_t* samples, int64_t* alg_bytes
   return SG_OK;
 }
 
+int sg_plan_sine_tasks(const sg_plan* plan, int64_t* counts) {
+  if (!plan || !counts) return SG_E_ARG;
+  const sg::DevicePlan& D = plan->D;
+  counts[0] = (int64_t)D.tlong_host.size();
+  counts[1] = (int64_t)D.tshort_host.size();
+  counts[2] = (int64_t)D.tall_host.size();
+  counts[3] = (int64_t)D.tallp_host.size();
+  counts[4] = (int64_t)D.thp_host.size();
+  return SG_OK;
+}
+
 int64_t sg_plan_amp_count(const sg_plan* plan) { return plan && !plan->host_released ? plan->B.amp_total : 0; }
 
 int sg_plan_debug_amps(const sg_plan* plan, float* out, int64_t n) {

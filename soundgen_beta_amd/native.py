@@ -81,6 +81,8 @@ def lib():
     L.sg_set_fp64_policy.argtypes = [C.c_int32, C.c_double]
     L.sg_set_amp_policy.argtypes = [C.c_int32]
     L.sg_set_uniform_gather.argtypes = [C.c_int32]
+    if hasattr(L, "sg_plan_sine_tasks"):  # ABI 4 (an older library still loads for A/B runs)
+        L.sg_plan_sine_tasks.argtypes = [vp, i64p]
     L.sg_set_sine_table.argtypes = [C.c_int32]
     L.sg_plan_table_stats.argtypes = [C.c_void_p, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)]
     L.sg_host_cache_trim.argtypes = []
