@@ -1689,6 +1689,10 @@ __device__ __forceinline__ void mix_body(const SgMixTile* __restrict__ tiles, co
       if (j0 + (E - 1) * 256 < 0 || j0 >= it.len) continue;  // no sample of this thread in the item
       const float nscale = it.ola >= 0 ? 1.f / olamax[it.ola] : 1.f;
       const bool flat = it.strength.kind == 1;
+      // the chunk's samples of the item all inside its fade ramps' complement: factor 1
+      // exactly (wave-uniform test on the chunk's item range [jc, jc + E 256))
+      const int64_t jc = kc - it.off;
+      const bool ramp = it.fade >= 2 && (jc < it.fade || jc + E * 256 > it.len - it.fade);
       const float sflat = flat ? (float)contour_at(it.strength, cknots, it.len, 0) : 1.f;
       V raw[E];
       const bool f64 = HP && (it.flags & SG_ITEM_F64);
@@ -1714,7 +1718,7 @@ __device__ __forceinline__ void mix_body(const SgMixTile* __restrict__ tiles, co
           } else
             nv = (V)((double)nv * sgd::contour_at_cursor(it.strength, cknots, it.len, j, cur));
         }
-        nv *= (V)fade_in_out(it.fade, it.len, j);
+        if (ramp) nv *= (V)fade_in_out(it.fade, it.len, j);
         v[e] += nv;
       }
       if (i < NC) curs[i][threadIdx.x] = cur;

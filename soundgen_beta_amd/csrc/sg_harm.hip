@@ -963,7 +963,7 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
                                               const SgSyllable* __restrict__ syls, const double* __restrict__ cknots,
                                               const V* __restrict__ W, const float* __restrict__ maxes,
                                               V* __restrict__ out_buf, V* __restrict__ fs,
-                                              int wv, double* lkw) {
+                                              int wv, double* lkw, float* lkf, int* lki) {
   const SgSyllable& sy = syls[tl.syl];
   int ecur = -1;  // a lane's samples increase: the envelope interval is found by stepping
   constexpr bool F64 = sizeof(V) == 8;
@@ -1013,15 +1013,41 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
 #pragma unroll
       for (int t = 1; t < KW - 1; ++t)
         if (lane == t) { xv = xs[t]; yv = ys[t]; x1 = xs[t + 1]; y1 = ys[t + 1]; }
+      const double sl = x1 > xv ? (y1 - yv) / (x1 - xv) : 0.0;
       lkw[3 * lane] = xv;
       lkw[3 * lane + 1] = yv;
-      lkw[3 * lane + 2] = x1 > xv ? (y1 - yv) / (x1 - xv) : 0.0;
+      lkw[3 * lane + 2] = sl;
+      if constexpr (!F64) {
+        // fp32 chunk form of interval t = lane: the line's value at the chunk's first
+        // sample and its step per sample, dm(c0 + r) = a_t + b_t r, and the first r
+        // whose u reaches the interval's left knot (r >= kb_t); a sample next to a knot
+        // may take the neighbouring line, equal there to within one sample's step
+        const double u0 = u_at(c0);
+        lkf[2 * lane] = (float)fma(sl, u0 - xv, yv);
+        lkf[2 * lane + 1] = (float)(sl * dby);
+        int kb = 0;
+        if (lane > 0) {
+          const double r = std::ceil((xv - u0) / dby);
+          kb = d0 + lane > dr.nk - 2 ? 1 << 20 : (r <= 0.0 ? 0 : (r >= 512.0 ? 512 : (int)r));
+        }
+        lki[lane] = kb;
+      }
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+  // fp32 drift (V = float, the chunk inside the staged intervals, u increasing): the
+  // interval by integer compares against the wave-uniform kb_t, then one FMA. The fp64
+  // evaluation per sample (interval compares, approx arithmetic, the product) was 38 %
+  // of this kernel (r05r: 3.36 -> 2.07 ms per C5 launch without drift)
+  const bool fast32 = !F64 && drift && local_knots && dby > 0;
+  int kbr[KW - 2];
+#pragma unroll
+  for (int q = 0; q < KW - 2; ++q) kbr[q] = fast32 ? lki[q + 1] : 0;
   int p = pu, di = d0;
+  // a chunk clear of both fade ramps multiplies by exactly 1: skip it (wave-uniform)
+  const bool ramp = sy.fade >= 2 && (c0 < sy.fade || c1 > sy.L - sy.fade);
   V res[4];  // every load of the chunk before its stores
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -1041,8 +1067,15 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
       x = (V)((double)x * sgd::contour_at_cursor(sy.env, cknots, sy.L, k, ecur));
     }
     x *= inv_max;
-    if (sy.fade >= 2) x *= fade_at<V>(sy.fade, sy.L, k);
-    if (drift) {
+    if (ramp) x *= fade_at<V>(sy.fade, sy.L, k);
+    if (fast32) {
+      const int r = (int)(k - c0);
+      int t = 0;
+#pragma unroll
+      for (int q = 0; q < KW - 2; ++q) t += r >= kbr[q] ? 1 : 0;
+      const float2 ab = reinterpret_cast<const float2*>(lkf)[t];
+      x *= (V)fmaf(ab.y, (float)r, ab.x);
+    } else if (drift) {
       double dm;
       if (local_knots) {  // linear_at's interval and arithmetic, knots from registers
         const double u = u_at(k);
@@ -1078,13 +1111,15 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, const float* __restrict__ W,
     const float* __restrict__ maxes, float* __restrict__ out_buf, float* __restrict__ fs) {
   __shared__ double lk[4][3 * 8];  // per wave: drift intervals (x, y, slope)
-  double* lkw = lk[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
+  __shared__ float lkf[4][2 * 8];  // per wave: their fp32 chunk lines (a, b)
+  __shared__ int lki[4][8];        // per wave: their first samples in the chunk
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  double* lkw = lk[wv];
 #pragma unroll 1
   for (int i = 0; i < SG_FIN_TILES; ++i) {
     const int64_t t = (int64_t)blockIdx.x * SG_FIN_TILES + i;
     if (t >= ntiles) break;
-    finalize_tile(stiles[t], pieces, syls, cknots, W, maxes, out_buf, fs, wv, lkw);
+    finalize_tile(stiles[t], pieces, syls, cknots, W, maxes, out_buf, fs, wv, lkw, lkf[wv], lki[wv]);
   }
 }
 
@@ -1097,7 +1132,7 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize_hp(
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t t = blockIdx.x;
   if (t >= ntiles) return;
-  finalize_tile<double>(stiles[t], pieces, syls, cknots, W64, maxes, fh, fh, wv, lk[wv]);
+  finalize_tile<double>(stiles[t], pieces, syls, cknots, W64, maxes, fh, fh, wv, lk[wv], nullptr, nullptr);
 }
 
 // ---------------------------------------------------------------- launchers
