@@ -963,7 +963,7 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
                                               const SgSyllable* __restrict__ syls, const double* __restrict__ cknots,
                                               const V* __restrict__ W, const float* __restrict__ maxes,
                                               V* __restrict__ out_buf, V* __restrict__ fs,
-                                              int wv, double* lkw, float* lkf, int* lki) {
+                                              int wv, double* lkw) {
   const SgSyllable& sy = syls[tl.syl];
   int ecur = -1;  // a lane's samples increase: the envelope interval is found by stepping
   constexpr bool F64 = sizeof(V) == 8;
@@ -994,7 +994,42 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
     if (k == sy.L - 1) return dr.x1;
     return (k < sy.L / 2) ? dr.x0 + (double)k * dby : dr.x1 - (double)(sy.L - 1 - k) * dby;
   };
-  if (drift) {
+  // fp32 drift (V = float): the planner's per-interval lines (kb_t, a_t, b_t) after the
+  // drift knots (sg_plan_harm.cpp); a chunk inside intervals d0 .. d0 + 6 picks its
+  // interval by integer compares against the wave-uniform kb_t and takes one FMA, with
+  // no per-chunk fp64 set-up. The fp64 evaluation per sample (interval compares, approx
+  // arithmetic, the product) was 38 % of this kernel (r05r: 3.36 -> 2.07 ms per C5
+  // launch without drift); a sample next to a knot may take the neighbouring line, equal
+  // there to within one sample's step.
+  // (lane q < 8 loads line d0 + q into the wave's LDS slot, a view of lkw: kb relative to
+  // c0 as int [0, 8), then (a, b) float pairs; the uniform values stay out of SGPRs,
+  // which this kernel spills)
+  bool fast32 = false;
+  int* const lkb = reinterpret_cast<int*>(lkw);
+  float* const lab = reinterpret_cast<float*>(lkw) + KW;
+  int kbr[KW - 2];
+  if (!F64 && drift) {
+    const double* lt = cknots + dr.k_off + 2 * (int64_t)dr.nk;
+    const int last = dr.nk - 2;  // intervals 0 .. nk - 2
+    if (lane < KW) {
+      const int t = d0 + lane <= last ? d0 + lane : last;
+      const uint64_t bits = __builtin_bit_cast(uint64_t, lt[2 * t + 1]);
+      const int64_t rel = (int64_t)lt[2 * t] - c0;
+      lkb[lane] = d0 + lane <= last ? (int)(rel < (1 << 30) ? rel : (1 << 30)) : 1 << 30;
+      lab[2 * lane] = __builtin_bit_cast(float, (uint32_t)bits);
+      lab[2 * lane + 1] = __builtin_bit_cast(float, (uint32_t)(bits >> 32));
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    fast32 = (int)(c1 - 1 - c0) < lkb[KW - 1];  // every sample inside intervals d0 .. d0 + 6
+#pragma unroll
+    for (int q = 0; q < KW - 2; ++q) kbr[q] = lkb[q + 1];
+    __builtin_amdgcn_wave_barrier();  // the slow path's set-up below rewrites the slot
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  if (drift && !fast32) {
     const double* x = cknots + dr.k_off;
 #pragma unroll
     for (int t = 0; t < KW; ++t) {
@@ -1013,38 +1048,15 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
 #pragma unroll
       for (int t = 1; t < KW - 1; ++t)
         if (lane == t) { xv = xs[t]; yv = ys[t]; x1 = xs[t + 1]; y1 = ys[t + 1]; }
-      const double sl = x1 > xv ? (y1 - yv) / (x1 - xv) : 0.0;
       lkw[3 * lane] = xv;
       lkw[3 * lane + 1] = yv;
-      lkw[3 * lane + 2] = sl;
-      if constexpr (!F64) {
-        // fp32 chunk form of interval t = lane: the line's value at the chunk's first
-        // sample and its step per sample, dm(c0 + r) = a_t + b_t r, and the first r
-        // whose u reaches the interval's left knot (r >= kb_t); a sample next to a knot
-        // may take the neighbouring line, equal there to within one sample's step
-        const double u0 = u_at(c0);
-        lkf[2 * lane] = (float)fma(sl, u0 - xv, yv);
-        lkf[2 * lane + 1] = (float)(sl * dby);
-        int kb = 0;
-        if (lane > 0) {
-          const double r = std::ceil((xv - u0) / dby);
-          kb = d0 + lane > dr.nk - 2 ? 1 << 20 : (r <= 0.0 ? 0 : (r >= 512.0 ? 512 : (int)r));
-        }
-        lki[lane] = kb;
-      }
+      lkw[3 * lane + 2] = x1 > xv ? (y1 - yv) / (x1 - xv) : 0.0;
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  // fp32 drift (V = float, the chunk inside the staged intervals, u increasing): the
-  // interval by integer compares against the wave-uniform kb_t, then one FMA. The fp64
-  // evaluation per sample (interval compares, approx arithmetic, the product) was 38 %
-  // of this kernel (r05r: 3.36 -> 2.07 ms per C5 launch without drift)
-  const bool fast32 = !F64 && drift && local_knots && dby > 0;
-  int kbr[KW - 2];
-#pragma unroll
-  for (int q = 0; q < KW - 2; ++q) kbr[q] = fast32 ? lki[q + 1] : 0;
+
   int p = pu, di = d0;
   // a chunk clear of both fade ramps multiplies by exactly 1: skip it (wave-uniform)
   const bool ramp = sy.fade >= 2 && (c0 < sy.fade || c1 > sy.L - sy.fade);
@@ -1073,8 +1085,8 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
       int t = 0;
 #pragma unroll
       for (int q = 0; q < KW - 2; ++q) t += r >= kbr[q] ? 1 : 0;
-      const float2 ab = reinterpret_cast<const float2*>(lkf)[t];
-      x *= (V)fmaf(ab.y, (float)r, ab.x);
+      const float2 ab = reinterpret_cast<const float2*>(lab)[t];
+      x *= (V)fmaf(ab.y, (float)(r - lkb[t]), ab.x);
     } else if (drift) {
       double dm;
       if (local_knots) {  // linear_at's interval and arithmetic, knots from registers
@@ -1111,15 +1123,13 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     const SgSyllable* __restrict__ syls, const double* __restrict__ cknots, const float* __restrict__ W,
     const float* __restrict__ maxes, float* __restrict__ out_buf, float* __restrict__ fs) {
   __shared__ double lk[4][3 * 8];  // per wave: drift intervals (x, y, slope)
-  __shared__ float lkf[4][2 * 8];  // per wave: their fp32 chunk lines (a, b)
-  __shared__ int lki[4][8];        // per wave: their first samples in the chunk
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   double* lkw = lk[wv];
 #pragma unroll 1
   for (int i = 0; i < SG_FIN_TILES; ++i) {
     const int64_t t = (int64_t)blockIdx.x * SG_FIN_TILES + i;
     if (t >= ntiles) break;
-    finalize_tile(stiles[t], pieces, syls, cknots, W, maxes, out_buf, fs, wv, lkw, lkf[wv], lki[wv]);
+    finalize_tile(stiles[t], pieces, syls, cknots, W, maxes, out_buf, fs, wv, lkw);
   }
 }
 
@@ -1132,7 +1142,7 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_finalize_hp(
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t t = blockIdx.x;
   if (t >= ntiles) return;
-  finalize_tile<double>(stiles[t], pieces, syls, cknots, W64, maxes, fh, fh, wv, lk[wv], nullptr, nullptr);
+  finalize_tile<double>(stiles[t], pieces, syls, cknots, W64, maxes, fh, fh, wv, lk[wv]);
 }
 
 // ---------------------------------------------------------------- launchers

@@ -1211,6 +1211,40 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
     sy.drift.x1 = gc_up[nGC - 1];
     B.cknots.insert(B.cknots.end(), gc_up.begin(), gc_up.begin() + nGC);
     B.cknots.insert(B.cknots.end(), drift.begin(), drift.end());
+    // per interval t, for sg_harm_finalize's fp32 chunk path: the first sample kb_t whose
+    // u (xout = seq.int(x0, x1, L), as the device forms it) reaches x_t, and the line
+    // dm(k) = a_t + b_t (k - kb_t) of approx() over the interval in samples, as
+    // (double kb_t, float a_t | float b_t bits) after x[] and y[]
+    const double* xk = &B.cknots[sy.drift.k_off];
+    const double* yk = xk + nGC;
+    const int64_t L = Lsyl;
+    const double x0 = sy.drift.x0, x1 = sy.drift.x1;
+    const double by = L > 1 ? (x1 - x0) / (double)(L - 1) : 0.0;
+    auto u_at = [&](int64_t k) -> double {
+      if (k == 0) return x0;
+      if (k == L - 1) return x1;
+      return (k < L / 2) ? x0 + (double)k * by : x1 - (double)(L - 1 - k) * by;
+    };
+    std::vector<double> lines((size_t)(2 * nGC));
+    for (int64_t t = 0; t < nGC; ++t) {
+      int64_t kb = 0;
+      if (t > 0 && by > 0) {
+        kb = (int64_t)std::ceil((xk[t] - x0) / by);
+        kb = std::max<int64_t>(0, std::min<int64_t>(kb, L));
+        while (kb > 0 && u_at(kb - 1) >= xk[t]) --kb;
+        while (kb < L && u_at(kb) < xk[t]) ++kb;
+      }
+      const double sl = t + 1 < nGC && xk[t + 1] > xk[t] ? (yk[t + 1] - yk[t]) / (xk[t + 1] - xk[t]) : 0.0;
+      const double uk = kb < L ? u_at(kb) : x1;
+      const float a = (float)std::fma(sl, uk - xk[t], yk[t]), bstep = (float)(sl * by);
+      uint32_t ua, ub;
+      std::memcpy(&ua, &a, 4);
+      std::memcpy(&ub, &bstep, 4);
+      const uint64_t bits = (uint64_t)ua | ((uint64_t)ub << 32);
+      lines[(size_t)(2 * t)] = (double)kb;
+      std::memcpy(&lines[(size_t)(2 * t + 1)], &bits, 8);
+    }
+    B.cknots.insert(B.cknots.end(), lines.begin(), lines.end());
   }
   const int32_t seg_off = (int32_t)B.segs.size();
   for (const HSeg& h : HS.segs) {
