@@ -1,8 +1,12 @@
 // sg_exec.cpp — HBM arena for a plan and the per-batch launch sequence.
 #include "sg_exec.h"
 #include "sg_amp.h"
+#include "sg_prof.h"
 
 #include <algorithm>
+#include <chrono>
+#include <exception>
+#include <thread>
 #include <cmath>
 #include <climits>
 #include <atomic>
@@ -200,14 +204,53 @@ struct ColumnReader {
     return 0;
   }
 };
-static TabSpans group_tables(const Batch& B) {
-  TabSpans S;
-  const int64_t ntask = bulk_size(B.tasks_x, B.tasks);
-  S.in_tab.assign((size_t)ntask, 0);
+// The batch's task blocks (Blocks<SgWTask>: one per planning part, then the
+// batch's own vector). A syllable's tasks never straddle two blocks (a part plans
+// whole calls), so the per-block passes below run on host threads independently.
+struct TaskBlock {
+  int64_t o;
+  const SgWTask* p;
+  int64_t n;
+};
+static std::vector<TaskBlock> task_blocks(const Batch& B) {
+  std::vector<TaskBlock> tb;
+  bulk_each(B.tasks_x, B.tasks, [&](int64_t o, const SgWTask* p, int64_t n) { tb.push_back(TaskBlock{o, p, n}); });
+  return tb;
+}
+// f(i) for i in [0, n) on up to 16 host threads (the upload's per-block passes)
+template <class F>
+static void for_blocks(size_t n, F&& f) {
+  const size_t nt = std::min<size_t>(n, std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
+  if (nt <= 1) {
+    for (size_t i = 0; i < n; ++i) f(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  std::vector<std::exception_ptr> errs(nt);
+  auto work = [&](size_t t) {
+    try {
+      for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
+    } catch (...) {
+      errs[t] = std::current_exception();
+    }
+  };
+  std::vector<std::thread> pool;
+  for (size_t t = 1; t < nt; ++t) pool.emplace_back(work, t);
+  work(0);
+  for (auto& th : pool) th.join();
+  for (auto& e : errs)
+    if (e) std::rethrow_exception(e);
+}
+// the runs of one block (jobs in task order; in_tab and direct_syl entries of the
+// block's tasks and syllables, which no other block touches)
+struct TabBlock {
+  std::vector<SgTabJob> jobs;
+  int64_t direct = 0, samples = 0, terms = 0;
+};
+static void group_block(const Batch& B, const ColumnReader& cols, const TaskBlock& blk, TabSpans& S, TabBlock& out) {
   auto tab_task = [](const SgWTask& t) {
     return t.flags == (SG_TASK_CONST | SG_TASK_LIN) && t.R <= SG_ROWS_F32 && t.Rn > 0;
   };
-  S.direct_syl.assign(B.syls.size(), 0);
   // a whole syllable of direct (or zero) pieces without envelope or drift: the job
   // writes its final samples (sg_sine_bank_tab's direct mode)
   auto direct_ok = [&](const SgWTask& t, int64_t r0, int64_t r1) {
@@ -219,9 +262,7 @@ static TabSpans group_tables(const Batch& B) {
       if (B.pieces[(size_t)p].nterms > 0) return false;
     return true;
   };
-  ColumnReader cols(B);
   const int per_job = SG_TAB_TASKS;
-  std::vector<SgTabJob> jobs;
   int64_t run0 = -1, run_samples = 0;
   SgWTask first{};
   auto close_run = [&](int64_t end) {  // tasks [run0, end)
@@ -231,34 +272,88 @@ static TabSpans group_tables(const Batch& B) {
       const bool dir = end - run0 <= per_job && direct_ok(first, run0, end);
       if (dir) {
         S.direct_syl[(size_t)first.syl] = 1;
-        ++S.direct;
+        ++out.direct;
       }
       for (int64_t i = run0; i < end; i += per_job) {
         const int32_t n = (int32_t)std::min<int64_t>(per_job, end - i);
-        jobs.push_back(SgTabJob{first.a_off, first.Rn, (int32_t)i, n, logn, first.syl, dir ? SG_TAB_DIRECT : 0});
+        out.jobs.push_back(SgTabJob{first.a_off, first.Rn, (int32_t)i, n, logn, first.syl, dir ? SG_TAB_DIRECT : 0});
         for (int64_t q = i; q < i + n; ++q) S.in_tab[(size_t)q] = 1;
       }
-      S.samples += run_samples;
-      S.terms += run_samples * first.Rn;
+      out.samples += run_samples;
+      out.terms += run_samples * first.Rn;
     }
     run0 = -1;
   };
-  bulk_each(B.tasks_x, B.tasks, [&](int64_t o, const SgWTask* p, int64_t n) {
-    for (int64_t k = 0; k < n; ++k) {
-      const SgWTask& t = p[k];
-      const bool ok = tab_task(t);
-      if (run0 >= 0 && !(ok && t.a_off == first.a_off && t.Rn == first.Rn && t.syl == first.syl)) close_run(o + k);
-      if (ok && run0 < 0) {
-        run0 = o + k;
-        first = t;
-        run_samples = 0;
-      }
-      if (ok) run_samples += t.len;
+  for (int64_t k = 0; k < blk.n; ++k) {
+    const SgWTask& t = blk.p[k];
+    const bool ok = tab_task(t);
+    if (run0 >= 0 && !(ok && t.a_off == first.a_off && t.Rn == first.Rn && t.syl == first.syl)) close_run(blk.o + k);
+    if (ok && run0 < 0) {
+      run0 = blk.o + k;
+      first = t;
+      run_samples = 0;
     }
+    if (ok) run_samples += t.len;
+  }
+  close_run(blk.o + blk.n);
+}
+// sine-bank task classes (each task's class depends on the task alone): fp64, tall
+// (sg_sine_bank_tall, short ones two per wave in _tall_pairs), short fp32 (two per
+// wave, sg_sine_bank_pairs), other fp32 (sg_sine_bank); tasks in a wavetable span
+// have none
+struct TaskClasses {
+  std::vector<int32_t> tlong, tshort, tall, tallp, thp;
+};
+static void classify_block(const TaskBlock& blk, const std::vector<uint8_t>& in_tab, TaskClasses& c) {
+  for (int64_t k = 0; k < blk.n; ++k) {
+    const SgWTask& t = blk.p[k];
+    const int32_t i = (int32_t)(blk.o + k);
+    const bool shrt = t.len <= 64 && !(t.flags & SG_TASK_ENV);
+    if (!in_tab.empty() && in_tab[(size_t)i]) continue;
+    if (t.flags & SG_TASK_HP) c.thp.push_back(i);
+    else if (t.R > SG_ROWS_F32) (shrt ? c.tallp : c.tall).push_back(i);
+    else if (shrt) c.tshort.push_back(i);
+    else c.tlong.push_back(i);
+  }
+}
+// Wavetable spans and task classes of a batch, block by block on host threads;
+// the result is what one pass over the tasks in order gives
+static TabSpans group_tables(const Batch& B, bool tables, TaskClasses* classes) {
+  TabSpans S;
+  const std::vector<TaskBlock> tb = task_blocks(B);
+  std::vector<TabBlock> tabs(tb.size());
+  std::vector<TaskClasses> cls(classes ? tb.size() : 0);
+  if (tables) {
+    S.in_tab.assign((size_t)bulk_size(B.tasks_x, B.tasks), 0);
+    S.direct_syl.assign(B.syls.size(), 0);
+  }
+  const ColumnReader cols(B);
+  for_blocks(tb.size(), [&](size_t i) {
+    if (tables) group_block(B, cols, tb[i], S, tabs[i]);
+    if (classes) classify_block(tb[i], S.in_tab, cls[i]);
   });
-  close_run(ntask);
-  for (const SgTabJob& j : jobs) S.tasks += j.n;
-  S.jobs = std::move(jobs);
+  for (TabBlock& t : tabs) {
+    S.jobs.insert(S.jobs.end(), t.jobs.begin(), t.jobs.end());
+    S.direct += t.direct;
+    S.samples += t.samples;
+    S.terms += t.terms;
+  }
+  for (const SgTabJob& j : S.jobs) S.tasks += j.n;
+  if (classes) {
+    auto cat = [&](std::vector<int32_t> TaskClasses::*m) {
+      std::vector<int32_t>& dst = classes->*m;
+      dst.clear();
+      size_t n = 0;
+      for (const TaskClasses& c : cls) n += (c.*m).size();
+      dst.reserve(n);
+      for (const TaskClasses& c : cls) dst.insert(dst.end(), (c.*m).begin(), (c.*m).end());
+    };
+    cat(&TaskClasses::tlong);
+    cat(&TaskClasses::tshort);
+    cat(&TaskClasses::tall);
+    cat(&TaskClasses::tallp);
+    cat(&TaskClasses::thp);
+  }
   return S;
 }
 
@@ -278,7 +373,7 @@ void finalize_plan(Batch& B) {
                    fry, (long long)nfry, B.epochs.size());
     }
     {
-      const TabSpans T = group_tables(B);
+      const TabSpans T = group_tables(B, true, nullptr);
       int64_t cl = 0, cl_samples = 0;
       bulk_each(B.tasks_x, B.tasks, [&](int64_t, const SgWTask* p, int64_t n) {
         for (int64_t k = 0; k < n; ++k)
@@ -413,12 +508,21 @@ extern "C" int sg_set_sine_table(int32_t on) {
 namespace sg {
 
 void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
+  // SG_PLAN_PROF=1: seconds of each upload stage on stderr
+  auto tprev = std::chrono::steady_clock::now();
+  auto stage = [&](const char* what) {
+    if (!g_prof_on) return;
+    const auto t = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "sg_upload_prof %-10s %.3f s\n", what, std::chrono::duration<double>(t - tprev).count());
+    tprev = t;
+  };
   Layout L(B);
   if (D.arena && D.arena_bytes < L.total) device_free(D);
   if (!D.arena) {
     HIPCHK(hipMalloc(&D.arena, L.total));
     D.arena_bytes = L.total;
   }
+  stage("malloc");
   char* a = D.arena;
   D.segs = (SgSeg*)(a + L.segs);
   D.epochs = (SgEpoch*)(a + L.epochs);
@@ -479,18 +583,16 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   cp((void*)D.ampjobs, B.ampjobs.data(), B.ampjobs.size() * sizeof(SgAmpJob));
   cp((void*)D.ampsrc, B.ampsrc.data(), B.ampsrc.size() * sizeof(float));
   bulk_each(B.tasks_x, B.tasks, [&](int64_t o, const SgWTask* p, int64_t n) { cp(D.tasks + o, p, n * sizeof(SgWTask)); });
-  // task classes (each task's class depends on the task alone): tall (sg_sine_bank_tall),
-  // short fp32 (two per wave, sg_sine_bank_pairs), other fp32 (sg_sine_bank)
-  D.tall_host.clear();
-  D.tlong_host.clear();
-  D.tshort_host.clear();
-  D.tallp_host.clear();
-  D.thp_host.clear();
-  // wavetable spans (SgTabJob, sg_dev.h)
-  TabSpans T;
-  if (tab_on()) T = group_tables(B);
+  stage("copy_tasks");
+  // wavetable spans (SgTabJob, sg_dev.h) and the task classes, block by block
+  TaskClasses C;
+  TabSpans T = group_tables(B, tab_on(), &C);
+  D.tlong_host.swap(C.tlong);
+  D.tshort_host.swap(C.tshort);
+  D.tall_host.swap(C.tall);
+  D.tallp_host.swap(C.tallp);
+  D.thp_host.swap(C.thp);
   D.tabjobs_host.swap(T.jobs);
-  const std::vector<uint8_t>& in_tab = T.in_tab;
   D.tab_samples = T.samples;
   D.tab_terms = T.terms;
   if (!D.tabjobs_host.empty()) {  // one allocation kept across uploads
@@ -505,18 +607,7 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
     }
     D.tabjobs = (SgTabJob*)D.tabbuf;
   }
-  bulk_each(B.tasks_x, B.tasks, [&](int64_t o, const SgWTask* p, int64_t n) {
-    for (int64_t k = 0; k < n; ++k) {
-      const SgWTask& t = p[k];
-      const int32_t i = (int32_t)(o + k);
-      const bool shrt = t.len <= 64 && !(t.flags & SG_TASK_ENV);
-      if (!in_tab.empty() && in_tab[(size_t)i]) continue;
-      if (t.flags & SG_TASK_HP) D.thp_host.push_back(i);
-      else if (t.R > SG_ROWS_F32) (shrt ? D.tallp_host : D.tall_host).push_back(i);
-      else if (t.len <= 64 && !(t.flags & SG_TASK_ENV)) D.tshort_host.push_back(i);
-      else D.tlong_host.push_back(i);
-    }
-  });
+  stage("classify");
   cp(D.tall, D.tall_host.data(), D.tall_host.size() * sizeof(int32_t));
   cp(D.tlong, D.tlong_host.data(), D.tlong_host.size() * sizeof(int32_t));
   cp(D.tshort, D.tshort_host.data(), D.tshort_host.size() * sizeof(int32_t));
@@ -559,6 +650,7 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   cp(D.envjobs, B.envjobs.data(), B.envjobs.size() * sizeof(SgEnvJob));
   cp(D.envtasks, B.envtasks.data(), B.envtasks.size() * sizeof(SgEnvTask));
   cp(D.elog2, B.elog2.data(), B.elog2.size() * sizeof(double));
+  stage("copy_rest");
   launch_amp_build(D, (int64_t)B.ampjobs.size(), s);  // the amplitude blocks, from the jobs just copied
   // gathered noise uniforms: the union of the draw ranges and the item jobs in a
   // temporary buffer, expanded into the uniform area
@@ -571,6 +663,7 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
     launch_ugather((const SgUJob*)((char*)ug + ub), (int64_t)B.ujobs.size(), (const float*)ug, D.fl, s);
   }
   HIPCHK(hipStreamSynchronize(s));
+  stage("amps_sync");
   if (ug) (void)hipFree(ug);
   while (D.ev_slice.size() < B.slices.size()) {
     hipEvent_t e;
