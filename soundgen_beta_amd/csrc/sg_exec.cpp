@@ -386,6 +386,21 @@ void finalize_plan(Batch& B) {
                    (size_t)T.tasks, (long long)T.samples, (double)T.terms, (long long)cl,
                    (long long)cl_samples);
     }
+    {  // pre-filter mixes that only place voiced syllables (raw items, no envelope, no noise)
+      int64_t all = 0, ident = 0, ni = 0, ident_items = 0;
+      for (const SgMix& m : B.mixes[0]) {
+        all += m.len;
+        bool id = m.mult.kind == 0 && m.am_lo == 0 && m.to_fs == 1 && m.base_kind == SG_BASE_NONE;
+        for (int32_t i = m.item0; i < m.item0 + m.nitems && id; ++i) {
+          const SgNoiseItem& it = B.items[(size_t)i];
+          id = it.ola < 0 && it.fade < 2 && it.strength.kind == 0 && !(it.flags & SG_ITEM_F64);
+        }
+        if (id) { ident += m.len; ident_items += m.nitems; }
+        ni += m.nitems;
+      }
+      std::fprintf(stderr, "sg plan: pre-filter mixes %zu, %lld samples; voiced-only %lld samples (%lld of %lld items)\n",
+                   B.mixes[0].size(), (long long)all, (long long)ident, (long long)ident_items, (long long)ni);
+    }
     std::vector<SgWTask> tasks;  // the merged task list (debug statistics only)
     bulk_each(B.tasks_x, B.tasks, [&](int64_t, const SgWTask* p, int64_t n) { tasks.insert(tasks.end(), p, p + n); });
     // sine-bank work: (sample, row) terms of the fp32 and the tall tasks, rows histogram of the tall ones

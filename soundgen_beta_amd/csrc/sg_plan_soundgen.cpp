@@ -654,25 +654,85 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
           }
       }
     }
-    const int64_t sound_fs = hp ? fh_alloc(B, std::max<int64_t>(Ls, 1)) : fs_alloc(B, std::max<int64_t>(Ls, 1));
-    SgMix pre{};
-    pre.dst = sound_fs;
-    pre.len = Ls;
-    pre.to_fs = hp ? 2 : 1;
-    pre.base_kind = SG_BASE_NONE;
-    ncontent = emit(sound, pre.item0);
-    pre.nitems = ncontent;
-    pre.mult.kind = 0;
-    {  // amplAnchorsGlobal (R/soundgen.R:715-733)
+    SgContour mult{};  // amplAnchorsGlobal (R/soundgen.R:715-733)
+    mult.kind = 0;
+    {
       bool below = false;
       for (double v : amplG.v) if (v < -A.throwaway) below = true;
       if (amplG.n() > 0 && below) {
         Anc g2 = amplG;
         for (auto& v : g2.v) v = std::pow(2.0, v / 10);
-        pre.mult = contour_desc(B, g2.view(), Ls, true, 0, true, -A.throwaway, false, sr);
+        mult = contour_desc(B, g2.view(), Ls, true, 0, true, -A.throwaway, false, sr);
       }
     }
-    B.mixes[0].push_back(pre);
+    // The pre-filter mix writes the bout's sound: its voiced syllables, the breathing
+    // noise and the global envelope (addVectors and `sound * amplEnvelope`). A bout
+    // whose sound is its voiced syllables alone (noise filtered separately, or none;
+    // no global envelope; fp32 path) is placed instead of mixed: each syllable's
+    // finalize writes its samples straight into the sound buffer at the syllable's
+    // offset, and mixes write only the zeros between the syllables. A syllable
+    // moves only when its offset keeps the 16-B residue of its old buffer (sg_harm_copy's
+    // aligned runs pair the W scratch with it, sg_plan_harm.cpp); the buffer's start is
+    // chosen so that the longest syllable does, and any other is copied by a one-item mix.
+    const bool place = !hp && mult.kind == 0 && (postNoise || noises.empty()) && !sound.items.empty() &&
+                       sound.items.size() == bout_syls.size();
+    int64_t sound_fs;
+    if (place) {
+      size_t big = 0;
+      for (size_t i = 1; i < sound.items.size(); ++i)
+        if (sound.items[i].len > sound.items[big].len) big = i;
+      const int64_t r = (4 - sound.items[big].off % 4) % 4;
+      sound_fs = fs_alloc(B, std::max<int64_t>(Ls, 1) + 3) + r;
+      auto zero_mix = [&](int64_t a, int64_t n) {
+        if (n <= 0) return;
+        SgMix z{};
+        z.dst = sound_fs + a;
+        z.len = n;
+        z.to_fs = 1;
+        z.base_kind = SG_BASE_NONE;
+        z.item0 = (int32_t)B.items.size();
+        z.mult.kind = 0;
+        B.mixes[0].push_back(z);
+      };
+      int64_t at = 0;
+      ncontent = 0;
+      for (size_t i = 0; i < sound.items.size(); ++i) {
+        const SgNoiseItem& it = sound.items[i];
+        zero_mix(at, it.off - at);
+        at = std::max(at, it.off + it.len);
+        if (it.len <= 0) continue;
+        ++ncontent;
+        SgSyllable& sy = B.syls[(size_t)bout_syls[i]];
+        if ((sound_fs + it.off) % 4 == sy.out_off % 4) {
+          sy.out_off = sound_fs + it.off;
+          continue;
+        }
+        SgMix c{};
+        c.dst = sound_fs + it.off;
+        c.len = it.len;
+        c.to_fs = 1;
+        c.base_kind = SG_BASE_NONE;
+        c.item0 = (int32_t)B.items.size();
+        c.nitems = 1;
+        c.mult.kind = 0;
+        SgNoiseItem ci = it;
+        ci.off = 0;
+        B.items.push_back(ci);
+        B.mixes[0].push_back(c);
+      }
+      zero_mix(at, Ls - at);
+    } else {
+      sound_fs = hp ? fh_alloc(B, std::max<int64_t>(Ls, 1)) : fs_alloc(B, std::max<int64_t>(Ls, 1));
+      SgMix pre{};
+      pre.dst = sound_fs;
+      pre.len = Ls;
+      pre.to_fs = hp ? 2 : 1;
+      pre.base_kind = SG_BASE_NONE;
+      ncontent = emit(sound, pre.item0);
+      pre.nitems = ncontent;
+      pre.mult = mult;
+      B.mixes[0].push_back(pre);
+    }
     // formant filter (R/soundgen.R:736-807); skipped when sum(sound) == 0,
     // which here means: nothing synthesized (no syllable, no noise content)
     Layout post;
