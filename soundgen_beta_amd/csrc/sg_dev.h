@@ -125,7 +125,8 @@ struct SgPiece {
 // of a syllable without envelope / drift lying in ONE piece that is either a
 // direct copy of the epoch waveform or zeros (crossFade's leading 0, 0):
 //   out[dst + q] = W[src + q] / max * fade(k0 + q)    (zeros: 0)
-// SG_COPY_VEC: source and destination 16-B aligned and n % 4 == 0 (float4 path).
+// SG_COPY_VEC: source and destination share their 16-B residue (float4 path between
+// scalar head and tail).
 constexpr int SG_COPY_TILE = 2048;      // planner's merge target
 constexpr int SG_COPY_TILE_MAX = 4096;  // kernel limit (16 float4 per lane)
 constexpr int SG_COPY_FS = 1;     // destination is the spectral scratch fs

@@ -135,7 +135,7 @@ static void split_finalize_tiles(Batch& B) {
       c.fade = sy.fade;
       c.syl = t.syl;
       c.flags = (sy.dst_fs ? SG_COPY_FS : 0) | (zero ? SG_COPY_ZERO : 0) |
-                (!zero && (c.src & 3) == 0 && (c.dst & 3) == 0 && (c.n & 3) == 0 ? SG_COPY_VEC : 0);
+                (!zero && ((c.src - c.dst) & 3) == 0 ? SG_COPY_VEC : 0);
       if (!B.copy_tiles.empty()) {  // extend the previous aligned run
         SgCopyTile& q = B.copy_tiles.back();
         if ((q.flags & SG_COPY_VEC) && (c.flags & SG_COPY_VEC) && q.syl == c.syl && q.flags == c.flags &&
@@ -387,7 +387,7 @@ void finalize_plan(Batch& B) {
                    (long long)cl_samples);
     }
     {  // pre-filter mixes that only place voiced syllables (raw items, no envelope, no noise)
-      int64_t all = 0, ident = 0, ni = 0, ident_items = 0;
+      int64_t all = 0, ident = 0, ni = 0, ident_items = 0, noisy = 0, noisy_cov = 0, other = 0;
       for (const SgMix& m : B.mixes[0]) {
         all += m.len;
         bool id = m.mult.kind == 0 && m.am_lo == 0 && m.to_fs == 1 && m.base_kind == SG_BASE_NONE;
@@ -397,9 +397,25 @@ void finalize_plan(Batch& B) {
         }
         if (id) { ident += m.len; ident_items += m.nitems; }
         ni += m.nitems;
+        if (!id && m.mult.kind == 0 && m.to_fs == 1) {  // noise-carrying mixes: samples under a noise item
+          std::vector<std::pair<int64_t, int64_t>> iv;
+          for (int32_t i = m.item0; i < m.item0 + m.nitems; ++i) {
+            const SgNoiseItem& it = B.items[(size_t)i];
+            if (it.ola >= 0) iv.push_back({std::max<int64_t>(0, it.off), std::min(m.len, it.off + it.len)});
+          }
+          std::sort(iv.begin(), iv.end());
+          int64_t cov = 0, e = 0;
+          for (auto& q : iv) { const int64_t a0 = std::max(q.first, e); if (q.second > a0) cov += q.second - a0; e = std::max(e, q.second); }
+          noisy += m.len;
+          noisy_cov += cov;
+        } else if (!id) {
+          other += m.len;
+        }
       }
       std::fprintf(stderr, "sg plan: pre-filter mixes %zu, %lld samples; voiced-only %lld samples (%lld of %lld items)\n",
                    B.mixes[0].size(), (long long)all, (long long)ident, (long long)ident_items, (long long)ni);
+      std::fprintf(stderr, "sg plan: pre-filter mixes with noise %lld samples (%lld under noise), enveloped or fp64 %lld\n",
+                   (long long)noisy, (long long)noisy_cov, (long long)other);
     }
     std::vector<SgWTask> tasks;  // the merged task list (debug statistics only)
     bulk_each(B.tasks_x, B.tasks, [&](int64_t, const SgWTask* p, int64_t n) { tasks.insert(tasks.end(), p, p + n); });

@@ -908,9 +908,9 @@ extern "C" __global__ __launch_bounds__(256) void sg_piece_max_hp(
 }
 
 // out[k] = assembled[k] * env[k] / max * fade[k] * drift[k]   (R/source.R:436-467)
-// A tile lying inside one direct piece with a 16-B aligned source and
-// destination moves float4s (4 consecutive samples per thread); otherwise
-// each thread takes samples k0 + 256 e + tid.
+// A tile lying inside one direct piece whose source and destination share their
+// 16-B residue moves float4s (4 consecutive samples per thread); otherwise each
+// thread takes samples k0 + 256 e + tid.
 
 // Fast path of the finalize (tiles from the planner's split, SgCopyTile):
 // one wavefront per tile of <= SG_COPY_TILE_MAX samples; aligned tiles keep up to
@@ -929,21 +929,34 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_copy(const SgCopyTile*
   const float inv_max = 1.f / maxes[T.max_slot];
   constexpr int E = SG_COPY_TILE_MAX / 256;
   if (T.flags & SG_COPY_VEC) {
+    // source and destination share their 16-B residue: a scalar head up to the
+    // destination's alignment, float4s, a scalar tail (h, nt < 4; wave-uniform)
+    const int h = min((4 - (int)(T.dst & 3)) & 3, T.n);
+    const int nb = (T.n - h) & ~3, nt = T.n - h - nb;
+    if (lane < h || (lane >= 4 && lane < 4 + nt)) {
+      const int q = lane < h ? lane : h + nb + lane - 4;
+      float v = src[q] * inv_max;
+      if (T.fade >= 2) v *= fade_at(T.fade, T.L, T.k0 + q);
+      dst[q] = v;
+    }
+    const float* __restrict__ s4 = src + h;
+    float* __restrict__ d4 = dst + h;
+    const int64_t k4 = T.k0 + h;
     float4 v[E];
 #pragma unroll
     for (int e = 0; e < E; ++e)
-      if (256 * e + 4 * lane < T.n) v[e] = *reinterpret_cast<const float4*>(src + 256 * e + 4 * lane);
-    const bool ramp = T.fade >= 2 && (T.k0 < T.fade || T.k0 + T.n > T.L - T.fade);
+      if (256 * e + 4 * lane < nb) v[e] = *reinterpret_cast<const float4*>(s4 + 256 * e + 4 * lane);
+    const bool ramp = T.fade >= 2 && (k4 < T.fade || k4 + nb > T.L - T.fade);
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      if (256 * e + 4 * lane >= T.n) break;
+      if (256 * e + 4 * lane >= nb) break;
       v[e].x *= inv_max; v[e].y *= inv_max; v[e].z *= inv_max; v[e].w *= inv_max;
       if (ramp) {
-        const int64_t k = T.k0 + 256 * e + 4 * lane;
+        const int64_t k = k4 + 256 * e + 4 * lane;
         v[e].x *= fade_at(T.fade, T.L, k); v[e].y *= fade_at(T.fade, T.L, k + 1);
         v[e].z *= fade_at(T.fade, T.L, k + 2); v[e].w *= fade_at(T.fade, T.L, k + 3);
       }
-      *reinterpret_cast<float4*>(dst + 256 * e + 4 * lane) = v[e];
+      *reinterpret_cast<float4*>(d4 + 256 * e + 4 * lane) = v[e];
     }
   } else {  // misaligned or short runs, zero pieces
     const bool zero = T.flags & SG_COPY_ZERO;

@@ -210,6 +210,7 @@ struct HarmProbe {
   double f0;
   std::vector<double> amp;
 };
+// With to_fs, out_off & 3 is the residue (mod 4 floats) of the fs slot allocated.
 int64_t plan_harmonics(Batch& B, const double* pitch, int64_t len, const sg_harm_params& P,
                        const sg_anchors& amplAnchors, Rng& R, int64_t out_off, bool dry_run, bool to_fs = false,
                        int64_t* fs_off = nullptr, std::vector<HarmProbe>* probes = nullptr);

@@ -1187,8 +1187,8 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
       probes->push_back(std::move(hp));
     }
   }
-  if (to_fs) {
-    out_off = fs_alloc(B, Lsyl);
+  if (to_fs) {  // a fresh fs slot whose 16-B residue is out_off's (the syllable's offset in its bout)
+    out_off = fs_alloc(B, Lsyl + 3) + (out_off & 3);
     if (fs_off) *fs_off = out_off;
   }
 

@@ -543,7 +543,8 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
       } else {
         int64_t fs_off = 0;
         const size_t np0 = probes.size();
-        sylLen = plan_harmonics(B, pc.data(), (int64_t)pc.size(), HPs, aA.view(), R, 0, false, true, &fs_off,
+        // the slot keeps the residue of the syllable's offset in the bout (a placed bout, below)
+        sylLen = plan_harmonics(B, pc.data(), (int64_t)pc.size(), HPs, aA.view(), R, voiced.len & 3, false, true, &fs_off,
                                 &probes);
         for (size_t q = np0; q < probes.size(); ++q) probe_pos.push_back(voiced.len + probes[q].t);
         bout_syls.push_back((int)B.syls.size() - 1);
@@ -670,19 +671,16 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
     // whose sound is its voiced syllables alone (noise filtered separately, or none;
     // no global envelope; fp32 path) is placed instead of mixed: each syllable's
     // finalize writes its samples straight into the sound buffer at the syllable's
-    // offset, and mixes write only the zeros between the syllables. A syllable
-    // moves only when its offset keeps the 16-B residue of its old buffer (sg_harm_copy's
-    // aligned runs pair the W scratch with it, sg_plan_harm.cpp); the buffer's start is
-    // chosen so that the longest syllable does, and any other is copied by a one-item mix.
+    // offset, and mixes write only the zeros between the syllables. Each syllable's slot
+    // was allocated with the residue (mod 4 floats) of its offset, and the sound buffer
+    // starts 16-B aligned, so a syllable keeps its residue when it moves (its W scratch
+    // was aligned against it for sg_harm_copy's float4 runs, sg_plan_harm.cpp); one that
+    // does not (none, by construction) is copied by a one-item mix.
     const bool place = !hp && mult.kind == 0 && (postNoise || noises.empty()) && !sound.items.empty() &&
                        sound.items.size() == bout_syls.size();
     int64_t sound_fs;
     if (place) {
-      size_t big = 0;
-      for (size_t i = 1; i < sound.items.size(); ++i)
-        if (sound.items[i].len > sound.items[big].len) big = i;
-      const int64_t r = (4 - sound.items[big].off % 4) % 4;
-      sound_fs = fs_alloc(B, std::max<int64_t>(Ls, 1) + 3) + r;
+      sound_fs = fs_alloc(B, std::max<int64_t>(Ls, 1));
       auto zero_mix = [&](int64_t a, int64_t n) {
         if (n <= 0) return;
         SgMix z{};
