@@ -6,6 +6,7 @@ inside libc (memcpy, memset, malloc) or libm is charged to the planner code
 that called it.
 
     python tools/plan_profile.py [calls] [top]
+    (SG_PP_RNG=1: the calls draw from one RRng stream through callbacks, as from R)
 
 Development tool; CPU only.
 """
@@ -77,6 +78,10 @@ def main(n_calls=4096, top=40):
     S.sg_sampler_stacks.restype = C.POINTER(C.c_uint64)
     depth = S.sg_sampler_depth()
     calls = bench.c5_calls(int(n_calls))
+    if os.environ.get("SG_PP_RNG"):  # one R-RNG stream through callbacks (the R shim's path): serial planning
+        from soundgen_beta_amd.rrng import RRng
+        g = RRng(7)
+        calls = [{"kind": "soundgen", "args": c["args"], "rng": g} for c in calls]
     # load the library, warm the size estimates (SG_PP_WARM=1: a whole plan first, so that the
     # host block cache is as warm as for bench.py's later chunks)
     batch.Plan(calls if os.environ.get("SG_PP_WARM") else calls[:max(64, len(calls) // 4)], None).close()
