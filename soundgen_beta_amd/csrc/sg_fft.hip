@@ -180,9 +180,13 @@ __device__ __forceinline__ int udiv(int n, uint32_t magic) {
   return magic ? (int)__umulhi((uint32_t)n, magic) : n;
 }
 
+// twS: the geometry's stage-ordered twiddles (SgFftGeom::tws: stage s with stride Ns
+// holds W_{Ns R}^{q jm} at Ns - 1 + (q - 1) Ns + jm), so that consecutive butterflies
+// read consecutive entries (a W_M table read at q jm M / (Ns R) put every lane of an
+// early stage in the same LDS bank)
 template <int R, bool INV>
-__device__ __forceinline__ void stage_ip(float2* X, int M, int Ns, const float2* twM, int fb, uint32_t mr_magic,
-                                         uint32_t ns_magic, int tstep) {
+__device__ __forceinline__ void stage_ip(float2* X, int M, int Ns, const float2* twS, int fb, uint32_t mr_magic,
+                                         uint32_t ns_magic) {
   constexpr int NB = NbOf<R>::value;
   constexpr bool ODD = (R % 2) == 1;
   constexpr int H = ODD ? (R - 1) / 2 : 1;
@@ -205,9 +209,10 @@ __device__ __forceinline__ void stage_ip(float2* X, int M, int Ns, const float2*
     for (int r = 0; r < R; ++r) v[r] = x[j + r * MR];
     const int jm = j - udiv(j, ns_magic) * Ns;
     if (Ns > 1) {
+      const float2* tw = twS + (Ns - 1) + jm;
 #pragma unroll
       for (int r = 1; r < R; ++r) {
-        const float2 w = twM[r * jm * tstep];
+        const float2 w = tw[(r - 1) * Ns];
         v[r] = INV ? cmulc(v[r], w) : cmul(v[r], w);
       }
     }
@@ -251,18 +256,16 @@ __device__ __forceinline__ void stage_ip(float2* X, int M, int Ns, const float2*
 }
 
 template <bool INV>
-__device__ void fft_ip(float2* X, const SgFftGeom& g, const float2* twM, int fb) {
+__device__ void fft_ip(float2* X, const SgFftGeom& g, const float2* twS, int fb) {
   int Ns = 1;
   for (int s = 0; s < g.nstages; ++s) {
     const int R = g.radix[s];
     const uint32_t mm = g.mr_magic[s], nm = g.ns_magic[s];
     int Ms = g.M;
     Ms = __builtin_amdgcn_readfirstlane(Ms);  // wave-uniform also when called out of line
-
-    const int ts = udiv(Ms / R, nm);      // M / (Ns R)
     switch (R) {
 #define SG_STAGE(RR) \
-      case RR: stage_ip<RR, INV>(X, Ms, Ns, twM, fb, mm, nm, ts); break;
+      case RR: stage_ip<RR, INV>(X, Ms, Ns, twS, fb, mm, nm); break;
       SG_STAGE(2) SG_STAGE(3) SG_STAGE(4) SG_STAGE(5) SG_STAGE(7) SG_STAGE(11) SG_STAGE(13) SG_STAGE(17)
       SG_STAGE(19) SG_STAGE(23) SG_STAGE(29) SG_STAGE(31)
 #undef SG_STAGE
@@ -543,8 +546,8 @@ __device__ void cdft(float2* X, const SgCdft& c, const SgFftGeom* __restrict__ g
                      float2* Z, float2* tw) {
   const SgFftGeom& gs = geoms[c.geom];
   const int T = c.L ? c.L : c.n;
-  const float2* twg = reinterpret_cast<const float2*>(fl + gs.tw);  // W_T^t, t < T
-  for (int t = threadIdx.x; t < T; t += SG_FFT_THREADS) tw[t] = twg[t];
+  const float2* twg = reinterpret_cast<const float2*>(fl + gs.tws);  // stage-ordered, T - 1 pairs
+  for (int t = threadIdx.x; t < T - 1; t += SG_FFT_THREADS) tw[t] = twg[t];
   if (!c.L) {
     __syncthreads();
     fft_ip<INV>(X, gs, tw, 1);
@@ -634,9 +637,11 @@ extern "C" __global__ __launch_bounds__(SG_FFT_THREADS) void sg_fft_frames(
   const int M = g.M, N = g.wl, fb = G.nf;
   const float2* twg = reinterpret_cast<const float2*>(fl + g.tw);
   const float2* twN = twg + M;  // L1/L2 resident (one read per bin pair)
-  float2* twM = A + fb * M;     // W_M table in LDS behind the frames (SG_FFT_DFT: the Bluestein buffers)
-  if (g.kind != SG_FFT_DFT)
-    for (int t = threadIdx.x; t < M; t += SG_FFT_THREADS) twM[t] = twg[t];
+  float2* twM = A + fb * M;     // stage-ordered twiddles in LDS behind the frames (SG_FFT_DFT: the Bluestein buffers)
+  if (g.kind != SG_FFT_DFT) {
+    const float2* tsg = reinterpret_cast<const float2*>(fl + g.tws);
+    for (int t = threadIdx.x; t < M - 1; t += SG_FFT_THREADS) twM[t] = tsg[t];
+  }
   if (threadIdx.x < fb) fr[threadIdx.x] = frames[G.f0 + threadIdx.x];
   __syncthreads();
   const float* ham = fl + g.win;
