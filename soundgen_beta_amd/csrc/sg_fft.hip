@@ -526,14 +526,16 @@ __device__ __forceinline__ void stage29_mfma(float2* X, const float4* tab, int l
 // order 2, 19, 29) -> 9.15 (29 first, VALU) -> 8.88 (29 first, MFMA); the noise
 // kernel 2.53 -> 2.44 -> 2.56 (3 waves per SIMD: the MFMA stage's accumulators
 // push it into spills), so the noise kernel keeps the VALU stage.
-template <bool INV, int CM, int R0, int R1, int R2, bool MFMA = true>
+// LAST = false stops before the last stage (the forward M = 1102 filter transform fuses
+// it with the untangle, r2_untangle_1102)
+template <bool INV, int CM, int R0, int R1, int R2, bool MFMA = true, bool LAST = true>
 __device__ __forceinline__ void fft_wc(float2* X, const float2* twS, const float4* A29, int lane SG_ST_PARAMS) {
   if constexpr (MFMA && CM == 1102 && R0 == 29) stage29_mfma<INV>(X, A29, lane);
   else stage_w<R0, INV, CM, 1>(X, CM, 1, twS, 0u, lane);
   SG_ST(INV ? 5 : 1);
   stage_w<R1, INV, CM, R0>(X, CM, R0, twS, 0u, lane);
   SG_ST(INV ? 6 : 2);
-  stage_w<R2, INV, CM, R0 * R1>(X, CM, R0 * R1, twS, 0u, lane);
+  if constexpr (LAST) stage_w<R2, INV, CM, R0 * R1>(X, CM, R0 * R1, twS, 0u, lane);
   SG_ST(INV ? 7 : 3);
 }
 
@@ -769,6 +771,10 @@ struct FramePf {
   __device__ __forceinline__ const float2& b(int i) const { return s[i]; }
 };
 
+// FUSED (M = 1102 filter frames, r2_untangle_1102): envelope pairs by unit, lane's
+// unit u = 1 + lane + 64 q (q < 5, u <= 275): a[2q] = (env[u], env[M - u]),
+// a[2q + 1] = (env[551 - u], env[551 + u]); xh = env[551], xh2 = env[0]
+template <bool FUSED = false>
 __device__ __forceinline__ void frame_prefetch(FramePf& P, const SgFrame& F, int mode, int M,
                                                const float* __restrict__ fl, const float* __restrict__ fs, int lane) {
   const int half = M / 2;
@@ -779,6 +785,20 @@ __device__ __forceinline__ void frame_prefetch(FramePf& P, const SgFrame& F, int
     for (int i = 0; i < SG_PF_SRC; ++i) {
       const int n = 64 * i + lane;
       if (n < M) P.s[i] = make_float2(src[2 * n], src[2 * n + 1]);
+    }
+    if constexpr (FUSED) {
+      static_assert(2 * 5 <= SG_PF_PAIR, "fused untangle: 5 units of two envelope pairs per lane");
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        const int u = 1 + lane + 64 * q;
+        if (u <= 275) {
+          P.a[2 * q] = make_float2(env[u], env[1102 - u]);
+          P.a[2 * q + 1] = make_float2(env[551 - u], env[551 + u]);
+        }
+      }
+      P.xh = env[551];
+      P.xh2 = env[0];
+      return;
     }
 #pragma unroll
     for (int i = 0; i < SG_PF_PAIR; ++i) {
@@ -803,6 +823,70 @@ __device__ __forceinline__ void frame_prefetch(FramePf& P, const SgFrame& F, int
   }
 }
 
+// The forward M = 1102 filter transform's last stage (radix 2, Ns = 551: butterfly j
+// maps Z[j], Z[j + 551] from X[j], X[j + 551] W^j) fused with the real-FFT untangle
+// (frame_front's pair k reads Z[k] and Z[M - k]). Butterflies u and 551 - u hold both
+// pairs (u, M - u) and (551 - u, 551 + u), so unit u (1 <= u <= 275; lane 1 + 64 q)
+// reads four slots, transforms and untangles in registers and writes the same four
+// slots: one LDS write and one read per point fewer than the separate passes. Units
+// touch disjoint slots; lane 0 also takes butterfly 0 and the pair k = 0 (slots 0
+// and 551) with its unit's Z[1] and Z[M - 1]. Same operations as stage_w<2> and the
+// untangle, in the same order.
+__device__ __forceinline__ void r2_untangle_1102(float2* A, const FramePf& P, const float2* twS, const float2* twN,
+                                                 int lane) {
+  constexpr int M = 1102, H = 551;
+  const float invN = 1.f / (float)(2 * M);
+  // one untangled pair (k, M - k) from Z_k = za, Z_{M-k} = zb (frame_front's packed form)
+  auto pair = [&](int kk, float2 za, float2 zb, float ek, float em) {
+    const v2 a = V(za), b = V(zb);
+    const v2 s = add_conjb(a, b), d = sub_conjb(a, b);
+    const v2 wk = V(twN[kk]);
+    const v2 p = vmul(d, wk);
+    const v2 yk = add_miq(s, p) * splat(0.5f * ek);
+    const v2 um = add_piq(s, p) * splat(0.5f * em);
+    const v2 q = vmulc(yk - um, wk);
+    const v2 e = yk + um;
+    const v2 zk = add_piq(e, q), zm = add_miq(e, q);
+    A[kk] = F(zk);
+    A[M - kk] = make_float2(zm.x, -zm.y);
+  };
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const int u = 1 + lane + 64 * q;
+    if (u > 275) continue;
+    const int v = H - u;
+    const float2 au = A[u], cu = A[u + H], av = A[v], cv = A[v + H];
+    const float2 tu = cmul(cu, twS[H - 1 + u]), tv = cmul(cv, twS[H - 1 + v]);
+    const float2 zu = cadd(au, tu), zuh = csub(au, tu);  // Z[u], Z[u + 551]
+    const float2 zv = cadd(av, tv), zvh = csub(av, tv);  // Z[v], Z[v + 551] = Z[M - u]
+    if (q == 0 && lane == 0) {  // butterfly 0 and the pair k = 0: Z[1] = zu, Z[M - 1] = zvh (u = 1)
+      const float2 a0 = A[0], c0 = A[H];
+      const float2 t0 = cmul(c0, twS[H - 1]);
+      const float2 z0 = cadd(a0, t0), zh = csub(a0, t0);
+      auto X_at = [&](float2 a, float2 b, int t) -> float2 {
+        const float2 e = make_float2(0.5f * (a.x + b.x), 0.5f * (a.y - b.y));
+        const float2 dd = make_float2(a.x - b.x, a.y + b.y);
+        const float2 o = make_float2(0.5f * dd.y, -0.5f * dd.x);
+        return cadd(e, cmul(o, twN[t]));
+      };
+      const float ek = P.xh2 * invN, em = P.a[0].y * invN;  // env[0], env[M - 1]
+      const float2 x0 = X_at(z0, z0, 0), xl = X_at(zvh, zu, M - 1);
+      const float y0 = x0.x * ek;
+      const float nyq = xl.x * em;
+      A[0] = make_float2(y0 + nyq, y0 - nyq);
+      const float2 xk = X_at(zh, zh, H);
+      const float eh = P.xh * invN;
+      const float2 yk = make_float2(xk.x * eh, xk.y * eh);
+      float2 a, b;
+      pack_pair(yk, yk, twN[H], a, b);
+      A[H] = a;
+    }
+    pair(u, zu, zvh, P.a[2 * q].x * invN, P.a[2 * q].y * invN);
+    pair(v, zv, zuh, P.a[2 * q + 1].x * invN, P.a[2 * q + 1].y * invN);
+  }
+  sg_wave_fence();
+}
+
 // Consume P: the frame's packed inverse-FFT input lands in A (FILTER: sound x
 // hamming -> forward FFT -> untangle, /wl x envelope, seewave's Hermitian
 // mirror; NOISE: uniforms x filter). Tables in LDS: ham (wl floats), twN (M pairs).
@@ -822,6 +906,11 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
     }
     sg_wave_fence();
     SG_ST(0);
+    if constexpr (CM == 1102 && R0 == 29 && R1 == 19 && R2 == 2) {  // the last stage fused with the untangle
+      fft_wc<false, CM, R0, R1, R2, true, false>(A, twS, A29, lane SG_ST_ARGS);
+      r2_untangle_1102(A, P, twS, twN, lane);
+      return;
+    }
     if constexpr (CM != 0) fft_wc<false, CM, R0, R1, R2>(A, twS, A29, lane SG_ST_ARGS);  // filter frames only
     else fft_w<false>(A, g, twS, lane SG_ST_ARGS);
     // untangle X[k] = E + W_N^k O (E, O from Z_k, conj Z_{M-k}), Y = X / wl x env,
@@ -960,7 +1049,8 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
     {
       int Mk = M;
       if (!CM) __asm__ __volatile__("" : "+s"(Mk));
-      frame_prefetch(P, frames[S.fdev + k], mode, Mk, fl, fs, lane);
+      frame_prefetch<CM == 1102 && R0 == 29 && R1 == 19 && R2 == 2 && MODE == SG_FRAME_FILTER>(
+          P, frames[S.fdev + k], mode, Mk, fl, fs, lane);
     }
     frame_front<CM, R0, R1, R2>(A, P, mode, g, twS, twN, ham, A29, lane SG_ST_ARGS);
     SG_ST(4);
