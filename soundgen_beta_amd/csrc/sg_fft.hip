@@ -1032,9 +1032,16 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
   const float scale = O.scale;
   float* out = fs + O.out;
   float m = -INFINITY;
-  float2 C[CP];
+  // M = 1102 filter frames: the inverse transform's last stage (radix 2, Ns = 551)
+  // fused with the window and the carry, which then lives in the butterflies' layout
+  // (lane l, q: elements j = l + 64 q and j + 551)
+  constexpr bool FUSED = CM == 1102 && R0 == 29 && R1 == 19 && R2 == 2 && MODE == SG_FRAME_FILTER;
+  constexpr int CR = FUSED ? 9 : CP;  // carry registers per half
+  float2 C[CR], C2[FUSED ? 9 : 1];
 #pragma unroll
-  for (int r = 0; r < CP; ++r) C[r] = make_float2(0.f, 0.f);
+  for (int r = 0; r < CR; ++r) C[r] = make_float2(0.f, 0.f);
+#pragma unroll
+  for (int r = 0; r < (FUSED ? 9 : 1); ++r) C2[r] = make_float2(0.f, 0.f);
   FramePf P;
   constexpr int W = MODE == SG_FRAME_NOISE ? SG_FFT_WAVES_NOISE : SG_FFT_WAVES;
   const float4* A29 = reinterpret_cast<const float4*>(twS + M * (4 + W));  // radix-29 fragments (M = 1102)
@@ -1049,24 +1056,40 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
     {
       int Mk = M;
       if (!CM) __asm__ __volatile__("" : "+s"(Mk));
-      frame_prefetch<CM == 1102 && R0 == 29 && R1 == 19 && R2 == 2 && MODE == SG_FRAME_FILTER>(
-          P, frames[S.fdev + k], mode, Mk, fl, fs, lane);
+      frame_prefetch<FUSED>(P, frames[S.fdev + k], mode, Mk, fl, fs, lane);
     }
     frame_front<CM, R0, R1, R2>(A, P, mode, g, twS, twN, ham, A29, lane SG_ST_ARGS);
     SG_ST(4);
-    if constexpr (CM != 0) fft_wc<true, CM, R0, R1, R2, MODE == SG_FRAME_FILTER>(A, twS, A29, lane SG_ST_ARGS);
-    else fft_w<true>(A, g, twS, lane SG_ST_ARGS);
-    int Mk = M, Nk = N;
-    if (!CM) __asm__ __volatile__("" : "+s"(Mk), "+s"(Nk));
-    // window (han holds hanning / wl: one packed FMA per pair) and add the carry
-    // (pairs n = 64 r + lane)
     const float2* han2 = reinterpret_cast<const float2*>(han);
+    if constexpr (FUSED) {
+      fft_wc<true, CM, R0, R1, R2, true, false>(A, twS, A29, lane SG_ST_ARGS);
+      // butterfly j: Z[j], Z[j + 551] from X[j], X[j + 551] conj(W^j) (stage_w<2>'s
+      // operations), each windowed (han holds hanning / wl) and added to its carry
 #pragma unroll
-    for (int r = 0; r < CP; ++r) {
-      const int n = 64 * r + lane;
-      if (n < Mk) A[n] = F(pfma(V(A[n]), V(han2[n]), V(C[r])));
+      for (int q = 0; q < 9; ++q) {
+        const int j = 64 * q + lane;
+        if (j >= 551) continue;
+        const float2 a = A[j], c = A[j + 551];
+        const float2 t = cmulc(c, twS[550 + j]);
+        A[j] = F(pfma(V(cadd(a, t)), V(han2[j]), V(C[q])));
+        A[j + 551] = F(pfma(V(csub(a, t)), V(han2[j + 551]), V(C2[q])));
+      }
+    } else {
+      if constexpr (CM != 0) fft_wc<true, CM, R0, R1, R2, MODE == SG_FRAME_FILTER>(A, twS, A29, lane SG_ST_ARGS);
+      else fft_w<true>(A, g, twS, lane SG_ST_ARGS);
+      int Mk = M;
+      if (!CM) __asm__ __volatile__("" : "+s"(Mk));
+      // window (han holds hanning / wl: one packed FMA per pair) and add the carry
+      // (pairs n = 64 r + lane)
+#pragma unroll
+      for (int r = 0; r < CP; ++r) {
+        const int n = 64 * r + lane;
+        if (n < Mk) A[n] = F(pfma(V(A[n]), V(han2[n]), V(C[r])));
+      }
+      for (int n = 64 * CP + lane; n < Mk; n += 64) A[n] = F(V(A[n]) * V(han2[n]));
     }
-    for (int n = 64 * CP + lane; n < Mk; n += 64) A[n] = F(V(A[n]) * V(han2[n]));
+    int Nk = N;
+    if (!CM) __asm__ __volatile__("" : "+s"(Nk));
     sg_wave_fence();
     SG_ST(8);
     const bool lastf = k == S.nf - 1;
@@ -1105,11 +1128,21 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
     if (!lastf) {
       // the next carry: every read unconditional (index clamped into the slice), all
       // in flight at once; i0 >= Nk exactly when the pair lies past the carried tail
-#pragma unroll
-      for (int r = 0; r < CP; ++r) {
-        const int i0 = 2 * (64 * r + lane) + D;
+      auto carry = [&](int n) {
+        const int i0 = 2 * n + D;
         const float a = Af[min(i0, Nk - 1)], b = Af[min(i0 + 1, Nk - 1)];
-        C[r] = make_float2(i0 < Nk ? a : 0.f, i0 + 1 < Nk ? b : 0.f);
+        return make_float2(i0 < Nk ? a : 0.f, i0 + 1 < Nk ? b : 0.f);
+      };
+      if constexpr (FUSED) {
+#pragma unroll
+        for (int q = 0; q < 9; ++q) {
+          const int j = 64 * q + lane;
+          C[q] = carry(j);
+          C2[q] = carry(j + 551);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < CP; ++r) C[r] = carry(64 * r + lane);
       }
     }
     sg_wave_fence();  // the next frame overwrites the slice
