@@ -1035,7 +1035,7 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
   // M = 1102 filter frames: the inverse transform's last stage (radix 2, Ns = 551)
   // fused with the window and the carry, which then lives in the butterflies' layout
   // (lane l, q: elements j = l + 64 q and j + 551)
-  constexpr bool FUSED = CM == 1102 && R0 == 29 && R1 == 19 && R2 == 2 && MODE == SG_FRAME_FILTER;
+  constexpr bool FUSED = CM == 1102 && R0 == 29 && R1 == 19 && R2 == 2;
   constexpr int CR = FUSED ? 9 : CP;  // carry registers per half
   float2 C[CR], C2[FUSED ? 9 : 1];
 #pragma unroll
@@ -1056,13 +1056,13 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
     {
       int Mk = M;
       if (!CM) __asm__ __volatile__("" : "+s"(Mk));
-      frame_prefetch<FUSED>(P, frames[S.fdev + k], mode, Mk, fl, fs, lane);
+      frame_prefetch<FUSED && MODE == SG_FRAME_FILTER>(P, frames[S.fdev + k], mode, Mk, fl, fs, lane);
     }
     frame_front<CM, R0, R1, R2>(A, P, mode, g, twS, twN, ham, A29, lane SG_ST_ARGS);
     SG_ST(4);
     const float2* han2 = reinterpret_cast<const float2*>(han);
     if constexpr (FUSED) {
-      fft_wc<true, CM, R0, R1, R2, true, false>(A, twS, A29, lane SG_ST_ARGS);
+      fft_wc<true, CM, R0, R1, R2, MODE == SG_FRAME_FILTER, false>(A, twS, A29, lane SG_ST_ARGS);
       // butterfly j: Z[j], Z[j + 551] from X[j], X[j + 551] conj(W^j) (stage_w<2>'s
       // operations), each windowed (han holds hanning / wl) and added to its carry
 #pragma unroll
