@@ -1648,7 +1648,11 @@ __device__ __forceinline__ void roots64(const double2* __restrict__ TN, int N, d
 // the M = 1102 transform of frame A (in place, LDS), forward or inverse; TN = W_N^t, t < N.
 // Each stage's twiddles are loaded one stage ahead (their latency under the previous
 // stage's arithmetic).
-__device__ __forceinline__ void fft64w_1102(double2* A, const double2* __restrict__ TN, bool inv, int lane) {
+// The caller owns tw2 (radix 2's twiddles, loaded here one stage ahead); the radix-2
+// stage itself runs only without SKIP2 (the callers fuse it with the untangle or the output)
+template <bool SKIP2 = false>
+__device__ __forceinline__ void fft64w_1102(double2* A, const double2* __restrict__ TN, bool inv, int lane,
+                                            double2 (&tw2)[9]) {
   constexpr int N = 2 * SG_F64W_M;
   // radix 19's twiddles W_551^(r jm) = W_2204^(4 r jm), jm = j mod 29 (j = lane < 58)
   const int j19 = lane < 58 ? lane : 0, jm19 = j19 < 29 ? j19 : j19 - 29;
@@ -1668,7 +1672,6 @@ __device__ __forceinline__ void fft64w_1102(double2* A, const double2* __restric
     sg_wave_fence();
   }
   // radix 2's twiddles W_1102^j = W_2204^(2 j), j = 64 i + lane
-  double2 tw2[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) tw2[i] = TN[2 * min(64 * i + lane, 550)];
   // radix 19 (Ns = 29, 58 butterflies): inputs j + 58 r times W_551^(r jm), outputs
@@ -1686,6 +1689,7 @@ __device__ __forceinline__ void fft64w_1102(double2* A, const double2* __restric
     if (lane < 58) bfly64_store<19>(x, A + 19 * (j19 - jm19) + jm19, 29, c, sn, inv);
     sg_wave_fence();
   }
+  if constexpr (SKIP2) return;
   // radix 2 (Ns = 551, 551 butterflies): j and j + 551, the second times W_1102^j; in place
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
@@ -1725,8 +1729,8 @@ extern "C" __global__ __launch_bounds__(SG_F64W_WAVES * 64) void sg_fft_frames64
       A[n] = make_double2(x[2 * n] * h.x, x[2 * n + 1] * h.y);
     }
     sg_wave_fence();
-    fft64w_1102(A, TN, false, lane);
   }
+  double2 tw2[9];
   // FILTER: untangle, / N, x env; NOISE: uniforms x filter (real). Then seewave's
   // Hermitian extension packed for the inverse: slot k <- Y_k and conj Y_{M-k} (k = 0:
   // Re Y_{M-1}). Lane pair k owns slots k and M - k; the k = 0 lane also reads slots 1
@@ -1746,36 +1750,76 @@ extern "C" __global__ __launch_bounds__(SG_F64W_WAVES * 64) void sg_fft_frames64
     const double2 t = cmul64(df, conj_if(TN[k], true));  // W_N^-k (X'_k - X'_{k+M})
     return make_double2(sm.x - t.y, sm.y + t.x);
   };
-#pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    const int k = 64 * i + lane;
-    const bool act = k <= half;
-    const int kk = act ? k : 0, km = kk == 0 ? 0 : M - kk;
-    const double2 p = A[kk], q = A[km];
-    double2 p1 = p, pM1 = p;
-    if (i == 0) {
-      p1 = A[1];
-      pM1 = A[M - 1];
-    }
-    sg_wave_fence();
-    if (!act) continue;
-    if (kk == 0) {
-      const double2 y0 = Yat(0, p, p), yl = Yat(M - 1, pM1, p1);
-      A[0] = pack(0, y0, make_double2(yl.x, 0.0));
-    } else {
-      const double2 yk = Yat(kk, p, q), ym = Yat(km, q, p);
+  if (!noise) {
+    // the forward transform's radix-2 stage fused with the untangle (as the fp32
+    // r2_untangle_1102): butterflies u and 551 - u give Z[u], Z[M - u], Z[551 - u],
+    // Z[551 + u], i.e. the pairs (u, M - u) and (551 - u, 551 + u); lane 0 also takes
+    // butterfly 0 and the pairs k = 0 and k = 551 (self-paired)
+    fft64w_1102<true>(A, TN, false, lane, tw2);
+    auto bfly = [&](int j, double2& z0, double2& z1) {  // stage 2's operations, forward
+      const double2 u = A[j], v = cmul64(A[j + half], TN[2 * j]);
+      z0 = make_double2(u.x + v.x, u.y + v.y);
+      z1 = make_double2(u.x - v.x, u.y - v.y);
+    };
+    auto pair = [&](int kk, double2 p, double2 q) {  // Z_kk = p, Z_{M-kk} = q
+      const double2 yk = Yat(kk, p, q), ym = Yat(M - kk, q, p);
       A[kk] = pack(kk, yk, make_double2(ym.x, -ym.y));
-      if (km != kk) A[km] = pack(km, ym, make_double2(yk.x, -yk.y));
+      A[M - kk] = pack(M - kk, ym, make_double2(yk.x, -yk.y));
+    };
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      const int u = 1 + lane + 64 * q;
+      if (u > 275) continue;
+      const int v = half - u;
+      double2 zu, zuh, zv, zvh;  // Z[u], Z[u + 551], Z[v], Z[v + 551] = Z[M - u]
+      bfly(u, zu, zuh);
+      bfly(v, zv, zvh);
+      if (q == 0 && lane == 0) {  // u = 1: Z[1] = zu, Z[M - 1] = zvh
+        double2 z0, zh;
+        bfly(0, z0, zh);
+        const double2 y0 = Yat(0, z0, z0), yl = Yat(M - 1, zvh, zu);
+        A[0] = pack(0, y0, make_double2(yl.x, 0.0));
+        const double2 yh = Yat(half, zh, zh);
+        A[half] = pack(half, yh, make_double2(yh.x, -yh.y));
+      }
+      pair(u, zu, zvh);
+      pair(v, zv, zuh);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int k = 64 * i + lane;
+      if (k > half) continue;
+      const int km = k == 0 ? 0 : M - k;
+      const double2 z = make_double2(0.0, 0.0);  // noise: Y from the uniforms alone
+      if (k == 0) {
+        const double2 y0 = Yat(0, z, z), yl = Yat(M - 1, z, z);
+        A[0] = pack(0, y0, make_double2(yl.x, 0.0));
+      } else {
+        const double2 yk = Yat(k, z, z), ym = Yat(km, z, z);
+        A[k] = pack(k, yk, make_double2(ym.x, -ym.y));
+        if (km != k) A[km] = pack(km, ym, make_double2(yk.x, -yk.y));
+      }
     }
   }
   sg_wave_fence();
-  fft64w_1102(A, TN, true, lane);
+  // the inverse transform's radix-2 stage fused with the output: butterfly j's two points
+  // are the frame's samples 2j, 2j + 1 and 2j + 1102, 2j + 1103 (/ N x hann), stored
+  // without a pass through LDS
+  fft64w_1102<true>(A, TN, true, lane, tw2);
   float* out = fs + F.dst;
-#pragma unroll 6
-  for (int n = lane; n < M; n += 64) {
-    const double2 h = han[n], c = A[n];
-    out[2 * n] = (float)(c.x * invN * h.x);
-    out[2 * n + 1] = (float)(c.y * invN * h.y);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int j = 64 * i + lane;
+    if (j < half) {
+      const double2 u = A[j], v = cmul64(A[j + half], conj_if(tw2[i], true));
+      const double2 c0 = make_double2(u.x + v.x, u.y + v.y), c1 = make_double2(u.x - v.x, u.y - v.y);
+      const double2 h0 = han[j], h1 = han[j + half];
+      out[2 * j] = (float)(c0.x * invN * h0.x);
+      out[2 * j + 1] = (float)(c0.y * invN * h0.y);
+      out[2 * (j + half)] = (float)(c1.x * invN * h1.x);
+      out[2 * (j + half) + 1] = (float)(c1.y * invN * h1.y);
+    }
   }
 }
 
