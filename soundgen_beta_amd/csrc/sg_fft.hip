@@ -1650,9 +1650,12 @@ __device__ __forceinline__ void roots64(const double2* __restrict__ TN, int N, d
 // stage's arithmetic).
 // The caller owns tw2 (radix 2's twiddles, loaded here one stage ahead); the radix-2
 // stage itself runs only without SKIP2 (the callers fuse it with the untangle or the output)
+// xs (forward filter frames): the first stage reads the frame straight from the fp64
+// sound times hamming (hm) instead of from A (no LDS pass for the window)
 template <bool SKIP2 = false>
 __device__ __forceinline__ void fft64w_1102(double2* A, const double2* __restrict__ TN, bool inv, int lane,
-                                            double2 (&tw2)[9]) {
+                                            double2 (&tw2)[9], const double* __restrict__ xs = nullptr,
+                                            const double2* __restrict__ hm = nullptr) {
   constexpr int N = 2 * SG_F64W_M;
   // radix 19's twiddles W_551^(r jm) = W_2204^(4 r jm), jm = j mod 29 (j = lane < 58)
   const int j19 = lane < 58 ? lane : 0, jm19 = j19 < 29 ? j19 : j19 - 29;
@@ -1665,8 +1668,17 @@ __device__ __forceinline__ void fft64w_1102(double2* A, const double2* __restric
     roots64<29>(TN, N, c, sn);
     double2 x[29];
     const int j = lane < 38 ? lane : 0;
+    if (xs) {
 #pragma unroll
-    for (int r = 0; r < 29; ++r) x[r] = A[j + 38 * r];
+      for (int r = 0; r < 29; ++r) {
+        const int n = j + 38 * r;
+        const double2 h = hm[n];
+        x[r] = make_double2(xs[2 * n] * h.x, xs[2 * n + 1] * h.y);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 29; ++r) x[r] = A[j + 38 * r];
+    }
     sg_wave_fence();  // every read of the stage before the first write
     if (lane < 38) bfly64_store<29>(x, A + 29 * j, 1, c, sn, inv);
     sg_wave_fence();
@@ -1721,15 +1733,6 @@ extern "C" __global__ __launch_bounds__(SG_F64W_WAVES * 64) void sg_fft_frames64
   const bool noise = F.mode == SG_F64_NOISE;
   const double invN = 1.0 / (double)N;
   const float* env = fl + F.env;
-  if (!noise) {
-    const double* x = fh + F.src;
-#pragma unroll 6
-    for (int n = lane; n < M; n += 64) {  // hamming (seewave ftwindow), packed pairs
-      const double2 h = ham[n];
-      A[n] = make_double2(x[2 * n] * h.x, x[2 * n + 1] * h.y);
-    }
-    sg_wave_fence();
-  }
   double2 tw2[9];
   // FILTER: untangle, / N, x env; NOISE: uniforms x filter (real). Then seewave's
   // Hermitian extension packed for the inverse: slot k <- Y_k and conj Y_{M-k} (k = 0:
@@ -1755,7 +1758,7 @@ extern "C" __global__ __launch_bounds__(SG_F64W_WAVES * 64) void sg_fft_frames64
     // r2_untangle_1102): butterflies u and 551 - u give Z[u], Z[M - u], Z[551 - u],
     // Z[551 + u], i.e. the pairs (u, M - u) and (551 - u, 551 + u); lane 0 also takes
     // butterfly 0 and the pairs k = 0 and k = 551 (self-paired)
-    fft64w_1102<true>(A, TN, false, lane, tw2);
+    fft64w_1102<true>(A, TN, false, lane, tw2, fh + F.src, ham);  // hamming (seewave ftwindow) in the first stage's loads
     auto bfly = [&](int j, double2& z0, double2& z1) {  // stage 2's operations, forward
       const double2 u = A[j], v = cmul64(A[j + half], TN[2 * j]);
       z0 = make_double2(u.x + v.x, u.y + v.y);
