@@ -381,8 +381,8 @@ def roofline(st, prof, steps, config, kern):
     if issue:
         r["issue"] = issue
     if kern == "sg_stft_ola":
-        r["binding"] = ("latency at 2 waves/SIMD (241 VGPRs): per wave ~37 % issuing, ~35 % parked on s_waitcnt; "
-                        "radix-29 stage on the matrix pipe (MFMA), radix 19 and 2 on the VALU; see issue")
+        r["binding"] = ("LDS passes and latency at 2 waves/SIMD (221 VGPRs): radix-29 stage on the matrix pipe "
+                        "(MFMA), radix 19 on the VALU, radix 2 fused with the untangle and the window; see issue")
     return r
 
 
