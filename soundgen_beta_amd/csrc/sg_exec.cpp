@@ -387,7 +387,7 @@ void finalize_plan(Batch& B) {
                    (long long)cl_samples);
     }
     {  // pre-filter mixes that only place voiced syllables (raw items, no envelope, no noise)
-      int64_t all = 0, ident = 0, ni = 0, ident_items = 0, noisy = 0, noisy_cov = 0, other = 0;
+      int64_t all = 0, ident = 0, ni = 0, ident_items = 0, noisy = 0, noisy_cov = 0, other = 0, env_only = 0, env_kind[4] = {0, 0, 0, 0};
       for (const SgMix& m : B.mixes[0]) {
         all += m.len;
         bool id = m.mult.kind == 0 && m.am_lo == 0 && m.to_fs == 1 && m.base_kind == SG_BASE_NONE;
@@ -410,12 +410,17 @@ void finalize_plan(Batch& B) {
           noisy_cov += cov;
         } else if (!id) {
           other += m.len;
+          bool vo = m.to_fs == 1;
+          for (int32_t i = m.item0; i < m.item0 + m.nitems && vo; ++i) vo = B.items[(size_t)i].ola < 0;
+          if (vo && m.mult.kind != 0) { env_only += m.len; env_kind[m.mult.kind & 3]++; }
         }
       }
       std::fprintf(stderr, "sg plan: pre-filter mixes %zu, %lld samples; voiced-only %lld samples (%lld of %lld items)\n",
                    B.mixes[0].size(), (long long)all, (long long)ident, (long long)ident_items, (long long)ni);
-      std::fprintf(stderr, "sg plan: pre-filter mixes with noise %lld samples (%lld under noise), enveloped or fp64 %lld\n",
-                   (long long)noisy, (long long)noisy_cov, (long long)other);
+      std::fprintf(stderr, "sg plan: pre-filter mixes with noise %lld samples (%lld under noise), enveloped or fp64 %lld "
+                   "(voiced-only with the global envelope %lld; contour kinds 1/2/3: %lld %lld %lld)\n",
+                   (long long)noisy, (long long)noisy_cov, (long long)other, (long long)env_only, (long long)env_kind[1],
+                   (long long)env_kind[2], (long long)env_kind[3]);
     }
     std::vector<SgWTask> tasks;  // the merged task list (debug statistics only)
     bulk_each(B.tasks_x, B.tasks, [&](int64_t, const SgWTask* p, int64_t n) { tasks.insert(tasks.end(), p, p + n); });
