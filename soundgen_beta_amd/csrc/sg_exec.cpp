@@ -422,6 +422,16 @@ void finalize_plan(Batch& B) {
                    (long long)noisy, (long long)noisy_cov, (long long)other, (long long)env_only, (long long)env_kind[1],
                    (long long)env_kind[2], (long long)env_kind[3]);
     }
+    {  // spectral envelopes: jobs by column count, wave tasks, bins
+      int64_t j1 = 0, jm = 0, cols = 0, bins = 0;
+      for (const SgEnvJob& j : B.envjobs) {
+        (j.nc == 1 ? j1 : jm)++;
+        cols += j.nc;
+        bins += (int64_t)j.nc * j.nr;
+      }
+      std::fprintf(stderr, "sg plan: envelope jobs %zu (%lld one-column), %lld columns, %lld bins, %zu wave tasks\n",
+                   B.envjobs.size(), (long long)j1, (long long)cols, (long long)bins, B.envtasks.size());
+    }
     std::vector<SgWTask> tasks;  // the merged task list (debug statistics only)
     bulk_each(B.tasks_x, B.tasks, [&](int64_t, const SgWTask* p, int64_t n) { tasks.insert(tasks.end(), p, p + n); });
     // sine-bank work: (sample, row) terms of the fp32 and the tall tasks, rows histogram of the tall ones
