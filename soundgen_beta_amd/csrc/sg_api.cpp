@@ -359,6 +359,7 @@ void merge_parts(sg::Batch& D, std::vector<sg::Batch>& parts, int threads) {
       s.out_off += s.hp ? b.fh : (s.dst_fs ? b.fs : b.out);
       s.piece0 += (int32_t)b.piece; s.max_slot += (int32_t)b.syl; s.task0 += b.task;
       ck(s.env);
+      ck(s.genv);
       if (s.drift.nk > 0) s.drift.k_off += b.ck;
     }
     for (auto& t : S.syl_tiles) {

@@ -183,6 +183,11 @@ struct SgSyllable {
   int32_t hp;        // 1: fp64 syllable: pieces read W64, out_off indexes the fp64 scratch fh
   SgContour env;     // amplEnvelope (kind 0 = none)
   SgLinear drift;
+  // a syllable placed in its bout's sound buffer under the bout's global envelope
+  // (amplAnchorsGlobal, R/soundgen.R:721-733): x *= genv at bout sample genv_off + k,
+  // the bout genv_len long (kind 0 = none)
+  SgContour genv;
+  int64_t genv_off, genv_len;
 };
 
 // assemble/finalize tiles over syllable samples

@@ -114,7 +114,7 @@ static void split_finalize_tiles(Batch& B) {
     }
     const int64_t end = std::min<int64_t>(t.k0 + 1024, sy.L);
     const int pend = sy.piece0 + sy.npiece;
-    bool ok = sy.env.kind == 0 && sy.drift.nk == 0;
+    bool ok = sy.env.kind == 0 && sy.drift.nk == 0 && sy.genv.kind == 0;
     for (int p = t.piece; ok && p < pend && B.pieces[p].start < end; ++p) ok = B.pieces[p].nterms <= 0;
     if (!ok) {
       B.fin_tiles.push_back(t);
@@ -256,7 +256,7 @@ static void group_block(const Batch& B, const ColumnReader& cols, const TaskBloc
   auto direct_ok = [&](const SgWTask& t, int64_t r0, int64_t r1) {
     if (t.syl < 0 || t.syl >= (int32_t)B.syls.size() || !direct_on()) return false;
     const SgSyllable& sy = B.syls[(size_t)t.syl];
-    if (sy.hp || sy.env.kind != 0 || sy.drift.nk != 0 || sy.nptile != 0) return false;
+    if (sy.hp || sy.env.kind != 0 || sy.genv.kind != 0 || sy.drift.nk != 0 || sy.nptile != 0) return false;
     if (r0 != sy.task0 || r1 != sy.task0 + sy.ntask || r1 - r0 > SG_TAB_TASKS) return false;
     for (int32_t p = sy.piece0; p < sy.piece0 + sy.npiece; ++p)
       if (B.pieces[(size_t)p].nterms > 0) return false;

@@ -979,6 +979,7 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
                                               int wv, double* lkw) {
   const SgSyllable& sy = syls[tl.syl];
   int ecur = -1;  // a lane's samples increase: the envelope interval is found by stepping
+  int gcur = -1;  // the same for the bout's global envelope (placed syllables)
   constexpr bool F64 = sizeof(V) == 8;
   V* __restrict__ out = (!F64 && sy.dst_fs) ? fs : out_buf;
   const V inv_max = (V)1 / (V)maxes[sy.max_slot];
@@ -1116,6 +1117,8 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
     } else if (dr.nk == 1) {
       x = (V)((double)x * cknots[dr.k_off + 1]);
     }
+    if (sy.genv.kind != 0)  // placed under the bout's global envelope (the pre-filter mix's product)
+      x = (V)((double)x * sgd::contour_at_cursor(sy.genv, cknots, sy.genv_len, sy.genv_off + k, gcur));
     res[e] = x;
   }
 #pragma unroll

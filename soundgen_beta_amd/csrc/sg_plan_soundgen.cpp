@@ -669,14 +669,15 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
     // The pre-filter mix writes the bout's sound: its voiced syllables, the breathing
     // noise and the global envelope (addVectors and `sound * amplEnvelope`). A bout
     // whose sound is its voiced syllables alone (noise filtered separately, or none;
-    // no global envelope; fp32 path) is placed instead of mixed: each syllable's
-    // finalize writes its samples straight into the sound buffer at the syllable's
-    // offset, and mixes write only the zeros between the syllables. Each syllable's slot
+    // fp32 path) is placed instead of mixed: each syllable's finalize writes its samples
+    // straight into the sound buffer at the syllable's offset, times the global envelope
+    // at that offset if there is one (the mix's own product), and mixes write only the
+    // zeros between the syllables (zero under any envelope). Each syllable's slot
     // was allocated with the residue (mod 4 floats) of its offset, and the sound buffer
     // starts 16-B aligned, so a syllable keeps its residue when it moves (its W scratch
     // was aligned against it for sg_harm_copy's float4 runs, sg_plan_harm.cpp); one that
     // does not (none, by construction) is copied by a one-item mix.
-    const bool place = !hp && mult.kind == 0 && (postNoise || noises.empty()) && !sound.items.empty() &&
+    const bool place = !hp && (postNoise || noises.empty()) && !sound.items.empty() &&
                        sound.items.size() == bout_syls.size();
     int64_t sound_fs;
     if (place) {
@@ -703,6 +704,9 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
         SgSyllable& sy = B.syls[(size_t)bout_syls[i]];
         if ((sound_fs + it.off) % 4 == sy.out_off % 4) {
           sy.out_off = sound_fs + it.off;
+          sy.genv = mult;  // the global envelope, applied by the finalize (kind 0: none)
+          sy.genv_off = it.off;
+          sy.genv_len = Ls;
           continue;
         }
         SgMix c{};
@@ -712,7 +716,7 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
         c.base_kind = SG_BASE_NONE;
         c.item0 = (int32_t)B.items.size();
         c.nitems = 1;
-        c.mult.kind = 0;
+        c.mult = mult;
         SgNoiseItem ci = it;
         ci.off = 0;
         B.items.push_back(ci);
