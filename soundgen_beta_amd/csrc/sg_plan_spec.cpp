@@ -942,10 +942,11 @@ void finalize_spec(Batch& B) {
       if (B.olas_dev[oi].fused) order.push_back(oi);
     auto geom_of = [&](size_t oi) { return B.frame_geom[ph][B.olas_dev[oi].fidx - fbase]; };
     std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return geom_of(a) < geom_of(b); });
-    // Segment length: SG_SEG_FRAMES frames would leave a partial last round of
+    // Segment length: sg_seg_frames(ph) frames would leave a partial last round of
     // workgroups (one per CU), so pick the length that packs the segments into
-    // whole rounds of sg_resident_waves(ph) (the fewest rounds SG_SEG_FRAMES needs).
-    int64_t seg_frames = SG_SEG_FRAMES;
+    // whole rounds of sg_resident_waves(ph) (the fewest rounds sg_seg_frames(ph) needs).
+    const int64_t SEG = sg_seg_frames(ph);
+    int64_t seg_frames = SEG;
     {
       auto segs_at = [&](int64_t S) {
         int64_t tot = 0, run = 0;
@@ -963,11 +964,11 @@ void finalize_spec(Batch& B) {
         }
         return tot + (WPH - run % WPH) % WPH;
       };
-      const int64_t base = segs_at(SG_SEG_FRAMES);
+      const int64_t base = segs_at(SEG);
       const int64_t rounds = (base + sg_resident_waves(ph) - 1) / sg_resident_waves(ph);
       int64_t S = SG_SEG_MIN_FRAMES;
-      while (S < SG_SEG_FRAMES && segs_at(S) > rounds * sg_resident_waves(ph)) S = std::max(S + 1, S * 9 / 8);
-      seg_frames = std::min<int64_t>(S, SG_SEG_FRAMES);
+      while (S < SEG && segs_at(S) > rounds * sg_resident_waves(ph)) S = std::max(S + 1, S * 9 / 8);
+      seg_frames = std::min<int64_t>(S, SEG);
     }
     int cur_geom = -1;
     auto pad = [&]() {
