@@ -421,15 +421,36 @@ __device__ __forceinline__ void fft_w(float2* X, const SgFftGeom& g, const float
 // as two real products [16 x 16] x [16 x 80] on v_mfma_f32_16x16x4_f32 (exact
 // fp32: a k-ordered fmaf chain, like the VALU form). Rows: k; the cos matrix's
 // column m = 0 is 1 (x_0 enters P), row 15 / column 15 are zero padding.
-// Columns: n < 38 the real parts of butterfly j = n, 38 <= n < 76 the imaginary
-// parts of j = n - 38, 76..79 padding. Q's operand carries the OTHER component
-// of the same column, so one lane holds P_k.c and (Q_k).c' for its column c and
-// finishes y_k.c, y_{29-k}.c alone: y.re = P.re +- Q.im, y.im = P.im -+ Q.re.
-// Per lane: 40 two-point LDS reads, 40 MFMAs (1,280 matrix-pipe cycles per
-// wave), 40 single-float writes and ~80 VALU, instead of ~520 VALU with 38 of 64
-// lanes busy (stage_w<29>). Reference: the DFT of seewave's stft/istft,
-// seewave.r:7782-7819, :3447-3486 (R's fft).
+// Columns: the real (c = 0) and imaginary (c = 1) parts of the 38 butterflies.
+// Q's operand carries the OTHER component of the same column, so one lane holds
+// P_k.c and (Q_k).c' for its column and finishes y_k.c, y_{29-k}.c alone:
+// y.re = P.re +- Q.im, y.im = P.im -+ Q.re. Reference: the DFT of seewave's
+// stft/istft, seewave.r:7782-7819, :3447-3486 (R's fft).
+//
+// Layout (round 6; LDS bank rule: ds_read_b64 serves lanes 0-31 and 32-63 as
+// two groups over 64 banks, ds_write_b64 four 16-lane quarters over 32 banks,
+// ds_write_b32 two groups over 32 banks):
+//  - Column groups 0 / 3 hold the real / imaginary parts of butterflies
+//    j = col (0..15), groups 1 / 4 those of j = 16 + col: ONE lane holds both
+//    components of its butterfly, so its operands are read once for two column
+//    groups and y_k, y_{29-k} are written as whole pairs (ds_write_b64; a quarter's
+//    16 pairs at a 58-word stride cover the 32 banks once). Group 2 holds both
+//    parts of j = 32..37 (col < 6 real, 6 <= col < 12 imaginary, 12..15 padding
+//    reading j = 32..35: same addresses, broadcast).
+//  - K rows: k-step ks, lane quarter mg takes row m29_row(ks, mg) = 2 ks +
+//    (mg >> 1) + 8 (mg & 1): the two quarters of a read group read rows 8 apart,
+//    2 x 38 x 8 = 608 = 32 (mod 64) words, the other half of the banks.
+//  - D rows: result row i = 4 (lane >> 4) + r is output k = m29_out(i), so the two
+//    quarters of a group-2 ds_write_b32 write outputs 8 apart (16 words apart: the
+//    other half of the 32 banks for those 6 butterflies' stride).
+// Per lane: 24 pair reads, 40 MFMAs (1,280 matrix-pipe cycles per wave), 16 pair
+// and 8 single-float writes, instead of ~520 VALU with 38 of 64 lanes busy
+// (stage_w<29>). Round 5's layout (16 butterflies' real or imaginary parts per
+// group, rows 4 ks + mg) read 40 pairs and wrote 40 floats per lane with 2-way
+// conflicts on both: 1.0 conflict cycles per LDS instruction in sg_stft_ola (r05zz).
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ constexpr int m29_row(int ks, int mg) { return 2 * ks + (mg >> 1) + 8 * (mg & 1); }
+__device__ __forceinline__ constexpr int m29_out(int i) { return (i & 3) + 8 * ((i >> 2) & 1) + 4 * (i >> 3); }
 // The A fragments live in a 2 KB LDS table shared by the workgroup (lane l:
 // cos fragments of k-steps 0..3 at tab[l], sin fragments at tab[64 + l]) and
 // are read where the stage starts, so they hold no registers across the frame.
@@ -438,13 +459,14 @@ constexpr int SG_MAT29_BYTES = 128 * 16;
 // t < 1102: W_29^t = W_2204^{76 t}, and W_2204^{t + 1102} = -W_2204^t. Threads
 // 0..63 of the workgroup; the caller's barrier publishes it. LDS: after the
 // workgroup's frame slices (planner: SG_MAT29_BYTES more for M = 1102).
+// A operand of v_mfma_f32_16x16x4_f32: lane t holds A[i = t & 15][kk = t >> 4].
 __device__ __forceinline__ void mat29_fill(float4* tab, const float2* twN, int t) {
   if (t >= 64) return;
-  const int k = t & 15;
+  const int k = m29_out(t & 15);
   float p[4], q[4];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
-    const int m = 4 * ks + (t >> 4);
+    const int m = m29_row(ks, t >> 4);
     const int idx = 76 * ((m * k) % 29);
     const float2 w = idx < 1102 ? twN[idx] : make_float2(-twN[idx - 1102].x, -twN[idx - 1102].y);
     p[ks] = (k <= 14 && m <= 14) ? w.x : 0.f;
@@ -456,63 +478,83 @@ __device__ __forceinline__ void mat29_fill(float4* tab, const float2* twN, int t
 
 template <bool INV>
 __device__ __forceinline__ void stage29_mfma(float2* X, const float4* tab, int lane) {
-  constexpr int MR = 38, NT = 5;
+  constexpr int MR = 38;
   const int col = lane & 15, mg = lane >> 4;
   const float4 ap = tab[lane], aq = tab[64 + lane];
   const float Ap[4] = {ap.x, ap.y, ap.z, ap.w}, Aq[4] = {aq.x, aq.y, aq.z, aq.w};
-  // column group nt: lane column n = 16 nt + col is the real (n < 38) or the
-  // imaginary (38 <= n < 76) part of butterfly j; k-step ks: row m = 4 ks + mg
-  auto load = [&](int nt, float2 (&la)[4], float2 (&lb)[4]) {
-    const int n = 16 * nt + col;
-    const int j = n < 2 * MR ? (n >= MR ? n - MR : n) : 0;  // padding columns read butterfly 0 (finite, discarded)
+  // row 0: x_0 enters P alone (b weighted 0); rows without a second operand keep the
+  // bank image of their group's partner row: row 0's b reads row 8's b address - 32
+  // words, row 15 (padding, A's column zero) row 7's addresses + 32 words (finite data)
+  const float w0 = mg == 0 ? 0.f : 1.f;
+  auto load = [&](int j, float2 (&la)[4], float2 (&lb)[4]) {
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      const int m = 4 * ks + mg;        // 0..15
-      const int ma = m <= 14 ? m : 14;  // column 15: any finite value (A's column is zero)
-      const int mb = ma == 0 ? 0 : 29 - ma;
-      la[ks] = X[j + MR * ma];
-      lb[ks] = X[j + MR * mb];
+      const int m = m29_row(ks, mg);
+      const int ia = m == 15 ? MR * 7 + 16 : MR * m;
+      const int ib = m == 15 ? MR * 22 + 16 : m == 0 ? MR * 13 : MR * (29 - m);
+      la[ks] = X[j + ia];
+      lb[ks] = X[j + ib];
     }
   };
-  f32x4 P[NT], Q[NT];
+  // operand sums of k-step ks: s = a + b (row 0: a), d = a - b
+  auto sums = [&](int ks, float2 a, float2 b, v2& s, v2& d) {
+    s = ks == 0 ? pfma(V(b), splat(w0), V(a)) : V(a) + V(b);
+    d = V(a) - V(b);
+  };
+  f32x4 P[5], Q[5];
   float2 la[2][4], lb[2][4];
-  load(0, la[0], lb[0]);
+  // butterflies j = 16 g + col, g = 0, 1: column groups g (real) and g + 3 (imaginary)
+  load(col, la[0], lb[0]);
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    // the next group's operands are in flight while this group's MFMAs issue
-    if (nt + 1 < NT) load(nt + 1, la[(nt + 1) & 1], lb[(nt + 1) & 1]);
-    const int c = 16 * nt + col >= MR ? 1 : 0;
-    P[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    Q[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int g = 0; g < 2; ++g) {
+    if (g == 0) load(16 + col, la[1], lb[1]);  // in flight while group 0's MFMAs issue
+    else load(32 + (col < 12 ? col % 6 : col - 12), la[0], lb[0]);
+    P[g] = Q[g] = P[g + 3] = Q[g + 3] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      const float2 a = la[nt & 1][ks], b = lb[nt & 1][ks];
-      const bool m0 = ks == 0 && mg == 0;
-      const float bp = c ? (m0 ? a.y : a.y + b.y) : (m0 ? a.x : a.x + b.x);
-      const float bq = c ? a.x - b.x : a.y - b.y;  // the other component (m = 0: A's column is zero)
-      P[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ap[ks], bp, P[nt], 0, 0, 0);
-      Q[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Aq[ks], bq, Q[nt], 0, 0, 0);
+      v2 s, d;
+      sums(ks, la[g][ks], lb[g][ks], s, d);
+      P[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ap[ks], s.x, P[g], 0, 0, 0);
+      Q[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(Aq[ks], d.y, Q[g], 0, 0, 0);
+      P[g + 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ap[ks], s.y, P[g + 3], 0, 0, 0);
+      Q[g + 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(Aq[ks], d.x, Q[g + 3], 0, 0, 0);
     }
-    // at most two column groups' operands live (all 20 k-step groups at once
-    // would take 80 VGPRs on top of the 40 accumulators)
     __builtin_amdgcn_sched_barrier(0);
   }
-  sg_wave_fence();  // every read above precedes the in-place writes below
-  float* Yf = reinterpret_cast<float*>(X);
+  // group 2: butterflies 32..37, the lane's component c2
+  const bool c2 = col >= 6;
+  P[2] = Q[2] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    const int n = 16 * nt + col;
-    if (n >= 2 * MR) continue;
-    const int c = n >= MR ? 1 : 0;
-    const int j = n - c * MR;
-    const float sg = (c == 0) != INV ? 1.f : -1.f;
-    float* y = Yf + 2 * 29 * j + c;
+  for (int ks = 0; ks < 4; ++ks) {
+    v2 s, d;
+    sums(ks, la[0][ks], lb[0][ks], s, d);
+    P[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ap[ks], c2 ? s.y : s.x, P[2], 0, 0, 0);
+    Q[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(Aq[ks], c2 ? d.x : d.y, Q[2], 0, 0, 0);
+  }
+  sg_wave_fence();  // every read above precedes the in-place writes below
+  // y_k = P_k -+ i Q_k: forward (re, im) = (P.re + Q.im, P.im - Q.re), the inverse swaps the signs
+  const v2 sgn = INV ? v2{-1.f, 1.f} : v2{1.f, -1.f};
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    float2* y = X + 29 * (16 * g + col);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int k = 4 * mg + r;  // D layout: column = lane & 15, row = 4 (lane / 16) + r
+      const int k = m29_out(4 * mg + r);  // D layout: column = lane & 15, row = 4 (lane / 16) + r
       if (k > 14) continue;
-      const float p = P[nt][r], q = sg * Q[nt][r];
-      y[2 * k] = p + q;  // k = 0: Q_0 = 0
+      const v2 p = v2{P[g][r], P[g + 3][r]}, q = v2{Q[g][r], Q[g + 3][r]};  // p: (P.re, P.im), q: (Q.im, Q.re)
+      y[k] = F(pfma(q, sgn, p));  // k = 0: Q_0 = 0
+      if (k > 0) y[29 - k] = F(pfma(q, -sgn, p));
+    }
+  }
+  if (col < 12) {
+    float* y = reinterpret_cast<float*>(X + 29 * (32 + col % 6)) + (c2 ? 1 : 0);
+    const float sg = c2 == INV ? 1.f : -1.f;  // re: P.re + sgn.x Q.im; im: P.im + sgn.y Q.re
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = m29_out(4 * mg + r);
+      if (k > 14) continue;
+      const float p = P[2][r], q = sg * Q[2][r];
+      y[2 * k] = p + q;
       if (k > 0) y[2 * (29 - k)] = p - q;
     }
   }
