@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SG_ABI_VERSION 4
+#define SG_ABI_VERSION 5
 
 enum {
   SG_OK = 0,
@@ -67,7 +67,11 @@ typedef struct sg_formants {
  * are used first; once one is exhausted (or NULL) the matching callback is
  * called if set, else the call fails with SG_E_RANDOM. The R shim binds the
  * callbacks to R's own norm_rand()/unif_rand()/rgamma() so that draws follow
- * set.seed() exactly; tests inject arrays. */
+ * set.seed() exactly; tests inject arrays.
+ * unif_n_cb (ABI 5, may be NULL): n consecutive uniforms into out, the same
+ * values n unif_cb calls would return -- R: runif(n), i.e. unif_rand() in one C
+ * loop. The planner takes generateNoise()'s runif(nr * nc) (R/source.R:111; ~8 k
+ * draws per C5 call) through it in blocks instead of one callback per draw. */
 typedef struct sg_random {
   const double* normals;
   int64_t n_normals;
@@ -77,6 +81,7 @@ typedef struct sg_random {
   double (*unif_cb)(void* user);
   double (*gamma_cb)(void* user, double shape, double rate);
   void* user;
+  void (*unif_n_cb)(void* user, double* out, int64_t n);
 } sg_random;
 
 /* R's default random number generation (R 3.4.0: Mersenne-Twister,
@@ -93,6 +98,7 @@ int sg_rrng_create(int32_t seed, sg_rrng** out);  /* = set.seed(seed) */
 void sg_rrng_destroy(sg_rrng* g);
 void sg_rrng_set_seed(sg_rrng* g, int32_t seed);
 double sg_rrng_unif(sg_rrng* g);                  /* runif(1) */
+void sg_rrng_unif_n(sg_rrng* g, double* out, int64_t n); /* runif(n) (ABI 5) */
 double sg_rrng_norm(sg_rrng* g);                  /* rnorm(1) */
 double sg_rrng_exp(sg_rrng* g);                   /* rexp(1) */
 double sg_rrng_gamma(sg_rrng* g, double shape, double scale); /* rgamma(1, shape, scale = scale) */
@@ -188,9 +194,11 @@ const char* sg_node_last_error(const sg_node* node);
  * messages are those of the WHOLE batch in call order with sg_plan_batch's
  * layout, and every call's samples equal what sg_plan_batch of the whole batch
  * produces (a call's arithmetic does not depend on the batch around it). With
- * draw callbacks (R's RNG) the calls are first planned in call order recording
- * each call's draws -- R's stream, R's order; a failing call ends it as
- * lapply() would -- and the shards are then planned from the recorded draws. */
+ * draw callbacks (R's RNG) the calls are first run in call order in a draws-only
+ * pass that records each call's draws -- R's stream, R's order; a failing call ends
+ * it as lapply() would -- and the shards are then planned, on host threads, from
+ * the recorded draws (ABI 5: the recording pass no longer plans the device work).
+ * Calls that carry only injected arrays are planned as given. */
 int sg_node_plan_batch(sg_node* node, const sg_call_desc* calls, int64_t n_calls, sg_node_plan** out);
 void sg_node_plan_destroy(sg_node_plan* plan);
 int64_t sg_node_plan_n_calls(const sg_node_plan* plan);
@@ -203,9 +211,23 @@ int sg_node_plan_owner(const sg_node_plan* plan, int32_t* owner);
 /* the analytic cost per call the assignment used (ns of one MI355X) */
 int sg_node_plan_costs(const sg_node_plan* plan, double* cost);
 int64_t sg_node_plan_shard_samples(const sg_node_plan* plan, int32_t k);
-/* Synchronous: every device uploads, synthesizes its shard on its own stream
+/* ABI 5: chunk plans of shard k (consecutive calls of the shard, <= SG_NODE_CHUNK
+ * calls -- default 4096 -- and ~2^27 samples each: the unit of the execute pipeline) */
+int32_t sg_node_plan_chunks(const sg_node_plan* plan, int32_t k);
+/* ABI 5: 1 when a call failed in the shard planning after its recorded draws
+ * succeeded (a failure behind a call's last draw that the draws-only recording pass
+ * does not raise): later callback calls are then "not planned" as R's loop would
+ * leave them, but their draws were consumed. 0 otherwise. */
+int32_t sg_node_plan_diverged(const sg_node_plan* plan);
+/* ABI 5: sg_plan_call_work per call of the whole batch (rows, flops: n_calls
+ * doubles each, either may be NULL; unplanned calls are left untouched) */
+int sg_node_plan_call_work(const sg_node_plan* plan, double* rows, double* fft_flops);
+/* Synchronous: every device uploads, synthesizes its shard on its own streams
  * and copies it over its own link; each call's samples land in out_host at its
- * whole-batch offset (sg_node_plan_total_samples values in all). */
+ * whole-batch offset (sg_node_plan_total_samples values in all). ABI 5: pipelined
+ * by chunk (the D2H of a chunk overlaps the compute of the later ones and the host
+ * scatter of the earlier one); the device output and two pinned staging slots of
+ * the largest chunk stay allocated per device until sg_node_destroy. */
 int sg_node_execute_to_host(sg_node* node, sg_node_plan* plan, double* out_host);
 int sg_node_execute_to_host_f32(sg_node* node, sg_node_plan* plan, float* out_host);
 

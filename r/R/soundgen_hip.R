@@ -114,9 +114,11 @@ soundgen_hip = function(repeatBout = 1, nSyl = 1, sylLen = 300, pauseLen = 200,
 # population loop of matchPars (R/matchPars.R:176-190). R's RNG is drawn in call
 # order, so after set.seed() it returns what
 # lapply(calls, function(cl) do.call(soundgen, cl)) returns. The batch runs on
-# every device of `devices` (default: all visible MI355X), sharded by calls
-# inside the library (sg_node), each device's shard over its own link.
-soundgen_batch = function(calls, devices = getOption("soundgen_hip.devices", NULL)) {
+# the devices of `devices` (device ordinals; default: device 0, the device the
+# other entry points use, so one R process per GPU stays on its GPU; "all": every
+# visible MI355X), sharded by calls inside the library (sg_node), each device's
+# shard over its own link.
+soundgen_batch = function(calls, devices = getOption("soundgen_hip.devices", 0L)) {
   dflt = formals(soundgen_hip)
   dflt$... = dflt$plot = dflt$play = dflt$savePath = NULL
   dflt = lapply(dflt, eval)
@@ -125,7 +127,7 @@ soundgen_batch = function(calls, devices = getOption("soundgen_hip.devices", NUL
     a[names(cl)] = cl
     .sg_soundgen_args(a)
   })
-  .Call(C_sg_soundgen_batch, args, if (is.null(devices)) NULL else as.integer(devices))
+  .Call(C_sg_soundgen_batch, args, if (identical(devices, "all")) -1L else as.integer(devices))
 }
 
 # R/source.R:57-68: the reference's formals and defaults verbatim

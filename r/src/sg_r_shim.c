@@ -38,8 +38,8 @@ static sg_ctx* ctx(void) {
 }
 
 /* The node of soundgen_batch: the devices of the last call's `devices`
- * (getOption("soundgen_hip.devices"); NULL = every visible device), kept across
- * calls while they stay the same. */
+ * (getOption("soundgen_hip.devices"); NULL = device 0, as ctx(); -1 = every
+ * visible device), kept across calls while they stay the same. */
 static sg_node* g_node = NULL;
 static int32_t g_node_dev[64];
 static int32_t g_node_n = -1;
@@ -47,7 +47,11 @@ static int32_t g_node_n = -1;
 static sg_node* node(SEXP devices) {
   int32_t dv[64];
   int32_t n = 0;
-  if (!Rf_isNull(devices)) {
+  if (Rf_isNull(devices)) {
+    dv[n++] = 0;  /* the single device of the other entry points */
+  } else if (TYPEOF(devices) == INTSXP && Rf_xlength(devices) == 1 && INTEGER(devices)[0] == -1) {
+    n = 0;  /* opt-in fan-out: every visible device */
+  } else {
     const R_xlen_t m = Rf_xlength(devices);
     if (TYPEOF(devices) != INTSXP || m < 1 || m > 64)
       Rf_error("soundgen_hip: devices must be an integer vector of 1 to 64 device ordinals");
@@ -57,6 +61,7 @@ static sg_node* node(SEXP devices) {
       dv[n++] = (int32_t)v;
     }
   }
+  if (sg_device_count() <= 0) Rf_error("soundgen_hip: no usable MI355X (no HIP device)");
   if (g_node && n == g_node_n && (n == 0 || !memcmp(dv, g_node_dev, (size_t)n * sizeof(int32_t)))) return g_node;
   if (g_node) sg_node_destroy(g_node);
   g_node = NULL;
@@ -68,6 +73,11 @@ static sg_node* node(SEXP devices) {
 
 static double cb_norm(void* u) { (void)u; return norm_rand(); }
 static double cb_unif(void* u) { (void)u; return unif_rand(); }
+/* runif(n) in one C loop: generateNoise's runif(nr * nc) without a callback per draw */
+static void cb_unif_n(void* u, double* out, int64_t n) {
+  (void)u;
+  for (int64_t i = 0; i < n; ++i) out[i] = unif_rand();
+}
 static double cb_gamma(void* u, double shape, double rate) { (void)u; return rgamma(shape, 1.0 / rate); }
 
 static sg_random r_rng(void) {
@@ -76,6 +86,7 @@ static sg_random r_rng(void) {
   r.norm_cb = cb_norm;
   r.unif_cb = cb_unif;
   r.gamma_cb = cb_gamma;
+  r.unif_n_cb = cb_unif_n;
   return r;
 }
 

@@ -45,13 +45,14 @@ class sg_mel_params(C.Structure):
 NORM_CB = C.CFUNCTYPE(C.c_double, C.c_void_p)
 UNIF_CB = C.CFUNCTYPE(C.c_double, C.c_void_p)
 GAMMA_CB = C.CFUNCTYPE(C.c_double, C.c_void_p, C.c_double, C.c_double)
+UNIF_N_CB = C.CFUNCTYPE(None, C.c_void_p, _dp, C.c_int64)  # ABI 5: runif(n) into out
 
 
 class sg_random(C.Structure):
     _fields_ = [("normals", _dp), ("n_normals", C.c_int64),
                 ("uniforms", _dp), ("n_uniforms", C.c_int64),
                 ("norm_cb", NORM_CB), ("unif_cb", UNIF_CB), ("gamma_cb", GAMMA_CB),
-                ("user", C.c_void_p)]
+                ("user", C.c_void_p), ("unif_n_cb", UNIF_N_CB)]
 
 
 HARM_FIELDS = ["attackLen", "nonlinBalance", "nonlinDep", "jitterDep", "jitterLen",

@@ -107,6 +107,20 @@ class NodePlan:
     def shard_samples(self, k):
         return int(native.lib().sg_node_plan_shard_samples(self.ptr, k))
 
+    def chunks(self, k):
+        return int(native.lib().sg_node_plan_chunks(self.ptr, k))
+
+    @property
+    def diverged(self):
+        return bool(native.lib().sg_node_plan_diverged(self.ptr))
+
+    def call_work(self):
+        """Per call: sine-bank (sample, row) terms and FFT flops the shard plans emit."""
+        rows, flops = np.zeros(self.n), np.zeros(self.n)
+        dp = C.POINTER(C.c_double)
+        native.lib().sg_node_plan_call_work(self.ptr, rows.ctypes.data_as(dp), flops.ctypes.data_as(dp))
+        return rows, flops
+
     def execute_to_host(self, dtype=np.float64):
         """The packed batch (sg_node_plan_total_samples values, call i at offsets[i])."""
         out = np.zeros(max(self.total, 1), dtype=dtype)

@@ -162,7 +162,8 @@ GrowthEstimate g_growth;
 // stream_stop: the calls' draw callbacks are one sequential stream (R's RNG), so a
 // failing call ends the planning of later callback calls; false when every call's
 // callbacks replay its own recorded draws (sg_node's second pass)
-void plan_range(sg::Batch& B, const sg_call_desc* calls, int64_t c0, int64_t c1, bool stream_stop = true) {
+void plan_range(sg::Batch& B, const sg_call_desc* calls, int64_t c0, int64_t c1, bool stream_stop = true,
+                const std::function<void(int64_t)>* on_done = nullptr) {
   const int64_t n = c1 - c0;
   B.call_len.assign(n, 0);
   B.call_off.assign(n, 0);
@@ -202,9 +203,9 @@ void plan_range(sg::Batch& B, const sg_call_desc* calls, int64_t c0, int64_t c1,
       int64_t L = 0;
       if (d.kind == SG_CALL_HARMONICS) {
         if (!d.pitch || !d.harm) throw sg::SgError(SG_E_ARG, "harmonics call without pitch/params");
-        L = sg::plan_harmonics(B, d.pitch, d.pitch_len, *d.harm, d.amplAnchors, R, off, false);
+        L = sg::plan_harmonics(B, d.pitch, d.pitch_len, *d.harm, d.amplAnchors, R, off, B.draws_only);
         sg::ProfScope pt(sg::PF_TILES);
-        sg::tile_syllables(B, first_syl);
+        if (!B.draws_only) sg::tile_syllables(B, first_syl);
       } else if (d.kind == SG_CALL_SOUNDGEN) {
         if (!d.args) throw sg::SgError(SG_E_ARG, "soundgen call without args");
         {
@@ -212,7 +213,7 @@ void plan_range(sg::Batch& B, const sg_call_desc* calls, int64_t c0, int64_t c1,
           L = sg::plan_soundgen(B, *d.args, R, off, first_syl);
         }
         sg::ProfScope pt(sg::PF_TILES);
-        sg::tile_syllables(B, first_syl);
+        if (!B.draws_only) sg::tile_syllables(B, first_syl);
       } else {
         throw sg::SgError(SG_E_ARG, "unknown call kind");
       }
@@ -233,6 +234,7 @@ void plan_range(sg::Batch& B, const sg_call_desc* calls, int64_t c0, int64_t c1,
       B.call_len[i] = 0;
       if (cb && cb_failed < 0) cb_failed = i;
     }
+    if (on_done) (*on_done)(c0 + i);
   }
   B.total_out = off;
 }
@@ -485,7 +487,28 @@ int sg_plan_batch(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, sg_pl
 }  // extern "C"
 
 namespace sg {
-int plan_batch_ex(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, bool independent_draws, sg_plan** out) {
+// The draws of every call in call order (one stream: a failing call ends it, as in
+// plan_range), emitting nothing: Batch::draws_only. Per call status and message.
+void record_draws(const sg_call_desc* calls, int64_t n_calls, std::vector<int32_t>& status,
+                  std::vector<std::string>& msg, const std::function<void(int64_t, int32_t)>& on_call) {
+  Batch B;
+  B.draws_only = true;
+  const std::function<void(int64_t)> done = [&](int64_t i) {
+    if (on_call) on_call(i, B.call_status[(size_t)i]);
+  };
+  plan_range(B, calls, 0, n_calls, true, &done);
+  if (sg::g_prof_on) {
+    static const char* names[] = {"harmonics", "rolloff", "contour", "envelope", "noise", "filter", "finalize",
+                                  "finalize_spec", "fry", "crossfade", "emit", "tasks", "tiles", "soundgen"};
+    for (int i = 0; i < sg::PF_N; ++i)
+      std::fprintf(stderr, "sg_plan_prof record %-14s %.3f s\n", names[i], sg::g_prof_ns[i].exchange(0) * 1e-9);
+  }
+  status = std::move(B.call_status);
+  msg = std::move(B.call_msg);
+}
+
+int plan_batch_ex(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, bool independent_draws, sg_plan** out,
+                  int max_threads) {
   return guarded(ctx, [&]() {
     auto P = std::make_unique<sg_plan>();
     sg::Batch& B = P->B;
@@ -499,7 +522,7 @@ int plan_batch_ex(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, bool 
     for (int64_t c = 0; c < n_calls && !callbacks; ++c)
       callbacks = calls[c].random.norm_cb || calls[c].random.unif_cb || calls[c].random.gamma_cb;
     const bool serial = callbacks && !independent_draws;
-    const int threads = serial ? 1 : plan_threads(n_calls);
+    const int threads = serial ? 1 : std::min(plan_threads(n_calls), max_threads > 0 ? max_threads : 1 << 30);
     g_growth.decay();
     if (threads <= 1) {
       g_growth.reserve(B, n_calls);

@@ -120,10 +120,32 @@ __device__ __forceinline__ double linear_at_cursor(const SgLinear& l, const doub
   return y[i] + (y[j] - y[i]) * ((u - x[i]) / (x[j] - x[i]));
 }
 
+// Max over the wavefront, in every lane: DPP within each 16-lane row (quad_perm
+// [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror), then the four rows' values by
+// readlane. All VALU: the __shfl_xor form took six ds_bpermute round trips through
+// the LDS per reduction (round 6; each short-task sine-bank wave reduces twice).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  const int x = __builtin_bit_cast(int, v);
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(x, x, CTRL, 0xf, 0xf, false));
+}
 __device__ __forceinline__ float wave_max(float v) {
+#ifdef SG_WAVE_MAX_SHFL
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
   return v;
+#else
+  v = fmaxf(v, dpp_f<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = fmaxf(v, dpp_f<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = fmaxf(v, dpp_f<0x141>(v));  // row_half_mirror: max over 8 lanes
+  v = fmaxf(v, dpp_f<0x140>(v));  // row_mirror: max over the row of 16
+  const int x = __builtin_bit_cast(int, v);
+  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(x, 0));
+  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(x, 16));
+  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(x, 32));
+  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(x, 48));
+  return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
+#endif
 }
 
 // XCD-aware workgroup order: the dispatcher deals workgroups round-robin over

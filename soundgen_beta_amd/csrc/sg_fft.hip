@@ -288,6 +288,9 @@ struct NbW {
   static constexpr int value = SG_WAVE_STATE / R > 0 ? SG_WAVE_STATE / R : 1;
 };
 
+#ifndef SG_R19_REMAP
+#define SG_R19_REMAP 1
+#endif
 // CM, CNS > 0: the frame size and the stage's stride are compile-time constants
 // (the dominant geometry's specialisation: index math folds away)
 template <int R, bool INV, int CM = 0, int CNS = 0>
@@ -297,15 +300,31 @@ __device__ __forceinline__ void stage_w(float2* X, int M_, int Ns_, const float2
   constexpr int H = ODD ? (R - 1) / 2 : 1;
   const int M = CM ? CM : M_, Ns = CNS ? CNS : Ns_;
   const int MR = M / R;
+  // HALVES: a stride of <= 32 butterflies with two blocks (MR = 2 Ns; M = 1102's
+  // radix-19 stage: Ns = 29): lane half h takes block h, jm = lane & 31, so a
+  // 16-lane quarter's ds_write_b64 never straddles the two blocks' outputs (lanes
+  // 29..31 and 61..63 idle; with j = lane, lanes 29..31 wrote block 1's first
+  // outputs beside block 0's last: 2-way conflicts, round 6)
+  constexpr bool HALVES = SG_R19_REMAP && CM > 0 && CNS > 0 && CNS <= 32 && CM / R == 2 * CNS;
+  auto slot = [&](int q, int& j, int& jm) -> bool {
+    if constexpr (HALVES) {
+      jm = lane & 31;
+      j = (lane >> 5) * CNS + jm;
+      return q == 0 && jm < CNS;
+    }
+    j = lane + q * 64;
+    if (j >= MR) return false;
+    jm = CNS ? j % CNS : j - udiv(j, ns_magic) * Ns;
+    return true;
+  };
   v2 st[NB][R];
   int base_o[NB];
 #pragma unroll
   for (int q = 0; q < NB; ++q) {
     if (q * 64 >= MR) break;
-    const int j = lane + q * 64;
+    int j, jm;
     base_o[q] = 0;
-    if (j >= MR) continue;
-    const int jm = CNS ? j % CNS : j - udiv(j, ns_magic) * Ns;
+    if (!slot(q, j, jm)) continue;
     base_o[q] = (j - jm) * R + jm;
     if constexpr (ODD) {
       // pairs (m, R - m) one at a time: inputs, twiddles and the symmetric
@@ -346,7 +365,8 @@ __device__ __forceinline__ void stage_w(float2* X, int M_, int Ns_, const float2
 #pragma unroll
   for (int q = 0; q < NB; ++q) {
     if (q * 64 >= MR) break;
-    if (lane + q * 64 >= MR) continue;
+    int j, jm;
+    if (!slot(q, j, jm)) continue;
     float2* y = X + base_o[q];
     if constexpr (ODD) {
       v2 y0 = st[q][0];
@@ -1044,6 +1064,12 @@ __device__ __forceinline__ void frame_front(float2* A, const FramePf& P, int mod
   sg_wave_fence();
 }
 
+#ifndef SG_CARRY64
+#define SG_CARRY64 0
+#endif
+#ifndef SG_NOISE_MFMA
+#define SG_NOISE_MFMA 0
+#endif
 // Fused STFT x envelope -> ISTFT -> overlap-add (seewave istft,
 // seewave.r:3462-3484) -> matchLengths trim. Each wavefront owns one segment
 // (a run of consecutive frames of one OLA) and walks it frame by frame with
@@ -1113,7 +1139,7 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
     // inside the LDS-bound loop at 2 waves per SIMD), so the filter keeps the LDS pass.
     const bool direct = FUSED && MODE == SG_FRAME_NOISE && bf >= S.pa && bf - first >= 0 && bn - first <= len && D <= 1102;
     if constexpr (FUSED) {
-      fft_wc<true, CM, R0, R1, R2, MODE == SG_FRAME_FILTER, false>(A, twS, A29, lane SG_ST_ARGS);
+      fft_wc<true, CM, R0, R1, R2, MODE == SG_FRAME_FILTER || SG_NOISE_MFMA, false>(A, twS, A29, lane SG_ST_ARGS);
       // butterfly j: Z[j], Z[j + 551] from X[j], X[j + 551] conj(W^j) (stage_w<2>'s
       // operations), each windowed (han holds hanning / wl) and added to its carry
       float* __restrict__ o = out + (bf - first);
@@ -1195,8 +1221,88 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
       }
     }
     if (!lastf) {
-      // the next carry: every read unconditional (index clamped into the slice), all
-      // in flight at once; i0 >= Nk exactly when the pair lies past the carried tail
+      // the next carry: pair n holds samples 2n + D, 2n + D + 1 of this frame (zero
+      // past its end); every read unconditional (index clamped into the slice), all
+      // in flight at once. SG_CARRY64: pair reads (ds_read_b64, consecutive lanes on
+      // consecutive pairs: no bank conflicts) -- D even: pair n + D/2; D odd (the
+      // usual hop, wl/4 = 551): the odd half of pair p = n + (D-1)/2 and the even
+      // half of p + 1. (Two float reads 2 words apart per lane were 2-way conflicts.)
+#if SG_CARRY64 == 2
+      // odd D: one pair read per lane; the even half of pair p + 1 is the next lane's
+      // (DPP wave_shl:1), lane 63 takes lane 0 of the next block
+      const float2* __restrict__ A2 = A;
+      const int ph = D >> 1;
+      auto carry_even = [&](int n) {
+        const int p = n + ph;
+        const float2 a = A2[min(p, M - 1)];
+        return p < M ? a : make_float2(0.f, 0.f);
+      };
+      auto shl1 = [](float v) {
+        return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xf, 0xf, false));
+      };
+      constexpr int NQ = FUSED ? 9 : CP;
+      auto carry_odd_set = [&](int n0, float2 (&Cs)[NQ]) {
+        float2 a[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) a[q] = A2[min(n0 + 64 * q + lane + ph, M - 1)];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const int p = n0 + 64 * q + lane + ph;
+          float nx = shl1(a[q].x);
+          if (q + 1 < NQ) nx = lane == 63 ? __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a[q + 1].x), 0)) : nx;
+          Cs[q] = make_float2(p < M ? a[q].y : 0.f, p + 1 < M ? nx : 0.f);
+        }
+      };
+      if (D & 1) {
+        if constexpr (FUSED) {
+          carry_odd_set(0, C);
+          carry_odd_set(551, C2);
+        } else {
+          carry_odd_set(0, C);
+        }
+      } else {
+        if constexpr (FUSED) {
+#pragma unroll
+          for (int q = 0; q < 9; ++q) {
+            const int j = 64 * q + lane;
+            C[q] = carry_even(j);
+            C2[q] = carry_even(j + 551);
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < CP; ++r) C[r] = carry_even(64 * r + lane);
+        }
+      }
+#elif SG_CARRY64
+      const float2* __restrict__ A2 = A;
+      const int ph = D >> 1;
+      auto carry_even = [&](int n) {
+        const int p = n + ph;
+        const float2 a = A2[min(p, M - 1)];
+        return p < M ? a : make_float2(0.f, 0.f);
+      };
+      auto carry_odd = [&](int n) {
+        const int p = n + ph;
+        const float2 a = A2[min(p, M - 1)], b = A2[min(p + 1, M - 1)];
+        return make_float2(p < M ? a.y : 0.f, p + 1 < M ? b.x : 0.f);
+      };
+#define SG_CARRY_LOOP(carry)                      \
+  if constexpr (FUSED) {                          \
+    _Pragma("unroll") for (int q = 0; q < 9; ++q) { \
+      const int j = 64 * q + lane;                \
+      C[q] = carry(j);                            \
+      C2[q] = carry(j + 551);                     \
+    }                                             \
+  } else {                                        \
+    _Pragma("unroll") for (int r = 0; r < CP; ++r) C[r] = carry(64 * r + lane); \
+  }
+      if (D & 1) {
+        SG_CARRY_LOOP(carry_odd)
+      } else {
+        SG_CARRY_LOOP(carry_even)
+      }
+#undef SG_CARRY_LOOP
+#else
       auto carry = [&](int n) {
         const int i0 = 2 * n + D;
         const float a = Af[min(i0, Nk - 1)], b = Af[min(i0 + 1, Nk - 1)];
@@ -1213,6 +1319,7 @@ __device__ __forceinline__ void stft_segment(const SgSegment& S, const SgOla* __
 #pragma unroll
         for (int r = 0; r < CP; ++r) C[r] = carry(64 * r + lane);
       }
+#endif
     }
     sg_wave_fence();  // the next frame overwrites the slice
     bf = bn;
@@ -1271,7 +1378,7 @@ __device__ __forceinline__ void stft_ola_body(
     // hamming, then hanning times 1 / wl (the inverse transform's scale)
     const float hs = 1.f / (float)N;
     for (int t = threadIdx.x; t < 2 * N; t += NT) ham[t] = t < N ? wg[t] : wg[t] * hs;
-    if (MODE == SG_FRAME_FILTER && geom_1102(g)) mat29_fill(reinterpret_cast<float4*>(twS + M * (4 + W)), tng, threadIdx.x);
+    if ((MODE == SG_FRAME_FILTER || SG_NOISE_MFMA) && geom_1102(g)) mat29_fill(reinterpret_cast<float4*>(twS + M * (4 + W)), tng, threadIdx.x);
   }
   __syncthreads();
   const SgSegment S = segs[blockIdx.x * W + w];

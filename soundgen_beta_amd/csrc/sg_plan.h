@@ -3,6 +3,7 @@
 // crossing trims, output lengths) is done here in fp64, bit-exact with R.
 #pragma once
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <utility>
 #include <vector>
@@ -88,6 +89,12 @@ struct Slice {
 };
 
 struct Batch {
+  // draws_only: a planning pass that only consumes each call's random draws in the
+  // reference's order and raises the errors that precede its last draw, emitting
+  // nothing (sg_node's recording pass over one R stream: the per-sample work after a
+  // call's last draw -- amplitude columns, phase segments, wave tasks, envelope terms,
+  // frames, mixes -- runs once, in the parallel replay)
+  bool draws_only = false;
   // ---- harmonic source ----
   bulk<SgSeg> segs;
   bulk<SgEpoch> epochs;
@@ -283,7 +290,7 @@ vec get_rolloff(const vec& pitch, int64_t nH, const vec& rolloff, const vec& rol
                 double rolloffParabHarm, const vec& rolloffKHz, double baseline, double throwaway, double sr,
                 int64_t& H, double rolloffParabCeiling = NAN);  // NaN: NULL
 vec get_random_walk(Rng& R, int64_t len, double rw_range, double rw_smoothing, int method, const vec& trend,
-                    bool trend_lazy_rnorm);
+                    bool trend_lazy_rnorm, bool draws_only = false);
 void clumper(vec& s, const vec& minLen);
 double noise_threshold(int which, double nonlinBalance);
 
@@ -293,5 +300,12 @@ namespace sg {
 // sg_plan_batch with the draw-independence of the calls stated by the caller:
 // independent_draws = every call's callbacks replay that call's own recorded
 // draws (sg_node.cpp), so the batch may plan on host threads like injected draws
-int plan_batch_ex(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, bool independent_draws, sg_plan** out);
+// max_threads > 0 caps the host threads (sg_node: one core records R's stream meanwhile)
+int plan_batch_ex(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, bool independent_draws, sg_plan** out,
+                  int max_threads = 0);
+// The calls' draws in call order without planning their device work (Batch::draws_only):
+// per call status (0 or SG_E_*) and message; a failing call ends a callback stream
+// on_call(i, status) after each call (its draws recorded), on the calling thread
+void record_draws(const sg_call_desc* calls, int64_t n_calls, std::vector<int32_t>& status,
+                  std::vector<std::string>& msg, const std::function<void(int64_t, int32_t)>& on_call = {});
 }  // namespace sg

@@ -169,7 +169,7 @@ static void zero_one(vec& x) {
 
 // getRandomWalk(), R/utilities_math.R:289-326 (method: 0 linear, 1 spline)
 vec get_random_walk(Rng& R, int64_t len, double rw_range, double rw_smoothing, int method,
-                    const vec& trend_in, bool trend_lazy_rnorm) {
+                    const vec& trend_in, bool trend_lazy_rnorm, bool draws_only) {
   if (len < 2) return vec{R.rgamma(1.0 / (rw_range * rw_range), 1.0 / (rw_range * rw_range))};
   vec trend = trend_in;
   if (trend_lazy_rnorm) trend = vec{R.rnorm(0, 1)};
@@ -181,6 +181,11 @@ vec get_random_walk(Rng& R, int64_t len, double rw_range, double rw_smoothing, i
     const int64_t each = (int64_t)(nd / (double)trend.size());
     for (double tv : trend) for (int64_t e = 0; e < each; ++e) tshort.push_back(tv);
   } else tshort = trend;
+  if (draws_only) {  // the same draws, no walk (a planning pass that only consumes draws)
+    const int64_t cnt = nd > (double)len ? len : (int64_t)nd;
+    for (int64_t i = 0; i < cnt; ++i) (void)R.rnorm(tshort[i % tshort.size()], 1.0);
+    return vec{};
+  }
   vec rw_long;
   if (nd > (double)len) {
     vec z(len);
@@ -1170,7 +1175,7 @@ int64_t plan_harmonics(Batch& B, const double* pitch_in, int64_t len, const sg_h
   A.P.push_back(HPiece{0, 1, {}});  // waveform = 0
   for (size_t e = 0; e < mats.size(); ++e) cross_fade(A, HE[e], (int64_t)e, sr, 15);
   const int64_t Lsyl = A.L();
-  if (dry_run) return Lsyl;
+  if (dry_run || B.draws_only) return Lsyl;  // every draw of the syllable precedes this
   if (probes) {  // up to 4 glottal cycles' spectra (formant-filter conditioning)
     const int64_t np = std::min<int64_t>(4, nGC);
     for (int64_t q = 0; q < np; ++q) {

@@ -544,10 +544,10 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
         int64_t fs_off = 0;
         const size_t np0 = probes.size();
         // the slot keeps the residue of the syllable's offset in the bout (a placed bout, below)
-        sylLen = plan_harmonics(B, pc.data(), (int64_t)pc.size(), HPs, aA.view(), R, voiced.len & 3, false, true, &fs_off,
-                                &probes);
+        sylLen = plan_harmonics(B, pc.data(), (int64_t)pc.size(), HPs, aA.view(), R, voiced.len & 3, B.draws_only, true,
+                                &fs_off, &probes);
         for (size_t q = np0; q < probes.size(); ++q) probe_pos.push_back(voiced.len + probes[q].t);
-        bout_syls.push_back((int)B.syls.size() - 1);
+        if (!B.draws_only) bout_syls.push_back((int)B.syls.size() - 1);
         SgNoiseItem it = raw_item(fs_off, sylLen, voiced.len);
         voiced.items.push_back(it);
       }
@@ -616,8 +616,12 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
       nInt = moving ? nc : 1;
       filt_env = plan_envelope(B, R, (double)wl / 2, nInt, &Fm, A.formantDep, A.rolloffLip, mouthA.view(), 0, 0,
                                A.vocalTract, T, A.tempEffects[1], A.tempEffects[2], A.formantDepStoch, 1, sr, 35400);
-      grid.emplace(B, B.envjobs.back());
-      const int mode = hp_mode();
+      // draws_only: the bout's last draw is behind; what may still fail before the next
+      // bout's draws (the filter's FFT geometry; the global envelope's contour, below)
+      // runs, the rest does not
+      if (B.draws_only) geometry(B, wl);
+      else grid.emplace(B, B.envjobs.back());
+      const int mode = B.draws_only ? 0 : hp_mode();
       // the fp64 frame kernel takes even windows with a 31-smooth half M <= 2048
       if (mode > 0 && !bout_syls.empty() && wl % 2 == 0 && wl <= 4096 && smooth31(wl / 2)) {  // M <= 2048
         if (mode == 2) {
@@ -666,6 +670,7 @@ int64_t plan_soundgen(Batch& B, const sg_soundgen_args& a_in, Rng& R, int64_t ou
         mult = contour_desc(B, g2.view(), Ls, true, 0, true, -A.throwaway, false, sr);
       }
     }
+    if (B.draws_only) continue;
     // The pre-filter mix writes the bout's sound: its voiced syllables, the breathing
     // noise and the global envelope (addVectors and `sound * amplEnvelope`). A bout
     // whose sound is its voiced syllables alone (noise filtered separately, or none;

@@ -414,7 +414,7 @@ bool plan_noise(Batch& B, Rng& R, int64_t len, const sg_anchors& noiseAnchors, d
   const bool dev = filt_env < 0;  // device envelope job, rolloff included
   const int64_t ncolF = filterNoise || dev ? fnc : 1;
   int64_t filt_off = filt_env;
-  if (!dev) {
+  if (!dev && !B.draws_only) {
     vec filt((size_t)(nr * ncolF));
     for (int64_t c = 0; c < ncolF; ++c)
       for (int64_t k = 0; k < nr; ++k)
@@ -423,7 +423,7 @@ bool plan_noise(Batch& B, Rng& R, int64_t len, const sg_anchors& noiseAnchors, d
     filt_off = fl_push(B, filt.data(), (int64_t)filt.size());
   }
   vec fri((size_t)nc, 1.0);
-  if (filterNoise || dev) {
+  if ((filterNoise || dev) && !B.draws_only) {
     const vec s = r_seq_len(1, (double)ncolF, nc);
     for (int64_t c = 0; c < nc; ++c) fri[c] = r_round(s[c]);
   }
@@ -432,6 +432,13 @@ bool plan_noise(Batch& B, Rng& R, int64_t len, const sg_anchors& noiseAnchors, d
   // keeps as.integer(nr) rows of them)
   const int64_t ndraw = (int64_t)((double)wl / 2 * (double)nc);
   const int64_t nu = std::min<int64_t>(ndraw, nr * nc);
+  if (B.draws_only) {  // the item's length is all the caller's bout needs
+    R.unif_f32(ndraw, nullptr);
+    *item = SgNoiseItem{};
+    item->len = len;
+    item->ola = -1;
+    return true;
+  }
   int64_t u_off;
   if (ugather_on() && R.s && R.s->uniforms && R.iu + ndraw <= R.s->n_uniforms) {
     // every draw from the injected array: recorded, expanded on the device at upload
@@ -599,10 +606,13 @@ int64_t plan_envelope(Batch& B, Rng& R, double nrd, int64_t nc, const sg_formant
     std::vector<Track> fu(nF);
     int64_t off = 0;
     for (int f = 0; f < nF; ++f) {
-      fu[f].time = col_upsample(&t0[off], &t0[off], np[f], nPoints, slf, nc);
-      fu[f].freq = col_upsample(&t0[off], &f0[off], np[f], nPoints, slf, nc);
-      fu[f].amp = col_upsample(&t0[off], &a0[off], np[f], nPoints, slf, nc);
-      fu[f].width = col_upsample(&t0[off], &w0[off], np[f], nPoints, slf, nc);
+      // draws_only: the stochastic formants read the last track's frequencies alone
+      if (!B.draws_only || f == nF - 1) fu[f].freq = col_upsample(&t0[off], &f0[off], np[f], nPoints, slf, nc);
+      if (!B.draws_only) {
+        fu[f].time = col_upsample(&t0[off], &t0[off], np[f], nPoints, slf, nc);
+        fu[f].amp = col_upsample(&t0[off], &a0[off], np[f], nPoints, slf, nc);
+        fu[f].width = col_upsample(&t0[off], &w0[off], np[f], nPoints, slf, nc);
+      }
       off += np[f];
     }
     if (temperature > 0) {  // stochastic formants   R/sourceSpectrum.R:347-415
@@ -625,7 +635,7 @@ int64_t plan_envelope(Batch& B, Rng& R, double nrd, int64_t nc, const sg_formant
           if (rw.size() > 1) { const double m = r_mean(rw); for (auto& v : rw) v = v - m + 1; }
           const double g1 = R.rgamma(fdisp * fdisp / (sdG * sdG), fdisp / (sdG * sdG));
           Track t;
-          t.time = fu[0].time;
+          if (!B.draws_only) t.time = fu[0].time;
           t.freq.resize(nc);
           for (int64_t c = 0; c < nc; ++c) t.freq[c] = fu.back().freq[c] + r_round(g1 * rw[rw.size() > 1 ? c : 0]);
           const double sh = (formantDep / temperature) * (formantDep / temperature);
@@ -633,7 +643,7 @@ int64_t plan_envelope(Batch& B, Rng& R, double nrd, int64_t nc, const sg_formant
           const double g2 = R.rgamma(sh, rt);
           t.amp.resize(nc);
           t.width.resize(nc);
-          for (int64_t c = 0; c < nc; ++c) {
+          for (int64_t c = 0; c < nc && !B.draws_only; ++c) {
             t.amp[c] = r_round(g2 * rw[rw.size() > 1 ? c : 0]);
             t.width[c] = 50 + (std::log2(t.freq[c]) - 5) * 20;
           }
@@ -643,20 +653,15 @@ int64_t plan_envelope(Batch& B, Rng& R, double nrd, int64_t nc, const sg_formant
       }
       for (auto& tr : fu)
         for (int cc = 0; cc < 3; ++cc) {
-          vec rw = get_random_walk(R, nc, temperature * formDrift, 0.3, 1, vec{}, true);
+          vec rw = get_random_walk(R, nc, temperature * formDrift, 0.3, 1, vec{}, true, B.draws_only);
+          if (B.draws_only) continue;
           if (rw.size() > 1) { const double m = r_mean(rw); for (auto& v : rw) v = v - m + 1; }
           vec& col = cc == 0 ? tr.freq : cc == 1 ? tr.amp : tr.width;
           for (int64_t c = 0; c < nc; ++c) col[c] *= rw[rw.size() > 1 ? c : 0];
         }
     }
-    // Hz -> bins   R/sourceSpectrum.R:417-424
-    const double bw = sr / 2 / nrd;
-    for (auto& tr : fu)
-      for (int64_t c = 0; c < nc; ++c) {
-        tr.freq[c] = (tr.freq[c] - bw / 2) / bw + 1;
-        tr.width[c] = tr.width[c] / bw;
-      }
-    // mouth opening   R/sourceSpectrum.R:426-456
+    // mouth opening   R/sourceSpectrum.R:426-456 (no draws: computed ahead of the bins, whose
+    // shift below reads it)
     bool mouthNA = mouthAnchors.n < 1;
     for (int i = 0; i < mouthAnchors.n; ++i)
       if (std::isnan(mouthAnchors.value[i]) || std::isnan(mouthAnchors.time[i])) mouthNA = true;
@@ -670,6 +675,20 @@ int64_t plan_envelope(Batch& B, Rng& R, double nrd, int64_t nc, const sg_formant
         mbin[c] = v > 0 ? 1 : 0;
       }
     }
+    bool anyClosed = false;
+    for (int64_t c = 0; c < nc; ++c) if (mbin[c] == 0) anyClosed = true;
+    if (B.draws_only) {  // the envelope's last draw is behind; its one later error (the track count) in place
+      if (fu.size() + (anyClosed && f1_index >= 0 ? 2 : 0) > 2 * 64)
+        throw SgError(SG_E_UNSUPPORTED, "spectral envelope: more than 128 formant tracks");
+      return 0;
+    }
+    // Hz -> bins   R/sourceSpectrum.R:417-424
+    const double bw = sr / 2 / nrd;
+    for (auto& tr : fu)
+      for (int64_t c = 0; c < nc; ++c) {
+        tr.freq[c] = (tr.freq[c] - bw / 2) / bw + 1;
+        tr.width[c] = tr.width[c] / bw;
+      }
     const bool adj = !vtNull && std::isfinite(VT);
     for (auto& tr : fu)
       for (int64_t c = 0; c < nc; ++c) {
@@ -682,8 +701,6 @@ int64_t plan_envelope(Batch& B, Rng& R, double nrd, int64_t nc, const sg_formant
         if (tr.freq[c] < 1) tr.freq[c] = 1;
       }
     // nasalization when the mouth is closed   R/sourceSpectrum.R:469-504
-    bool anyClosed = false;
-    for (int64_t c = 0; c < nc; ++c) if (mbin[c] == 0) anyClosed = true;
     if (anyClosed && f1_index >= 0) {
       Track p = fu[f1_index], z = fu[f1_index];
       Track& f1 = fu[f1_index];
@@ -758,6 +775,7 @@ int64_t plan_envelope(Batch& B, Rng& R, double nrd, int64_t nc, const sg_formant
         }
       }
   }
+  if (B.draws_only) return 0;  // no formants: no draws
   // lip radiation, open-mouth boost, dB -> linear (2^(x/10))   R/sourceSpectrum.R:524-541
   job.col0 = (int64_t)B.ecols.size();
   for (int64_t c = 0; c < nc; ++c)

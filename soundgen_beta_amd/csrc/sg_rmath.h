@@ -238,7 +238,8 @@ struct Rng {
     if (s && s->unif_cb) return s->unif_cb(s->user);
     throw SgError(SG_E_RANDOM, "uniform stream exhausted");
   }
-  // n consecutive runif() draws as floats (out may be null: draws consumed, discarded)
+  // n consecutive runif() draws as floats (out may be null: draws consumed, discarded);
+  // past the injected array, blocks through the bulk callback when there is one
   void unif_f32(int64_t n, float* out) {
     int64_t k = 0;
     if (s) {
@@ -247,6 +248,16 @@ struct Rng {
         for (int64_t q = 0; q < avail; ++q) out[q] = (float)s->uniforms[iu + q];
       iu += avail;
       k = avail;
+      if (k < n && s->unif_n_cb) {
+        double blk[1024];
+        while (k < n) {
+          const int64_t m = std::min<int64_t>(n - k, 1024);
+          s->unif_n_cb(s->user, blk, m);
+          if (out)
+            for (int64_t q = 0; q < m; ++q) out[k + q] = (float)blk[q];
+          k += m;
+        }
+      }
     }
     for (; k < n; ++k) {
       const double x = unif();

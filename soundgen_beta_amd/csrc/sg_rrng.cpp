@@ -12,6 +12,7 @@
 // unif_rand (sg_plan_soundgen.cpp), so binding these three draws to an
 // sg_random reproduces R's whole stream. Pinned by R's published outputs
 // (tests/test_rrng.py); rgamma's acceptance branches are parity-unpinned.
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <new>
@@ -151,6 +152,32 @@ void sg_rrng_set_seed(sg_rrng* g, int32_t seed) {  // RNG_Init(MERSENNE_TWISTER,
 }
 
 double sg_rrng_unif(sg_rrng* g) { return fixup(mt_genrand(g)); }
+// runif(n): the same values as n sg_rrng_unif calls. The state's words are tempered
+// and scaled a block at a time (a loop the compiler vectorises); mt_genrand refills
+// the state exactly as it would one word at a time.
+void sg_rrng_unif_n(sg_rrng* g, double* out, int64_t n) {
+  uint32_t* mt = g->dummy + 1;
+  int64_t i = 0;
+  while (i < n) {
+    int mti = (int)g->dummy[0];
+    if (mti >= N) {  // refill (and the set.seed-less first call) through the one-word path
+      out[i++] = fixup(mt_genrand(g));
+      continue;
+    }
+    const int64_t m = std::min<int64_t>(n - i, N - mti);
+    for (int64_t q = 0; q < m; ++q) {
+      uint32_t y = mt[mti + q];
+      y ^= (y >> 11);
+      y ^= (y << 7) & TEMPERING_MASK_B;
+      y ^= (y << 15) & TEMPERING_MASK_C;
+      y ^= (y >> 18);
+      const double x = (double)y * 2.3283064365386963e-10;
+      out[i + q] = x <= 0.0 ? 0.5 * i2_32m1 : ((1.0 - x) <= 0.0 ? 1.0 - 0.5 * i2_32m1 : x);
+    }
+    g->dummy[0] = (uint32_t)(mti + m);
+    i += m;
+  }
+}
 
 double sg_rrng_norm(sg_rrng* g) {
   const double BIG = 134217728;  // 2^27: unif_rand() alone is not precise enough
@@ -270,6 +297,7 @@ double sg_rrng_gamma(sg_rrng* g, double a, double scale) {
 
 static double rrng_norm_cb(void* u) { return sg_rrng_norm(static_cast<sg_rrng*>(u)); }
 static double rrng_unif_cb(void* u) { return sg_rrng_unif(static_cast<sg_rrng*>(u)); }
+static void rrng_unif_n_cb(void* u, double* out, int64_t n) { sg_rrng_unif_n(static_cast<sg_rrng*>(u), out, n); }
 static double rrng_gamma_cb(void* u, double shape, double rate) {
   return sg_rrng_gamma(static_cast<sg_rrng*>(u), shape, 1.0 / rate);  // rgamma(n, shape, rate): scale = 1/rate
 }
@@ -278,6 +306,7 @@ void sg_random_bind_rrng(sg_random* r, sg_rrng* g) {
   r->norm_cb = rrng_norm_cb;
   r->unif_cb = rrng_unif_cb;
   r->gamma_cb = rrng_gamma_cb;
+  r->unif_n_cb = rrng_unif_n_cb;
   r->user = g;
 }
 

@@ -132,7 +132,11 @@ def lib():
     L.sg_noise_threshold.argtypes = [C.c_int32, C.c_double]
     L.sg_noise_threshold.restype = C.c_double
     L.sg_abi_version.restype = C.c_int
-    # whole-node batch path (sg_node.cpp)
+    # whole-node batch path (sg_node.cpp; ABI 3, chunks and divergence ABI 5). Guarded
+    # like sg_plan_sine_tasks: an older library still loads for A/B runs
+    if not hasattr(L, "sg_node_create"):
+        _lib = L
+        return L
     L.sg_device_count.restype = C.c_int
     L.sg_node_create.argtypes = [C.POINTER(C.c_int32), C.c_int32, C.POINTER(vp)]
     L.sg_node_destroy.argtypes = [vp]
@@ -156,6 +160,14 @@ def lib():
     L.sg_node_plan_shard_samples.restype = i64
     L.sg_node_execute_to_host.argtypes = [vp, vp, dp]
     L.sg_node_execute_to_host_f32.argtypes = [vp, vp, C.POINTER(C.c_float)]
+    if hasattr(L, "sg_node_plan_chunks"):
+        L.sg_node_plan_chunks.argtypes = [vp, C.c_int32]
+        L.sg_node_plan_chunks.restype = C.c_int32
+        L.sg_node_plan_diverged.argtypes = [vp]
+        L.sg_node_plan_diverged.restype = C.c_int32
+        L.sg_node_plan_call_work.argtypes = [vp, dp, dp]
+    if hasattr(L, "sg_rrng_unif_n"):
+        L.sg_rrng_unif_n.argtypes = [vp, dp, i64]
     _lib = L
     return L
 

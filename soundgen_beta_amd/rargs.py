@@ -332,11 +332,14 @@ class Holder:
             rng.bind(r)
             self.keep.append(rng)
         elif rng is not None:
+            def unif_n(_u, out, n):  # runif(n) in one call (ABI 5 bulk callback)
+                np.ctypeslib.as_array(out, (n,))[:] = rng.random(n)
             cbs = (_abi.NORM_CB(lambda _u: float(rng.standard_normal())),
                    _abi.UNIF_CB(lambda _u: float(rng.random())),
-                   _abi.GAMMA_CB(lambda _u, shape, rate: float(rng.gamma(shape, 1.0 / rate))))
+                   _abi.GAMMA_CB(lambda _u, shape, rate: float(rng.gamma(shape, 1.0 / rate))),
+                   _abi.UNIF_N_CB(unif_n))
             self.keep.extend(cbs)
-            r.norm_cb, r.unif_cb, r.gamma_cb = cbs
+            r.norm_cb, r.unif_cb, r.gamma_cb, r.unif_n_cb = cbs
         return r
 
 

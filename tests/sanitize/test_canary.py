@@ -17,4 +17,4 @@ def test_sanitized_libraries_are_loaded():
     maps = open("/proc/self/maps").read()
     assert "libsoundgen_hip_san.so" in maps and "libsg_oracle_san.so" in maps and "libasan" in maps
     assert hasattr(C.CDLL(None), "__asan_report_load8")  # the ASan runtime is in the process
-    assert L.sg_abi_version() == 4
+    assert L.sg_abi_version() == 5

@@ -7,7 +7,7 @@ from soundgen_beta_amd import native
 
 def test_library_loads():
     L = native.lib()
-    assert L.sg_abi_version() == 4
+    assert L.sg_abi_version() == 5
 
 
 def test_exports_every_declared_symbol():

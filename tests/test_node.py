@@ -85,3 +85,54 @@ def test_node_callback_stream_stops_at_failing_call():
     assert g1.random() == g2.random()
     p.close()
     node.close()
+
+
+def test_node_draws_only_recording_equals_serial_plan_c5():
+    """C5 presets (noise, stochastic formants, vocal fry, several bouts) drawing from
+    ONE RRng stream: the node's draws-only recording pass (Batch::draws_only, no device
+    work planned) plus the parallel replay gives every call the plan serial planning
+    gives it -- lengths, statuses, the sine-bank terms and FFT flops each call emits
+    (both depend on every draw) -- and leaves the stream where serial planning does."""
+    args = [c["args"] for c in _c5(192)]
+    g1, g2 = RRng(2026), RRng(2026)
+    whole = batch.Plan([{"kind": "soundgen", "args": a, "rng": g1} for a in args], None)
+    node = native.Node([0, 0, 0, 0])
+    p = batch.NodePlan([{"kind": "soundgen", "args": a, "rng": g2} for a in args], node)
+    assert np.array_equal(p.lengths, whole.lengths)
+    assert np.array_equal(p.status, whole.status) and not p.diverged
+    rows_w, flops_w = whole.call_work()
+    rows_n, flops_n = p.call_work()
+    # rows are integer counts; a call's flops are a difference of the batch's running
+    # fp64 total, so they carry its rounding (the batch around the call differs)
+    assert np.array_equal(rows_n, rows_w)
+    np.testing.assert_allclose(flops_n, flops_w, rtol=1e-9)
+    assert g1.random() == g2.random()
+    p.close()
+    node.close()
+
+
+def test_node_chunks_and_bulk_uniform_callback():
+    """Shards are planned in chunks of consecutive calls (SG_NODE_CHUNK calls, default
+    4096): a small batch is one chunk per shard. The Python draw callbacks (numpy
+    Generator) pass runs of uniforms through the bulk callback (ABI 5): the same plan
+    as one uniform per callback."""
+    calls = _c5(24)
+    node = native.Node([0, 0])
+    p = batch.NodePlan(calls, node)
+    assert [p.chunks(k) for k in range(2)] == [1, 1]
+    p.close()
+    node.close()
+    args = [dict(c["args"]) for c in calls[:6]]
+    plans = []
+    for bulk in (True, False):
+        rng = np.random.default_rng(5)
+        pl = batch.Plan([{"kind": "soundgen", "args": a, "rng": rng} for a in args], None)
+        plans.append((pl.lengths.copy(), pl.call_work(), rng.random()))
+        pl.close()
+        if bulk:
+            from soundgen_beta_amd import _abi
+            orig = _abi.UNIF_N_CB
+            _abi.UNIF_N_CB = lambda f: orig()  # a NULL bulk callback: one draw per callback
+    _abi.UNIF_N_CB = orig
+    (l1, (r1, f1), x1), (l2, (r2, f2), x2) = plans
+    assert np.array_equal(l1, l2) and np.array_equal(r1, r2) and np.array_equal(f1, f2) and x1 == x2

@@ -224,7 +224,7 @@ def sg_soundgen_args(R, call):
 
 
 def r_soundgen_batch(R, calls, devices=None):
-    """soundgen_batch(calls, devices): the node of `devices` (NULL: every visible device)."""
+    """soundgen_batch(calls, devices): the node of `devices` (NULL: device 0; [-1]: every visible device)."""
     dev = R.null() if devices is None else R.int_(devices)
     out = R.call("C_sg_soundgen_batch", R.list([sg_soundgen_args(R, c) for c in calls], named=False), dev)
     assert R.L.rm_type(out) == VECSXP and R.L.rm_length(out) == len(calls)

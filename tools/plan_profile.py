@@ -85,9 +85,13 @@ def main(n_calls=4096, top=40):
     # load the library, warm the size estimates (SG_PP_WARM=1: a whole plan first, so that the
     # host block cache is as warm as for bench.py's later chunks)
     batch.Plan(calls if os.environ.get("SG_PP_WARM") else calls[:max(64, len(calls) // 4)], None).close()
+    node = None
+    if os.environ.get("SG_PP_NODE"):  # the node path (with SG_PP_RNG: draws-only recording + replay)
+        from soundgen_beta_amd import native
+        node = native.Node([0])
     S.sg_sampler_start(2000, 1)
     t0 = time.perf_counter()
-    p = batch.Plan(calls, None)
+    p = batch.NodePlan(calls, node) if node else batch.Plan(calls, None)
     wall = time.perf_counter() - t0
     n = S.sg_sampler_stop()
     p.close()
@@ -108,6 +112,10 @@ def main(n_calls=4096, top=40):
     sym = _symbolize(lib, {o for _, _, m in samples for o in m}) if lib else {}
     self_fn, incl_fn, leaf_obj = collections.Counter(), collections.Counter(), collections.Counter()
     self_line = collections.Counter()
+    under = os.environ.get("SG_PP_UNDER")  # only samples with this planner frame on the stack
+    if under:
+        samples = [x for x in samples if any(under in _short(fn) for o in x[2] for fn, _ in sym.get(o, []))]
+        n = len(samples)
     for leaf_path, leaf_off, mine in samples:
         leaf_obj[os.path.basename(leaf_path or "?")] += 1
         if not mine:
