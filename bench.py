@@ -398,6 +398,76 @@ def relaunch(args):
     return subprocess.call(cmd)
 
 
+def node_bench(args):
+    """The whole-node path behind the C ABI (sg_node_plan_batch + sg_node_execute_to_host[_f32],
+    soundgen_batch()'s path from R): one process, every device of --node-devices, the batch
+    sharded by calls inside the library (LPT), each shard pipelined by chunk (the D2H of a
+    chunk beside the compute of the later ones). Timed: sg_node_execute_to_host entry to
+    every call's samples in the caller's host buffer at its whole-batch offset (a plain
+    numpy array: pageable memory, as a C or R caller holds it)."""
+    from soundgen_beta_amd import batch, native
+    devs = [int(x) for x in args.node_devices.split(",") if x.strip()]
+    make, n_default, desc = CONFIGS[args.config]
+    n_calls = args.calls or n_default
+    calls = make(n_calls)
+    node = native.Node(devs)
+    t_plan = time.perf_counter()
+    plan = batch.NodePlan(calls, node)
+    t_plan = time.perf_counter() - t_plan
+    native.lib().sg_host_cache_trim()
+    dtype = np.float64 if args.node_f64 else np.float32
+    host = np.empty(max(plan.total, 1), dtype=dtype)
+    L = native.lib()
+    if args.node_f64:
+        fn, ptr = L.sg_node_execute_to_host, host.ctypes.data_as(C.POINTER(C.c_double))
+    else:
+        fn, ptr = L.sg_node_execute_to_host_f32, host.ctypes.data_as(C.POINTER(C.c_float))
+
+    def step():
+        node.check(fn(node.ptr, plan.ptr, ptr))
+    for _ in range(args.warmup):
+        step()
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    dt = time.perf_counter() - t
+    samples = int(plan.lengths[plan.status == 0].sum())
+    failed = int((plan.status != 0).sum())
+    rms = None
+    if args.rms_calls > 0:  # the timed outputs against the oracle, calls spread over the batch
+        from concurrent.futures import ThreadPoolExecutor
+        from oracle import oracle as O
+        O.lib()
+        ok = np.nonzero(plan.status == 0)[0]
+        pick = ok[np.linspace(0, len(ok) - 1, min(args.rms_calls, len(ok))).round().astype(int)] if len(ok) else []
+
+        def one(i):
+            ref = oracle_call(O, calls[int(i)])
+            y = host[plan.offsets[i]:plan.offsets[i] + plan.lengths[i]].astype(np.float64)
+            return float(np.sqrt(np.mean((y - ref) ** 2))) if len(ref) == len(y) else float("inf")
+        with ThreadPoolExecutor(host_cores()) as ex:
+            errs = list(ex.map(one, pick))
+        rms = {"calls": len(errs), "max": max(errs) if errs else None, "tolerance": 1e-5,
+               "within_tolerance": int(sum(e <= 1e-5 for e in errs))}
+    res = {"metric": METRIC, "value": samples * args.steps / dt, "unit": "samples/s", "n_gpus": len(devs),
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+           "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32 (fp64 phase)",
+           "data": "synthetic (PCG64 seed %d; random draws injected)" % SEED,
+           "config": {"workload": desc % n_calls, "calls": n_calls, "samples": samples, "failed_calls": failed,
+                      "parallelism": "node: one process over devices %s (sg_node, LPT shards)" % devs,
+                      "chunks_per_shard": [plan.chunks(k) for k in range(len(devs))]},
+           "path": "sg_node_plan_batch + sg_node_execute_to_host%s (the C-ABI whole-node path; soundgen_batch() "
+                   "from R)" % ("" if args.node_f64 else "_f32"),
+           "timing": "sg_node_execute_to_host entry to every call's samples in the caller's pageable %s host "
+                     "buffer at its whole-batch offset" % ("float64" if args.node_f64 else "float32"),
+           "plan_s": t_plan, "value_incl_planning": samples / (t_plan + dt / args.steps),
+           "rms_error_vs_oracle": rms["max"] if rms else None, "rms_check": rms}
+    print(json.dumps(res), flush=True)
+    plan.close()
+    node.close()
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -419,7 +489,14 @@ def main():
                     help="N>1: skip the timed gather of every rank's packed output to rank 0 after the timed steps")
     ap.add_argument("--rms-calls", type=int, default=66,
                     help="calls checked against the oracle after timing, spread over every plan")
+    ap.add_argument("--node", action="store_true",
+                    help="the whole-node C-ABI path R reaches (sg_node_*): one process, --node-devices, "
+                         "the batch planned once and executed into a caller's (pageable) host buffer")
+    ap.add_argument("--node-devices", default="0", help="--node: comma-separated device ordinals")
+    ap.add_argument("--node-f64", action="store_true", help="--node: into doubles (R's numeric vectors)")
     args = ap.parse_args()
+    if args.node:
+        return node_bench(args)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(relaunch(args))
 

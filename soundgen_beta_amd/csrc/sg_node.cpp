@@ -45,6 +45,7 @@
 #include <queue>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "sg_plan.h"
@@ -282,6 +283,7 @@ struct sg_node_plan {
     sg_plan* plan = nullptr;
     int64_t dev_off = 0, samples = 0;
     std::vector<int64_t> keep;  // while planning: the chunk's planned calls
+    bool uploaded = false;       // uploaded, host copies released (sg_plan_release_host)
   };
   std::vector<std::vector<int64_t>> idx;
   std::vector<std::vector<Chunk>> chunks;
@@ -710,20 +712,35 @@ void run_shard(sg_node* node, sg_node_plan* p, int32_t k, T* out_host, int threa
     d.ev.push_back(e);
   }
   for (size_t c = 0; c < nc; ++c) {
+    if (!cs[c].uploaded) {  // first execute: upload, then free the chunk's host copies (~0.7 MB per C5 call)
+      int rc = sg_plan_upload(d.ctx, cs[c].plan);
+      if (rc) throw sg::SgError(rc, std::string("shard upload: ") + sg_last_error(d.ctx));
+      rc = sg_plan_release_host(cs[c].plan);
+      if (rc) throw sg::SgError(rc, "shard upload: releasing host copies failed");
+      cs[c].uploaded = true;
+    }
     const int rc = sg_execute(d.ctx, cs[c].plan, d.d_out + cs[c].dev_off, d.run);
     if (rc) throw sg::SgError(rc, std::string("shard execute: ") + sg_last_error(d.ctx));
     NODE_HIPCHK(hipEventRecord(d.ev[2 * c], d.run));
   }
   const std::vector<int64_t>& idx = p->idx[k];
+  // a chunk of consecutive calls of the batch (one device: every chunk) is one block
+  // of the whole-batch layout: fp32 goes straight into the caller's buffer
+  auto direct = [&](size_t c) {
+    if (!std::is_same<T, float>::value || p->diverged) return false;  // diverged: calls unplanned after planning
+    return idx[(size_t)(cs[c].j1 - 1)] - idx[(size_t)cs[c].j0] == cs[c].j1 - 1 - cs[c].j0;
+  };
   auto copy = [&](size_t c) {
     NODE_HIPCHK(hipStreamWaitEvent(d.copy, d.ev[2 * c], 0));
     if (cs[c].samples)
-      NODE_HIPCHK(hipMemcpyAsync(d.pin[c % 2], d.d_out + cs[c].dev_off, (size_t)cs[c].samples * sizeof(float),
+      NODE_HIPCHK(hipMemcpyAsync(direct(c) ? (void*)(out_host + p->off[idx[(size_t)cs[c].j0]]) : d.pin[c % 2],
+                                 d.d_out + cs[c].dev_off, (size_t)cs[c].samples * sizeof(float),
                                  hipMemcpyDeviceToHost, d.copy));
     NODE_HIPCHK(hipEventRecord(d.ev[2 * c + 1], d.copy));
   };
   auto scatter = [&](size_t c) {
     NODE_HIPCHK(hipEventSynchronize(d.ev[2 * c + 1]));
+    if (direct(c)) return;
     const float* h = static_cast<const float*>(d.pin[c % 2]);
     const int64_t n = cs[c].j1 - cs[c].j0;
     std::vector<int64_t> l((size_t)n), o((size_t)n);
