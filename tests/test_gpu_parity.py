@@ -77,7 +77,7 @@ def test_sine_table_direct_output_equals_w_path():
     import torch
     from soundgen_beta_amd import batch, native
     # 441 Hz and 2205 Hz: phase grids of 100 and 20 points per cycle (f0 / fs = 1 / 100, 1 / 20),
-    # coarser than the table, so the candidate search may fall back to the full pass
+    # coarser than the table: the max pass evaluates every sample on that grid
     calls = [{"kind": "harmonics", "pitch": np.full(n, f), "params": dict(C2, attackLen=a)}
              for f, n, a in ((97.0, 3500, 50), (210.0, 1200, 10), (333.3, 5000, 0), (150.0, 800, 300),
                              (441.0, 2000, 50), (2205.0, 2000, 50), (1000.0, 3000, 20), (201.0, 7000, 50))]
