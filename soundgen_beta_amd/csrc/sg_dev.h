@@ -58,6 +58,11 @@ constexpr int SG_TASK_LIN = 2;    // phase segment linear (c2 = c3 = c4 = 0): on
 // sg_plan_soundgen.cpp): fp64 angle and recurrence, w_off indexes the fp64 epoch scratch W64
 constexpr int SG_TASK_HP = 8;
 constexpr int SG_TASK_MAX = 1024;  // samples per task (16 slots of 64 lanes)
+// short tasks (<= 64 samples) run in runs of consecutive tasks of one syllable, two per
+// wave step, one wave per run (sg_sine_bank_pairs / _tall_pairs; round 6)
+#ifndef SG_RUN_TASKS
+#define SG_RUN_TASKS 8
+#endif
 struct SgWTask {
   int64_t w_off;       // W offset of epoch sample 0
   int64_t a_off;       // float offset of A[i][0..R)

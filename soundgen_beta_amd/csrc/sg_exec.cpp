@@ -30,7 +30,7 @@ constexpr size_t ALIGN = 256;
 size_t up(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
 struct Layout {
-  size_t tall, tlong, tshort, tallp, thp, fin_tiles_hp, W64, fh, frames64, frames64_tab, roots64, roots64_wl,
+  size_t tall, tlong, tshort, tallp, srun, trun, thp, fin_tiles_hp, W64, fh, frames64, frames64_tab, roots64, roots64_wl,
       roots64_off;
   size_t segs, epochs, knots, amps, ampcols, ampjobs, ampsrc, tasks, pieces, syls, syl_tiles, copy_tiles, ptiles, cknots, W, taskmax, ptilemax, maxes, total;
   size_t geoms, frames, fgroups, olas, olatiles, olasegs, olatilemax, olamax, items, mixes, mixtiles, fl, fs;
@@ -51,6 +51,8 @@ struct Layout {
     tlong = take(ntask * sizeof(int32_t));
     tshort = take(ntask * sizeof(int32_t));
     tallp = take(ntask * sizeof(int32_t));
+    srun = take((ntask + 1) * sizeof(int32_t));
+    trun = take((ntask + 1) * sizeof(int32_t));
     thp = take(ntask * sizeof(int32_t));
     fin_tiles_hp = take(B.fin_tiles_hp.size() * sizeof(SgSylTile));
     W64 = take((size_t)B.w64_total * sizeof(double));
@@ -303,17 +305,35 @@ static void group_block(const Batch& B, const ColumnReader& cols, const TaskBloc
 // have none
 struct TaskClasses {
   std::vector<int32_t> tlong, tshort, tall, tallp, thp;
+  std::vector<int32_t> srun, trun;  // run starts in tshort / tallp (block-local positions)
 };
+// a new run starts at a task of another syllable or after SG_RUN_TASKS tasks
+static void run_start(std::vector<int32_t>& runs, const std::vector<int32_t>& list, int32_t& syl, const SgWTask& t) {
+  const int32_t pos = (int32_t)list.size() - 1;
+  if (runs.empty() || t.syl != syl || pos - runs.back() >= SG_RUN_TASKS) runs.push_back(pos);
+  syl = t.syl;
+}
 static void classify_block(const TaskBlock& blk, const std::vector<uint8_t>& in_tab, TaskClasses& c) {
+  int32_t ssyl = -1, tsyl = -1;
   for (int64_t k = 0; k < blk.n; ++k) {
     const SgWTask& t = blk.p[k];
     const int32_t i = (int32_t)(blk.o + k);
     const bool shrt = t.len <= 64 && !(t.flags & SG_TASK_ENV);
     if (!in_tab.empty() && in_tab[(size_t)i]) continue;
     if (t.flags & SG_TASK_HP) c.thp.push_back(i);
-    else if (t.R > SG_ROWS_F32) (shrt ? c.tallp : c.tall).push_back(i);
-    else if (shrt) c.tshort.push_back(i);
-    else c.tlong.push_back(i);
+    else if (t.R > SG_ROWS_F32) {
+      if (shrt) {
+        c.tallp.push_back(i);
+        run_start(c.trun, c.tallp, tsyl, t);
+      } else {
+        c.tall.push_back(i);
+      }
+    } else if (shrt) {
+      c.tshort.push_back(i);
+      run_start(c.srun, c.tshort, ssyl, t);
+    } else {
+      c.tlong.push_back(i);
+    }
   }
 }
 // Wavetable spans and task classes of a batch, block by block on host threads;
@@ -348,6 +368,19 @@ static TabSpans group_tables(const Batch& B, bool tables, TaskClasses* classes) 
       dst.reserve(n);
       for (const TaskClasses& c : cls) dst.insert(dst.end(), (c.*m).begin(), (c.*m).end());
     };
+    // the runs of each block, rebased to the concatenated list, then the list's size
+    auto runs = [&](std::vector<int32_t> TaskClasses::*r, std::vector<int32_t> TaskClasses::*m) {
+      std::vector<int32_t>& dst = classes->*r;
+      dst.clear();
+      int32_t base = 0;
+      for (const TaskClasses& c : cls) {
+        for (int32_t x : c.*r) dst.push_back(base + x);
+        base += (int32_t)(c.*m).size();
+      }
+      dst.push_back(base);
+    };
+    runs(&TaskClasses::srun, &TaskClasses::tshort);
+    runs(&TaskClasses::trun, &TaskClasses::tallp);
     cat(&TaskClasses::tlong);
     cat(&TaskClasses::tshort);
     cat(&TaskClasses::tall);
@@ -582,6 +615,8 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   D.tlong = (int32_t*)(a + L.tlong);
   D.tshort = (int32_t*)(a + L.tshort);
   D.tallp = (int32_t*)(a + L.tallp);
+  D.srun = (int32_t*)(a + L.srun);
+  D.trun = (int32_t*)(a + L.trun);
   D.thp = (int32_t*)(a + L.thp);
   D.fin_tiles_hp = (SgSylTile*)(a + L.fin_tiles_hp);
   D.W64 = (double*)(a + L.W64);
@@ -637,6 +672,8 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   D.tshort_host.swap(C.tshort);
   D.tall_host.swap(C.tall);
   D.tallp_host.swap(C.tallp);
+  D.srun_host.swap(C.srun);
+  D.trun_host.swap(C.trun);
   D.thp_host.swap(C.thp);
   D.tabjobs_host.swap(T.jobs);
   D.tab_samples = T.samples;
@@ -658,6 +695,8 @@ void device_upload(const Batch& B, DevicePlan& D, hipStream_t s) {
   cp(D.tlong, D.tlong_host.data(), D.tlong_host.size() * sizeof(int32_t));
   cp(D.tshort, D.tshort_host.data(), D.tshort_host.size() * sizeof(int32_t));
   cp(D.tallp, D.tallp_host.data(), D.tallp_host.size() * sizeof(int32_t));
+  cp(D.srun, D.srun_host.data(), D.srun_host.size() * sizeof(int32_t));
+  cp(D.trun, D.trun_host.data(), D.trun_host.size() * sizeof(int32_t));
   cp(D.thp, D.thp_host.data(), D.thp_host.size() * sizeof(int32_t));
   if (!D.tabjobs_host.empty()) cp(D.tabjobs, D.tabjobs_host.data(), D.tabjobs_host.size() * sizeof(SgTabJob));
   cp(D.fin_tiles_hp, B.fin_tiles_hp.data(), B.fin_tiles_hp.size() * sizeof(SgSylTile));
@@ -747,12 +786,26 @@ static void device_execute_harm(const Batch& B, DevicePlan& D, float* d_out, hip
       int64_t k0 = 0, n = 0;
       n = range(D.tlong_host, k0);
       launch_sine_bank(D, k0, n, h);
+      // the runs of the slice's short tasks: [r0, r1) with starts inside [k0, k0 + n)
+      auto runs = [&](const std::vector<int32_t>& rs, int64_t a, int64_t n, int64_t& r0) {
+        const auto lo = std::lower_bound(rs.begin(), rs.end() - 1, (int32_t)a);
+        const auto hi = std::lower_bound(lo, rs.end() - 1, (int32_t)(a + n));
+        r0 = lo - rs.begin();
+        return (int64_t)(hi - lo);
+      };
+      int64_t r0 = 0;
       n = range(D.tshort_host, k0);
-      launch_sine_bank_pairs(D, k0, n, h);
+      if (n > 0) {
+        const int64_t nr = runs(D.srun_host, k0, n, r0);
+        launch_sine_bank_pairs(D, r0, nr, h);
+      }
       n = range(D.tall_host, k0);
       launch_sine_bank_tall(D, k0, n, h);
       n = range(D.tallp_host, k0);
-      launch_sine_bank_tall_pairs(D, k0, n, h);
+      if (n > 0) {
+        const int64_t nr = runs(D.trun_host, k0, n, r0);
+        launch_sine_bank_tall_pairs(D, r0, nr, h);
+      }
       if (!D.tabjobs_host.empty()) {  // the jobs whose first task lies in the slice, one launch
         const auto& J = D.tabjobs_host;
         const auto lo = std::partition_point(J.begin(), J.end(), [&](const SgTabJob& j) { return j.t0 < sl.t0; });

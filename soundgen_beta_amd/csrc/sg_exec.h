@@ -41,6 +41,12 @@ struct DevicePlan {
   std::vector<int32_t> tshort_host;
   int32_t* tallp = nullptr;          // tall tasks of <= 64 samples, two per wave (sg_sine_bank_tall_pairs)
   std::vector<int32_t> tallp_host;
+  // runs of the two short lists: consecutive entries of one syllable, <= SG_RUN_TASKS each,
+  // one wave per run (positions in tshort / tallp where each run starts, then the list size)
+  int32_t* srun = nullptr;
+  std::vector<int32_t> srun_host;
+  int32_t* trun = nullptr;
+  std::vector<int32_t> trun_host;
   int32_t* thp = nullptr;            // SG_TASK_HP tasks (sg_sine_bank_hp)
   std::vector<int32_t> thp_host;
   // wavetable path (SgTabJob): tasks of long static-tone spans

@@ -293,18 +293,63 @@ __device__ __forceinline__ float run_one(const SgWTask& T, float* __restrict__ l
 // task. Their rows interleave in LDS (la[2r] = A_P[r], la[2r + 1] = A_Q[r],
 // zero above a task's R; the dA rows likewise, zero for a CONST task), and one
 // broadcast ds_read_b128 yields rows r, r + 1 of both.
+// The last amplitude column a run step loaded (rows lane, lane + 64 of its epoch block;
+// SG_ROWS_F32 <= 128): consecutive glottal cycles share a column (task t's A[i + 1] is
+// task t + 1's A[i]), so a run reads each column once.
+struct ColCache {
+  int64_t off = -1;
+  float v[2] = {0.f, 0.f};
+};
+static_assert(SG_ROWS_F32 <= 128, "ColCache holds two rows per lane");
+#ifndef SG_RUN_CACHE
+#define SG_RUN_CACHE 1
+#endif
+
 template <bool TWO>
 __device__ __forceinline__ void run_pair(const SgWTask& P, const SgWTask& Q, float* __restrict__ la,
                                          float* __restrict__ ld, const float* __restrict__ amps,
-                                         float* __restrict__ W, int lane, float& mp, float& mq) {
+                                         float* __restrict__ W, int lane, float& mp, float& mq,
+                                         ColCache* cc = nullptr) {
+#ifdef SG_DIAG_PAIR_NOROWS  // diagnostic build only: the pair's set-up, staging and stores without the rows
+  const int R = 0;
+#else
   const int R = P.Rn > Q.Rn ? P.Rn : Q.Rn;  // multiples of 16
-  for (int r = lane; r < R; r += 64) {
-    const float ap = r < P.Rn ? amps[P.a_off + r] : 0.f, aq = r < Q.Rn ? amps[Q.a_off + r] : 0.f;
-    *reinterpret_cast<float2*>(la + 2 * r) = make_float2(ap, aq);
-    if (TWO)
-      *reinterpret_cast<float2*>(ld + 2 * r) =
-          make_float2(r < P.Rn && !(P.flags & SG_TASK_CONST) ? amps[P.d_off + r] - ap : 0.f,
-                      r < Q.Rn && !(Q.flags & SG_TASK_CONST) ? amps[Q.d_off + r] - aq : 0.f);
+#endif
+  if (SG_RUN_CACHE && cc) {
+    // Rows of a column past its task's Rn are zero (Rn covers both of the task's columns), so
+    // a column read up to its epoch's R (the block's rows) is the same for every task that
+    // shares it: reuse by offset is exact. The old form's masks (r < Rn) select the same values.
+    const bool pc = P.flags & SG_TASK_CONST, qc = Q.flags & SG_TASK_CONST;
+    ColCache nc;
+    const int hn = (P.R > 64 || Q.R > 64) ? 2 : 1;  // whole columns (R <= SG_ROWS_F32 < 128), so the cache is
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {                   // valid for any later R
+      if (h >= hn) break;
+      const int r = lane + 64 * h;
+      auto load = [&](int64_t off, int rows) { return r < rows ? amps[off + r] : 0.f; };
+      const float pa = P.a_off == cc->off ? cc->v[h] : load(P.a_off, P.R);
+      const float pd = TWO && !pc ? (P.d_off == cc->off ? cc->v[h] : load(P.d_off, P.R)) : pa;
+      const float qa = Q.a_off == P.a_off ? pa
+                       : Q.a_off == P.d_off && TWO && !pc ? pd
+                       : Q.a_off == cc->off ? cc->v[h] : load(Q.a_off, Q.R);
+      const float qd = TWO && !qc ? (Q.d_off == P.d_off && !pc ? pd : load(Q.d_off, Q.R)) : qa;
+      if (r < R) {
+        *reinterpret_cast<float2*>(la + 2 * r) = make_float2(pa, qa);
+        if (TWO) *reinterpret_cast<float2*>(ld + 2 * r) = make_float2(pc ? 0.f : pd - pa, qc ? 0.f : qd - qa);
+      }
+      nc.v[h] = TWO && !qc ? qd : qa;
+    }
+    nc.off = TWO && !qc ? Q.d_off : Q.a_off;
+    *cc = nc;
+  } else {
+    for (int r = lane; r < R; r += 64) {
+      const float ap = r < P.Rn ? amps[P.a_off + r] : 0.f, aq = r < Q.Rn ? amps[Q.a_off + r] : 0.f;
+      *reinterpret_cast<float2*>(la + 2 * r) = make_float2(ap, aq);
+      if (TWO)
+        *reinterpret_cast<float2*>(ld + 2 * r) =
+            make_float2(r < P.Rn && !(P.flags & SG_TASK_CONST) ? amps[P.d_off + r] - ap : 0.f,
+                        r < Q.Rn && !(Q.flags & SG_TASK_CONST) ? amps[Q.d_off + r] - aq : 0.f);
+    }
   }
   const bool vp = lane < P.len, vq = lane < Q.len;
   float tp, alp, snp, tq, alq, snq;
@@ -359,31 +404,47 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
   if (lane == 0) taskmax[ti] = wm;
 }
 
-// Short fp32 tasks (<= 64 samples, no envelope; listed in idx), two per wave in
-// the halves of packed pairs (run_pair). The arithmetic of a task does not
-// depend on its partner (the last odd one pairs with itself).
-extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_pairs(
-    const int32_t* __restrict__ idx, int64_t n, const SgWTask* __restrict__ tasks, const float* __restrict__ amps,
-    float* __restrict__ W, float* __restrict__ taskmax) {
-  __shared__ __attribute__((aligned(16))) float rows[4][2][SG_LDS_ROWS];
+// A run of short tasks (consecutive entries of one syllable in the class list idx:
+// idx[rs[r] .. rs[r + 1]), <= SG_RUN_TASKS) on one wave, two tasks per step in the
+// halves of packed pairs (PAIR: run_pair or run_pair_rs; a task's arithmetic does not
+// depend on its partner, the last odd one pairs with itself). The syllable max needs
+// only the max over its tasks (sg_syl_max), so the run's max goes to its first task's
+// slot and -inf to the others: one wave reduction per run instead of two per step
+// (round 6; the per-step set-up, staging and stores stay per step).
+template <class PAIR>
+__device__ __forceinline__ void run_of_pairs(const int32_t* __restrict__ idx, const int32_t* __restrict__ rs,
+                                             int64_t nruns, const SgWTask* __restrict__ tasks,
+                                             float* __restrict__ taskmax, PAIR&& pair) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t k = ((int64_t)sgd::xcd_swizzle(blockIdx.x, gridDim.x) * 4 + wave) * 2;
-  if (k >= n) return;
-  const int64_t tp = idx[k];
-  const bool has_q = k + 1 < n;
-  const int64_t tq = has_q ? idx[k + 1] : tp;
-  const SgWTask P = tasks[tp];
-  const SgWTask Q = tasks[tq];
-  float mp, mq;
-  if ((P.flags & Q.flags) & SG_TASK_CONST) run_pair<false>(P, Q, rows[wave][0], rows[wave][1], amps, W, lane, mp, mq);
-  else run_pair<true>(P, Q, rows[wave][0], rows[wave][1], amps, W, lane, mp, mq);
-  mp = wave_max(mp);
-  mq = wave_max(mq);
-  if (lane == 0) {
-    taskmax[tp] = mp;
-    if (has_q) taskmax[tq] = mq;
+  const int64_t r = (int64_t)sgd::xcd_swizzle(blockIdx.x, gridDim.x) * 4 + wave;
+  if (r >= nruns) return;
+  const int32_t k0 = rs[r], k1 = rs[r + 1];
+  float m = -INFINITY;
+  for (int32_t k = k0; k < k1; k += 2) {
+    const SgWTask P = tasks[idx[k]];
+    const SgWTask Q = tasks[idx[k + 1 < k1 ? k + 1 : k]];
+    float mp, mq;
+    pair(P, Q, wave, lane, mp, mq);
+    m = fmaxf(m, fmaxf(mp, mq));
+    __asm__ __volatile__("" ::: "memory");  // the next step's staging follows this step's row reads
   }
+  m = wave_max(m);
+  for (int32_t k = k0 + lane; k < k1; k += 64) taskmax[idx[k]] = k == k0 ? m : -INFINITY;
+}
+
+// Short fp32 tasks (<= 64 samples, no envelope), runs of them (run_of_pairs).
+extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_pairs(
+    const int32_t* __restrict__ idx, const int32_t* __restrict__ rs, int64_t nruns,
+    const SgWTask* __restrict__ tasks, const float* __restrict__ amps, float* __restrict__ W,
+    float* __restrict__ taskmax) {
+  __shared__ __attribute__((aligned(16))) float rows[4][2][SG_LDS_ROWS];
+  ColCache cc;
+  run_of_pairs(idx, rs, nruns, tasks, taskmax,
+               [&](const SgWTask& P, const SgWTask& Q, int wave, int lane, float& mp, float& mq) {
+                 if ((P.flags & Q.flags) & SG_TASK_CONST) run_pair<false>(P, Q, rows[wave][0], rows[wave][1], amps, W, lane, mp, mq, &cc);
+                 else run_pair<true>(P, Q, rows[wave][0], rows[wave][1], amps, W, lane, mp, mq, &cc);
+               });
 }
 
 // ---------------------------------------------- tall tasks, fp32 Reinsch
@@ -511,30 +572,17 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_tall(
   if (lane == 0) taskmax[ti] = wm;
 }
 
-// Short tall tasks, two per wave, fp32 Reinsch (run_pair_rs); a task's arithmetic
-// does not depend on its partner.
+// Short tall tasks, runs of them, fp32 Reinsch (run_pair_rs).
 extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_tall_pairs(
-    const int32_t* __restrict__ idx, int64_t n, const SgWTask* __restrict__ tasks, const float* __restrict__ amps,
-    float* __restrict__ W, float* __restrict__ taskmax) {
+    const int32_t* __restrict__ idx, const int32_t* __restrict__ rs, int64_t nruns,
+    const SgWTask* __restrict__ tasks, const float* __restrict__ amps, float* __restrict__ W,
+    float* __restrict__ taskmax) {
   __shared__ __attribute__((aligned(16))) float rows[4][2][SG_LDS_ROWS];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t k = ((int64_t)sgd::xcd_swizzle(blockIdx.x, gridDim.x) * 4 + wave) * 2;
-  if (k >= n) return;
-  const int64_t tp = idx[k];
-  const bool has_q = k + 1 < n;
-  const int64_t tq = has_q ? idx[k + 1] : tp;
-  const SgWTask P = tasks[tp];
-  const SgWTask Q = tasks[tq];
-  float mp, mq;
-  if ((P.flags & Q.flags) & SG_TASK_CONST) run_pair_rs<false>(P, Q, rows[wave][0], rows[wave][1], amps, W, lane, mp, mq);
-  else run_pair_rs<true>(P, Q, rows[wave][0], rows[wave][1], amps, W, lane, mp, mq);
-  mp = wave_max(mp);
-  mq = wave_max(mq);
-  if (lane == 0) {
-    taskmax[tp] = mp;
-    if (has_q) taskmax[tq] = mq;
-  }
+  run_of_pairs(idx, rs, nruns, tasks, taskmax,
+               [&](const SgWTask& P, const SgWTask& Q, int wave, int lane, float& mp, float& mq) {
+                 if ((P.flags & Q.flags) & SG_TASK_CONST) run_pair_rs<false>(P, Q, rows[wave][0], rows[wave][1], amps, W, lane, mp, mq);
+                 else run_pair_rs<true>(P, Q, rows[wave][0], rows[wave][1], amps, W, lane, mp, mq);
+               });
 }
 
 // ------------------------------------------- fp64 path (SG_TASK_HP tasks)
@@ -1203,10 +1251,11 @@ void launch_sine_bank(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s)
                      D.syls, D.cknots, D.W, D.taskmax);
   SG_LAUNCHED("sg_sine_bank");
 }
-void launch_sine_bank_pairs(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s) {
+// r0, n: the runs (D.srun) of the slice
+void launch_sine_bank_pairs(const DevicePlan& D, int64_t r0, int64_t n, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(sg_sine_bank_pairs, dim3((unsigned)((n + 7) / 8)), dim3(256), 0, s, D.tshort + k0, n, D.tasks,
-                     D.amps, D.W, D.taskmax);
+  hipLaunchKernelGGL(sg_sine_bank_pairs, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, D.tshort, D.srun + r0, n,
+                     D.tasks, D.amps, D.W, D.taskmax);
   SG_LAUNCHED("sg_sine_bank_pairs");
 }
 void launch_sine_bank_tall(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s) {
@@ -1215,10 +1264,11 @@ void launch_sine_bank_tall(const DevicePlan& D, int64_t k0, int64_t n, hipStream
                      D.amps, D.syls, D.cknots, D.W, D.taskmax);
   SG_LAUNCHED("sg_sine_bank_tall");
 }
-void launch_sine_bank_tall_pairs(const DevicePlan& D, int64_t k0, int64_t n, hipStream_t s) {
+// r0, n: the runs (D.trun) of the slice
+void launch_sine_bank_tall_pairs(const DevicePlan& D, int64_t r0, int64_t n, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(sg_sine_bank_tall_pairs, dim3((unsigned)((n + 7) / 8)), dim3(256), 0, s, D.tallp + k0, n,
-                     D.tasks, D.amps, D.W, D.taskmax);
+  hipLaunchKernelGGL(sg_sine_bank_tall_pairs, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, D.tallp,
+                     D.trun + r0, n, D.tasks, D.amps, D.W, D.taskmax);
   SG_LAUNCHED("sg_sine_bank_tall_pairs");
 }
 void launch_sine_bank_tab(const DevicePlan& D, int logn, int64_t j0, int64_t n, float* out, hipStream_t s) {
