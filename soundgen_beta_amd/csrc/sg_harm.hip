@@ -295,14 +295,17 @@ __device__ __forceinline__ float run_one(const SgWTask& T, float* __restrict__ l
 // broadcast ds_read_b128 yields rows r, r + 1 of both.
 // The last amplitude column a run step loaded (rows lane, lane + 64 of its epoch block;
 // SG_ROWS_F32 <= 128): consecutive glottal cycles share a column (task t's A[i + 1] is
-// task t + 1's A[i]), so a run reads each column once.
+// task t + 1's A[i]), so a run reads each column once. Off by default (SG_RUN_CACHE=1
+// enables it): the second read hits L2 and the cache's selects cost more (r06h: pairs
+// 1.888 ms without, 1.965 ms with; a variant that also loaded step s + 1's columns and
+// descriptors during step s's rows took 2.466 ms).
 struct ColCache {
   int64_t off = -1;
   float v[2] = {0.f, 0.f};
 };
 static_assert(SG_ROWS_F32 <= 128, "ColCache holds two rows per lane");
 #ifndef SG_RUN_CACHE
-#define SG_RUN_CACHE 1
+#define SG_RUN_CACHE 0
 #endif
 
 template <bool TWO>
