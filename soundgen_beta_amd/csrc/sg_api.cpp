@@ -472,11 +472,14 @@ int sg_ctx_create(int device, sg_ctx** out) {
 
 void sg_ctx_destroy(sg_ctx* ctx) {
   if (!ctx) return;
+  int prev = -1;  // the caller's current device, restored afterwards
+  const bool had = hipGetDevice(&prev) == hipSuccess;
   (void)hipSetDevice(ctx->device);
   for (auto& ev : ctx->prof_events) { (void)hipEventDestroy(ev.e0); (void)hipEventDestroy(ev.e1); }
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
   delete ctx;
+  if (had && prev >= 0) (void)hipSetDevice(prev);
 }
 
 const char* sg_last_error(const sg_ctx* ctx) { return ctx ? ctx->err.c_str() : ""; }

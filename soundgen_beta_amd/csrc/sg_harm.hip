@@ -308,6 +308,57 @@ static_assert(SG_ROWS_F32 <= 128, "ColCache holds two rows per lane");
 #define SG_RUN_CACHE 0
 #endif
 
+// Rows [r0, r0 + n) of a pair's columns into LDS, interleaved (la[2r] = A_P[r],
+// la[2r + 1] = A_Q[r]; ld the column differences, zero for a CONST task). A column
+// holds its epoch block's R rows, so each lane reads row min(r, R - 1) of all four
+// columns unconditionally, against wave-uniform column bases (SGPR base + 32-bit
+// lane offset), and one wait covers the four reads; rows at or past a task's Rn are
+// zero as before (selects). The masked, per-column form waited after each read.
+template <bool TWO>
+__device__ __forceinline__ void stage_pair(const SgWTask& P, const SgWTask& Q, const float* __restrict__ amps,
+                                           float* __restrict__ la, float* __restrict__ ld, int r0, int n, int lane) {
+  const bool pc = P.flags & SG_TASK_CONST, qc = Q.flags & SG_TASK_CONST;
+  const float* __restrict__ pa = amps + P.a_off;
+  const float* __restrict__ qa = amps + Q.a_off;
+  const float* __restrict__ pd = amps + (pc ? P.a_off : P.d_off);
+  const float* __restrict__ qd = amps + (qc ? Q.a_off : Q.d_off);
+  // n <= 128: the pairs' R <= SG_ROWS_F32, the tall pairs' chunks SG_LDS_ROWS / 2
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (h == 1 && n <= 64) break;  // wave-uniform
+    const int r = lane + 64 * h;
+    if (r >= n) break;
+    const int rr = r0 + r;
+    // byte offsets as 32-bit values: the SGPR-base + VGPR-offset load form
+    const unsigned bp = 4u * (unsigned)(rr < P.R ? rr : P.R - 1), bq = 4u * (unsigned)(rr < Q.R ? rr : Q.R - 1);
+    auto at = [](const float* __restrict__ c, unsigned b) {
+      return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(c) + b);
+    };
+    const float ap0 = at(pa, bp), aq0 = at(qa, bq);
+    const float dp0 = TWO ? at(pd, bp) : 0.f, dq0 = TWO ? at(qd, bq) : 0.f;
+    const bool inp = rr < P.Rn, inq = rr < Q.Rn;
+    const float ap = inp ? ap0 : 0.f, aq = inq ? aq0 : 0.f;
+    *reinterpret_cast<float2*>(la + 2 * r) = make_float2(ap, aq);
+    if (TWO)
+      *reinterpret_cast<float2*>(ld + 2 * r) = make_float2(inp && !pc ? dp0 - ap : 0.f, inq && !qc ? dq0 - aq : 0.f);
+  }
+}
+
+static_assert(SG_ROWS_F32 <= 128 && SG_LDS_ROWS / 2 <= 128, "stage_pair stages at most 128 rows per call");
+
+// A pair's samples to W (wave-uniform destination bases) and their masked maxima
+__device__ __forceinline__ void pair_store(const SgWTask& P, const SgWTask& Q, float yp, float yq,
+                                           float* __restrict__ W, int lane, float& mp, float& mq) {
+  const bool vp = lane < P.len, vq = lane < Q.len;
+  float* __restrict__ wp = W + (P.w_off + P.j0);
+  float* __restrict__ wq = W + (Q.w_off + Q.j0);
+  if (vp) wp[(unsigned)lane] = yp;
+  if (vq) wq[(unsigned)lane] = yq;
+  const int jp = P.j0 + lane, jq = Q.j0 + lane;
+  mp = vp && jp >= P.dj0 && jp < P.dj1 ? yp : 0.f;
+  mq = vq && jq >= Q.dj0 && jq < Q.dj1 ? yq : 0.f;
+}
+
 template <bool TWO>
 __device__ __forceinline__ void run_pair(const SgWTask& P, const SgWTask& Q, float* __restrict__ la,
                                          float* __restrict__ ld, const float* __restrict__ amps,
@@ -345,14 +396,7 @@ __device__ __forceinline__ void run_pair(const SgWTask& P, const SgWTask& Q, flo
     nc.off = TWO && !qc ? Q.d_off : Q.a_off;
     *cc = nc;
   } else {
-    for (int r = lane; r < R; r += 64) {
-      const float ap = r < P.Rn ? amps[P.a_off + r] : 0.f, aq = r < Q.Rn ? amps[Q.a_off + r] : 0.f;
-      *reinterpret_cast<float2*>(la + 2 * r) = make_float2(ap, aq);
-      if (TWO)
-        *reinterpret_cast<float2*>(ld + 2 * r) =
-            make_float2(r < P.Rn && !(P.flags & SG_TASK_CONST) ? amps[P.d_off + r] - ap : 0.f,
-                        r < Q.Rn && !(Q.flags & SG_TASK_CONST) ? amps[Q.d_off + r] - aq : 0.f);
-    }
+    stage_pair<TWO>(P, Q, amps, la, ld, 0, R, lane);
   }
   const bool vp = lane < P.len, vq = lane < Q.len;
   float tp, alp, snp, tq, alq, snq;
@@ -380,13 +424,7 @@ __device__ __forceinline__ void run_pair(const SgWTask& P, const SgWTask& Q, flo
     SG_PROW((f2{A0.x, A0.y}), (f2{D0.x, D0.y}))
   }
 #undef SG_PROW
-  const float yp = b1.x * snp;
-  const float yq = b1.y * snq;
-  const int jp = P.j0 + lane, jq = Q.j0 + lane;
-  if (vp) W[P.w_off + jp] = yp;
-  if (vq) W[Q.w_off + jq] = yq;
-  mp = vp && jp >= P.dj0 && jp < P.dj1 ? yp : 0.f;
-  mq = vq && jq >= Q.dj0 && jq < Q.dj1 ? yq : 0.f;
+  pair_store(P, Q, b1.x * snp, b1.y * snq, W, lane, mp, mq);
 }
 
 // Tasks of the fp32 class (listed in idx), one per wave. (A grid of resident waves
@@ -414,7 +452,10 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 // only the max over its tasks (sg_syl_max), so the run's max goes to its first task's
 // slot and -inf to the others: one wave reduction per run instead of two per step
 // (round 6; the per-step set-up, staging and stores stay per step).
-template <class PAIR>
+// IDXPF: the next step's two task indices are loaded with this step's descriptors, so a
+// step waits for one scalar round trip instead of two (r06l, same box: sg_sine_bank_pairs
+// 1.670 -> 1.631 ms; sg_sine_bank_tall_pairs 1.686 -> 1.719 ms, so off there)
+template <bool IDXPF, class PAIR>
 __device__ __forceinline__ void run_of_pairs(const int32_t* __restrict__ idx, const int32_t* __restrict__ rs,
                                              int64_t nruns, const SgWTask* __restrict__ tasks,
                                              float* __restrict__ taskmax, PAIR&& pair) {
@@ -424,9 +465,18 @@ __device__ __forceinline__ void run_of_pairs(const int32_t* __restrict__ idx, co
   if (r >= nruns) return;
   const int32_t k0 = rs[r], k1 = rs[r + 1];
   float m = -INFINITY;
+  int32_t ip = idx[k0], iq = idx[k0 + 1 < k1 ? k0 + 1 : k0];
   for (int32_t k = k0; k < k1; k += 2) {
-    const SgWTask P = tasks[idx[k]];
-    const SgWTask Q = tasks[idx[k + 1 < k1 ? k + 1 : k]];
+    if (!IDXPF) {
+      ip = idx[k];
+      iq = idx[k + 1 < k1 ? k + 1 : k];
+    }
+    const SgWTask P = tasks[ip];
+    const SgWTask Q = tasks[iq];
+    if (IDXPF && k + 2 < k1) {
+      ip = idx[k + 2];
+      iq = idx[k + 3 < k1 ? k + 3 : k + 2];
+    }
     float mp, mq;
     pair(P, Q, wave, lane, mp, mq);
     m = fmaxf(m, fmaxf(mp, mq));
@@ -443,7 +493,7 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_pairs(
     float* __restrict__ taskmax) {
   __shared__ __attribute__((aligned(16))) float rows[4][2][SG_LDS_ROWS];
   ColCache cc;
-  run_of_pairs(idx, rs, nruns, tasks, taskmax,
+  run_of_pairs<true>(idx, rs, nruns, tasks, taskmax,
                [&](const SgWTask& P, const SgWTask& Q, int wave, int lane, float& mp, float& mq) {
                  if ((P.flags & Q.flags) & SG_TASK_CONST) run_pair<false>(P, Q, rows[wave][0], rows[wave][1], amps, W, lane, mp, mq, &cc);
                  else run_pair<true>(P, Q, rows[wave][0], rows[wave][1], amps, W, lane, mp, mq, &cc);
@@ -515,15 +565,7 @@ __device__ __forceinline__ void run_pair_rs(const SgWTask& P, const SgWTask& Q, 
 #pragma unroll 1
   for (int r0 = (R - 1) / CH * CH; r0 >= 0; r0 -= CH) {
     const int n = R - r0 < CH ? R - r0 : CH;  // multiple of 16
-    for (int r = lane; r < n; r += 64) {
-      const int rr = r0 + r;
-      const float ap = rr < P.Rn ? amps[P.a_off + rr] : 0.f, aq = rr < Q.Rn ? amps[Q.a_off + rr] : 0.f;
-      *reinterpret_cast<float2*>(la + 2 * r) = make_float2(ap, aq);
-      if (TWO)
-        *reinterpret_cast<float2*>(ld + 2 * r) =
-            make_float2(rr < P.Rn && !(P.flags & SG_TASK_CONST) ? amps[P.d_off + rr] - ap : 0.f,
-                        rr < Q.Rn && !(Q.flags & SG_TASK_CONST) ? amps[Q.d_off + rr] - aq : 0.f);
-    }
+    stage_pair<TWO>(P, Q, amps, la, ld, r0, n, lane);
 #pragma unroll 1
     for (int r = n - 4; r >= 0; r -= 4) {
       const float4 A1 = *reinterpret_cast<const float4*>(la + 2 * r + 4);
@@ -537,13 +579,7 @@ __device__ __forceinline__ void run_pair_rs(const SgWTask& P, const SgWTask& Q, 
     }
   }
 #undef SG_RPROW
-  const float yp = b.x * snp;
-  const float yq = b.y * snq;
-  const int jp = P.j0 + lane, jq = Q.j0 + lane;
-  if (vp) W[P.w_off + jp] = yp;
-  if (vq) W[Q.w_off + jq] = yq;
-  mp = vp && jp >= P.dj0 && jp < P.dj1 ? yp : 0.f;
-  mq = vq && jq >= Q.dj0 && jq < Q.dj1 ? yq : 0.f;
+  pair_store(P, Q, b.x * snp, b.y * snq, W, lane, mp, mq);
 }
 
 __device__ __forceinline__ float run_one_tall(const SgWTask& T, float* __restrict__ la, float* __restrict__ ld,
@@ -581,7 +617,7 @@ extern "C" __global__ __launch_bounds__(256) void sg_sine_bank_tall_pairs(
     const SgWTask* __restrict__ tasks, const float* __restrict__ amps, float* __restrict__ W,
     float* __restrict__ taskmax) {
   __shared__ __attribute__((aligned(16))) float rows[4][2][SG_LDS_ROWS];
-  run_of_pairs(idx, rs, nruns, tasks, taskmax,
+  run_of_pairs<false>(idx, rs, nruns, tasks, taskmax,
                [&](const SgWTask& P, const SgWTask& Q, int wave, int lane, float& mp, float& mq) {
                  if ((P.flags & Q.flags) & SG_TASK_CONST) run_pair_rs<false>(P, Q, rows[wave][0], rows[wave][1], amps, W, lane, mp, mq);
                  else run_pair_rs<true>(P, Q, rows[wave][0], rows[wave][1], amps, W, lane, mp, mq);
