@@ -44,6 +44,7 @@ __device__ __forceinline__ void env_column(const SgEnvJob& J, int c, const SgEnv
     khi[g] = in ? e.khi : -1;
   }
   float* __restrict__ dst = fe + J.out + (int64_t)c * J.nr;
+  const char* __restrict__ tb = reinterpret_cast<const char*>(tm);
 #pragma unroll 1
   for (int k0 = 0; k0 < J.nr; k0 += 64) {
     const int k = k0 + lane;
@@ -55,8 +56,10 @@ __device__ __forceinline__ void env_column(const SgEnvJob& J, int c, const SgEnv
       uint64_t m = __ballot(klo[g] <= k0 + 64 && khi[g] >= k0 + 1);
       while (m) {
         const int t = __builtin_ctzll(m);
-        m &= m - 1;
-        const SgEnvTerm* __restrict__ e = tm + g * 64 + t;  // wave-uniform: scalar loads into SGPRs
+        m ^= 1ull << t;
+        // wave-uniform: scalar loads into SGPRs, at a 32-bit byte offset from the column's terms
+        const SgEnvTerm* __restrict__ e =
+            reinterpret_cast<const SgEnvTerm*>(tb + (unsigned)(g * 64 + t) * (unsigned)sizeof(SgEnvTerm));
         const double a = e->A, r = e->Rr, l = e->Lm;
         const float am = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amp[g]), t));
         const double d = fma(a, lx, fma(-r, x, -l));
@@ -68,6 +71,65 @@ __device__ __forceinline__ void env_column(const SgEnvJob& J, int c, const SgEnv
     const float lxf = (float)lx;
     const float v = fmaf(fmaf(C.lip, lxf, acc), C.boost, J.slope * lxf);
     if (k < J.nr) dst[k] = exp2f(v * 0.1f);
+  }
+}
+
+// Two bins per lane (SG_ENV_K2): chunks of 128 bins, lane l owns bins k0 + l and
+// k0 + 64 + l. The per-track scalar work (ballot walk, term address, scalar loads,
+// amplitude broadcast) is shared by both bins: the pair loop issued ~11 SALU next to
+// ~9 VALU per (chunk, track), so the scalar pipe bounded it as much as the vector pipe.
+// A track whose band misses a lane's bin contributes nothing there (the band is a
+// superset of the bins within the cut, and the cut is tested per bin), so the sums
+// are the 64-bin form's, term for term in the same track order.
+#ifndef SG_ENV_K2
+#define SG_ENV_K2 1
+#endif
+template <bool LG>
+__device__ __forceinline__ void env_column2(const SgEnvJob& J, int c, const SgEnvTerm* __restrict__ tm,
+                                            const SgEnvCol& C, const double* __restrict__ lg2, const double* lgs,
+                                            float* __restrict__ fe, int lane) {
+  const float thrf = -SG_ENV_CUT;
+  float amp[2];
+  int klo[2], khi[2];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int t = g * 64 + lane;
+    const bool in = t < J.ntr;
+    const SgEnvTerm& e = tm[in ? t : 0];
+    amp[g] = (float)e.amp;
+    klo[g] = in ? e.klo : 1 << 30;
+    khi[g] = in ? e.khi : -1;
+  }
+  float* __restrict__ dst = fe + J.out + (int64_t)c * J.nr;
+  const char* __restrict__ tb = reinterpret_cast<const char*>(tm);
+#pragma unroll 1
+  for (int k0 = 0; k0 < J.nr; k0 += 128) {
+    const int ka = k0 + lane, kb = ka + 64;
+    const int ca = ka < J.nr ? ka : J.nr - 1, cb = kb < J.nr ? kb : J.nr - 1;  // table reads in range
+    const double xa = (double)(ka + 1), xb = (double)(kb + 1);
+    const double lxa = LG ? lgs[ca] : lg2[ca], lxb = LG ? lgs[cb] : lg2[cb];
+    float acca = 0.f, accb = 0.f;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      uint64_t m = __ballot(klo[g] <= k0 + 128 && khi[g] >= k0 + 1);
+      while (m) {
+        const int t = __builtin_ctzll(m);
+        m ^= 1ull << t;
+        const SgEnvTerm* __restrict__ e =
+            reinterpret_cast<const SgEnvTerm*>(tb + (unsigned)(g * 64 + t) * (unsigned)sizeof(SgEnvTerm));
+        const double a = e->A, r = e->Rr, l = e->Lm;
+        const float am = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amp[g]), t));
+        const double da = fma(a, lxa, fma(-r, xa, -l)), db = fma(a, lxb, fma(-r, xb, -l));
+        const float dfa = (float)da, dfb = (float)db;
+        if (dfa > thrf) acca = fmaf(am, __builtin_amdgcn_exp2f(dfa), acca);
+        if (dfb > thrf) accb = fmaf(am, __builtin_amdgcn_exp2f(dfb), accb);
+      }
+    }
+    const float lfa = (float)lxa, lfb = (float)lxb;
+    const float va = fmaf(fmaf(C.lip, lfa, acca), C.boost, J.slope * lfa);
+    const float vb = fmaf(fmaf(C.lip, lfb, accb), C.boost, J.slope * lfb);
+    if (ka < J.nr) dst[ka] = exp2f(va * 0.1f);
+    if (kb < J.nr) dst[kb] = exp2f(vb * 0.1f);
   }
 }
 
@@ -101,8 +163,13 @@ extern "C" __global__ __launch_bounds__(256) void sg_spec_env(const SgEnvTask* _
   for (int c = T.c0; c < c1; ++c) {
     const SgEnvTerm* __restrict__ tm = terms + J.term0 + (int64_t)c * J.ntr;
     const SgEnvCol C = cols[J.col0 + c];
-    if (lds) env_column<true>(J, c, tm, C, lg2, lgs, fe, lane);
-    else env_column<false>(J, c, tm, C, lg2, lgs, fe, lane);
+    if (SG_ENV_K2) {
+      if (lds) env_column2<true>(J, c, tm, C, lg2, lgs, fe, lane);
+      else env_column2<false>(J, c, tm, C, lg2, lgs, fe, lane);
+    } else {
+      if (lds) env_column<true>(J, c, tm, C, lg2, lgs, fe, lane);
+      else env_column<false>(J, c, tm, C, lg2, lgs, fe, lane);
+    }
   }
 }
 
