@@ -309,9 +309,9 @@ static_assert(SG_ROWS_F32 <= 128, "ColCache holds two rows per lane");
 #endif
 
 // Rows [r0, r0 + n) of a pair's columns into LDS, interleaved (la[2r] = A_P[r],
-// la[2r + 1] = A_Q[r]; ld the column differences, zero for a CONST task). A column
-// holds its epoch block's R rows, so each lane reads row min(r, R - 1) of all four
-// columns unconditionally, against wave-uniform column bases (SGPR base + 32-bit
+// la[2r + 1] = A_Q[r]; ld the column differences, zero for a CONST task). Each lane
+// reads row min(r, Rn - 1) of all four columns unconditionally (the rows the masked
+// form read, no more bytes), against wave-uniform column bases (SGPR base + 32-bit
 // lane offset), and one wait covers the four reads; rows at or past a task's Rn are
 // zero as before (selects). The masked, per-column form waited after each read.
 template <bool TWO>
@@ -322,6 +322,7 @@ __device__ __forceinline__ void stage_pair(const SgWTask& P, const SgWTask& Q, c
   const float* __restrict__ qa = amps + Q.a_off;
   const float* __restrict__ pd = amps + (pc ? P.a_off : P.d_off);
   const float* __restrict__ qd = amps + (qc ? Q.a_off : Q.d_off);
+  const int lp = P.Rn > 0 ? P.Rn - 1 : 0, lq = Q.Rn > 0 ? Q.Rn - 1 : 0;  // last row read: no bytes past Rn
   // n <= 128: the pairs' R <= SG_ROWS_F32, the tall pairs' chunks SG_LDS_ROWS / 2
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -330,7 +331,7 @@ __device__ __forceinline__ void stage_pair(const SgWTask& P, const SgWTask& Q, c
     if (r >= n) break;
     const int rr = r0 + r;
     // byte offsets as 32-bit values: the SGPR-base + VGPR-offset load form
-    const unsigned bp = 4u * (unsigned)(rr < P.R ? rr : P.R - 1), bq = 4u * (unsigned)(rr < Q.R ? rr : Q.R - 1);
+    const unsigned bp = 4u * (unsigned)(rr < P.Rn ? rr : lp), bq = 4u * (unsigned)(rr < Q.Rn ? rr : lq);
     auto at = [](const float* __restrict__ c, unsigned b) {
       return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(c) + b);
     };
