@@ -1056,6 +1056,9 @@ extern "C" __global__ __launch_bounds__(256) void sg_harm_copy(const SgCopyTile*
   }
 }
 
+#ifndef SG_FIN_PRELOAD
+#define SG_FIN_PRELOAD 1
+#endif
 // General path: the tiles the planner did not give to sg_harm_copy (crossfade
 // pieces, amplitude envelope, drift, misaligned slots).
 // V = double: an fp64 syllable (W64 -> fh; out_buf is fh, fs unused)
@@ -1162,6 +1165,24 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
   int p = pu, di = d0;
   // a chunk clear of both fade ramps multiplies by exactly 1: skip it (wave-uniform)
   const bool ramp = sy.fade >= 2 && (c0 < sy.fade || c1 > sy.L - sy.fade);
+  // a chunk inside one direct piece (most of them): its four epoch-waveform reads are
+  // issued together, unconditionally (a lane past c1 rereads sample c1 - 1), before
+  // the per-sample work; in the loop below each read sat behind its own branch and
+  // waited alone (one read in flight per lane)
+  V pre[4];
+  bool direct1 = false;
+  if (SG_FIN_PRELOAD && one_piece) {
+    const SgPiece& pc = pieces[pu];
+    if (pc.nterms < 0) {
+      direct1 = true;
+      const V* __restrict__ src = W + (pc.t[0].src - pc.start);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t k = c0 + 64 * e + lane;
+        pre[e] = src[k < c1 ? k : c1 - 1];
+      }
+    }
+  }
   V res[4];  // every load of the chunk before its stores
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -1169,7 +1190,9 @@ __device__ __forceinline__ void finalize_tile(const SgSylTile& tl, const SgPiece
     res[e] = 0;
     if (k >= c1) break;
     V x;
-    if (one_piece) {
+    if (direct1) {
+      x = pre[e];
+    } else if (one_piece) {
       const SgPiece& pc = pieces[pu];
       x = pc.nterms == 0 ? (V)0 : piece_value(pc, W, k - pc.start);
     } else {
