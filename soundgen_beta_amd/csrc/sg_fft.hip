@@ -1445,6 +1445,9 @@ extern "C" __global__ __launch_bounds__(64) void sg_fft_probe(const SgFftGeom* _
 using sgd::contour_at;
 __device__ __forceinline__ float wave_max_f(float v) { return sgd::wave_max(v); }
 
+#ifndef SG_OLA_PF
+#define SG_OLA_PF 4  // frames per sample read together (wl / hop = 4 at seewave's 75 % overlap)
+#endif
 // Overlap-add gather: out[q] = scale * sum over frames f covering sample
 // p = first + q of frame_f[p - floor(f h)], zero outside [0, xlen).
 extern "C" __global__ __launch_bounds__(256) void sg_ola(const SgOlaTile* __restrict__ tiles,
@@ -1465,7 +1468,19 @@ extern "C" __global__ __launch_bounds__(256) void sg_ola(const SgOlaTile* __rest
       if (f > O.nframes - 1) f = O.nframes - 1;
       int i = pi - f * O.hi;
       const float* fr0 = fs + O.frames;
-      for (; f >= 0 && i < O.wl; --f, i += O.hi) acc += fr0[(int64_t)f * O.wl + i];
+      // the first SG_OLA_PF frames' reads issued together (clamped to frame f, sample i),
+      // then added in frame order as the loop below adds them
+      constexpr int PF = SG_OLA_PF;
+      float v[PF];
+#pragma unroll
+      for (int t = 0; t < PF; ++t) {
+        const bool ok = f - t >= 0 && i + t * O.hi < O.wl;
+        v[t] = fr0[ok ? (int64_t)(f - t) * O.wl + i + t * O.hi : (int64_t)f * O.wl + i];
+      }
+#pragma unroll
+      for (int t = 0; t < PF; ++t)
+        if (f - t >= 0 && i + t * O.hi < O.wl) acc += v[t];
+      for (f -= PF, i += PF * O.hi; f >= 0 && i < O.wl; --f, i += O.hi) acc += fr0[(int64_t)f * O.wl + i];
       acc *= O.scale;
     } else if (p >= 0 && p < O.xlen) {
       // frames f with floor(f h) <= p < floor(f h) + wl
