@@ -255,7 +255,10 @@ constexpr int SG_FFT_WAVES = 8;    // wavefronts (segments) per sg_stft_ola work
 
 // sg_stft_ola_noise (no forward FFT: its specialised path fits 168 VGPRs, 3 waves per
 // SIMD, and (12 + 4) M pairs of LDS fit 160 KB for every M <= 64 SG_PF_SRC)
-constexpr int SG_FFT_WAVES_NOISE = 12;
+#ifndef SG_NOISE_WAVES
+#define SG_NOISE_WAVES 12
+#endif
+constexpr int SG_FFT_WAVES_NOISE = SG_NOISE_WAVES;
 constexpr int sg_fft_waves(int phase) { return phase == 0 ? SG_FFT_WAVES_NOISE : SG_FFT_WAVES; }
 constexpr int SG_PF_SRC = 20;      // sg_stft_ola register prefetch: sound pairs per lane (M <= 1280)
 constexpr int SG_PF_PAIR = 10;     // bin pairs per lane (M / 2 + 1 <= 640)
@@ -393,7 +396,8 @@ struct SgMixTile {
 struct SgEnvTerm {
   double A, Rr, Lm, amp;
   int32_t klo, khi;
-  int32_t pad[2];
+  float ampf;  // (float)amp: sg_spec_env reads it as a scalar operand
+  int32_t pad;
 };
 static_assert(sizeof(SgEnvTerm) == 48, "SgEnvTerm layout");
 struct SgEnvCol {

@@ -5,19 +5,19 @@
 // the noise filter of generateNoise() with its rolloff slope (R/source.R:103-105).
 //
 // One wave per task = SG_ENV_COLS columns of one job. Per column, lane t holds
-// the term of track t (and t + 64) in registers. Lanes then own bins, 64 per
-// chunk: a ballot over the tracks' bin ranges gives the tracks that reach the
-// chunk (a formant is nonzero within a band of a few tens of bins), and only
-// those are summed, their parameters broadcast from the owning lane. The
-// log-density difference A log2 k - Rr k - Lm is formed in fp64 from a log2(k)
-// table (its two products reach ~1e6 for narrow formants, so fp32 would lose
-// the difference); the power of two and the sum over formants run in fp32.
-// Each chunk ends with 64 consecutive fp32 stores (coalesced).
+// the band of track t (and t + 64). Lanes then own bins, two per lane in chunks of
+// 128 (env_column2; env_column is the 64-bin form): a ballot over the tracks' bands
+// gives the tracks that reach the chunk (a formant is nonzero within a band of a few
+// tens of bins), and only those are summed, each track's parameters and fp32
+// amplitude by scalar loads. The log-density difference A log2 k - Rr k - Lm is
+// formed in fp64 from a log2(k) table (its two products reach ~1e6 for narrow
+// formants, so fp32 would lose the difference); the power of two and the sum over
+// formants run in fp32. Each chunk ends with coalesced fp32 stores.
 //
-// Work per active (chunk, track): 2 fp64 FMA + cvt + v_exp_f32 + FMA + select,
-// the track's parameters from scalar loads (v_readlane broadcasts were 7 more VALU
-// instructions per pair, and the kernel is VALU-bound: PMC ~94 % VALU-busy SIMDs). Output 4 B per bin and column, ~48 B per track and
-// column read once: VALU/issue-bound, not HBM-bound.
+// Work per selected (chunk, track): per bin 2 fp64 FMA + cvt + v_exp_f32 + FMA, and
+// per track ~8 scalar instructions (ballot walk, address, loads) shared by the two
+// bins. Output 4 B per bin and column, ~48 B per track and column read once: issue-
+// bound (vector and scalar), not HBM-bound.
 #include <hip/hip_runtime.h>
 
 #include "sg_dev.h"
@@ -78,11 +78,19 @@ __device__ __forceinline__ void env_column(const SgEnvJob& J, int c, const SgEnv
 // k0 + 64 + l. The per-track scalar work (ballot walk, term address, scalar loads,
 // amplitude broadcast) is shared by both bins: the pair loop issued ~11 SALU next to
 // ~9 VALU per (chunk, track), so the scalar pipe bounded it as much as the vector pipe.
-// A track whose band misses a lane's bin contributes nothing there (the band is a
-// superset of the bins within the cut, and the cut is tested per bin), so the sums
-// are the 64-bin form's, term for term in the same track order.
+// SG_ENV_NOCUT: a selected track adds its term at every bin of the chunk, with no
+// per-bin cut (a compare and a select per bin fewer). Outside its band a term is below
+// 2^-SG_ENV_CUT of its column max (the band is a superset of the bins within the cut),
+// so a bin's dB sum moves by less than |amp| 2^-30 against the cut form (which took the
+// 64-bin form's terms exactly); the oracle sums every term.
 #ifndef SG_ENV_K2
 #define SG_ENV_K2 1
+#endif
+#ifndef SG_ENV_AMPF
+#define SG_ENV_AMPF 1
+#endif
+#ifndef SG_ENV_NOCUT  // r06v: 2.377 -> 2.213 ms per C5 launch without the per-bin cut
+#define SG_ENV_NOCUT 1
 #endif
 template <bool LG>
 __device__ __forceinline__ void env_column2(const SgEnvJob& J, int c, const SgEnvTerm* __restrict__ tm,
@@ -118,11 +126,18 @@ __device__ __forceinline__ void env_column2(const SgEnvJob& J, int c, const SgEn
         const SgEnvTerm* __restrict__ e =
             reinterpret_cast<const SgEnvTerm*>(tb + (unsigned)(g * 64 + t) * (unsigned)sizeof(SgEnvTerm));
         const double a = e->A, r = e->Rr, l = e->Lm;
-        const float am = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amp[g]), t));
+        // the amplitude as a scalar load (the planner's (float)amp) or broadcast from its lane
+        const float am = SG_ENV_AMPF ? e->ampf
+                                     : __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amp[g]), t));
         const double da = fma(a, lxa, fma(-r, xa, -l)), db = fma(a, lxb, fma(-r, xb, -l));
         const float dfa = (float)da, dfb = (float)db;
-        if (dfa > thrf) acca = fmaf(am, __builtin_amdgcn_exp2f(dfa), acca);
-        if (dfb > thrf) accb = fmaf(am, __builtin_amdgcn_exp2f(dfb), accb);
+        if (SG_ENV_NOCUT) {  // every selected track's term at both bins (below the cut they add < 2^-30 amp)
+          acca = fmaf(am, __builtin_amdgcn_exp2f(dfa), acca);
+          accb = fmaf(am, __builtin_amdgcn_exp2f(dfb), accb);
+        } else {
+          if (dfa > thrf) acca = fmaf(am, __builtin_amdgcn_exp2f(dfa), acca);
+          if (dfb > thrf) accb = fmaf(am, __builtin_amdgcn_exp2f(dfb), accb);
+        }
       }
     }
     const float lfa = (float)lxa, lfb = (float)lxb;

@@ -754,6 +754,7 @@ int64_t plan_envelope(Batch& B, Rng& R, double nrd, int64_t nc, const sg_formant
         const double k0 = std::floor(kmax), k1 = std::min((double)nr, std::ceil(kmax));
         e.Lm = std::max(l2(k0), l2(k1));
         e.amp = tr.amp[c] * formantDep;
+        e.ampf = (float)e.amp;
         // bins where the term is within 2^-SG_ENV_CUT of its column max (sg_dev.h): superset
         // from ln u - u + 1 <= -(u-1)^2/(2 max(u, 1))
         e.klo = 1;
