@@ -325,7 +325,13 @@ constexpr int SG_SEG_LAST = 2;
 // recompute more warm-up frames but balance the waves better (round 5, C5 per launch:
 // noise 48 / 40 / 32 / 24 frames 2.31 / 2.24 / 2.17 / 2.12 ms, filter 48 / 40 / 32 / 24
 // 8.05 / 8.01 / 7.96 / 8.11 ms; profiles/r05zx_seg_ab.txt)
-constexpr int sg_seg_frames(int phase) { return phase == 0 ? 24 : 32; }
+#ifndef SG_SEG_NOISE
+#define SG_SEG_NOISE 24
+#endif
+#ifndef SG_SEG_FILTER
+#define SG_SEG_FILTER 32
+#endif
+constexpr int sg_seg_frames(int phase) { return phase == 0 ? SG_SEG_NOISE : SG_SEG_FILTER; }
 constexpr int SG_SEG_MIN_FRAMES = 8;  // shortest segment the planner picks (3 recomputed frames each)
 constexpr int64_t SG_RESIDENT_WAVES = 256 * SG_FFT_WAVES;  // sg_stft_ola waves resident on a 256-CU MI355X
 constexpr int64_t sg_resident_waves(int phase) { return 256 * (int64_t)sg_fft_waves(phase); }

@@ -19,6 +19,10 @@
 #include "sg_plan.h"
 #include "sg_prof.h"
 
+#ifndef SG_SEG_SORT
+#define SG_SEG_SORT 1
+#endif
+
 namespace sg {
 
 namespace {
@@ -990,7 +994,16 @@ void finalize_spec(Batch& B) {
       seg_frames = std::min<int64_t>(S, SEG);
     }
     int cur_geom = -1;
+    size_t group0 = B.olasegs.size();  // first segment of the current geometry
     auto pad = [&]() {
+      // a workgroup lasts as long as its longest segment: the geometry's segments go
+      // longest first, so each workgroup's WPH segments have about the same length
+      // (in OLA order the idle share was 10 % of the filter and 16 % of the noise
+      // workgroups' wave-frames at C5). A segment's outputs and max slot are its own,
+      // so the order changes no value.
+      if (SG_SEG_SORT)
+        std::stable_sort(B.olasegs.begin() + (std::ptrdiff_t)group0, B.olasegs.end(),
+                         [](const SgSegment& a, const SgSegment& b) { return a.nf > b.nf; });
       while (((int64_t)B.olasegs.size() - B.seg_range[ph][0]) % WPH) {
         SgSegment d{};
         d.geom = cur_geom;
@@ -1003,6 +1016,7 @@ void finalize_spec(Batch& B) {
       if (gi != cur_geom) {
         pad();
         cur_geom = gi;
+        group0 = B.olasegs.size();
       }
       auto bstart = [&](int64_t f) -> int64_t {
         return o.hi > 0 ? f * o.hi : (int64_t)std::floor((double)f * o.h);
@@ -1065,6 +1079,17 @@ void finalize_spec(Batch& B) {
         if (B.olasegs[i].nf > 0) { fr += B.olasegs[i].nf; ++sgs; }
       std::fprintf(stderr, "sg plan: phase %d: %lld frames computed in %lld segments (%zu frames, %zu unfused groups)\n", ph,
                    (long long)fr, (long long)sgs, B.frames[ph].size(), (size_t)(B.fgroup_range[ph][2] - B.fgroup_range[ph][1]));
+      // workgroup balance: a workgroup lasts as long as its longest segment
+      const int WPH = sg_fft_waves(ph);
+      int64_t wmax = 0, wsum = 0;
+      for (int64_t i = B.seg_range[ph][0]; i < B.seg_range[ph][1]; i += WPH) {
+        int64_t mx = 0;
+        for (int w = 0; w < WPH && i + w < B.seg_range[ph][1]; ++w) mx = std::max<int64_t>(mx, B.olasegs[i + w].nf);
+        wmax += mx * WPH;
+        for (int w = 0; w < WPH && i + w < B.seg_range[ph][1]; ++w) wsum += std::max<int32_t>(0, B.olasegs[i + w].nf);
+      }
+      std::fprintf(stderr, "sg plan: phase %d: workgroup wave-frames %lld, used %lld (%.1f%% idle)\n", ph, (long long)wmax,
+                   (long long)wsum, wmax ? 100.0 * (double)(wmax - wsum) / (double)wmax : 0.0);
     }
     std::map<int32_t, int64_t> gfr;  // fused frames per geometry
     for (const SgSegment& sg : B.olasegs)
