@@ -381,8 +381,9 @@ def roofline(st, prof, steps, config, kern):
     if issue:
         r["issue"] = issue
     if kern == "sg_stft_ola":
-        r["binding"] = ("LDS passes and latency at 2 waves/SIMD (221 VGPRs): radix-29 stage on the matrix pipe "
-                        "(MFMA), radix 19 on the VALU, radix 2 fused with the untangle and the window; see issue")
+        r["binding"] = ("latency at 2 waves/SIMD (221 VGPRs; the LDS array ~0.4 busy, DESIGN.md section 5): radix-29 "
+                        "stage on the matrix pipe (MFMA), radix 19 on the VALU, radix 2 fused with the untangle and "
+                        "the window; workgroups of equal-length segments; see issue")
     return r
 
 
