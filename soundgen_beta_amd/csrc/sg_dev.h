@@ -321,15 +321,18 @@ struct SgSegment {
 };
 constexpr int SG_SEG_FIRST = 1;
 constexpr int SG_SEG_LAST = 2;
-// target frames owned per segment (one wavefront each), per phase: shorter segments
-// recompute more warm-up frames but balance the waves better (round 5, C5 per launch:
-// noise 48 / 40 / 32 / 24 frames 2.31 / 2.24 / 2.17 / 2.12 ms, filter 48 / 40 / 32 / 24
-// 8.05 / 8.01 / 7.96 / 8.11 ms; profiles/r05zx_seg_ab.txt)
+// target frames owned per segment (one wavefront each), per phase. Shorter segments
+// recompute more warm-up frames; round 5 (segments in OLA order) measured shorter ones
+// faster because they balanced the workgroups (C5 per launch: noise 48 / 40 / 32 / 24
+// frames 2.31 / 2.24 / 2.17 / 2.12 ms, filter 8.05 / 8.01 / 7.96 / 8.11 ms;
+// profiles/r05zx_seg_ab.txt). With the segments sorted by length (round 6, SG_SEG_SORT)
+// the balance no longer depends on it: noise 24 / 32 / 48 1.975 / 1.912 / 1.880 ms,
+// filter 32 / 48 / 64 7.102 / 6.907 / 6.930 ms (profiles/r06za_seglen_ab_*.csv)
 #ifndef SG_SEG_NOISE
-#define SG_SEG_NOISE 24
+#define SG_SEG_NOISE 48
 #endif
 #ifndef SG_SEG_FILTER
-#define SG_SEG_FILTER 32
+#define SG_SEG_FILTER 48
 #endif
 constexpr int sg_seg_frames(int phase) { return phase == 0 ? SG_SEG_NOISE : SG_SEG_FILTER; }
 constexpr int SG_SEG_MIN_FRAMES = 8;  // shortest segment the planner picks (3 recomputed frames each)
