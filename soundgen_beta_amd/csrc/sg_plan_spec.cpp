@@ -22,6 +22,9 @@
 #ifndef SG_SEG_SORT
 #define SG_SEG_SORT 1
 #endif
+#ifndef SG_ENV_SORT
+#define SG_ENV_SORT 1
+#endif
 
 namespace sg {
 
@@ -875,6 +878,25 @@ void finalize_spec(Batch& B) {
   B.envtasks.clear();
   for (size_t j = 0; j < B.envjobs.size(); ++j)
     for (int32_t c0 = 0; c0 < B.envjobs[j].nc; c0 += SG_ENV_COLS) B.envtasks.push_back(SgEnvTask{(int32_t)j, c0});
+  auto cost = [&](const SgEnvTask& t) {  // sg_spec_env work of a task ~ columns x 128-bin chunks x tracks
+    const SgEnvJob& J = B.envjobs[t.job];
+    return (double)std::min<int32_t>(SG_ENV_COLS, J.nc - t.c0) * (double)((J.nr + 127) / 128) * (double)J.ntr;
+  };
+  // the costliest tasks first, so each workgroup's four waves carry about the same work
+  // (in job order a workgroup mixed a job's last, partial task with the next job's)
+  if (SG_ENV_SORT)
+    std::stable_sort(B.envtasks.begin(), B.envtasks.end(),
+                     [&](const SgEnvTask& a, const SgEnvTask& b) { return cost(a) > cost(b); });
+  if (std::getenv("SG_DEBUG_PLAN")) {  // sg_spec_env workgroup balance
+    double wmax = 0, wsum = 0;
+    for (size_t i = 0; i < B.envtasks.size(); i += 4) {
+      double mx = 0;
+      for (size_t w = i; w < i + 4 && w < B.envtasks.size(); ++w) { mx = std::max(mx, cost(B.envtasks[w])); wsum += cost(B.envtasks[w]); }
+      wmax += 4 * mx;
+    }
+    std::fprintf(stderr, "sg plan: envelope tasks %zu, workgroup cost %.3g, used %.3g (%.1f%% idle)\n", B.envtasks.size(), wmax,
+                 wsum, wmax > 0 ? 100.0 * (wmax - wsum) / wmax : 0.0);
+  }
   // frames: per phase, sorted by (kernel, geometry), stable so that the
   // frames of one OLA stay consecutive; groups for the workgroup kernel only
   B.fgroups.clear();
