@@ -282,14 +282,19 @@ def pmc_from_profiles(config, kernel):
       valu_busy_per_simd       SQ_ACTIVE_INST_VALU / SQ_BUSY_CU_CYCLES: the share of a
                                SIMD's cycles issuing VALU (waves x issue share)
       mfma_busy_per_simd       SQ_VALU_MFMA_BUSY_CYCLES / (4 SQ_BUSY_CU_CYCLES)
-    The last three need SQ_BUSY_CU_CYCLES in the summary (tools/gpu_pmc_head.sh since
-    round 5)."""
+      lds_conflicts_per_instr  SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS (summed over launches)
+      lds_conflict_share       SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE: the conflicts' share of
+                               the LDS array's busy cycles
+      lds_array_busy           SQ_LDS_IDX_ACTIVE / SQ_BUSY_CU_CYCLES
+    The busy-cycle ratios need SQ_BUSY_CU_CYCLES in the summary (tools/gpu_pmc_head.sh since
+    round 5), the LDS ones its third pass (round 6)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_%s_pmc.json" % config)))
     if not files:
         return None
     d = json.load(open(files[-1]))
     acc = {}
+    lds = {}
     for k, v in d.get("kernels", {}).items():
         if k.split(" ")[0] != kernel or not v.get("SQ_WAVE_CYCLES"):
             continue
@@ -303,13 +308,23 @@ def pmc_from_profiles(config, kernel):
                 acc.setdefault("valu_busy", []).append(v["SQ_ACTIVE_INST_VALU"] / busy)
             if "SQ_VALU_MFMA_BUSY_CYCLES" in v:
                 acc.setdefault("mfma_busy", []).append(v["SQ_VALU_MFMA_BUSY_CYCLES"] / (4 * busy))
+            if "SQ_LDS_IDX_ACTIVE" in v:
+                acc.setdefault("lds_busy", []).append(v["SQ_LDS_IDX_ACTIVE"] / busy)
+        n = v.get("launches", 1)
+        for c in ("SQ_LDS_BANK_CONFLICT", "SQ_INSTS_LDS", "SQ_LDS_IDX_ACTIVE"):
+            if c in v:
+                lds[c] = lds.get(c, 0.0) + v[c] * n
     if not acc:
         return None
     m = {c: float(np.mean(x)) for c, x in acc.items()}
+    conf = lds.get("SQ_LDS_BANK_CONFLICT")
+    m["lds_conf_instr"] = conf / lds["SQ_INSTS_LDS"] if conf is not None and lds.get("SQ_INSTS_LDS") else None
+    m["lds_conf_share"] = conf / lds["SQ_LDS_IDX_ACTIVE"] if conf is not None and lds.get("SQ_LDS_IDX_ACTIVE") else None
     return {"valu_issue_per_wave": m.get("SQ_ACTIVE_INST_VALU"), "lds_issue_per_wave": m.get("SQ_ACTIVE_INST_LDS"),
             "waitcnt_per_wave": m.get("SQ_WAIT_INST_ANY"), "waves_per_simd": m.get("waves"),
             "valu_busy_per_simd": m.get("valu_busy"), "mfma_busy_per_simd": m.get("mfma_busy"),
-            "source": os.path.relpath(files[-1], ROOT)}
+            "lds_conflicts_per_instr": m.get("lds_conf_instr"), "lds_conflict_share": m.get("lds_conf_share"),
+            "lds_array_busy": m.get("lds_busy"), "source": os.path.relpath(files[-1], ROOT)}
 
 
 SG_WTASK_BYTES = 128  # sizeof(SgWTask), sg_dev.h

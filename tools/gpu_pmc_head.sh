@@ -15,9 +15,11 @@ export TMPDIR=/tmp
 # pmc_from_profiles), and each pass's issue shares are taken against its own wave cycles
 G1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT"
 G2="SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU"
+# LDS: conflict cycles against LDS instructions and against the LDS array's busy cycles
+G3="SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS"
 cd /tmp
 i=0
-for grp in "$G1" "$G2"; do
+for grp in "$G1" "$G2" "$G3"; do
   i=$((i+1))
   SG_OVERLAP=0 timeout -s KILL 240 rocprofv3 --pmc $grp --output-format csv -d "$R/gpurun_out/${TAG}_${CFG}sq_$i" -o run -- python3 "$R/bench.py" --config $CFG --steps 3 --warmup 1 --device-steps 0 --no-d2h --no-cpu-baseline --rms-calls 0 > "$R/gpurun_out/${TAG}_${CFG}sq_$i.log" 2>&1 || { tail -20 "$R/gpurun_out/${TAG}_${CFG}sq_$i.log"; exit 1; }
 done
