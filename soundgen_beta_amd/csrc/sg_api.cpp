@@ -502,7 +502,7 @@ void record_draws(const sg_call_desc* calls, int64_t n_calls, std::vector<int32_
   plan_range(B, calls, 0, n_calls, true, &done);
   if (sg::g_prof_on) {
     static const char* names[] = {"harmonics", "rolloff", "contour", "envelope", "noise", "filter", "finalize",
-                                  "finalize_spec", "fry", "crossfade", "emit", "tasks", "tiles", "soundgen"};
+                                  "finalize_spec", "fry", "crossfade", "emit", "tasks", "tiles", "soundgen", "env_upsample", "env_stochastic", "env_terms"};
     for (int i = 0; i < sg::PF_N; ++i)
       std::fprintf(stderr, "sg_plan_prof record %-14s %.3f s\n", names[i], sg::g_prof_ns[i].exchange(0) * 1e-9);
   }
@@ -575,7 +575,7 @@ int plan_batch_ex(sg_ctx* ctx, const sg_call_desc* calls, int64_t n_calls, bool 
     }
     if (sg::g_prof_on) {
       static const char* names[] = {"harmonics", "rolloff", "contour", "envelope", "noise", "filter", "finalize",
-                                    "finalize_spec", "fry", "crossfade", "emit", "tasks", "tiles", "soundgen"};
+                                    "finalize_spec", "fry", "crossfade", "emit", "tasks", "tiles", "soundgen", "env_upsample", "env_stochastic", "env_terms"};
       for (int i = 0; i < sg::PF_N; ++i)
         std::fprintf(stderr, "sg_plan_prof %-14s %.3f s\n", names[i], sg::g_prof_ns[i].exchange(0) * 1e-9);
       std::fprintf(stderr, "sg_plan_prof host MB: fl %.1f amps %.1f knots %.1f cknots %.1f tasks %.1f segs %.1f "

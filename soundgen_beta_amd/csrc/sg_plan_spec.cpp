@@ -613,6 +613,7 @@ int64_t plan_envelope(Batch& B, Rng& R, double nrd, int64_t nc, const sg_formant
     std::vector<Track> fu(nF);
     int64_t off = 0;
     for (int f = 0; f < nF; ++f) {
+      ProfScope pu(PF_ENV_UPS);
       // draws_only: the stochastic formants read the last track's frequencies alone
       if (!B.draws_only || f == nF - 1) fu[f].freq = col_upsample(&t0[off], &f0[off], np[f], nPoints, slf, nc);
       if (!B.draws_only) {
@@ -623,6 +624,7 @@ int64_t plan_envelope(Batch& B, Rng& R, double nrd, int64_t nc, const sg_formant
       off += np[f];
     }
     if (temperature > 0) {  // stochastic formants   R/sourceSpectrum.R:347-415
+      ProfScope pst(PF_ENV_STOCH);
       double fdisp;
       if (vtNull && nF > 1) {
         vec c2(nF);
@@ -741,6 +743,7 @@ int64_t plan_envelope(Batch& B, Rng& R, double nrd, int64_t nc, const sg_formant
     // plan_range's per-call try), not the whole batch at finalize_spec
     if (fu.size() > 2 * 64) throw SgError(SG_E_UNSUPPORTED, "spectral envelope: more than 128 formant tracks");
     job.ntr = (int32_t)fu.size();
+    ProfScope pte(PF_ENV_TERMS);
     B.eterms.resize(B.eterms.size() + (size_t)(nc * job.ntr));
     SgEnvTerm* tm = &B.eterms[job.term0];
     for (int64_t c = 0; c < nc; ++c)

@@ -9,7 +9,7 @@
 namespace sg {
 
 enum ProfId { PF_HARM, PF_ROLLOFF, PF_CONTOUR, PF_ENVELOPE, PF_NOISE, PF_FILTER, PF_FINALIZE, PF_SPEC, PF_FRY, PF_XFADE,
-              PF_EMIT, PF_TASKS, PF_TILES, PF_SOUNDGEN, PF_N };
+              PF_EMIT, PF_TASKS, PF_TILES, PF_SOUNDGEN, PF_ENV_UPS, PF_ENV_STOCH, PF_ENV_TERMS, PF_N };
 extern std::atomic<int64_t> g_prof_ns[PF_N];
 extern bool g_prof_on;
 
