@@ -1998,6 +1998,12 @@ extern "C" __global__ __launch_bounds__(256) void sg_ugather(const SgUJob* __res
   for (int64_t j = threadIdx.x; j < J.ntot; j += 256) fl[J.dst + j] = j < J.n ? us[J.src + j] : 0.f;
 }
 
+#ifndef SG_MIX_E
+#define SG_MIX_E 4  // samples per thread and chunk
+#endif
+#ifndef SG_MIX_WAVES
+#define SG_MIX_WAVES 8
+#endif
 // HP: the pre-filter sound of an fp64 bout: fp64 sum into fh (X.to_fs == 2), voiced
 // items (SG_ITEM_F64) read from fh, noise items from fs
 template <bool HP>
@@ -2012,7 +2018,7 @@ __device__ __forceinline__ void mix_body(const SgMixTile* __restrict__ tiles, co
   if constexpr (HP) dst = fh;
   else dst = X.to_fs ? fs : out;
   // samples per thread and chunk (r04: 4 at 8 waves per SIMD, 1.83 -> 1.74 ms per C5 launch over 8 at 5)
-  constexpr int E = 4;
+  constexpr int E = SG_MIX_E;
   const int64_t kend = T.k0 + SG_MIX_TILE < X.len ? T.k0 + SG_MIX_TILE : X.len;
   // per-tile constants, hoisted out of the sample loops (one scalar-load burst)
   const float base_scale = X.base_kind == SG_BASE_NORM ? 1.f / olamax[X.base_ola] : 1.f;
@@ -2111,7 +2117,7 @@ __device__ __forceinline__ void mix_body(const SgMixTile* __restrict__ tiles, co
 }
 
 // sg_mix's registers capped for 8 waves per SIMD (r04: 94 VGPRs = 5 waves uncapped)
-#define SG_MIX_ATTR __attribute__((amdgpu_waves_per_eu(8)))
+#define SG_MIX_ATTR __attribute__((amdgpu_waves_per_eu(SG_MIX_WAVES)))
 extern "C" __global__ __launch_bounds__(256) SG_MIX_ATTR void sg_mix(const SgMixTile* __restrict__ tiles,
                                                          const SgMix* __restrict__ mixes,
                                                          const SgNoiseItem* __restrict__ items,
